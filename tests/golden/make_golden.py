@@ -1,0 +1,190 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE GMAT code.
+
+Container-only (needs /root/reference).  The reference is imported through
+oracle/ref_shim.py (pandas_plink / cffi / np.int shims); everything it
+computes is written here as small data fixtures (inputs and expected outputs), never as
+code.  Re-run with:  python tests/golden/make_golden.py
+
+Fixtures ("reference code + its own C decoder in fp64"):
+  mouse/   examples/data/mouse (cfg1): agmat/dgmat summaries, REML [A,AxA] (with the
+           per-iteration history) and 5-GRM, exact epiAA/AD/DD hit files, a 5,000-pair
+           epiAA_pair file, parallel parts, annotation, and the C effect screen.
+  tiny/    a 150 x 200 related synthetic cohort (n % 4 == 2, two monomorphic SNPs and one
+           all-heterozygous SNP) with full K/D and every testable pair for AA/AD/DD.
+"""
+import gzip
+import hashlib
+import json
+import logging
+import os
+import shutil
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle.ref_shim import import_reference  # noqa: E402
+from gmat_amd import synth  # noqa: E402
+
+MOUSE = "/root/reference/examples/data/mouse"
+
+
+class _Capture(logging.Handler):
+    def __init__(self):
+        super().__init__()
+        self.msgs = []
+
+    def emit(self, record):
+        self.msgs.append(record.getMessage())
+
+
+def _history(msgs):
+    out = []
+    for m in msgs:
+        if m.startswith("Updated variances: "):
+            out.append([float(v) for v in m.split(": ", 1)[1].split()])
+    return np.array(out)
+
+
+def _md5(path):
+    return hashlib.md5(open(path, "rb").read()).hexdigest()
+
+
+def _grm_summary(k, path_txt, rng):
+    n = k.shape[0]
+    ia = rng.integers(0, n, 400)
+    ib = rng.integers(0, n, 400)
+    return dict(diag=np.diag(k).copy(), row0=k[0].copy(), ia=ia, ib=ib, val=k[ia, ib],
+                trace=np.trace(k), total=k.sum(), md5=np.array(_md5(path_txt)))
+
+
+def mouse(gmat, work, out):
+    from gmat.gmatrix import agmat, dgmat_as
+    from gmat.uvlmm import wemai_multi_gmat
+    from gmat.remma import annotation_snp_pos
+    from gmat.remma.remma_epiAA import remma_epiAA, remma_epiAA_pair, remma_epiAA_parallel, remma_epiAA_eff
+    from gmat.remma.remma_epiDD import remma_epiDD, remma_epiDD_eff
+    from gmat.remma.remma_epiAD import remma_epiAD, remma_epiAD_eff
+    os.makedirs(out, exist_ok=True)
+    for f in ("plink.bed", "plink.bim", "plink.fam", "pheno"):
+        shutil.copy(os.path.join(MOUSE, f), work)
+        shutil.copy(os.path.join(MOUSE, f), out)  # input data travels with the fixtures
+    bed = os.path.join(work, "plink")
+    pheno = os.path.join(work, "pheno")
+    rng = np.random.Generator(np.random.PCG64(11))
+    a, _ = agmat(bed)
+    np.savez(os.path.join(out, "agmat.npz"), **_grm_summary(a, bed + ".agrm0", rng))
+    d, _ = dgmat_as(bed)
+    np.savez(os.path.join(out, "dgmat_as.npz"), **_grm_summary(d, bed + ".dgrm_as0", rng))
+    # agmat with inv=True and the two text formats on a fixed 6x6 corner is covered by tiny/
+    cap = _Capture()
+    root = logging.getLogger()
+    root.addHandler(cap)
+    root.setLevel(logging.INFO)
+    var2 = wemai_multi_gmat(pheno, bed, [a, a * a], out_file=os.path.join(work, "var2"))
+    hist2 = _history(cap.msgs)
+    cap.msgs.clear()
+    var5 = wemai_multi_gmat(pheno, bed, [a, d, a * a, a * d, d * d], out_file=os.path.join(work, "var5"))
+    hist5 = _history(cap.msgs)
+    root.removeHandler(cap)
+    np.savez(os.path.join(out, "reml.npz"), var2=var2, hist2=hist2, var5=var5, hist5=hist5)
+    shutil.copy(os.path.join(work, "var2"), os.path.join(out, "wemai_multi_gmat.var2"))
+
+    g2 = [a, a * a]
+    g5 = [a, d, a * a, a * d, d * d]
+    remma_epiAA(pheno, bed, g2, var2, p_cut=1e-5, out_file=os.path.join(out, "epiAA_1e-5"))
+    remma_epiAA(pheno, bed, g2, var2, p_cut=1e-3, out_file=os.path.join(out, "epiAA_1e-3"))
+    remma_epiAD(pheno, bed, g5, var5, p_cut=1e-5, out_file=os.path.join(out, "epiAD_1e-5"))
+    remma_epiDD(pheno, bed, g5, var5, p_cut=1e-5, out_file=os.path.join(out, "epiDD_1e-5"))
+    for k in (1, 2, 3):
+        remma_epiAA_parallel(pheno, bed, g2, var2, [3, k], p_cut=1e-4,
+                             out_file=os.path.join(out, "epiAA_par3_1e-4"))
+    # fixed pair list (header + 5000 pairs i<j)
+    m = sum(1 for _ in open(bed + ".bim"))
+    pr = np.random.Generator(np.random.PCG64(5))
+    i = pr.integers(0, m - 1, 6000)
+    j = pr.integers(0, m, 6000)
+    keep = i < j
+    pairs = np.column_stack([i[keep], j[keep]])[:5000]
+    pair_file = os.path.join(out, "pairs5000")
+    np.savetxt(pair_file, pairs, fmt="%d", header="snp_0 snp_1", comments="")
+    remma_epiAA_pair(pheno, bed, g2, var2, pair_file, p_cut=1.0, out_file=os.path.join(out, "epiAA_pair5000"))
+    annotation_snp_pos(os.path.join(out, "epiAA_1e-3"), bed, p_cut=1e-4, dis=1000000)
+    # C effect screen: rows 0..199, fixed var_app so the threshold is known
+    rows = list(range(200))
+    cwd = os.getcwd()
+    os.chdir(work)
+    try:
+        remma_epiAA_eff(pheno, bed, g2, var2, snp_lst_0=rows, var_app=1470.0, p_cut=1e-2,
+                        out_file=os.path.join(out, "epiAA_eff_rows200"))
+        remma_epiDD_eff(pheno, bed, g5, var5, snp_lst_0=rows, var_app=490.0, p_cut=1e-2,
+                        out_file=os.path.join(out, "epiDD_eff_rows200"))
+        remma_epiAD_eff(pheno, bed, g5, var5, snp_lst_0=rows, var_app=960.0, p_cut=1e-2,
+                        out_file=os.path.join(out, "epiAD_eff_rows200"))
+    finally:
+        os.chdir(cwd)
+
+
+def tiny(gmat, work, out):
+    from gmat.gmatrix import agmat, dgmat_as
+    from gmat.uvlmm import wemai_multi_gmat
+    from gmat.remma.remma_epiAA import remma_epiAA
+    from gmat.remma.remma_epiDD import remma_epiDD
+    from gmat.remma.remma_epiAD import remma_epiAD
+    os.makedirs(out, exist_ok=True)
+    n, m = 150, 200
+    geno = synth.simulate_genotypes(n, m, seed=3, n_founder=20, n_gen=4, block=40)
+    geno[17] = 0          # monomorphic (all hom first allele)
+    geno[101] = 2         # monomorphic (all hom second allele)
+    geno[150] = 1         # every individual heterozygous: A coding is identically 0
+    prefix = os.path.join(out, "tiny")
+    synth.write_plink(prefix, geno, seed=3)
+    y = synth.simulate_phenotype(geno, seed=4)
+    ids = [("F%d" % (i // 10), "I%d" % i) for i in range(n)]
+    synth.write_pheno(prefix + ".pheno", ids, y)
+    for ext in (".bed", ".bim", ".fam", ".pheno"):
+        shutil.copy(prefix + ext, os.path.join(work, "tiny" + ext))
+    bed = os.path.join(work, "tiny")
+    pheno = bed + ".pheno"
+    a, ainv = agmat(bed, inv=True)
+    d, _ = dgmat_as(bed)
+    agmat(bed, out_fmt="row_col_val")
+    agmat(bed, out_fmt="id_id_val")
+    # text outputs: md5 + first lines only (the full matrices are in tiny_ref.npz)
+    with open(os.path.join(out, "text_outputs.json"), "w") as f:
+        json.dump({ext: {"md5": _md5(bed + ext), "head": open(bed + ext).read().splitlines()[:3]}
+                   for ext in (".agrm0", ".agrm1", ".agrm2", ".agiv0", ".dgrm_as0")}, f, indent=1)
+    cap = _Capture()
+    root = logging.getLogger()
+    root.addHandler(cap)
+    root.setLevel(logging.INFO)
+    var = wemai_multi_gmat(pheno, bed, [a, a * a], out_file=os.path.join(work, "var"))
+    hist = _history(cap.msgs)
+    root.removeHandler(cap)
+    np.savez(os.path.join(out, "tiny_ref.npz"), agmat=a, agmat_inv=ainv, dgmat=d, var=var, hist=hist)
+    remma_epiAA(pheno, bed, [a, a * a], var, p_cut=1.0, out_file=os.path.join(out, "epiAA_all"))
+    remma_epiDD(pheno, bed, [a, a * a], var, p_cut=1.0, out_file=os.path.join(out, "epiDD_all"))
+    remma_epiAD(pheno, bed, [a, a * a], var, p_cut=1.0, out_file=os.path.join(out, "epiAD_all"))
+    for name in ("epiAA_all", "epiDD_all", "epiAD_all"):
+        path = os.path.join(out, name)
+        with open(path, "rb") as fi, gzip.open(path + ".gz", "wb", compresslevel=9) as fo:
+            fo.write(fi.read())
+        os.remove(path)
+
+
+def main():
+    gmat = import_reference()
+    logging.getLogger().setLevel(logging.WARNING)
+    with tempfile.TemporaryDirectory() as work:
+        tiny(gmat, work, os.path.join(HERE, "tiny"))
+    with tempfile.TemporaryDirectory() as work:
+        mouse(gmat, work, os.path.join(HERE, "mouse"))
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+"""Pin the CPU oracle (oracle/gmat_oracle.py) to the golden fixtures the reference produced.
+
+These run without a GPU.  They make the oracle a trustworthy checker for the HIP path.
+"""
+import gzip
+import hashlib
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gmat_oracle as O
+
+MOUSE_DATA = os.path.join(os.path.dirname(__file__), "golden", "mouse")
+TINY = os.path.join(os.path.dirname(__file__), "golden", "tiny")
+
+
+def _load_hits(path):
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "rt") as f:
+        lines = f.read().splitlines()
+    if len(lines) <= 1:
+        return lines[0], np.zeros((0, 5))
+    return lines[0], np.loadtxt(io.StringIO("\n".join(lines[1:])), ndmin=2)
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    snp = O.read_plink(os.path.join(TINY, "tiny"))
+    ref = np.load(os.path.join(TINY, "tiny_ref.npz"))
+    y, x, col, nid = O.design_matrix(os.path.join(TINY, "tiny.pheno"), os.path.join(TINY, "tiny"))
+    return snp, ref, (y, x, col, nid)
+
+
+def test_tiny_grm(tiny):
+    snp, ref, _ = tiny
+    assert snp.shape == (150, 200)
+    np.testing.assert_allclose(O.agmat(snp), ref["agmat"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(O.dgmat_as(snp), ref["dgmat"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(np.linalg.inv(O.agmat(snp)), ref["agmat_inv"], rtol=1e-8, atol=1e-9)
+
+
+def test_tiny_reml(tiny):
+    snp, ref, (y, x, col, nid) = tiny
+    a = O.agmat(snp)
+    hist = []
+    var = O.wemai_multi_gmat(y, x, col, nid, [a, a * a], history=hist)
+    np.testing.assert_allclose(var, ref["var"], rtol=1e-8)
+    np.testing.assert_allclose(np.array(hist), ref["hist"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["AA", "AD", "DD"])
+def test_tiny_all_pairs(tiny, kind):
+    snp, ref, (y, x, col, nid) = tiny
+    a = O.agmat(snp)
+    pvp, py = O.projection(y, x, col, nid, [a, a * a], ref["var"])
+    got = O.epi_scan(kind, snp, pvp, py, p_cut=1.0)
+    hdr, exp = _load_hits(os.path.join(TINY, "epi%s_all.gz" % kind))
+    assert hdr == "snp_0 snp_1 eff chi p_val"
+    # NaN statistics (monomorphic / all-het SNPs) are dropped exactly as the reference does
+    assert got.shape == exp.shape
+    np.testing.assert_array_equal(got[:, :2], exp[:, :2])
+    np.testing.assert_allclose(got[:, 2:], exp[:, 2:], rtol=1e-9, atol=1e-12)
+
+
+def test_mouse_grm_summary():
+    snp = O.read_plink(os.path.join(MOUSE_DATA, "plink")) if os.path.exists(
+        os.path.join(MOUSE_DATA, "plink.bed")) else None
+    if snp is None:
+        pytest.skip("mouse data is only present in the build container")
+    for name, fn in (("agmat", O.agmat), ("dgmat_as", O.dgmat_as)):
+        ref = np.load(os.path.join(MOUSE_DATA, name + ".npz"))
+        k = fn(snp)
+        np.testing.assert_allclose(np.diag(k), ref["diag"], rtol=1e-12)
+        np.testing.assert_allclose(k[0], ref["row0"], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(k[ref["ia"], ref["ib"]], ref["val"], rtol=1e-10, atol=1e-12)
+        assert abs(np.trace(k) - ref["trace"]) < 1e-9
+
+
+def test_known_answer_reml_values():
+    # the reference repo's only known answer: examples/remma/remma_cpu.py:178
+    ref = np.load(os.path.join(MOUSE_DATA, "reml.npz"))
+    np.testing.assert_allclose(ref["var2"], [0.06289206, 0.07641075, 0.08121168], rtol=1e-6)
+
+
+def test_parallel_rows_cover():
+    for kind, total in (("AA", 1406), ("AD", 1407)):
+        for n_part in (1, 2, 3, 5, 8):
+            rows = sum((O.parallel_rows(1407, [n_part, k], kind) for k in range(1, n_part + 1)), [])
+            assert sorted(rows) == list(range(total))
+
+
+def test_parallel_parts_match_golden():
+    # the union of the three reference part files equals the subset of a full scan
+    parts = []
+    for k in (1, 2, 3):
+        _, h = _load_hits(os.path.join(MOUSE_DATA, "epiAA_par3_1e-4.%d" % k))
+        rows = set(O.parallel_rows(1407, [3, k]))
+        assert all(int(i) in rows for i in h[:, 0])
+        parts.append(h)
+    allh = np.concatenate(parts)
+    _, full = _load_hits(os.path.join(MOUSE_DATA, "epiAA_1e-3"))
+    sub = full[full[:, 4] < 1e-4]
+    key = lambda a: sorted(map(tuple, a[:, :2].astype(int)))  # noqa: E731
+    assert key(allh) == key(sub)
+
+
+def test_annotation_golden():
+    bim = open(os.path.join(MOUSE_DATA, "plink.bim")).read().splitlines() if os.path.exists(
+        os.path.join(MOUSE_DATA, "plink.bim")) else None
+    if bim is None:
+        pytest.skip("mouse data is only present in the build container")
+    res = open(os.path.join(MOUSE_DATA, "epiAA_1e-3")).read().splitlines()
+    got = O.annotation_snp_pos(res, bim, p_cut=1e-4, dis=1000000)
+    exp = open(os.path.join(MOUSE_DATA, "epiAA_1e-3.anno")).read().splitlines()
+    assert got == exp
+
+
+def test_text_format_matches_reference():
+    # rows written as the reference does (pandas to_csv of int, int, float64 repr)
+    hdr, h = _load_hits(os.path.join(MOUSE_DATA, "epiAA_1e-5"))
+    lines = open(os.path.join(MOUSE_DATA, "epiAA_1e-5")).read().splitlines()[1:]
+    assert O.format_rows(h, 3) == lines
+
+
+def test_tiny_text_outputs_md5():
+    meta = json.load(open(os.path.join(TINY, "text_outputs.json")))
+    ref = np.load(os.path.join(TINY, "tiny_ref.npz"))
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "k")
+        np.savetxt(p, ref["agmat"])  # np.savetxt default '%.18e', as gmatrix.py:12
+        assert hashlib.md5(open(p, "rb").read()).hexdigest() == meta[".agrm0"]["md5"]
