@@ -1,0 +1,113 @@
+"""ctypes binding of libgmat_hip.so (the C ABI declared in include/gmat_hip.h).
+
+The product path has no CPU fallback: if the library or a GPU is missing, every compute
+entry point raises ``GmatNativeError``.  (cffi is not importable in this image; the C ABI is
+plain ``extern "C"`` with POD arguments, so cffi ABI mode would bind it unchanged -- see
+INTEGRATION.md.)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GMAT_HIP_LIB", os.path.join(_HERE, "libgmat_hip.so"))
+
+GMAT_AA, GMAT_AD, GMAT_DD = 0, 1, 2
+GMAT_GRM_ADD, GMAT_GRM_DOM = 0, 1
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+_INT = ctypes.c_int
+
+_PROTOS = {
+    "gmat_last_error": (ctypes.c_char_p, []),
+    "gmat_version": (_INT, []),
+    "gmat_device_count": (_INT, [_P]),
+    "gmat_set_device": (_INT, [_INT]),
+    "gmat_geno_create": (_INT, [_P, _P, _I64, _I64, _I64]),
+    "gmat_geno_counts": (_INT, [_P, _P, _P, _P]),
+    "gmat_geno_destroy": (_INT, [_P]),
+    "gmat_grm": (_INT, [_P, _INT, _D, _P, _P]),
+    "gmat_spd_inverse": (_INT, [_I64, _P, _P, _P]),
+    "gmat_reml": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _INT, _D, _D, _P, _P, _P]),
+    "gmat_projection": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P]),
+    "gmat_epi_create": (_INT, [_P, _P, _P, _P, _INT]),
+    "gmat_epi_scan": (_INT, [_P, _INT, _P, _I64, _D, _D, _P]),
+    "gmat_epi_hits": (_INT, [_P, _I64, _P, _P, _P, _P, _P, _P]),
+    "gmat_epi_pairs": (_INT, [_P, _INT, _P, _I64, _P, _P, _P, _P]),
+    "gmat_epi_stats": (_INT, [_P, _P]),
+    "gmat_epi_destroy": (_INT, [_P]),
+}
+
+
+class GmatNativeError(RuntimeError):
+    pass
+
+
+_lib = None
+_device_set = False
+
+
+def load(required=True):
+    """Load the library (once).  Raises GmatNativeError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not required:
+            return None
+        raise GmatNativeError("libgmat_hip.so not found at %s -- build it with "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return sorted(_PROTOS)
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _lib.gmat_last_error().decode(errors="replace") if _lib else ""
+        raise GmatNativeError("%s failed (rc=%d): %s" % (what, rc, msg))
+
+
+def device_count():
+    lib = load()
+    n = ctypes.c_int(0)
+    check(lib.gmat_device_count(ctypes.byref(n)), "gmat_device_count")
+    return n.value
+
+
+def ensure_device():
+    """Bind this process to its GPU (LOCAL_RANK / GMAT_DEVICE, default 0); raise when
+    there is none -- the product path never falls back to the CPU."""
+    global _device_set
+    lib = load()
+    if _device_set:
+        return lib
+    if device_count() < 1:
+        raise GmatNativeError("no HIP device visible: the gmat_amd product path needs an MI355X")
+    dev = int(os.environ.get("GMAT_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    check(lib.gmat_set_device(dev % device_count()), "gmat_set_device")
+    _device_set = True
+    return lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)

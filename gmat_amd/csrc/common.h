@@ -1,0 +1,77 @@
+// Shared plumbing for libgmat_hip: error reporting, device buffers, MFMA vector types.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gmat_hip.h"
+
+namespace gmat {
+
+void set_error(const char *fmt, ...);
+
+#define GMAT_HIP(x)                                                                        \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      ::gmat::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return GMAT_E_HIP;                                                                   \
+    }                                                                                      \
+  } while (0)
+
+#define GMAT_CHECK(cond, code, ...)    \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::gmat::set_error(__VA_ARGS__);  \
+      return (code);                   \
+    }                                  \
+  } while (0)
+
+#define GMAT_TRY(x)          \
+  do {                       \
+    int rc_ = (x);           \
+    if (rc_ != GMAT_OK) return rc_; \
+  } while (0)
+
+// Owning device allocation (hipMalloc'd, freed on destruction).
+struct DBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DBuf() = default;
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  int alloc(size_t n) {
+    if (n <= bytes && p) return GMAT_OK;
+    release();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+      p = nullptr;
+      set_error("hipMalloc(%zu bytes): %s", n, hipGetErrorString(e));
+      return GMAT_E_NOMEM;
+    }
+    bytes = n;
+    return GMAT_OK;
+  }
+  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+inline int64_t cdiv(int64_t x, int64_t m) { return (x + m - 1) / m; }
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+}  // namespace gmat

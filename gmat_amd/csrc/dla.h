@@ -1,0 +1,47 @@
+// fp64 dense linear algebra building blocks (device side), used by the REML, the GRM
+// epilogue and the scan's exact (refine) and side-term passes.
+#pragma once
+#include "common.h"
+
+namespace gmat {
+
+// Operand views.  Element (r, c) of a logical matrix; `trans` means the storage holds the
+// transpose (element (r, c) at p[c*ld + r]).
+struct DView {
+  const double *p;
+  int64_t ld;
+  int trans;
+};
+struct I8View {
+  const int8_t *p;
+  int64_t ld;
+  int trans;
+};
+
+// C[M x N] = alpha * op(A)[M x K] * op(B)[K x N] + beta * C  (row-major C, ldc).
+// mask: 0 = every tile, 1 = only 64x64 tiles with tile_row >= tile_col (lower half).
+int dgemm(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DView A, DView B, double beta,
+          double *C, int64_t ldc, int mask = 0);
+// Same with an int8 A (values converted exactly to fp64).
+int dgemm_i8a(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, I8View A, DView B, double beta,
+              double *C, int64_t ldc);
+// Same with an int8 B.
+int dgemm_i8b(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DView A, I8View B, double beta,
+              double *C, int64_t ldc);
+
+// In-place blocked Cholesky of the lower triangle of a (n x n, ld = lda): a = L L'.
+// On return the lower triangle holds L, the upper triangle is unspecified.  The inverses of
+// the diagonal blocks are written to dinv (n x 64 doubles).  *logdet_dev (device double)
+// receives sum(log(diag(L)))*2; *info_dev (device int) > 0 marks a non-positive pivot.
+int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev);
+// ainv = (L L')^-1 from the factor (lower triangle of l) and its diagonal-block inverses;
+// work is n*n doubles of scratch.  ainv is fully populated (symmetric).
+int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv,
+                          double *work, double *ainv);
+
+// Small device helpers.
+int fill_sym_upper(hipStream_t s, int64_t n, double *a, int64_t lda);           // upper := lower'
+int dot_rows(hipStream_t s, int64_t rows, int64_t n, const double *a, int64_t lda, const double *b,
+             int64_t ldb, double *out);  // out[r] = sum_k a[r,k] * b[r,k]  (b==NULL -> vector of ones)
+
+}  // namespace gmat

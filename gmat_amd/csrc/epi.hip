@@ -1,0 +1,888 @@
+// Exhaustive epistasis scans (remma_epiAA.py:71-82, remma_epiAD.py:76-87,
+// remma_epiDD.py:75-86) and the pair-list test (remma_epiAA_pair.py:79-84).
+//
+// For a pair (i, j) with centred codes x_i = a_i - alpha_i, x_j = b_j - beta_j (a, b the
+// integer 0/1/2 dosage or 0/1 heterozygote codes), the reference computes
+//     e = x_i o x_j,  eff = e'Py,  var = e'Pe  (2n^2 fp64 flop per pair),
+// chi = eff^2/var, p = chi2.sf(chi, 1), and keeps p < p_cut.
+//
+// Here the scan runs in two passes:
+//  1. SCREEN.  With w = a_i o b_j (integers 0..4) the quadratic form expands into
+//       e'Pe = w'Pw - 2 beta L'_i.b_j - 2 alpha a_i.R'_j + (per-SNP and constant terms),
+//     L'_i = a_i o (P a_i - alpha_i P1),  R'_j = x_j o (P b_j).
+//     The O(n^2)-per-pair term w'Pw is evaluated EXACTLY for a sliced P:
+//       P ~ (pmax/127) sum_s 128^-s A_s,  A_s int8,
+//     as integer quadratic forms on v_mfma_i32_32x32x32_i8 (int32 accumulation, int64
+//     combination -- bit-deterministic), using the symmetry of A_s to visit only the
+//     block-upper half.  The O(n)-per-pair side terms are fp64 MFMA GEMMs.  The slicing
+//     error is bounded rigorously by delta * (sum w)^2, so every pair that COULD have
+//     p < p_cut becomes a candidate.
+//  2. REFINE.  Candidates are re-evaluated exactly as the reference does (fp64 e = x_i*x_j,
+//     var = e'Pe on f64 MFMA, p = erfc(sqrt(chi/2))) and the hits are kept.
+// The reported statistics therefore come from the same fp64 formula as the reference;
+// the screen only decides which pairs need it.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <numeric>
+
+#include "dla.h"
+#include "geno.h"
+
+using namespace gmat;
+
+namespace {
+
+constexpr int MT = 128;  // rows of P per K-block
+constexpr int LK = 64;   // inner (individual) depth per LDS stage
+constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
+constexpr int BI = 8;    // first-SNP rows per screen tile
+constexpr int BJ = 32;   // second-SNP columns per screen tile
+constexpr int ROWS_PER_LAUNCH = 128;
+
+// w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
+// j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
+// blocks of the symmetric quadratic form count twice: table 2T.
+constexpr unsigned T_LO = 0x01000000u, T_HI = 0x04020002u;
+constexpr unsigned T2_LO = 0x02000000u, T2_HI = 0x08040004u;
+
+__device__ __forceinline__ unsigned to_offset(unsigned v) { return (v << 1) + ((v >> 1) & 0x7f7f7f7fu); }
+
+struct ScreenArgs {
+  const int8_t *slices;
+  int64_t n_pad;
+  int n_slice;
+  const int8_t *left, *right;  // panels [m][n_pad]
+  int64_t m;
+  const int64_t *rows;
+  int n_rows;
+  const int *tiles;  // (row offset, J) pairs
+  int tri;           // 1: only j > i
+  const double *e13, *e2;
+  int64_t ld_e, j_lo;
+  const double *alpha, *qa, *ra, *sa;
+  const double *beta, *qb, *rb, *sb;
+  const uint8_t *mono_l, *mono_r;
+  double zz, spy, scale_main, delta, chi_cut;
+  unsigned long long *counter;
+  int64_t cap;
+  int64_t *cand_i, *cand_j;
+};
+
+__global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t sA[2][MT * AP];
+  __shared__ __attribute__((aligned(16))) int8_t sI[2][BI * AP];
+  __shared__ __attribute__((aligned(16))) int8_t sJ[2][BJ * AP];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  const int64_t J0 = (int64_t)J * BJ;
+  const int64_t n_pad = a.n_pad;
+
+  int64_t ti[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int r = roff + 2 * w + t;
+    ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
+  }
+  // staging roles
+  const int ch0 = tid, ch1 = tid + 256;  // A chunks
+  const int arow0 = ch0 >> 2, acol0 = (ch0 & 3) * 16, arow1 = ch1 >> 2, acol1 = (ch1 & 3) * 16;
+  int prow = -1, pcol = 0, pside = 0;  // panel chunk: side 1 = i-panel, 2 = j-panel
+  const int8_t *psrc = nullptr;
+  if (tid < 32) {
+    pside = 1;
+    prow = tid >> 2;
+    pcol = (tid & 3) * 16;
+    const int r = roff + prow;
+    if (r < a.n_rows) psrc = a.left + a.rows[r] * n_pad + pcol;
+  } else if (tid < 160) {
+    pside = 2;
+    prow = (tid - 32) >> 2;
+    pcol = ((tid - 32) & 3) * 16;
+    if (J0 + prow < a.m) psrc = a.right + (J0 + prow) * n_pad + pcol;
+  }
+
+  int64_t tot[2] = {0, 0};
+  unsigned sw[2] = {0, 0};
+
+  for (int s = 0; s < a.n_slice; ++s) {
+    const int8_t *As = a.slices + (int64_t)s * n_pad * n_pad;
+    const int shift = 7 * (a.n_slice - 1 - s);
+    for (int64_t K = 0; K < n_pad; K += MT) {
+      v16i acc[4][2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[r][t][e] = 0;
+      const int nst = (int)((n_pad - K) / LK);
+      v4i ra0, ra1, rp = {0, 0, 0, 0};
+      auto load = [&](int64_t L) {
+        ra0 = *(const v4i *)&As[(K + arow0) * n_pad + L + acol0];
+        ra1 = *(const v4i *)&As[(K + arow1) * n_pad + L + acol1];
+        if (psrc) rp = *(const v4i *)&psrc[L];
+      };
+      auto store = [&](int b) {
+        *(v4i *)&sA[b][arow0 * AP + acol0] = ra0;
+        *(v4i *)&sA[b][arow1 * AP + acol1] = ra1;
+        if (pside == 1) {
+          v4i o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
+          *(v4i *)&sI[b][prow * AP + pcol] = o;
+        } else if (pside == 2) {
+          *(v4i *)&sJ[b][prow * AP + pcol] = rp;
+        }
+      };
+      load(K);
+      store(0);
+      __syncthreads();
+      for (int st = 0; st < nst; ++st) {
+        const int cur = st & 1;
+        const int64_t L = K + (int64_t)st * LK;
+        if (st + 1 < nst) load(L + LK);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bool diag = (L + kk * 32) < (K + MT);
+          const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
+          v4i fb[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const v4i o = *(const v4i *)&sI[cur][(2 * w + t) * AP + kk * 32 + 16 * h];
+            const v4i v = *(const v4i *)&sJ[cur][c * AP + kk * 32 + 16 * h];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const v4i fa = *(const v4i *)&sA[cur][(r * 32 + c) * AP + kk * 32 + 16 * h];
+            acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], acc[r][0], 0, 0, 0);
+            acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], acc[r][1], 0, 0, 0);
+          }
+        }
+        if (st + 1 < nst) store(cur ^ 1);
+        __syncthreads();
+      }
+      // epilogue: sum_rows w[row] * acc[row]  (acc register e of this lane <-> storage slot 16h+e)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (ti[t] < 0) continue;
+        const int64_t j = J0 + c;
+        const int8_t *ol = a.left + ti[t] * n_pad + K + 16 * h;
+        const int8_t *vr = (j < a.m) ? a.right + j * n_pad + K + 16 * h : nullptr;
+        int64_t part64 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const v4i o = *(const v4i *)&ol[r * 32];
+          const v4i v = vr ? *(const v4i *)&vr[r * 32] : v4i{0, 0, 0, 0};
+          int part = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const unsigned wb = __builtin_amdgcn_perm(T_HI, T_LO, to_offset((unsigned)o[q]) + (unsigned)v[q]);
+            part += (int)(wb & 0xff) * acc[r][t][4 * q] + (int)((wb >> 8) & 0xff) * acc[r][t][4 * q + 1] +
+                    (int)((wb >> 16) & 0xff) * acc[r][t][4 * q + 2] + (int)(wb >> 24) * acc[r][t][4 * q + 3];
+            if (s == 0) sw[t] = __builtin_amdgcn_udot4(wb, 0x01010101u, sw[t], false);
+          }
+          part64 += part;
+        }
+        tot[t] += part64 * (int64_t)(1LL << shift);
+      }
+    }
+  }
+  // combine the two lane halves (disjoint rows of the same column), then test
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int64_t other = __shfl_xor(tot[t], 32);
+    const unsigned osw = __shfl_xor(sw[t], 32);
+    if (h != 0 || ti[t] < 0) continue;
+    const int64_t i = ti[t], j = J0 + c;
+    if (j >= a.m || (a.tri && j <= i)) continue;
+    if (a.mono_l[i] || a.mono_r[j]) continue;  // x == 0: the reference's statistic is NaN
+    const int ri = roff + 2 * w + t;
+    const double M = (double)(tot[t] + other) * a.scale_main;
+    const double sumw = (double)(sw[t] + osw);
+    const double E1 = a.e13[(int64_t)ri * a.ld_e + (j - a.j_lo)];
+    const double E3 = a.e13[(int64_t)(a.n_rows + ri) * a.ld_e + (j - a.j_lo)];
+    const double E2 = a.e2[(int64_t)ri * a.ld_e + (j - a.j_lo)];
+    const double al = a.alpha[i], be = a.beta[j];
+    const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
+                 t5 = al * al * a.qb[j], t6 = -2.0 * al * al * be * a.rb[j], t7 = al * al * be * be * a.zz;
+    const double var = M + t1 + t2 + t3 + t4 + t5 + t6 + t7;
+    const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
+    const double slack = 1e-12 * (fabs(M) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
+    const double var_lo = var - a.delta * sumw * sumw - slack;
+    const bool cand = !(var_lo > 0.0) || eff * eff * (1.0 + 1e-9) >= a.chi_cut * var_lo;
+    if (cand) {
+      const unsigned long long k = atomicAdd(a.counter, 1ULL);
+      if ((int64_t)k < a.cap) {
+        a.cand_i[k] = i;
+        a.cand_j[k] = j;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ exact fp64 refine
+// For pairs (pi[t], pj[t]): e = (a - alpha)(b - beta) in fp64 (storage order), var = e'Pe,
+// eff = e'Py.  64 pairs per workgroup; for every 64-row block of P the f64 MFMA tile
+// C = P[rows, :] E is formed over the full inner dimension and folded into var.
+constexpr int QT = 64, QK = 16;
+
+__device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double al, double be, int64_t q) {
+  const double x = (double)l[q] - al;
+  const double y = (double)r[q] - be;
+  return x * y;
+}
+
+__global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
+                                                     const double *__restrict__ py, const int8_t *left,
+                                                     const int8_t *right, const double *alpha, const double *beta,
+                                                     const int64_t *pi, const int64_t *pj, int64_t np, double *eff,
+                                                     double *var) {
+  __shared__ double As[QK][QT + 1];
+  __shared__ double Bs[QK][QT + 1];
+  __shared__ double red[4][QT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t p0 = (int64_t)blockIdx.x * QT;
+  // the column this thread generates E for during staging: col = tid & 63
+  const int gcol = tid & 63;
+  const int64_t gp = p0 + gcol;
+  const bool gval = gp < np;
+  const int8_t *gl = gval ? left + pi[gp] * n_pad : left;
+  const int8_t *gr = gval ? right + pj[gp] * n_pad : right;
+  const double gal = gval ? alpha[pi[gp]] : 0.0, gbe = gval ? beta[pj[gp]] : 0.0;
+  double vpart[2][2] = {{0, 0}, {0, 0}};  // per (j-subtile, lane) partial of var
+  double effp = 0.0;
+  for (int64_t rb = 0; rb < n_pad; rb += QT) {
+    v4d acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
+    for (int64_t k0 = 0; k0 < n_pad; k0 += QK) {
+      // A: P[rb + r][k0 + k], contiguous along k
+      {
+        const int k = tid & 15, r = tid >> 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) As[k][r + 16 * q] = P[(rb + r + 16 * q) * n_pad + k0 + k];
+      }
+      // B: E[k0 + k][col]
+      {
+        const int kq = tid >> 6;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = kq + 4 * q;
+          const double e = gval ? ecode(gl, gr, gal, gbe, k0 + k) : 0.0;
+          Bs[k][gcol] = e;
+          if (rb == 0) effp += e * py[k0 + k];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < QK / 4; ++ks) {
+        const int kk = ks * 4 + (lane >> 4);
+        const double a0 = As[kk][wm * 32 + (lane & 15)], a1 = As[kk][wm * 32 + 16 + (lane & 15)];
+        const double b0 = Bs[kk][wn * 32 + (lane & 15)], b1 = Bs[kk][wn * 32 + 16 + (lane & 15)];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    // fold: var[col] += sum_rows E[row][col] * C[row][col]
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const int col = wn * 32 + jt * 16 + (lane & 15);
+      const int64_t p = p0 + col;
+      if (p >= np) continue;
+      const int8_t *l = left + pi[p] * n_pad, *r = right + pj[p] * n_pad;
+      const double al = alpha[pi[p]], be = beta[pj[p]];
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t row = rb + wm * 32 + it * 16 + (lane >> 4) + 4 * e;
+          vpart[jt][0] += ecode(l, r, al, be, row) * acc[it][jt][e];
+        }
+    }
+  }
+  // reduce var partials: lanes with equal (lane & 15) in a wave, then the two wm waves
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    double v = vpart[jt][0];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 16) red[wm * 2 + jt][wn * 16 + lane] = v;  // [wm][jt] x [wn*16 + lane]
+  }
+  // eff partials: 4 threads per column (tid>>6), reduce via LDS after var
+  __syncthreads();
+  __shared__ double effr[4][QT];
+  effr[tid >> 6][gcol] = effp;
+  __syncthreads();
+  if (tid < QT) {
+    const int col = tid;
+    const int64_t p = p0 + col;
+    if (p < np) {
+      const int wn_ = col >> 5, jt = (col >> 4) & 1, ln = col & 15;
+      const double v = red[0 * 2 + jt][wn_ * 16 + ln] + red[1 * 2 + jt][wn_ * 16 + ln];
+      var[p] = v;
+      eff[p] = ((effr[0][col] + effr[1][col]) + effr[2][col]) + effr[3][col];
+    }
+  }
+}
+
+// p-values and hit compaction: chi = eff^2/var, p = chi2.sf(chi, 1) = erfc(sqrt(chi/2))
+__global__ void pvalue_kernel(int64_t np, const double *eff, const double *var, double *chi, double *p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  const double c = eff[t] * eff[t] / var[t];
+  chi[t] = c;
+  p[t] = (c < 0.0) ? 1.0 : erfc(sqrt(0.5 * c));
+}
+
+// ------------------------------------------------------------------ setup kernels
+
+// P_store[q][q'] = P[nat(q)][nat(q')], zero padded; z = P_store 1 computed later.
+__global__ void permute_p_kernel(int64_t n, int64_t n_pad, const double *P, double *Ps) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * n_pad) return;
+  const int64_t q = idx / n_pad, q2 = idx % n_pad;
+  const int64_t r = (q & ~31LL) + perm_nat((int)(q & 31)), c = (q2 & ~31LL) + perm_nat((int)(q2 & 31));
+  Ps[idx] = (r < n && c < n) ? P[r * n + c] : 0.0;
+}
+__global__ void permute_vec_kernel(int64_t n, int64_t n_pad, const double *v, double *vs) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_pad) return;
+  const int64_t r = (q & ~31LL) + perm_nat((int)(q & 31));
+  vs[q] = (r < n) ? v[r] : 0.0;
+}
+// slices A_s[rho][t] (rho natural row, t storage column) of P*127/pmax
+__global__ void slice_kernel(int64_t n, int64_t n_pad, const double *P, double inv_unit, int n_slice,
+                             int8_t *slices) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * n_pad) return;
+  const int64_t rho = idx / n_pad, t = idx % n_pad;
+  const int64_t c = (t & ~31LL) + perm_nat((int)(t & 31));
+  double r = (rho < n && c < n) ? P[rho * n + c] * inv_unit : 0.0;
+  for (int s = 0; s < n_slice; ++s) {
+    const double q = rint(r);
+    slices[(int64_t)s * n_pad * n_pad + idx] = (int8_t)q;
+    r = (r - q) * 128.0;
+  }
+}
+
+// per-SNP side vectors for the left coding: L' = a o (u - alpha z), L3 = a o py, and
+// scalars qa = a.u, ra = a.z, sa = a.py.  One workgroup per SNP.
+__global__ __launch_bounds__(256) void left_side_kernel(int64_t n_pad, const int8_t *panel, const double *U,
+                                                        const double *z, const double *py, const double *alpha,
+                                                        double *Lp, double *L3, double *qa, double *ra,
+                                                        double *sa) {
+  const int64_t j = blockIdx.x;
+  const double al = alpha[j];
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int64_t q = threadIdx.x; q < n_pad; q += 256) {
+    const double av = (double)panel[j * n_pad + q];
+    const double u = U[j * n_pad + q];
+    Lp[j * n_pad + q] = av * (u - al * z[q]);
+    L3[j * n_pad + q] = av * py[q];
+    s1 += av * u;
+    s2 += av * z[q];
+    s3 += av * py[q];
+  }
+  __shared__ double red[3][4];
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+    s3 += __shfl_xor(s3, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s1;
+    red[1][threadIdx.x >> 6] = s2;
+    red[2][threadIdx.x >> 6] = s3;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    qa[j] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    ra[j] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    sa[j] = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+  }
+}
+// right coding: R' = (b - beta) o v, qb = b.v, rb = b.z, sb = b.py
+__global__ __launch_bounds__(256) void right_side_kernel(int64_t n_pad, const int8_t *panel, const double *V,
+                                                         const double *z, const double *py, const double *beta,
+                                                         double *Rp, double *qb, double *rb, double *sb) {
+  const int64_t j = blockIdx.x;
+  const double be = beta[j];
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int64_t q = threadIdx.x; q < n_pad; q += 256) {
+    const double bv = (double)panel[j * n_pad + q];
+    const double v = V[j * n_pad + q];
+    Rp[j * n_pad + q] = (bv - be) * v;
+    s1 += bv * v;
+    s2 += bv * z[q];
+    s3 += bv * py[q];
+  }
+  __shared__ double red[3][4];
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+    s3 += __shfl_xor(s3, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s1;
+    red[1][threadIdx.x >> 6] = s2;
+    red[2][threadIdx.x >> 6] = s3;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    qb[j] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    rb[j] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    sb[j] = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+  }
+}
+
+// gather band rows: BL[t] = Lp[rows[t]], BL[R+t] = L3[rows[t]], BA[t] = panel[rows[t]]
+__global__ void gather_band_kernel(int64_t n_pad, int R, const int64_t *rows, const double *Lp, const double *L3,
+                                   const int8_t *panel, double *BL, int8_t *BA) {
+  const int t = blockIdx.x;
+  const int64_t src = rows[t];
+  for (int64_t q = threadIdx.x; q < n_pad; q += blockDim.x) {
+    BL[(int64_t)t * n_pad + q] = Lp[src * n_pad + q];
+    BL[(int64_t)(R + t) * n_pad + q] = L3[src * n_pad + q];
+    BA[(int64_t)t * n_pad + q] = panel[src * n_pad + q];
+  }
+}
+
+__global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= n_pad) return;
+  double s = 0.0;
+  for (int64_t k = lane; k < n_pad; k += 64) s += Ps[q * n_pad + k];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) z[q] = s;
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ plan object
+
+struct Coding {
+  bool ready = false;
+  DBuf U;                      // P * code panel  [m][n_pad]
+  DBuf off;                    // alpha/beta (centring offsets) [m]
+  DBuf Lp, L3, Rp;             // side vectors [m][n_pad]
+  DBuf qa, ra, sa, qb, rb, sb;  // per-SNP scalars
+  DBuf mono;                   // uint8 [m]
+};
+
+struct gmat_epi {
+  gmat_geno *g = nullptr;
+  int64_t n = 0, n_pad = 0, m = 0;
+  int n_slice = 3;
+  double pmax = 0, zz = 0, spy = 0;
+  DBuf Ps, py, z, slices;
+  Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
+  // scan state
+  DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
+  int64_t cand_cap = 0;
+  std::vector<int64_t> hit_i, hit_j;
+  std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
+  double stats[8] = {0};
+  hipStream_t s = 0;
+};
+
+namespace {
+
+int build_coding(gmat_epi *e, int which) {
+  Coding &cd = e->code[which];
+  if (cd.ready) return GMAT_OK;
+  const int64_t m = e->m, n_pad = e->n_pad, n = e->n;
+  const int8_t *panel = which == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  // centring offsets exactly as the reference: freq = sum/(2n); A: 2*freq, D: 2*freq*(1-freq)
+  std::vector<double> off(m);
+  std::vector<uint8_t> mono(m);
+  for (int64_t j = 0; j < m; ++j) {
+    const double freq = (double)e->g->sum_dose[j] / (2.0 * (double)n);
+    off[j] = which == 0 ? 2.0 * freq : 2.0 * freq * (1.0 - freq);
+    const int64_t sd = e->g->sum_dose[j];
+    mono[j] = which == 0 ? (sd == 0 || sd == 2 * n || e->g->n_het[j] == n) : (sd == 0 || sd == 2 * n);
+  }
+  const size_t vb = (size_t)m * n_pad * sizeof(double);
+  GMAT_TRY(cd.U.alloc(vb));
+  GMAT_TRY(cd.Lp.alloc(vb));
+  GMAT_TRY(cd.L3.alloc(vb));
+  GMAT_TRY(cd.Rp.alloc(vb));
+  for (DBuf *b : {&cd.off, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb}) GMAT_TRY(b->alloc(m * sizeof(double)));
+  GMAT_TRY(cd.mono.alloc(m));
+  GMAT_HIP(hipMemcpy(cd.off.p, off.data(), m * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(cd.mono.p, mono.data(), m, hipMemcpyHostToDevice));
+  // U[j][q] = sum_q' panel[j][q'] P[q'][q]
+  GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
+                     cd.U.as<double>(), n_pad));
+  hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), cd.Lp.as<double>(),
+                     cd.L3.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
+  GMAT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(right_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), cd.Rp.as<double>(),
+                     cd.qb.as<double>(), cd.rb.as<double>(), cd.sb.as<double>());
+  GMAT_HIP(hipGetLastError());
+  cd.U.release();
+  cd.ready = true;
+  return GMAT_OK;
+}
+
+// exact statistics for device pair lists (pi, pj) of length np -> device eff/var/chi/p
+int refine(gmat_epi *e, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp, const int64_t *pi,
+           const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
+  if (np <= 0) return GMAT_OK;
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, QT)), dim3(256), 0, e->s, e->n_pad, e->Ps.as<double>(),
+                     e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var);
+  GMAT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, e->s, np, eff, var, chi, p);
+  GMAT_HIP(hipGetLastError());
+  return GMAT_OK;
+}
+
+void kind_codings(int kind, int *lc, int *rc) {
+  *lc = (kind == GMAT_DD) ? 1 : 0;
+  *rc = (kind == GMAT_AA) ? 0 : 1;
+}
+
+}  // namespace
+
+extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
+  GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
+  GMAT_CHECK(n_slice >= 2 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 2..4");
+  GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
+  auto *e = new gmat_epi();
+  e->g = g;
+  e->n = g->n;
+  e->n_pad = g->n_pad;
+  e->m = g->m;
+  e->n_slice = n_slice;
+  const int64_t n = e->n, n_pad = e->n_pad;
+  double pmax = 0.0;
+  for (int64_t i = 0; i < n * n; ++i) pmax = std::max(pmax, std::fabs(pvp[i]));
+  e->pmax = pmax;
+  double spy = 0.0;
+  for (int64_t i = 0; i < n; ++i) spy += py[i];
+  e->spy = spy;
+  DBuf dp, dv;
+  int rc = GMAT_OK;
+  auto fail = [&](int code) {
+    delete e;
+    return code;
+  };
+  if ((rc = dp.alloc(n * n * sizeof(double))) || (rc = dv.alloc(n * sizeof(double))) ||
+      (rc = e->Ps.alloc(n_pad * n_pad * sizeof(double))) || (rc = e->py.alloc(n_pad * sizeof(double))) ||
+      (rc = e->z.alloc(n_pad * sizeof(double))) || (rc = e->slices.alloc((size_t)n_slice * n_pad * n_pad)))
+    return fail(rc);
+  if (hipMemcpy(dp.p, pvp, n * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dv.p, py, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    set_error("gmat_epi_create: upload failed");
+    return fail(GMAT_E_HIP);
+  }
+  const unsigned gb = (unsigned)cdiv(n_pad * n_pad, 256);
+  hipLaunchKernelGGL(permute_p_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), e->Ps.as<double>());
+  hipLaunchKernelGGL(permute_vec_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n, n_pad, dv.as<double>(),
+                     e->py.as<double>());
+  const double unit = pmax > 0 ? 127.0 / pmax : 1.0;
+  hipLaunchKernelGGL(slice_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, n_slice,
+                     e->slices.as<int8_t>());
+  hipLaunchKernelGGL(zsum_kernel, dim3((unsigned)cdiv(n_pad, 4)), dim3(256), 0, 0, n_pad, e->Ps.as<double>(),
+                     e->z.as<double>());
+  if (hipGetLastError() != hipSuccess) {
+    set_error("gmat_epi_create: setup kernels failed");
+    return fail(GMAT_E_HIP);
+  }
+  std::vector<double> hz(n_pad);
+  if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("gmat_epi_create: z download failed");
+    return fail(GMAT_E_HIP);
+  }
+  double zz = 0.0;
+  for (double v : hz) zz += v;
+  e->zz = zz;
+  *out = e;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_destroy(gmat_epi *e) {
+  delete e;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *eff, double *var,
+                              double *chi, double *p) {
+  GMAT_CHECK(e && (n_pairs == 0 || (pairs && eff && var && chi && p)), GMAT_E_ARG, "gmat_epi_pairs: bad arguments");
+  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_pairs: bad kind");
+  if (n_pairs == 0) return GMAT_OK;
+  int lc, rc;
+  kind_codings(kind, &lc, &rc);
+  GMAT_TRY(build_coding(e, lc));
+  GMAT_TRY(build_coding(e, rc));
+  std::vector<int64_t> hi(n_pairs), hj(n_pairs);
+  for (int64_t t = 0; t < n_pairs; ++t) {
+    hi[t] = pairs[2 * t];
+    hj[t] = pairs[2 * t + 1];
+    GMAT_CHECK(hi[t] >= 0 && hi[t] < e->m && hj[t] >= 0 && hj[t] < e->m, GMAT_E_ARG, "pair %lld out of range",
+               (long long)t);
+  }
+  const int8_t *lp = lc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int8_t *rp = rc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int64_t chunk = 1 << 16;
+  DBuf di, dj, de, dv, dc, dpv;
+  GMAT_TRY(di.alloc(chunk * 8));
+  GMAT_TRY(dj.alloc(chunk * 8));
+  GMAT_TRY(de.alloc(chunk * 8));
+  GMAT_TRY(dv.alloc(chunk * 8));
+  GMAT_TRY(dc.alloc(chunk * 8));
+  GMAT_TRY(dpv.alloc(chunk * 8));
+  for (int64_t t0 = 0; t0 < n_pairs; t0 += chunk) {
+    const int64_t np = std::min(chunk, n_pairs - t0);
+    GMAT_HIP(hipMemcpy(di.p, hi.data() + t0, np * 8, hipMemcpyHostToDevice));
+    GMAT_HIP(hipMemcpy(dj.p, hj.data() + t0, np * 8, hipMemcpyHostToDevice));
+    GMAT_TRY(refine(e, e->code[lc], e->code[rc], lp, rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(),
+                    dv.as<double>(), dc.as<double>(), dpv.as<double>()));
+    GMAT_HIP(hipMemcpy(eff + t0, de.p, np * 8, hipMemcpyDeviceToHost));
+    GMAT_HIP(hipMemcpy(var + t0, dv.p, np * 8, hipMemcpyDeviceToHost));
+    GMAT_HIP(hipMemcpy(chi + t0, dc.p, np * 8, hipMemcpyDeviceToHost));
+    GMAT_HIP(hipMemcpy(p + t0, dpv.p, np * 8, hipMemcpyDeviceToHost));
+  }
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+                             int64_t *n_hits) {
+  GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
+  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
+  const int64_t m = e->m, n_pad = e->n_pad;
+  for (int64_t t = 0; t < n_rows; ++t) {
+    GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
+    GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
+  }
+  const double t_start = now();
+  int lc, rc;
+  kind_codings(kind, &lc, &rc);
+  GMAT_TRY(build_coding(e, lc));
+  GMAT_TRY(build_coding(e, rc));
+  const Coding &L = e->code[lc], &R = e->code[rc];
+  const int8_t *lp = lc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int8_t *rp = rc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int tri = (kind != GMAT_AD);
+  for (double &v : e->stats) v = 0.0;
+  e->hit_i.clear();
+  e->hit_j.clear();
+  e->hit_eff.clear();
+  e->hit_var.clear();
+  e->hit_chi.clear();
+  e->hit_p.clear();
+
+  // launches: chunks of 64 rows, folded (chunk k with chunk NC-1-k) for equal work per launch
+  const int64_t half = ROWS_PER_LAUNCH / 2;
+  const int64_t nc = cdiv(n_rows, half);
+  std::vector<std::vector<int64_t>> launches;
+  for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
+    std::vector<int64_t> rws;
+    for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) rws.push_back(rows[t]);
+    if (l != k)
+      for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) rws.push_back(rows[t]);
+    launches.push_back(rws);
+  }
+  const double scale_main = e->pmax / 127.0 * std::pow(128.0, -(e->n_slice - 1));
+  const double delta = 0.5 * std::pow(128.0, -(e->n_slice - 1)) * e->pmax / 127.0;
+
+  DBuf drows, dtiles, bl, ba, e13, e2;
+  GMAT_TRY(drows.alloc(ROWS_PER_LAUNCH * 8));
+  GMAT_TRY(bl.alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad * sizeof(double)));
+  GMAT_TRY(ba.alloc((size_t)ROWS_PER_LAUNCH * n_pad));
+  GMAT_TRY(e13.alloc((size_t)2 * ROWS_PER_LAUNCH * m * sizeof(double)));
+  GMAT_TRY(e2.alloc((size_t)ROWS_PER_LAUNCH * m * sizeof(double)));
+  if (e->cand_cap == 0) {
+    e->cand_cap = 1 << 22;
+    GMAT_TRY(e->cand_i.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cand_j.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->ceff.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cvar.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cchi.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cp.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->counter.alloc(8));
+  }
+  hipEvent_t ev[6];
+  for (auto &x : ev) GMAT_HIP(hipEventCreate(&x));
+  double t_screen = 0, t_side = 0, t_ref = 0, pairs_tested = 0, ncand_total = 0, ops = 0;
+  int64_t launches_done = 0;
+  std::vector<int> tiles;
+  for (auto &rws : launches) {
+    const int Rn = (int)rws.size();
+    if (Rn == 0) continue;
+    // pairs tested and tile list
+    tiles.clear();
+    const int64_t j_lo = tri ? rws[0] + 1 : 0;
+    if (tri && j_lo >= m) continue;
+    for (int r0 = 0; r0 < Rn; r0 += BI) {
+      const int64_t imin = rws[r0];
+      const int64_t jb0 = tri ? (imin + 1) / BJ : 0;
+      for (int64_t J = jb0; J * BJ < m; ++J) {
+        tiles.push_back(r0);
+        tiles.push_back((int)J);
+      }
+    }
+    for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
+    const int64_t ntiles = (int64_t)tiles.size() / 2;
+    GMAT_TRY(dtiles.alloc(tiles.size() * sizeof(int)));
+    GMAT_HIP(hipMemcpyAsync(drows.p, rws.data(), Rn * 8, hipMemcpyHostToDevice, e->s));
+    GMAT_HIP(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(int), hipMemcpyHostToDevice, e->s));
+    GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+    const int64_t ncol = m - j_lo;
+    GMAT_HIP(hipEventRecord(ev[0], e->s));
+    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, e->s, n_pad, Rn, drows.as<int64_t>(),
+                       L.Lp.as<double>(), L.L3.as<double>(), lp, bl.as<double>(), ba.as<int8_t>());
+    GMAT_HIP(hipGetLastError());
+    // E1/E3 = [L'; L3]_band . b_j ;  E2 = a_band . R'_j
+    GMAT_TRY(dgemm_i8b(e->s, 2 * Rn, ncol, n_pad, 1.0, DView{bl.as<double>(), n_pad, 0},
+                       I8View{rp + j_lo * n_pad, n_pad, 1}, 0.0, e13.as<double>(), m));
+    GMAT_TRY(dgemm_i8a(e->s, Rn, ncol, n_pad, 1.0, I8View{ba.as<int8_t>(), n_pad, 0},
+                       DView{R.Rp.as<double>() + j_lo * n_pad, n_pad, 1}, 0.0, e2.as<double>(), m));
+    GMAT_HIP(hipEventRecord(ev[1], e->s));
+    ScreenArgs sa;
+    sa.slices = e->slices.as<int8_t>();
+    sa.n_pad = n_pad;
+    sa.n_slice = e->n_slice;
+    sa.left = lp;
+    sa.right = rp;
+    sa.m = m;
+    sa.rows = drows.as<int64_t>();
+    sa.n_rows = Rn;
+    sa.tiles = dtiles.as<int>();
+    sa.tri = tri;
+    sa.e13 = e13.as<double>();
+    sa.e2 = e2.as<double>();
+    sa.ld_e = m;
+    sa.j_lo = j_lo;
+    sa.alpha = L.off.as<double>();
+    sa.qa = L.qa.as<double>();
+    sa.ra = L.ra.as<double>();
+    sa.sa = L.sa.as<double>();
+    sa.beta = R.off.as<double>();
+    sa.qb = R.qb.as<double>();
+    sa.rb = R.rb.as<double>();
+    sa.sb = R.sb.as<double>();
+    sa.mono_l = L.mono.as<uint8_t>();
+    sa.mono_r = R.mono.as<uint8_t>();
+    sa.zz = e->zz;
+    sa.spy = e->spy;
+    sa.scale_main = scale_main;
+    sa.delta = delta;
+    sa.chi_cut = chi_cut;
+    sa.counter = e->counter.as<unsigned long long>();
+    sa.cap = e->cand_cap;
+    sa.cand_i = e->cand_i.as<int64_t>();
+    sa.cand_j = e->cand_j.as<int64_t>();
+    hipLaunchKernelGGL(screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa);
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipEventRecord(ev[2], e->s));
+    unsigned long long ncand = 0;
+    GMAT_HIP(hipMemcpyAsync(&ncand, e->counter.p, 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipStreamSynchronize(e->s));
+    GMAT_CHECK((int64_t)ncand <= e->cand_cap, GMAT_E_OVERFLOW,
+               "scan produced %llu candidates in one launch (capacity %lld): p_cut too large for a scan; "
+               "use the pair test", ncand, (long long)e->cand_cap);
+    GMAT_HIP(hipEventRecord(ev[3], e->s));
+    GMAT_TRY(refine(e, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), (int64_t)ncand,
+                    e->ceff.as<double>(), e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>()));
+    GMAT_HIP(hipEventRecord(ev[4], e->s));
+    if (ncand) {
+      std::vector<int64_t> ci(ncand), cj(ncand);
+      std::vector<double> ce(ncand), cv(ncand), cc(ncand), cp(ncand);
+      GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+      GMAT_HIP(hipStreamSynchronize(e->s));
+      for (unsigned long long k = 0; k < ncand; ++k) {
+        if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
+          e->hit_i.push_back(ci[k]);
+          e->hit_j.push_back(cj[k]);
+          e->hit_eff.push_back(ce[k]);
+          e->hit_var.push_back(cv[k]);
+          e->hit_chi.push_back(cc[k]);
+          e->hit_p.push_back(cp[k]);
+        }
+      }
+    } else {
+      GMAT_HIP(hipStreamSynchronize(e->s));
+    }
+    float ms01, ms12, ms34;
+    GMAT_HIP(hipEventElapsedTime(&ms01, ev[0], ev[1]));
+    GMAT_HIP(hipEventElapsedTime(&ms12, ev[1], ev[2]));
+    GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
+    t_side += ms01 * 1e-3;
+    t_screen += ms12 * 1e-3;
+    t_ref += ms34 * 1e-3;
+    ncand_total += (double)ncand;
+    // int8 MFMA ops: per tile and slice, sum over K-blocks of (n_pad-K)/32 k-steps x 32 MFMAs x 65536
+    ops += (double)ntiles * e->n_slice * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
+    ++launches_done;
+  }
+  for (auto &x : ev) (void)hipEventDestroy(x);
+  // sort hits by (i, j)
+  std::vector<int64_t> ord(e->hit_i.size());
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
+  });
+  auto apply = [&](auto &v) {
+    auto c2 = v;
+    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
+  };
+  apply(e->hit_i);
+  apply(e->hit_j);
+  apply(e->hit_eff);
+  apply(e->hit_var);
+  apply(e->hit_chi);
+  apply(e->hit_p);
+  *n_hits = (int64_t)e->hit_i.size();
+  e->stats[0] = pairs_tested;
+  e->stats[1] = ncand_total;
+  e->stats[2] = ops;
+  e->stats[3] = t_screen;
+  e->stats[4] = t_ref;
+  e->stats[5] = t_side;
+  e->stats[6] = now() - t_start;
+  e->stats[7] = (double)launches_done;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,
+                             double *p) {
+  GMAT_CHECK(e, GMAT_E_ARG, "gmat_epi_hits: null handle");
+  const int64_t n = (int64_t)e->hit_i.size();
+  GMAT_CHECK(cap >= n, GMAT_E_OVERFLOW, "gmat_epi_hits: capacity %lld < %lld hits", (long long)cap, (long long)n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (i) i[k] = e->hit_i[k];
+    if (j) j[k] = e->hit_j[k];
+    if (eff) eff[k] = e->hit_eff[k];
+    if (var) var[k] = e->hit_var[k];
+    if (chi) chi[k] = e->hit_chi[k];
+    if (p) p[k] = e->hit_p[k];
+  }
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_stats(const gmat_epi *e, double *out8) {
+  GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_stats: bad arguments");
+  for (int k = 0; k < 8; ++k) out8[k] = e->stats[k];
+  return GMAT_OK;
+}

@@ -1,0 +1,198 @@
+"""Shared host logic of the epistasis scans (AA / AD / DD, exact, parallel parts, pairs).
+
+The reference's per-row numpy loop (remma_epiAA.py:71-82 and siblings) is replaced by one
+device scan plan (gmat_epi: genotype panel, P and Py resident in HBM) that returns the
+hits; this module keeps the reference's argument handling, defaults, error conditions,
+output files and row order.
+"""
+import ctypes
+import logging
+import time
+
+import numpy as np
+from scipy.stats import chi2
+
+from .. import _native as N
+from ..plink import Geno, count_lines
+from ..uvlmm.uvlmm_varcom import projection
+
+KINDS = {"AA": N.GMAT_AA, "AD": N.GMAT_AD, "DD": N.GMAT_DD}
+SCAN_HEADER = "snp_0 snp_1 eff chi p_val"
+PAIR_HEADER = "snp_0 snp_1 eff var chi p"
+N_SLICE = 3
+
+
+class EpiPlan:
+    """gmat_epi handle: a genotype panel plus Z'PZ and Z'Py resident on the device."""
+
+    def __init__(self, geno, pvp, py, n_slice=N_SLICE):
+        self._lib = N.ensure_device()
+        self.geno = geno
+        pvp = N.f64(pvp)
+        py = N.f64(np.asarray(py).reshape(-1))
+        if pvp.shape != (geno.n, geno.n) or py.size != geno.n:
+            raise ValueError("P is %s and Py has %d entries for %d genotyped individuals"
+                             % (pvp.shape, py.size, geno.n))
+        h = ctypes.c_void_p()
+        N.check(self._lib.gmat_epi_create(ctypes.byref(h), geno.handle, N.ptr(pvp), N.ptr(py), int(n_slice)),
+                "gmat_epi_create")
+        self._h = h
+
+    def scan(self, kind, rows, p_cut):
+        """Hits (i, j, eff, var, chi, p) with p < p_cut over first-SNP rows `rows`
+        (strictly increasing), sorted by (i, j)."""
+        rows = N.i64(rows)
+        n_hits = ctypes.c_int64()
+        chi_cut = float(chi2.isf(p_cut, 1)) if p_cut < 1 else 0.0
+        N.check(self._lib.gmat_epi_scan(self._h, KINDS[kind], N.ptr(rows), rows.size, float(p_cut), chi_cut,
+                                        ctypes.byref(n_hits)), "gmat_epi_scan")
+        k = n_hits.value
+        out = [np.zeros(k, np.int64), np.zeros(k, np.int64)] + [np.zeros(k) for _ in range(4)]
+        N.check(self._lib.gmat_epi_hits(self._h, k, *[N.ptr(a) for a in out]), "gmat_epi_hits")
+        return tuple(out)
+
+    def pairs(self, kind, pairs):
+        pairs = N.i64(np.asarray(pairs).reshape(-1, 2))
+        k = pairs.shape[0]
+        out = [np.zeros(k) for _ in range(4)]
+        N.check(self._lib.gmat_epi_pairs(self._h, KINDS[kind], N.ptr(pairs), k, *[N.ptr(a) for a in out]),
+                "gmat_epi_pairs")
+        return tuple(out)
+
+    def stats(self):
+        s = np.zeros(8)
+        N.check(self._lib.gmat_epi_stats(self._h, N.ptr(s)), "gmat_epi_stats")
+        keys = ("pairs", "candidates", "int8_ops", "screen_s", "refine_s", "side_s", "total_s", "launches")
+        return dict(zip(keys, s.tolist()))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.gmat_epi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file):
+    """P / Py on the device (remma_epiAA.py:33-49), genotype panel decoded on the device."""
+    logging.info("Calculate the phenotypic covariance matrix and inversion")
+    pvp, py = projection(y, xmat, zmat, gmat_lst, var_com)
+    geno = Geno(bed_file)
+    if geno.n != pvp.shape[0]:
+        raise ValueError("Z has %d individuals, the .fam has %d" % (pvp.shape[0], geno.n))
+    return EpiPlan(geno, pvp, py)
+
+
+def format_rows(cols, n_float):
+    """Rows as pandas DataFrame.to_csv writes them: ints, then float64 reprs."""
+    i, j = cols[0], cols[1]
+    fl = cols[2:2 + n_float]
+    return "".join("%d %d %s\n" % (a, b, " ".join(repr(float(v[t])) for v in fl)) for t, (a, b) in
+                   enumerate(zip(i.tolist(), j.tolist())))
+
+
+def resolve_rows(kind, num_snp, snp_lst_0):
+    """Default and range check of snp_lst_0 (remma_epiAA.py:63-68; AD: remma_epiAD.py:66-72)."""
+    hi = num_snp if kind == "AD" else num_snp - 1
+    if snp_lst_0 is None:
+        return np.arange(hi, dtype=np.int64)
+    rows = np.asarray(list(snp_lst_0), dtype=np.int64)
+    if rows.size and (rows.max() > hi - 1 or rows.min() < 0):
+        logging.error("snp_lst_0 is out of range!")
+        raise ValueError("snp_lst_0 is out of range!")
+    return rows
+
+
+def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut, out_file):
+    """_remma_epiXX: header, then the hits of each row of snp_lst_0 in list order (the
+    reference appends each row's hits with j ascending)."""
+    with open(out_file, "w") as f:
+        f.write(SCAN_HEADER + "\n")
+    num_snp = count_lines(bed_file + ".bim")
+    rows = resolve_rows(kind, num_snp, snp_lst_0)
+    plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file)
+    try:
+        uniq = np.unique(rows)
+        t0 = time.perf_counter()
+        hi, hj, eff, var, chi, p = plan.scan(kind, uniq, p_cut)
+        logging.info("Running time: Clock time, {:.5f} sec.".format(time.perf_counter() - t0))
+        logging.info("scan stats: %s" % plan.stats())
+    finally:
+        plan.close()
+        plan.geno.close()
+    if rows.size == uniq.size and np.all(np.diff(rows) > 0):
+        order = np.arange(hi.size)
+    else:  # replay the caller's row order (and duplicates) like the reference's loop
+        starts = np.searchsorted(hi, uniq, side="left")
+        ends = np.searchsorted(hi, uniq, side="right")
+        pos = np.searchsorted(uniq, rows)
+        order = np.concatenate([np.arange(starts[k], ends[k]) for k in pos]) if rows.size else np.zeros(0, int)
+    with open(out_file, "a") as f:
+        f.write(format_rows([hi[order], hj[order], eff[order], chi[order], p[order]], 3))
+    return 0
+
+
+def parallel_rows(num_snp, parallel, kind):
+    """The triangle-folded part `parallel=[N, k]` (remma_epiAA.py:125-139; AD extends part 1
+    to num_snp, remma_epiAD.py:134-140)."""
+    n_part, k = int(parallel[0]), int(parallel[1])
+    s = int(num_snp / (2 * n_part))
+    p0, p1 = (k - 1) * s, k * s
+    p2, p3 = (2 * n_part - k) * s, (2 * n_part - k + 1) * s
+    if k == 1:
+        p3 = num_snp if kind == "AD" else num_snp - 1
+    return list(range(p0, p1)) + list(range(p2, p3))
+
+
+def run_parallel(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, parallel, p_cut, out_file):
+    logging.info("Parallel: " + str(parallel[0]) + ", " + str(parallel[1]))
+    num_snp = count_lines(bed_file + ".bim")
+    rows = parallel_rows(num_snp, parallel, kind)
+    return run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, rows, p_cut,
+                    out_file + "." + str(parallel[1]))
+
+
+def read_pair_file(snp_pair_file):
+    """First two columns of every line after the first (pd.read_csv(skiprows=1), :72-75)."""
+    out = []
+    with open(snp_pair_file) as f:
+        f.readline()
+        for line in f:
+            a = line.split()
+            if len(a) >= 2:
+                out.append((int(a[0]), int(a[1])))
+    return np.array(out, dtype=np.int64).reshape(-1, 2)
+
+
+def run_pairs(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_pair_file, max_test_pair, p_cut, out_file):
+    """_remma_epiXX_pair (remma_epiAA_pair.py:16-92): exact statistics of the listed pairs,
+    rows with p < p_cut in file order, columns snp_0 snp_1 eff var chi p."""
+    pairs = read_pair_file(snp_pair_file)
+    num_snp = count_lines(bed_file + ".bim")
+    plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file)
+    with open(out_file, "w") as f:
+        f.write(PAIR_HEADER + "\n")
+    try:
+        for t0 in range(0, pairs.shape[0], max(1, int(max_test_pair))):
+            chunk = pairs[t0:t0 + int(max_test_pair)]
+            if chunk.size and (chunk.max() > num_snp - 1 or chunk.min() < 0):
+                logging.error("snp_pair is out of range!")
+                raise ValueError("snp_pair is out of range!")
+            eff, var, chi, p = plan.pairs(kind, chunk)
+            keep = p < p_cut
+            with open(out_file, "a") as f:
+                f.write(format_rows([chunk[keep, 0], chunk[keep, 1], eff[keep], var[keep], chi[keep], p[keep]], 4))
+    finally:
+        plan.close()
+        plan.geno.close()
+    return 0

@@ -1,0 +1,106 @@
+/*
+ * gmat_hip.h -- C ABI of libgmat_hip.so, the MI355X (gfx950) implementation of GMAT's
+ * dense-linear-algebra hot path.  Plain pointers and sizes only; every function returns
+ * GMAT_OK (0) or a negative GMAT_E_* code and never exits the process (the reference's C
+ * code calls exit(1) on I/O errors: _remma_epi_eff_cpu.c:19-20,116-117).  The message of
+ * the last failure on the calling thread is available from gmat_last_error().
+ *
+ * Host arrays are row-major.  Genotype input is the body of a PLINK .bed file (the bytes
+ * after the 3-byte magic), SNP-major, ceil(n_id/4) bytes per SNP, decoded with the
+ * reference's convention (process_plink/_read_plink_bed.c:37): code 00->0, 10->1, 11->2,
+ * 01->missing.
+ *
+ * Which reference interface each entry point replaces is noted per function; the
+ * Python host layer (gmat_amd/) keeps the reference's Python signatures on top of it.
+ */
+#ifndef GMAT_HIP_H
+#define GMAT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  GMAT_OK = 0,
+  GMAT_E_ARG = -1,      /* invalid argument */
+  GMAT_E_HIP = -2,      /* HIP runtime error */
+  GMAT_E_NOMEM = -3,    /* device allocation failed */
+  GMAT_E_NOTPD = -4,    /* matrix not positive definite */
+  GMAT_E_OVERFLOW = -5, /* an output buffer was too small (see the *_needed argument) */
+  GMAT_E_STATE = -6     /* call sequence error */
+};
+
+enum { GMAT_AA = 0, GMAT_AD = 1, GMAT_DD = 2 };         /* epistasis kinds */
+enum { GMAT_GRM_ADD = 0, GMAT_GRM_DOM = 1 };             /* relationship matrices */
+
+const char *gmat_last_error(void);
+int gmat_version(void);
+int gmat_device_count(int *n);
+int gmat_set_device(int device);
+
+/* ---------------------------------------------------------------- genotype panel
+ * Uploads the packed .bed body once and decodes it on the device into SNP-major int8
+ * panels (dosage and heterozygote indicator).  Replaces the decode done by
+ * read_plink (process_plink.py:7-9 / pandas_plink) and read_plink_bed
+ * (_read_plink_bed.c:5-51) for every consumer below.  Missing genotypes must have been
+ * imputed by the caller (as gmatrix.py:47-49 / remma_epiAA.py:57-59 do); a panel that
+ * still contains missing codes is rejected by the consumers. */
+typedef struct gmat_geno gmat_geno;
+int gmat_geno_create(gmat_geno **out, const uint8_t *bed_body, int64_t body_bytes, int64_t n_id,
+                     int64_t n_snp);
+/* per-SNP sum of dosages, heterozygote count and missing count (each n_snp long; any may be NULL) */
+int gmat_geno_counts(const gmat_geno *g, int64_t *sum_dose, int64_t *n_het, int64_t *n_miss);
+int gmat_geno_destroy(gmat_geno *g);
+
+/* ---------------------------------------------------------------- relationship matrices
+ * kin (n_id x n_id, host) = additive GRM of agmat (gmatrix.py:52-66) for GMAT_GRM_ADD or the
+ * dominance GRM of dgmat_as (gmatrix.py:115-130) for GMAT_GRM_DOM, diagonal scaled by
+ * (1 + small_val).  *scale_out receives the scale factor. */
+int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, double *scale_out);
+
+/* ainv = a^-1 for a symmetric positive-definite n x n matrix (scipy.linalg.inv at
+ * gmatrix.py:84); *logdet = log|a| (may be NULL). */
+int gmat_spd_inverse(int64_t n, const double *a, double *ainv, double *logdet);
+
+/* ---------------------------------------------------------------- REML
+ * Weighted EM-AI REML of _wemai_multi_gmat (uvlmm_varcom.py:8-104).  z_col[r] is the
+ * individual (column of Z) of record r; gmat[k] points to an n_id x n_id matrix.
+ * var_out has n_gmat+1 entries (residual last); history (may be NULL) receives maxiter x
+ * (n_gmat+1) values (the variances after each iteration). */
+int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y,
+              const double *xmat, const int64_t *z_col, const double *const *gmat, const double *init,
+              int maxiter, double cc_par, double cc_gra, double *var_out, int *n_iter, double *history);
+
+/* pvp = Z'PZ (n_id x n_id) and py = Z'Py (n_id) of the scans' setup (remma_epiAA.py:33-49). */
+int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y,
+                    const double *xmat, const int64_t *z_col, const double *const *gmat,
+                    const double *var_com, double *pvp, double *py);
+
+/* ---------------------------------------------------------------- epistasis scans
+ * A scan plan keeps the genotype panel, P (= Z'PZ) and Py resident in HBM. */
+typedef struct gmat_epi gmat_epi;
+int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice);
+/* Exhaustive exact scan over first-SNP rows `rows` (sorted ascending): AA/DD test pairs
+ * (i, j>i) (remma_epiAA.py:71-82, remma_epiDD.py:75-86), AD tests (i, all j) including i==j
+ * (remma_epiAD.py:76-87).  A pair is a hit when p < p_cut with p = chi2.sf(eff^2/var, 1);
+ * chi_cut must be chi2.isf(p_cut, 1).  *n_hits receives the number of hits, retrieved with
+ * gmat_epi_hits (sorted by (i, j)). */
+int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+                  int64_t *n_hits);
+int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,
+                  double *p);
+/* Exact statistics of an explicit pair list (remma_epiAA_pair.py:79-84 and siblings). */
+int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *eff, double *var,
+                   double *chi, double *p);
+/* counters of the last scan: [0] pairs tested, [1] candidates refined, [2] int8 MFMA ops,
+ * [3] screen kernel seconds, [4] refine kernel seconds, [5] side-term kernel seconds,
+ * [6] total seconds, [7] screen kernel launches */
+int gmat_epi_stats(const gmat_epi *e, double *out8);
+int gmat_epi_destroy(gmat_epi *e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMAT_HIP_H */
