@@ -30,6 +30,7 @@ _PROTOS = {
     "gmat_geno_counts": (_INT, [_P, _P, _P, _P]),
     "gmat_geno_destroy": (_INT, [_P]),
     "gmat_grm": (_INT, [_P, _INT, _D, _P, _P]),
+    "gmat_grm_stats": (_INT, [_P]),
     "gmat_spd_inverse": (_INT, [_I64, _P, _P, _P]),
     "gmat_reml": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _INT, _D, _D, _P, _P, _P]),
     "gmat_projection": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P]),

@@ -218,6 +218,14 @@ extern "C" int gmat_geno_destroy(gmat_geno *g) {
   return GMAT_OK;
 }
 
+static double g_grm_stats[4] = {0, 0, 0, 0};
+
+extern "C" int gmat_grm_stats(double *out4) {
+  GMAT_CHECK(out4, GMAT_E_ARG, "gmat_grm_stats: null");
+  for (int k = 0; k < 4; ++k) out4[k] = g_grm_stats[k];
+  return GMAT_OK;
+}
+
 extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, double *scale_out) {
   GMAT_CHECK(g && kin, GMAT_E_ARG, "gmat_grm: bad arguments");
   GMAT_CHECK(kind == GMAT_GRM_ADD || kind == GMAT_GRM_DOM, GMAT_E_ARG, "gmat_grm: unknown kind %d", kind);
@@ -254,9 +262,22 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
                      dc.as<double>(), n, dr.as<double>());
   GMAT_HIP(hipGetLastError());
   const unsigned nt = (unsigned)(n_pad / GT);
+  hipEvent_t e0, e1;
+  GMAT_HIP(hipEventCreate(&e0));
+  GMAT_HIP(hipEventCreate(&e1));
+  GMAT_HIP(hipEventRecord(e0, 0));
   hipLaunchKernelGGL(grm_kernel, dim3(nt, nt), dim3(256), 0, 0, gt.as<int8_t>(), m_pad, n, dr.as<double>(), cc,
                      scale, small_val, dk.as<double>());
   GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipEventRecord(e1, 0));
+  GMAT_HIP(hipEventSynchronize(e1));
+  float ms = 0;
+  GMAT_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  g_grm_stats[0] = ms * 1e-3;
+  g_grm_stats[1] = (double)nt * (nt + 1) / 2 * 2.0 * GT * GT * (double)m_pad;  // int8 ops issued (lower tiles)
+  g_grm_stats[2] = 2.0 * (double)n * n * m;                                      // dense-equivalent flop 2n^2m
   GMAT_HIP(hipMemcpy(kin, dk.p, n * n * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }

@@ -59,6 +59,9 @@ int gmat_geno_destroy(gmat_geno *g);
  * dominance GRM of dgmat_as (gmatrix.py:115-130) for GMAT_GRM_DOM, diagonal scaled by
  * (1 + small_val).  *scale_out receives the scale factor. */
 int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, double *scale_out);
+/* last gmat_grm call: [0] seconds of the int8 MFMA product+epilogue kernel, [1] int8 ops it
+ * issued, [2] dense-equivalent flop 2 n^2 m, [3] reserved */
+int gmat_grm_stats(double *out4);
 
 /* ainv = a^-1 for a symmetric positive-definite n x n matrix (scipy.linalg.inv at
  * gmatrix.py:84); *logdet = log|a| (may be NULL). */
