@@ -722,6 +722,40 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   double t_screen = 0, t_side = 0, t_ref = 0, pairs_tested = 0, ncand_total = 0, ops = 0;
   int64_t launches_done = 0;
   std::vector<int> tiles;
+  int64_t pending = 0;  // candidates waiting in the device buffer
+  GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+  // exact refine of candidates [0, count) and collection of the hits
+  auto flush = [&](int64_t count) -> int {
+    if (count <= 0) return GMAT_OK;
+    GMAT_HIP(hipEventRecord(ev[3], e->s));
+    GMAT_TRY(refine(e, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), count, e->ceff.as<double>(),
+                    e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>()));
+    GMAT_HIP(hipEventRecord(ev[4], e->s));
+    std::vector<int64_t> ci(count), cj(count);
+    std::vector<double> ce(count), cv(count), cc(count), cp(count);
+    GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, count * 8, hipMemcpyDeviceToHost, e->s));
+    GMAT_HIP(hipStreamSynchronize(e->s));
+    float ms34;
+    GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
+    t_ref += ms34 * 1e-3;
+    ncand_total += (double)count;
+    for (int64_t k = 0; k < count; ++k) {
+      if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
+        e->hit_i.push_back(ci[k]);
+        e->hit_j.push_back(cj[k]);
+        e->hit_eff.push_back(ce[k]);
+        e->hit_var.push_back(cv[k]);
+        e->hit_chi.push_back(cc[k]);
+        e->hit_p.push_back(cp[k]);
+      }
+    }
+    return GMAT_OK;
+  };
   for (auto &rws : launches) {
     const int Rn = (int)rws.size();
     if (Rn == 0) continue;
@@ -742,7 +776,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(dtiles.alloc(tiles.size() * sizeof(int)));
     GMAT_HIP(hipMemcpyAsync(drows.p, rws.data(), Rn * 8, hipMemcpyHostToDevice, e->s));
     GMAT_HIP(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(int), hipMemcpyHostToDevice, e->s));
-    GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
     const int64_t ncol = m - j_lo;
     GMAT_HIP(hipEventRecord(ev[0], e->s));
     hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, e->s, n_pad, Rn, drows.as<int64_t>(),
@@ -788,54 +821,38 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cap = e->cand_cap;
     sa.cand_i = e->cand_i.as<int64_t>();
     sa.cand_j = e->cand_j.as<int64_t>();
-    hipLaunchKernelGGL(screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa);
-    GMAT_HIP(hipGetLastError());
-    GMAT_HIP(hipEventRecord(ev[2], e->s));
-    unsigned long long ncand = 0;
-    GMAT_HIP(hipMemcpyAsync(&ncand, e->counter.p, 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipStreamSynchronize(e->s));
-    GMAT_CHECK((int64_t)ncand <= e->cand_cap, GMAT_E_OVERFLOW,
-               "scan produced %llu candidates in one launch (capacity %lld): p_cut too large for a scan; "
-               "use the pair test", ncand, (long long)e->cand_cap);
-    GMAT_HIP(hipEventRecord(ev[3], e->s));
-    GMAT_TRY(refine(e, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), (int64_t)ncand,
-                    e->ceff.as<double>(), e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>()));
-    GMAT_HIP(hipEventRecord(ev[4], e->s));
-    if (ncand) {
-      std::vector<int64_t> ci(ncand), cj(ncand);
-      std::vector<double> ce(ncand), cv(ncand), cc(ncand), cp(ncand);
-      GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, ncand * 8, hipMemcpyDeviceToHost, e->s));
+    unsigned long long count = 0;
+    for (int attempt = 0;; ++attempt) {
+      hipLaunchKernelGGL(screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa);
+      GMAT_HIP(hipGetLastError());
+      GMAT_HIP(hipEventRecord(ev[2], e->s));
+      GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, e->s));
       GMAT_HIP(hipStreamSynchronize(e->s));
-      for (unsigned long long k = 0; k < ncand; ++k) {
-        if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
-          e->hit_i.push_back(ci[k]);
-          e->hit_j.push_back(cj[k]);
-          e->hit_eff.push_back(ce[k]);
-          e->hit_var.push_back(cv[k]);
-          e->hit_chi.push_back(cc[k]);
-          e->hit_p.push_back(cp[k]);
-        }
-      }
-    } else {
-      GMAT_HIP(hipStreamSynchronize(e->s));
+      if ((int64_t)count <= e->cand_cap) break;
+      // overflow in this launch: refine what earlier launches left, then redo this one
+      GMAT_CHECK(attempt == 0 && pending > 0, GMAT_E_OVERFLOW,
+                 "one screen launch produced %llu candidates (capacity %lld): p_cut too large for a scan; "
+                 "use the pair test", count, (long long)e->cand_cap);
+      GMAT_TRY(flush(pending));
+      pending = 0;
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
     }
-    float ms01, ms12, ms34;
+    pending = (int64_t)count;
+    float ms01, ms12;
     GMAT_HIP(hipEventElapsedTime(&ms01, ev[0], ev[1]));
     GMAT_HIP(hipEventElapsedTime(&ms12, ev[1], ev[2]));
-    GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
     t_side += ms01 * 1e-3;
     t_screen += ms12 * 1e-3;
-    t_ref += ms34 * 1e-3;
-    ncand_total += (double)ncand;
     // int8 MFMA ops: per tile and slice, sum over K-blocks of (n_pad-K)/32 k-steps x 32 MFMAs x 65536
     ops += (double)ntiles * e->n_slice * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
     ++launches_done;
+    if (pending > e->cand_cap / 2) {
+      GMAT_TRY(flush(pending));
+      pending = 0;
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+    }
   }
+  GMAT_TRY(flush(pending));
   for (auto &x : ev) (void)hipEventDestroy(x);
   // sort hits by (i, j)
   std::vector<int64_t> ord(e->hit_i.size());
