@@ -164,6 +164,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     screen_s = launches = ops = cands = hits = side_s = ref_s = 0.0
+    n_slice = 0
     for _ in range(args.steps):
         res = step()
         st = plan.stats()
@@ -173,6 +174,7 @@ def main():
         cands += st["candidates"]
         side_s += st["side_s"]
         ref_s += st["refine_s"]
+        n_slice = int(st["n_slice"])
         hits += res[0].size
     sync()
     dist.barrier()
@@ -182,9 +184,9 @@ def main():
     cands_all = dist.allreduce_sum(cands) / args.steps
 
     # roofline of the dominant kernel (screen): algorithmic int8 ops per launch / avg launch time.
-    # per pair the sliced symmetric quadratic form needs S * n * (n + 128) int8 multiply-adds x2
+    # per pair the sliced symmetric quadratic form needs S * n * (n + 128) / 2 int8 MACs
     my_pairs = float(sum(m - 1 - int(i) for i in rows))
-    alg_ops_step = my_pairs * 3 * n * (n + 128)
+    alg_ops_step = my_pairs * n_slice * n * (n + 128)
     avg_launch_s = screen_s / max(launches, 1)
     alg_ops_launch = alg_ops_step * args.steps / max(launches, 1)
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
@@ -197,7 +199,8 @@ def main():
     roofline = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
                 "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
                 "kernel": "screen_kernel (v_mfma_i32_32x32x32_i8)",
-                "ops_note": "int8 ops (TOP/s); algorithmic = 3 slices x n(n+128) MACs x 2 per pair",
+                "ops_note": "int8 ops (TOP/s); algorithmic = S slices x n(n+128)/2 MACs x 2 per pair",
+                "n_slice": n_slice,
                 "issued_int8_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
                 "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
 

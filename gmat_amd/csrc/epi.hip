@@ -69,14 +69,26 @@ struct ScreenArgs {
   int64_t *cand_i, *cand_j;
 };
 
+// One workgroup = one tile of BI first-SNP rows x BJ second-SNP columns (256 pairs); wave w
+// owns the col tiles of rows 2w, 2w+1.  The (slice, K-block, stage) sequence of the tile is
+// one flattened software pipeline: the next stage's A band (MT rows x LK individuals of
+// A_s) and genotype chunks are fetched into registers while the current stage multiplies,
+// across K-block and slice boundaries, so no K-block starts with a load bubble.  The
+// diagonal stages' genotype chunks are also kept in a ping-pong LDS region (eI/eJ) from
+// which the K-block epilogue rebuilds its weights w[row] without touching global memory.
+constexpr int EP = MT + 16;  // epilogue-region pitch (128 individuals + pad)
+
 __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t sA[2][MT * AP];
   __shared__ __attribute__((aligned(16))) int8_t sI[2][BI * AP];
   __shared__ __attribute__((aligned(16))) int8_t sJ[2][BJ * AP];
+  __shared__ __attribute__((aligned(16))) int8_t eI[2][BI * EP];
+  __shared__ __attribute__((aligned(16))) int8_t eJ[2][BJ * EP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
   const int64_t J0 = (int64_t)J * BJ;
   const int64_t n_pad = a.n_pad;
+  const int nK = (int)(n_pad / MT);
 
   int64_t ti[2];
 #pragma unroll
@@ -84,10 +96,9 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const int r = roff + 2 * w + t;
     ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
   }
-  // staging roles
-  const int ch0 = tid, ch1 = tid + 256;  // A chunks
-  const int arow0 = ch0 >> 2, acol0 = (ch0 & 3) * 16, arow1 = ch1 >> 2, acol1 = (ch1 & 3) * 16;
-  int prow = -1, pcol = 0, pside = 0;  // panel chunk: side 1 = i-panel, 2 = j-panel
+  // staging roles: two 16-byte A chunks per thread, one genotype chunk for tid < 160
+  const int arow0 = tid >> 2, acol0 = (tid & 3) * 16, arow1 = (tid + 256) >> 2;
+  int prow = 0, pcol = 0, pside = 0;  // 1 = i-panel (offset coded), 2 = j-panel
   const int8_t *psrc = nullptr;
   if (tid < 32) {
     pside = 1;
@@ -102,94 +113,112 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     if (J0 + prow < a.m) psrc = a.right + (J0 + prow) * n_pad + pcol;
   }
 
+  v4i ra0, ra1, rp = {0, 0, 0, 0};
+  auto load = [&](int s, int kb, int st) {
+    const int64_t K = (int64_t)kb * MT, L = K + (int64_t)st * LK;
+    const int8_t *As = a.slices + (int64_t)s * n_pad * n_pad + L + acol0;
+    ra0 = *(const v4i *)&As[(K + arow0) * n_pad];
+    ra1 = *(const v4i *)&As[(K + arow1) * n_pad];
+    if (psrc) rp = *(const v4i *)&psrc[L];
+  };
+  auto store = [&](int b, int st, int region) {
+    *(v4i *)&sA[b][arow0 * AP + acol0] = ra0;
+    *(v4i *)&sA[b][arow1 * AP + acol0] = ra1;
+    if (pside == 1) {
+      v4i o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
+      *(v4i *)&sI[b][prow * AP + pcol] = o;
+      if (st < MT / LK) *(v4i *)&eI[region][prow * EP + st * LK + pcol] = o;
+    } else if (pside == 2) {
+      *(v4i *)&sJ[b][prow * AP + pcol] = rp;
+      if (st < MT / LK) *(v4i *)&eJ[region][prow * EP + st * LK + pcol] = rp;
+    }
+  };
+
+  v16i acc[4][2];
   int64_t tot[2] = {0, 0};
   unsigned sw[2] = {0, 0};
-
-  for (int s = 0; s < a.n_slice; ++s) {
-    const int8_t *As = a.slices + (int64_t)s * n_pad * n_pad;
-    const int shift = 7 * (a.n_slice - 1 - s);
-    for (int64_t K = 0; K < n_pad; K += MT) {
-      v16i acc[4][2];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[r][t][e] = 0;
-      const int nst = (int)((n_pad - K) / LK);
-      v4i ra0, ra1, rp = {0, 0, 0, 0};
-      auto load = [&](int64_t L) {
-        ra0 = *(const v4i *)&As[(K + arow0) * n_pad + L + acol0];
-        ra1 = *(const v4i *)&As[(K + arow1) * n_pad + L + acol1];
-        if (psrc) rp = *(const v4i *)&psrc[L];
-      };
-      auto store = [&](int b) {
-        *(v4i *)&sA[b][arow0 * AP + acol0] = ra0;
-        *(v4i *)&sA[b][arow1 * AP + acol1] = ra1;
-        if (pside == 1) {
-          v4i o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
-          *(v4i *)&sI[b][prow * AP + pcol] = o;
-        } else if (pside == 2) {
-          *(v4i *)&sJ[b][prow * AP + pcol] = rp;
-        }
-      };
-      load(K);
-      store(0);
-      __syncthreads();
-      for (int st = 0; st < nst; ++st) {
-        const int cur = st & 1;
-        const int64_t L = K + (int64_t)st * LK;
-        if (st + 1 < nst) load(L + LK);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bool diag = (L + kk * 32) < (K + MT);
-          const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
-          v4i fb[2];
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const v4i o = *(const v4i *)&sI[cur][(2 * w + t) * AP + kk * 32 + 16 * h];
-            const v4i v = *(const v4i *)&sJ[cur][c * AP + kk * 32 + 16 * h];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const v4i fa = *(const v4i *)&sA[cur][(r * 32 + c) * AP + kk * 32 + 16 * h];
-            acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], acc[r][0], 0, 0, 0);
-            acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], acc[r][1], 0, 0, 0);
-          }
-        }
-        if (st + 1 < nst) store(cur ^ 1);
-        __syncthreads();
+  int s = 0, kb = 0, st = 0, gk = 0, cur = 0;
+  load(0, 0, 0);
+  store(0, 0, 0);
+  __syncthreads();
+  for (;;) {
+    const int64_t K = (int64_t)kb * MT, L = K + (int64_t)st * LK;
+    const int last_st = (int)((n_pad - K) / LK) - 1;
+    // coordinates of the next stage
+    int ns = s, nkb = kb, nst = st + 1;
+    if (st == last_st) {
+      nst = 0;
+      if (++nkb == nK) {
+        nkb = 0;
+        ++ns;
       }
-      // epilogue: sum_rows w[row] * acc[row]  (acc register e of this lane <-> storage slot 16h+e)
+    }
+    const bool has_next = ns < a.n_slice;
+    if (has_next) load(ns, nkb, nst);
+    // one 32-deep k-step: B fragments w = a_i*b_j generated from the staged genotype chunks,
+    // A fragments read from the staged band; `zero` starts a K-block (C operand 0, no reset)
+    auto kstep = [&](int kk, bool zero) {
+      const bool diag = (L + kk * 32) < (K + MT);
+      const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
+      v4i fb[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (ti[t] < 0) continue;
-        const int64_t j = J0 + c;
-        const int8_t *ol = a.left + ti[t] * n_pad + K + 16 * h;
-        const int8_t *vr = (j < a.m) ? a.right + j * n_pad + K + 16 * h : nullptr;
+        const v4i o = *(const v4i *)&sI[cur][(2 * w + t) * AP + kk * 32 + 16 * h];
+        const v4i v = *(const v4i *)&sJ[cur][c * AP + kk * 32 + 16 * h];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
+      }
+      const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const v4i fa = *(const v4i *)&sA[cur][(r * 32 + c) * AP + kk * 32 + 16 * h];
+        acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], zero ? z : acc[r][0], 0, 0, 0);
+        acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], zero ? z : acc[r][1], 0, 0, 0);
+      }
+    };
+    if (st == 0) {
+      kstep(0, true);
+#pragma unroll
+      for (int kk = 1; kk < LK / 32; ++kk) kstep(kk, false);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < LK / 32; ++kk) kstep(kk, false);
+    }
+    if (st == last_st) {
+      // epilogue: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage slot
+      // 16h+e of each 32-row tile, whose genotype bytes sit in the LDS epilogue region
+      const int reg = gk & 1;
+      const int shift = 7 * (a.n_slice - 1 - s);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
         int64_t part64 = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const v4i o = *(const v4i *)&ol[r * 32];
-          const v4i v = vr ? *(const v4i *)&vr[r * 32] : v4i{0, 0, 0, 0};
+          const v4i o = *(const v4i *)&eI[reg][(2 * w + t) * EP + r * 32 + 16 * h];
+          const v4i v = *(const v4i *)&eJ[reg][c * EP + r * 32 + 16 * h];
           int part = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const unsigned wb = __builtin_amdgcn_perm(T_HI, T_LO, to_offset((unsigned)o[q]) + (unsigned)v[q]);
+            const unsigned wb = __builtin_amdgcn_perm(T_HI, T_LO, (unsigned)o[q] + (unsigned)v[q]);
             part += (int)(wb & 0xff) * acc[r][t][4 * q] + (int)((wb >> 8) & 0xff) * acc[r][t][4 * q + 1] +
                     (int)((wb >> 16) & 0xff) * acc[r][t][4 * q + 2] + (int)(wb >> 24) * acc[r][t][4 * q + 3];
-            if (s == 0) sw[t] = __builtin_amdgcn_udot4(wb, 0x01010101u, sw[t], false);
+            if (s == 0) sw[t] = __builtin_amdgcn_udot4(wb, wb, sw[t], false);  // sum w^2
           }
           part64 += part;
         }
         tot[t] += part64 * (int64_t)(1LL << shift);
       }
+      ++gk;
     }
+    if (!has_next) break;
+    store(cur ^ 1, nst, gk & 1);
+    __syncthreads();
+    cur ^= 1;
+    s = ns;
+    kb = nkb;
+    st = nst;
   }
   // combine the two lane halves (disjoint rows of the same column), then test
 #pragma unroll
@@ -202,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     if (a.mono_l[i] || a.mono_r[j]) continue;  // x == 0: the reference's statistic is NaN
     const int ri = roff + 2 * w + t;
     const double M = (double)(tot[t] + other) * a.scale_main;
-    const double sumw = (double)(sw[t] + osw);
+    const double sumw2 = (double)(sw[t] + osw);
     const double E1 = a.e13[(int64_t)ri * a.ld_e + (j - a.j_lo)];
     const double E3 = a.e13[(int64_t)(a.n_rows + ri) * a.ld_e + (j - a.j_lo)];
     const double E2 = a.e2[(int64_t)ri * a.ld_e + (j - a.j_lo)];
@@ -212,7 +241,8 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const double var = M + t1 + t2 + t3 + t4 + t5 + t6 + t7;
     const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
     const double slack = 1e-12 * (fabs(M) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
-    const double var_lo = var - a.delta * sumw * sumw - slack;
+    // |w'(P - P~)w| <= ||P - P~||_2 * |w|^2  (a.delta = rigorous upper bound of the spectral norm)
+    const double var_lo = var - a.delta * sumw2 - slack;
     const bool cand = !(var_lo > 0.0) || eff * eff * (1.0 + 1e-9) >= a.chi_cut * var_lo;
     if (cand) {
       const unsigned long long k = atomicAdd(a.counter, 1ULL);
@@ -374,6 +404,17 @@ __global__ void slice_kernel(int64_t n, int64_t n_pad, const double *P, double i
   }
 }
 
+// residual of the slicing, R = P - P~ (natural order, zero padded), scaled by 1/rscale
+__global__ void residual_kernel(int64_t n, int64_t n_pad, const double *P, double inv_unit, int n_slice,
+                                double out_scale, double *R) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * n_pad) return;
+  const int64_t r0 = idx / n_pad, c0 = idx % n_pad;
+  double r = (r0 < n && c0 < n) ? P[r0 * n + c0] * inv_unit : 0.0;
+  for (int s = 0; s < n_slice; ++s) r = (r - rint(r)) * 128.0;
+  R[idx] = r * out_scale;
+}
+
 // per-SNP side vectors for the left coding: L' = a o (u - alpha z), L3 = a o py, and
 // scalars qa = a.u, ra = a.z, sa = a.py.  One workgroup per SNP.
 __global__ __launch_bounds__(256) void left_side_kernel(int64_t n_pad, const int8_t *panel, const double *U,
@@ -488,6 +529,7 @@ struct gmat_epi {
   int64_t n = 0, n_pad = 0, m = 0;
   int n_slice = 3;
   double pmax = 0, zz = 0, spy = 0;
+  double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P - sum_{s<S} A_s 128^-s pmax/127||_2
   DBuf Ps, py, z, slices;
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
@@ -495,7 +537,7 @@ struct gmat_epi {
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
-  double stats[8] = {0};
+  double stats[10] = {0};
   hipStream_t s = 0;
 };
 
@@ -604,6 +646,33 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
     set_error("gmat_epi_create: setup kernels failed");
     return fail(GMAT_E_HIP);
   }
+  // ||R||_2 <= ||R^16||_F^(1/16) (R symmetric): four fp64 MFMA squarings of R scaled to
+  // unit max entry (|R_kl| <= 0.5 * 128^-(S-1) / unit), for every usable slice count S
+  for (int S = 2; S <= n_slice; ++S) {
+    const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
+    DBuf r1, r2, rows;
+    if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
+        (rc = rows.alloc(n_pad * sizeof(double))))
+      return fail(rc);
+    hipLaunchKernelGGL(residual_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, S,
+                       1.0 / 64.0, r1.as<double>());  // final residual in [-64, 64] scaled units
+    double *src = r1.as<double>(), *dst = r2.as<double>();
+    for (int q = 0; q < 4; ++q) {
+      if ((rc = dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad)))
+        return fail(rc);
+      std::swap(src, dst);
+    }
+    if ((rc = dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rows.as<double>()))) return fail(rc);
+    std::vector<double> hr(n_pad);
+    if (hipMemcpy(hr.data(), rows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("gmat_epi_create: residual norm download failed");
+      return fail(GMAT_E_HIP);
+    }
+    double fro2 = 0.0;
+    for (double v : hr) fro2 += v;
+    // 5% margin for the fp64 rounding of the squarings, plus the rounding of P*unit itself
+    e->rho[S] = 1.05 * rmax * std::pow(std::sqrt(fro2), 1.0 / 16.0) + 1e-15 * pmax * (double)n;
+  }
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
     set_error("gmat_epi_create: z download failed");
@@ -662,7 +731,7 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
 }
 
 extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
-                             int64_t *n_hits) {
+                             int n_slice, int64_t *n_hits) {
   GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
   GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
   const int64_t m = e->m, n_pad = e->n_pad;
@@ -698,8 +767,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) rws.push_back(rows[t]);
     launches.push_back(rws);
   }
-  const double scale_main = e->pmax / 127.0 * std::pow(128.0, -(e->n_slice - 1));
-  const double delta = 0.5 * std::pow(128.0, -(e->n_slice - 1)) * e->pmax / 127.0;
+  // slices used: 2 when the candidate band of the 2-slice bound stays thin (small p_cut), else all
+  const int S = n_slice > 0 ? n_slice : (p_cut <= 1e-4 ? 2 : e->n_slice);
+  GMAT_CHECK(S >= 2 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [2, %d]", S, e->n_slice);
+  const double scale_main = e->pmax / 127.0 * std::pow(128.0, -(S - 1));
+  const double delta = e->rho[S];
 
   DBuf drows, dtiles, bl, ba, e13, e2;
   GMAT_TRY(drows.alloc(ROWS_PER_LAUNCH * 8));
@@ -790,7 +862,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     ScreenArgs sa;
     sa.slices = e->slices.as<int8_t>();
     sa.n_pad = n_pad;
-    sa.n_slice = e->n_slice;
+    sa.n_slice = S;
     sa.left = lp;
     sa.right = rp;
     sa.m = m;
@@ -844,7 +916,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     t_side += ms01 * 1e-3;
     t_screen += ms12 * 1e-3;
     // int8 MFMA ops: per tile and slice, sum over K-blocks of (n_pad-K)/32 k-steps x 32 MFMAs x 65536
-    ops += (double)ntiles * e->n_slice * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
+    ops += (double)ntiles * S * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
     ++launches_done;
     if (pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));
@@ -879,6 +951,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[5] = t_side;
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
+  e->stats[8] = S;
+  e->stats[9] = delta;
   return GMAT_OK;
 }
 
@@ -898,8 +972,8 @@ extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, d
   return GMAT_OK;
 }
 
-extern "C" int gmat_epi_stats(const gmat_epi *e, double *out8) {
-  GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_stats: bad arguments");
-  for (int k = 0; k < 8; ++k) out8[k] = e->stats[k];
+extern "C" int gmat_epi_stats(const gmat_epi *e, double *out10) {
+  GMAT_CHECK(e && out10, GMAT_E_ARG, "gmat_epi_stats: bad arguments");
+  for (int k = 0; k < 10; ++k) out10[k] = e->stats[k];
   return GMAT_OK;
 }

@@ -19,7 +19,7 @@ from ..uvlmm.uvlmm_varcom import projection
 KINDS = {"AA": N.GMAT_AA, "AD": N.GMAT_AD, "DD": N.GMAT_DD}
 SCAN_HEADER = "snp_0 snp_1 eff chi p_val"
 PAIR_HEADER = "snp_0 snp_1 eff var chi p"
-N_SLICE = 3
+N_SLICE = 3  # slices kept; each scan uses 2 or 3 (gmat_epi_scan n_slice=0)
 
 
 class EpiPlan:
@@ -38,14 +38,14 @@ class EpiPlan:
                 "gmat_epi_create")
         self._h = h
 
-    def scan(self, kind, rows, p_cut):
+    def scan(self, kind, rows, p_cut, n_slice=0):
         """Hits (i, j, eff, var, chi, p) with p < p_cut over first-SNP rows `rows`
         (strictly increasing), sorted by (i, j)."""
         rows = N.i64(rows)
         n_hits = ctypes.c_int64()
         chi_cut = float(chi2.isf(p_cut, 1)) if p_cut < 1 else 0.0
         N.check(self._lib.gmat_epi_scan(self._h, KINDS[kind], N.ptr(rows), rows.size, float(p_cut), chi_cut,
-                                        ctypes.byref(n_hits)), "gmat_epi_scan")
+                                        int(n_slice), ctypes.byref(n_hits)), "gmat_epi_scan")
         k = n_hits.value
         out = [np.zeros(k, np.int64), np.zeros(k, np.int64)] + [np.zeros(k) for _ in range(4)]
         N.check(self._lib.gmat_epi_hits(self._h, k, *[N.ptr(a) for a in out]), "gmat_epi_hits")
@@ -60,9 +60,10 @@ class EpiPlan:
         return tuple(out)
 
     def stats(self):
-        s = np.zeros(8)
+        s = np.zeros(10)
         N.check(self._lib.gmat_epi_stats(self._h, N.ptr(s)), "gmat_epi_stats")
-        keys = ("pairs", "candidates", "int8_ops", "screen_s", "refine_s", "side_s", "total_s", "launches")
+        keys = ("pairs", "candidates", "int8_ops", "screen_s", "refine_s", "side_s", "total_s", "launches",
+                "n_slice", "bound_coef")
         return dict(zip(keys, s.tolist()))
 
     def close(self):

@@ -84,14 +84,16 @@ int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, cons
 /* ---------------------------------------------------------------- epistasis scans
  * A scan plan keeps the genotype panel, P (= Z'PZ) and Py resident in HBM. */
 typedef struct gmat_epi gmat_epi;
+/* n_slice (2..4): int8 slices of P kept for the screen (see gmat_epi_scan). */
 int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice);
 /* Exhaustive exact scan over first-SNP rows `rows` (sorted ascending): AA/DD test pairs
  * (i, j>i) (remma_epiAA.py:71-82, remma_epiDD.py:75-86), AD tests (i, all j) including i==j
  * (remma_epiAD.py:76-87).  A pair is a hit when p < p_cut with p = chi2.sf(eff^2/var, 1);
- * chi_cut must be chi2.isf(p_cut, 1).  *n_hits receives the number of hits, retrieved with
- * gmat_epi_hits (sorted by (i, j)). */
+ * chi_cut must be chi2.isf(p_cut, 1).  n_slice: slices the screen uses (0 = automatic: 2 for
+ * p_cut <= 1e-4, else all); the hit set does not depend on it.  *n_hits receives the number
+ * of hits, retrieved with gmat_epi_hits (sorted by (i, j)). */
 int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
-                  int64_t *n_hits);
+                  int n_slice, int64_t *n_hits);
 int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,
                   double *p);
 /* Exact statistics of an explicit pair list (remma_epiAA_pair.py:79-84 and siblings). */
@@ -99,8 +101,8 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
                    double *chi, double *p);
 /* counters of the last scan: [0] pairs tested, [1] candidates refined, [2] int8 MFMA ops,
  * [3] screen kernel seconds, [4] refine kernel seconds, [5] side-term kernel seconds,
- * [6] total seconds, [7] screen kernel launches */
-int gmat_epi_stats(const gmat_epi *e, double *out8);
+ * [6] total seconds, [7] screen kernel launches, [8] slices used, [9] bound coefficient */
+int gmat_epi_stats(const gmat_epi *e, double *out10);
 int gmat_epi_destroy(gmat_epi *e);
 
 #ifdef __cplusplus

@@ -258,6 +258,12 @@ def test_scan_deterministic_and_row_split(synth_cohort):
         again = plan.scan("AA", np.arange(m - 1), 1e-3)
         for a, b in zip(full, again):
             np.testing.assert_array_equal(a, b)
+        # the hit set does not depend on how many int8 slices the screen used
+        for ns in (2, 3):
+            forced = plan.scan("AA", np.arange(m - 1), 1e-3, n_slice=ns)
+            assert plan.stats()["n_slice"] == ns
+            for a, b in zip(full, forced):
+                np.testing.assert_array_equal(a, b)
         parts = [plan.scan("AA", np.array(sorted(parallel_rows(m, [4, k], "AA"))), 1e-3) for k in (1, 2, 3, 4)]
         cat = [np.concatenate([p[t] for p in parts]) for t in range(6)]
         order = np.lexsort((cat[1], cat[0]))
