@@ -50,6 +50,9 @@ __device__ __forceinline__ unsigned to_offset(unsigned v) { return (v << 1) + ((
 
 struct ScreenArgs {
   const int8_t *slices;
+  int64_t slices_bytes;
+  const int8_t *panels;  // dosage then heterozygote panels, one allocation
+  int64_t panels_bytes, left_off, right_off;
   int64_t n_pad;
   int n_slice;
   const int8_t *left, *right;  // panels [m][n_pad]
@@ -70,13 +73,21 @@ struct ScreenArgs {
 };
 
 // One workgroup = one tile of BI first-SNP rows x BJ second-SNP columns (256 pairs); wave w
-// owns the col tiles of rows 2w, 2w+1.  The (slice, K-block, stage) sequence of the tile is
-// one flattened software pipeline: the next stage's A band (MT rows x LK individuals of
-// A_s) and genotype chunks are fetched into registers while the current stage multiplies,
-// across K-block and slice boundaries, so no K-block starts with a load bubble.  The
-// diagonal stages' genotype chunks are also kept in a ping-pong LDS region (eI/eJ) from
-// which the K-block epilogue rebuilds its weights w[row] without touching global memory.
+// owns the col tiles of rows 2w, 2w+1 (4 row tiles x 2 col tiles of 32 x 32).
+// Loop nest per tile: slice s -> K-block (MT rows of A_s) -> stage pairs (2 x LK individuals,
+// static LDS double-buffer parity).  The next stage's A band and genotype chunks are fetched
+// with buffer loads (per-lane constant voffset, scalar soffset) while the current stage
+// multiplies, including across K-block and slice boundaries.  The diagonal stage pair is
+// peeled: its MFMAs start from a zero C operand and its genotype chunks are also kept in a
+// ping-pong LDS region (eI/eJ) from which the K-block epilogue rebuilds w[row].
 constexpr int EP = MT + 16;  // epilogue-region pitch (128 individuals + pad)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
+  const uint64_t b = (uint64_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)nb, 0x00020000);
+}
 
 __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t sA[2][MT * AP];
@@ -87,8 +98,11 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
   const int64_t J0 = (int64_t)J * BJ;
-  const int64_t n_pad = a.n_pad;
-  const int nK = (int)(n_pad / MT);
+  const int n_pad = (int)a.n_pad;
+  const int nK = n_pad / MT;
+  const int nn = n_pad * n_pad;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(a.slices, a.slices_bytes);
+  const __amdgpu_buffer_rsrc_t rsP = make_rsrc(a.panels, a.panels_bytes);
 
   int64_t ti[2];
 #pragma unroll
@@ -98,30 +112,31 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   }
   // staging roles: two 16-byte A chunks per thread, one genotype chunk for tid < 160
   const int arow0 = tid >> 2, acol0 = (tid & 3) * 16, arow1 = (tid + 256) >> 2;
+  const int voffA0 = arow0 * n_pad + acol0, voffA1 = arow1 * n_pad + acol0;
   int prow = 0, pcol = 0, pside = 0;  // 1 = i-panel (offset coded), 2 = j-panel
-  const int8_t *psrc = nullptr;
+  unsigned voffP = 0xFFFFFFF0u;       // out of range -> the buffer load returns zeros
   if (tid < 32) {
     pside = 1;
     prow = tid >> 2;
     pcol = (tid & 3) * 16;
     const int r = roff + prow;
-    if (r < a.n_rows) psrc = a.left + a.rows[r] * n_pad + pcol;
+    if (r < a.n_rows) voffP = (unsigned)(a.left_off + a.rows[r] * n_pad + pcol);
   } else if (tid < 160) {
     pside = 2;
     prow = (tid - 32) >> 2;
     pcol = ((tid - 32) & 3) * 16;
-    if (J0 + prow < a.m) psrc = a.right + (J0 + prow) * n_pad + pcol;
+    if (J0 + prow < a.m) voffP = (unsigned)(a.right_off + (J0 + prow) * n_pad + pcol);
   }
 
   v4i ra0, ra1, rp = {0, 0, 0, 0};
-  auto load = [&](int s, int kb, int st) {
-    const int64_t K = (int64_t)kb * MT, L = K + (int64_t)st * LK;
-    const int8_t *As = a.slices + (int64_t)s * n_pad * n_pad + L + acol0;
-    ra0 = *(const v4i *)&As[(K + arow0) * n_pad];
-    ra1 = *(const v4i *)&As[(K + arow1) * n_pad];
-    if (psrc) rp = *(const v4i *)&psrc[L];
+  // fetch stage (A band at scalar byte offset soffA, genotype chunk at individual L)
+  auto load = [&](int soffA, int L) {
+    ra0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA0, soffA, 0);
+    ra1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA1, soffA, 0);
+    if (pside) rp = __builtin_amdgcn_raw_buffer_load_b128(rsP, voffP, L, 0);
   };
-  auto store = [&](int b, int st, int region) {
+  // write the fetched stage into buffer b; epi >= 0: also into epilogue region at column epi
+  auto store = [&](int b, int epi, int region) {
     *(v4i *)&sA[b][arow0 * AP + acol0] = ra0;
     *(v4i *)&sA[b][arow1 * AP + acol0] = ra1;
     if (pside == 1) {
@@ -129,96 +144,124 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
       *(v4i *)&sI[b][prow * AP + pcol] = o;
-      if (st < MT / LK) *(v4i *)&eI[region][prow * EP + st * LK + pcol] = o;
+      if (epi >= 0) *(v4i *)&eI[region][prow * EP + epi + pcol] = o;
     } else if (pside == 2) {
       *(v4i *)&sJ[b][prow * AP + pcol] = rp;
-      if (st < MT / LK) *(v4i *)&eJ[region][prow * EP + st * LK + pcol] = rp;
+      if (epi >= 0) *(v4i *)&eJ[region][prow * EP + epi + pcol] = rp;
     }
   };
 
   v16i acc[4][2];
+  // one 32-deep k-step on buffer b: B fragments w = a_i*b_j generated from the staged
+  // genotype chunks, A fragments from the staged band
+  auto kstep = [&](int b, int kk, bool diag, bool zero) {
+    const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
+    v4i fb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const v4i o = *(const v4i *)&sI[b][(2 * w + t) * AP + kk * 32 + 16 * h];
+      const v4i v = *(const v4i *)&sJ[b][c * AP + kk * 32 + 16 * h];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
+    }
+    const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const v4i fa = *(const v4i *)&sA[b][(r * 32 + c) * AP + kk * 32 + 16 * h];
+      acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], zero ? z : acc[r][0], 0, 0, 0);
+      acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], zero ? z : acc[r][1], 0, 0, 0);
+    }
+  };
+
   int64_t tot[2] = {0, 0};
   unsigned sw[2] = {0, 0};
-  int s = 0, kb = 0, st = 0, gk = 0, cur = 0;
-  load(0, 0, 0);
-  store(0, 0, 0);
-  __syncthreads();
-  for (;;) {
-    const int64_t K = (int64_t)kb * MT, L = K + (int64_t)st * LK;
-    const int last_st = (int)((n_pad - K) / LK) - 1;
-    // coordinates of the next stage
-    int ns = s, nkb = kb, nst = st + 1;
-    if (st == last_st) {
-      nst = 0;
-      if (++nkb == nK) {
-        nkb = 0;
-        ++ns;
-      }
-    }
-    const bool has_next = ns < a.n_slice;
-    if (has_next) load(ns, nkb, nst);
-    // one 32-deep k-step: B fragments w = a_i*b_j generated from the staged genotype chunks,
-    // A fragments read from the staged band; `zero` starts a K-block (C operand 0, no reset)
-    auto kstep = [&](int kk, bool zero) {
-      const bool diag = (L + kk * 32) < (K + MT);
-      const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
-      v4i fb[2];
+  // epilogue: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage slot 16h+e of
+  // each 32-row tile, whose genotype bytes sit in the LDS epilogue region (24-bit products:
+  // |acc| <= 127 * 8 * n_pad < 2^23 for n_pad <= 8192)
+  auto epilogue = [&](int region, int shift, bool first_slice) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const v4i o = *(const v4i *)&sI[cur][(2 * w + t) * AP + kk * 32 + 16 * h];
-        const v4i v = *(const v4i *)&sJ[cur][c * AP + kk * 32 + 16 * h];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
-      }
-      const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < 2; ++t) {
+      int64_t part64 = 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const v4i fa = *(const v4i *)&sA[cur][(r * 32 + c) * AP + kk * 32 + 16 * h];
-        acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], zero ? z : acc[r][0], 0, 0, 0);
-        acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], zero ? z : acc[r][1], 0, 0, 0);
-      }
-    };
-    if (st == 0) {
-      kstep(0, true);
+        const v4i o = *(const v4i *)&eI[region][(2 * w + t) * EP + r * 32 + 16 * h];
+        const v4i v = *(const v4i *)&eJ[region][c * EP + r * 32 + 16 * h];
+        int part = 0;
 #pragma unroll
-      for (int kk = 1; kk < LK / 32; ++kk) kstep(kk, false);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < LK / 32; ++kk) kstep(kk, false);
-    }
-    if (st == last_st) {
-      // epilogue: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage slot
-      // 16h+e of each 32-row tile, whose genotype bytes sit in the LDS epilogue region
-      const int reg = gk & 1;
-      const int shift = 7 * (a.n_slice - 1 - s);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        int64_t part64 = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const v4i o = *(const v4i *)&eI[reg][(2 * w + t) * EP + r * 32 + 16 * h];
-          const v4i v = *(const v4i *)&eJ[reg][c * EP + r * 32 + 16 * h];
-          int part = 0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const unsigned wb = __builtin_amdgcn_perm(T_HI, T_LO, (unsigned)o[q] + (unsigned)v[q]);
-            part += (int)(wb & 0xff) * acc[r][t][4 * q] + (int)((wb >> 8) & 0xff) * acc[r][t][4 * q + 1] +
-                    (int)((wb >> 16) & 0xff) * acc[r][t][4 * q + 2] + (int)(wb >> 24) * acc[r][t][4 * q + 3];
-            if (s == 0) sw[t] = __builtin_amdgcn_udot4(wb, wb, sw[t], false);  // sum w^2
-          }
-          part64 += part;
+        for (int q = 0; q < 4; ++q) {
+          const unsigned wb = __builtin_amdgcn_perm(T_HI, T_LO, (unsigned)o[q] + (unsigned)v[q]);
+          part += __mul24((int)(wb & 0xff), acc[r][t][4 * q]) + __mul24((int)((wb >> 8) & 0xff), acc[r][t][4 * q + 1]) +
+                  __mul24((int)((wb >> 16) & 0xff), acc[r][t][4 * q + 2]) + __mul24((int)(wb >> 24), acc[r][t][4 * q + 3]);
+          if (first_slice) sw[t] = __builtin_amdgcn_udot4(wb, wb, sw[t], false);  // sum w^2
         }
-        tot[t] += part64 * (int64_t)(1LL << shift);
+        part64 += part;
       }
-      ++gk;
+      tot[t] += (int64_t)((uint64_t)part64 << shift);
     }
-    if (!has_next) break;
-    store(cur ^ 1, nst, gk & 1);
-    __syncthreads();
-    cur ^= 1;
-    s = ns;
-    kb = nkb;
-    st = nst;
+  };
+
+  int gk = 0;  // K-blocks done (epilogue region parity)
+  load(0, 0);
+  store(0, 0, 0);
+  __syncthreads();
+  for (int s = 0; s < a.n_slice; ++s) {
+    const int shift = 7 * (a.n_slice - 1 - s);
+    for (int kb = 0; kb < nK; ++kb) {
+      const int K = kb * MT;
+      const int row0 = s * nn + K * n_pad;  // byte offset of row K of A_s
+      const int nst = 2 * (nK - kb);
+      int nxtA = -1, nxtL = 0;  // first stage of the next K-block (or slice)
+      if (kb + 1 < nK) {
+        nxtA = row0 + MT * n_pad + K + MT;
+        nxtL = K + MT;
+      } else if (s + 1 < a.n_slice) {
+        nxtA = (s + 1) * nn;
+        nxtL = 0;
+      }
+      // diagonal pair (stages 0, 1): table T, zero C, epilogue region fill
+      {
+        load(row0 + K + LK, K + LK);
+        kstep(0, 0, true, true);
+        kstep(0, 1, true, false);
+        store(1, LK, gk & 1);
+        __syncthreads();
+        const bool last = (nst == 2);
+        if (!last) load(row0 + K + 2 * LK, K + 2 * LK);
+        else if (nxtA >= 0) load(nxtA, nxtL);
+        kstep(1, 0, true, false);
+        kstep(1, 1, true, false);
+        if (last) {
+          epilogue(gk & 1, shift, s == 0);
+          ++gk;
+          if (nxtA >= 0) store(0, 0, gk & 1);
+        } else {
+          store(0, -1, 0);
+        }
+        __syncthreads();
+      }
+      // off-diagonal pairs: table 2T
+      for (int st = 2; st < nst; st += 2) {
+        const int L0 = K + st * LK;
+        load(row0 + L0 + LK, L0 + LK);
+        kstep(0, 0, false, false);
+        kstep(0, 1, false, false);
+        store(1, -1, 0);
+        __syncthreads();
+        const bool last = (st + 2 == nst);
+        if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
+        else if (nxtA >= 0) load(nxtA, nxtL);
+        kstep(1, 0, false, false);
+        kstep(1, 1, false, false);
+        if (last) {
+          epilogue(gk & 1, shift, s == 0);
+          ++gk;
+          if (nxtA >= 0) store(0, 0, gk & 1);
+        } else {
+          store(0, -1, 0);
+        }
+        __syncthreads();
+      }
+    }
   }
   // combine the two lane halves (disjoint rows of the same column), then test
 #pragma unroll
@@ -547,7 +590,7 @@ int build_coding(gmat_epi *e, int which) {
   Coding &cd = e->code[which];
   if (cd.ready) return GMAT_OK;
   const int64_t m = e->m, n_pad = e->n_pad, n = e->n;
-  const int8_t *panel = which == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int8_t *panel = which == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   // centring offsets exactly as the reference: freq = sum/(2n); A: 2*freq, D: 2*freq*(1-freq)
   std::vector<double> off(m);
   std::vector<uint8_t> mono(m);
@@ -605,6 +648,8 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
   GMAT_CHECK(n_slice >= 2 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 2..4");
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
+  GMAT_CHECK(g->n_pad <= 8192 && 2 * g->m * g->n_pad < (1LL << 32), GMAT_E_ARG,
+             "gmat_epi_create: supports n_id <= 8192 and 2 * n_snp * n_pad < 2^32 (32-bit buffer offsets)");
   auto *e = new gmat_epi();
   e->g = g;
   e->n = g->n;
@@ -706,8 +751,8 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
     GMAT_CHECK(hi[t] >= 0 && hi[t] < e->m && hj[t] >= 0 && hj[t] < e->m, GMAT_E_ARG, "pair %lld out of range",
                (long long)t);
   }
-  const int8_t *lp = lc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
-  const int8_t *rp = rc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int64_t chunk = 1 << 16;
   DBuf di, dj, de, dv, dc, dpv;
   GMAT_TRY(di.alloc(chunk * 8));
@@ -745,8 +790,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_TRY(build_coding(e, lc));
   GMAT_TRY(build_coding(e, rc));
   const Coding &L = e->code[lc], &R = e->code[rc];
-  const int8_t *lp = lc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
-  const int8_t *rp = rc == 0 ? e->g->dose.as<int8_t>() : e->g->het.as<int8_t>();
+  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int tri = (kind != GMAT_AD);
   for (double &v : e->stats) v = 0.0;
   e->hit_i.clear();
@@ -861,6 +906,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipEventRecord(ev[1], e->s));
     ScreenArgs sa;
     sa.slices = e->slices.as<int8_t>();
+    sa.slices_bytes = (int64_t)e->n_slice * n_pad * n_pad;
+    sa.panels = e->g->panels.as<int8_t>();
+    sa.panels_bytes = 2 * m * n_pad;
+    sa.left_off = lc == 0 ? 0 : m * n_pad;
+    sa.right_off = rc == 0 ? 0 : m * n_pad;
     sa.n_pad = n_pad;
     sa.n_slice = S;
     sa.left = lp;

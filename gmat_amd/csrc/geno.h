@@ -15,8 +15,10 @@ struct gmat_geno {
   int64_t n_pad = 0;     // individuals padded to a multiple of 128 (zero genotypes)
   int64_t nb = 0;        // packed bytes per SNP (ceil(n/4))
   gmat::DBuf packed;     // m * nb, PLINK order
-  gmat::DBuf dose;       // int8 [m][n_pad], dosage 0/1/2 (missing stored as 0), permuted individuals
-  gmat::DBuf het;        // int8 [m][n_pad], heterozygote indicator, permuted individuals
+  gmat::DBuf panels;     // int8 [2][m][n_pad]: dosage 0/1/2 (missing stored as 0), then the
+                         // heterozygote indicator; individuals in storage order
+  int8_t *dose_ptr() const { return panels.as<int8_t>(); }
+  int8_t *het_ptr() const { return panels.as<int8_t>() + m * n_pad; }
   std::vector<int64_t> sum_dose, n_het, n_miss;
   int64_t total_missing = 0;
 };

@@ -171,8 +171,7 @@ extern "C" int gmat_geno_create(gmat_geno **out, const uint8_t *bed_body, int64_
   g->nb = nb;
   g->n_pad = round_up(n_id, 128);
   int rc = g->packed.alloc(nb * n_snp);
-  if (rc == GMAT_OK) rc = g->dose.alloc(g->n_pad * n_snp);
-  if (rc == GMAT_OK) rc = g->het.alloc(g->n_pad * n_snp);
+  if (rc == GMAT_OK) rc = g->panels.alloc(2 * g->n_pad * n_snp);
   DBuf cnt;
   if (rc == GMAT_OK) rc = cnt.alloc(3 * n_snp * sizeof(int64_t));
   if (rc != GMAT_OK) {
@@ -182,7 +181,7 @@ extern "C" int gmat_geno_create(gmat_geno **out, const uint8_t *bed_body, int64_
   hipError_t e = hipMemcpy(g->packed.p, bed_body, nb * n_snp, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(decode_kernel, dim3((unsigned)n_snp), dim3(256), 0, 0, g->packed.as<uint8_t>(), nb, n_id,
-                       g->n_pad, g->dose.as<int8_t>(), g->het.as<int8_t>(), cnt.as<int64_t>());
+                       g->n_pad, g->dose_ptr(), g->het_ptr(), cnt.as<int64_t>());
     e = hipGetLastError();
   }
   std::vector<int64_t> h(3 * n_snp);
