@@ -89,6 +89,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, in
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)nb, 0x00020000);
 }
 
+// VAR selects tuning variants for in-process A/B runs (GMAT_SCREEN_VARIANT):
+//   bit 0: staging lane map (0 = 4 lanes per row, 1 = 8 rows per 8-lane group)
+//   bit 1: s_setprio(1) around the MFMA clusters
+template <int VAR>
 __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t sA[2][MT * AP];
   __shared__ __attribute__((aligned(16))) int8_t sI[2][BI * AP];
@@ -111,50 +115,58 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
   }
   // staging roles: two 16-byte A chunks per thread, one genotype chunk for tid < 160
-  const int arow0 = tid >> 2, acol0 = (tid & 3) * 16, arow1 = (tid + 256) >> 2;
+  // staging lanes: each group of 8 consecutive lanes writes 8 different rows at one 16-byte
+  // column (conflict-free ds_write_b128 with the 80-byte pitch) and 4 such groups read 8
+  // rows x 64 contiguous bytes from global memory
+  const int arow0 = (VAR & 1) ? (lane & 7) + 8 * (lane >> 5) + 16 * w : tid >> 2;
+  const int acol0 = (VAR & 1) ? ((lane >> 3) & 3) * 16 : (tid & 3) * 16;
+  const int arow1 = arow0 + 64;
   const int voffA0 = arow0 * n_pad + acol0, voffA1 = arow1 * n_pad + acol0;
   int prow = 0, pcol = 0, pside = 0;  // 1 = i-panel (offset coded), 2 = j-panel
   unsigned voffP = 0xFFFFFFF0u;       // out of range -> the buffer load returns zeros
   if (tid < 32) {
     pside = 1;
-    prow = tid >> 2;
-    pcol = (tid & 3) * 16;
+    prow = (VAR & 1) ? tid & 7 : tid >> 2;
+    pcol = (VAR & 1) ? ((tid >> 3) & 3) * 16 : (tid & 3) * 16;
     const int r = roff + prow;
     if (r < a.n_rows) voffP = (unsigned)(a.left_off + a.rows[r] * n_pad + pcol);
   } else if (tid < 160) {
     pside = 2;
-    prow = (tid - 32) >> 2;
-    pcol = ((tid - 32) & 3) * 16;
+    const int u = tid - 32;
+    prow = (VAR & 1) ? (u & 7) + 8 * (u >> 5) : u >> 2;
+    pcol = (VAR & 1) ? ((u >> 3) & 3) * 16 : (u & 3) * 16;
     if (J0 + prow < a.m) voffP = (unsigned)(a.right_off + (J0 + prow) * n_pad + pcol);
   }
 
   v4i ra0, ra1, rp = {0, 0, 0, 0};
   // fetch stage (A band at scalar byte offset soffA, genotype chunk at individual L)
-  auto load = [&](int soffA, int L) {
+  auto load = [&](int soffA, int L) __attribute__((always_inline)) {
     ra0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA0, soffA, 0);
     ra1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA1, soffA, 0);
     if (pside) rp = __builtin_amdgcn_raw_buffer_load_b128(rsP, voffP, L, 0);
   };
   // write the fetched stage into buffer b; epi >= 0: also into epilogue region at column epi
-  auto store = [&](int b, int epi, int region) {
-    *(v4i *)&sA[b][arow0 * AP + acol0] = ra0;
-    *(v4i *)&sA[b][arow1 * AP + acol0] = ra1;
+  auto store_set = [&](int b, int epi, int region, const v4i &x0, const v4i &x1, const v4i &xp)
+                       __attribute__((always_inline)) {
+    *(v4i *)&sA[b][arow0 * AP + acol0] = x0;
+    *(v4i *)&sA[b][arow1 * AP + acol0] = x1;
     if (pside == 1) {
       v4i o;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
+      for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)xp[q]);
       *(v4i *)&sI[b][prow * AP + pcol] = o;
       if (epi >= 0) *(v4i *)&eI[region][prow * EP + epi + pcol] = o;
     } else if (pside == 2) {
-      *(v4i *)&sJ[b][prow * AP + pcol] = rp;
-      if (epi >= 0) *(v4i *)&eJ[region][prow * EP + epi + pcol] = rp;
+      *(v4i *)&sJ[b][prow * AP + pcol] = xp;
+      if (epi >= 0) *(v4i *)&eJ[region][prow * EP + epi + pcol] = xp;
     }
   };
+  auto store = [&](int b, int epi, int region) __attribute__((always_inline)) { store_set(b, epi, region, ra0, ra1, rp); };
 
   v16i acc[4][2];
   // one 32-deep k-step on buffer b: B fragments w = a_i*b_j generated from the staged
   // genotype chunks, A fragments from the staged band
-  auto kstep = [&](int b, int kk, bool diag, bool zero) {
+  auto kstep = [&](int b, int kk, bool diag, bool zero) __attribute__((always_inline)) {
     const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
     v4i fb[2];
 #pragma unroll
@@ -165,12 +177,14 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
       for (int q = 0; q < 4; ++q) fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
     }
     const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (VAR & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const v4i fa = *(const v4i *)&sA[b][(r * 32 + c) * AP + kk * 32 + 16 * h];
       acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], zero ? z : acc[r][0], 0, 0, 0);
       acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], zero ? z : acc[r][1], 0, 0, 0);
     }
+    if (VAR & 2) __builtin_amdgcn_s_setprio(0);
   };
 
   int64_t tot[2] = {0, 0};
@@ -178,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   // epilogue: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage slot 16h+e of
   // each 32-row tile, whose genotype bytes sit in the LDS epilogue region (24-bit products:
   // |acc| <= 127 * 8 * n_pad < 2^23 for n_pad <= 8192)
-  auto epilogue = [&](int region, int shift, bool first_slice) {
+  auto epilogue = [&](int region, int shift, bool first_slice) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       int64_t part64 = 0;
@@ -200,9 +214,19 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     }
   };
 
+  // second staging register set for two-stage-deep prefetch (VAR & 4)
+  v4i rb0 = {0, 0, 0, 0}, rb1 = {0, 0, 0, 0}, rq = {0, 0, 0, 0};
+  auto loadB = [&](int soffA, int L) __attribute__((always_inline)) {
+    rb0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA0, soffA, 0);
+    rb1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA1, soffA, 0);
+    if (pside) rq = __builtin_amdgcn_raw_buffer_load_b128(rsP, voffP, L, 0);
+  };
+  constexpr bool DEEP = (VAR & 4) != 0;
+
   int gk = 0;  // K-blocks done (epilogue region parity)
   load(0, 0);
   store(0, 0, 0);
+  if (DEEP) loadB(LK, LK);  // stage 1 (the first K-block always has >= 2 stages)
   __syncthreads();
   for (int s = 0; s < a.n_slice; ++s) {
     const int shift = 7 * (a.n_slice - 1 - s);
@@ -218,40 +242,32 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
         nxtA = (s + 1) * nn;
         nxtL = 0;
       }
-      // diagonal pair (stages 0, 1): table T, zero C, epilogue region fill
-      {
-        load(row0 + K + LK, K + LK);
-        kstep(0, 0, true, true);
-        kstep(0, 1, true, false);
-        store(1, LK, gk & 1);
-        __syncthreads();
-        const bool last = (nst == 2);
-        if (!last) load(row0 + K + 2 * LK, K + 2 * LK);
-        else if (nxtA >= 0) load(nxtA, nxtL);
-        kstep(1, 0, true, false);
-        kstep(1, 1, true, false);
-        if (last) {
-          epilogue(gk & 1, shift, s == 0);
-          ++gk;
-          if (nxtA >= 0) store(0, 0, gk & 1);
-        } else {
-          store(0, -1, 0);
-        }
-        __syncthreads();
-      }
-      // off-diagonal pairs: table 2T
-      for (int st = 2; st < nst; st += 2) {
+      // stage pair (st, st+1): st in LDS buffer 0, st+1 in buffer 1.
+      // DEEP: set A (ra*) carries even stages, set B (rb*) odd stages, each issued two
+      // stages before its LDS store; otherwise set A carries every stage, one ahead.
+      auto pair = [&](int st, bool diag, bool zero) __attribute__((always_inline)) {
         const int L0 = K + st * LK;
-        load(row0 + L0 + LK, L0 + LK);
-        kstep(0, 0, false, false);
-        kstep(0, 1, false, false);
-        store(1, -1, 0);
-        __syncthreads();
         const bool last = (st + 2 == nst);
-        if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
-        else if (nxtA >= 0) load(nxtA, nxtL);
-        kstep(1, 0, false, false);
-        kstep(1, 1, false, false);
+        if (DEEP) {
+          if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
+          else if (nxtA >= 0) load(nxtA, nxtL);
+        } else {
+          load(row0 + L0 + LK, L0 + LK);
+        }
+        kstep(0, 0, diag, zero);
+        kstep(0, 1, diag, false);
+        if (DEEP) store_set(1, (st + 1 < 2) ? (st + 1) * LK : -1, gk & 1, rb0, rb1, rq);
+        else store(1, (st + 1 < 2) ? (st + 1) * LK : -1, gk & 1);
+        __syncthreads();
+        if (DEEP) {
+          if (!last) loadB(row0 + L0 + 3 * LK, L0 + 3 * LK);
+          else if (nxtA >= 0) loadB(nxtA + LK, nxtL + LK);
+        } else {
+          if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
+          else if (nxtA >= 0) load(nxtA, nxtL);
+        }
+        kstep(1, 0, diag, false);
+        kstep(1, 1, diag, false);
         if (last) {
           epilogue(gk & 1, shift, s == 0);
           ++gk;
@@ -260,7 +276,10 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
           store(0, -1, 0);
         }
         __syncthreads();
-      }
+      };
+      pair(0, true, true);
+#pragma unroll 1
+      for (int st = 2; st < nst; st += 2) pair(st, false, false);
     }
   }
   // combine the two lane halves (disjoint rows of the same column), then test
@@ -793,6 +812,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int tri = (kind != GMAT_AD);
+  const char *venv = getenv("GMAT_SCREEN_VARIANT");
+  const int variant = venv ? atoi(venv) : 0;
   for (double &v : e->stats) v = 0.0;
   e->hit_i.clear();
   e->hit_j.clear();
@@ -945,7 +966,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cand_j = e->cand_j.as<int64_t>();
     unsigned long long count = 0;
     for (int attempt = 0;; ++attempt) {
-      hipLaunchKernelGGL(screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa);
+      switch (variant) {
+        case 0: hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        case 1: hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        case 2: hipLaunchKernelGGL(screen_kernel<2>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        case 3: hipLaunchKernelGGL(screen_kernel<3>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        case 4: hipLaunchKernelGGL(screen_kernel<4>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        default: hipLaunchKernelGGL(screen_kernel<5>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+      }
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ev[2], e->s));
       GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, e->s));
