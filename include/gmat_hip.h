@@ -105,6 +105,25 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
 int gmat_epi_stats(const gmat_epi *e, double *out10);
 int gmat_epi_destroy(gmat_epi *e);
 
+/* ---- effect-only screen (the approximate pipeline's first pass) ----
+ * Replaces the OpenMP row loops of _remma_epi_eff_cpu.c (AA :61-137, AA maf :141-219,
+ * AD :226-314, AD maf :318-410, DD :415-496, DD maf :500-574).  eff(i, j) =
+ * sum_k x_ik x_jk py_k with the reference's fp64 codings and centring (freq accumulated as
+ * the reference does, missing = 1/3) for j > i over the listed first SNPs `rows` (in list
+ * order), keeping |eff| > cut (AD: >= for (i, j), > for (j, i)).  cut = eff_cut[0] when
+ * freq_i is NULL, else eff_cut[freq_i[i]*10 + freq_j[j]] (111 entries; freq values 0..10;
+ * AA/DD pass the same array twice, AD passes freqA, freqD).  Writes out_file: header
+ * "snp_0 snp_1 eff" then "%lld %lld %g" rows (rows in list order, j ascending, AD (i, j)
+ * before (j, i)); py is Z'Py in .fam order. */
+int gmat_eff_scan(gmat_geno *g, int kind, const double *py, const int64_t *rows, int64_t n_rows,
+                  const double *eff_cut, const int64_t *freq_i, const int64_t *freq_j, const char *out_file,
+                  int64_t *n_hits);
+/* Last gmat_eff_scan on this process: pairs tested, hits, device seconds, text-writing seconds. */
+int gmat_eff_stats(double *out4);
+/* Decoded fp64 dosage (m x n, SNP-major, .fam order; (c^2+c)/6: missing = 1/3) -- the
+ * reference's read_plink_bed (_read_plink_bed.c:5-51). */
+int gmat_geno_decode(const gmat_geno *g, double *marker_mat);
+
 #ifdef __cplusplus
 }
 #endif

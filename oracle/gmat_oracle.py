@@ -268,11 +268,12 @@ def annotation_snp_pos(res_lines, bim_lines, p_cut=1, dis=0):
     return out
 
 
-def epi_eff_screen(kind, snp_mat_dec, py, rows, eff_cut):
+def epi_eff_screen(kind, snp_mat_dec, py, rows, eff_cut, freq_i=None, freq_j=None):
     """Effect-only screen of the C kernel (_remma_epi_eff_cpu.c:61-137 AA, :226-314 AD,
     :415-491 DD) on a decoded (n_snp, n_id) matrix (missing = 1/3 kept, as the C code does).
     Returns a sorted list of (i, j, eff) with the reference's thresholds (AD: >= for (i,j),
-    > for (j,i))."""
+    > for (j,i)).  With freq_i / freq_j (the _maf forms, :141-166, :318-348, :500-522) the
+    threshold of (i, j) is eff_cut[freq_i[i]*10 + freq_j[j]] for both AD orientations."""
     m, n = snp_mat_dec.shape
     g = snp_mat_dec
     pf = np.zeros(m)
@@ -285,9 +286,11 @@ def epi_eff_screen(kind, snp_mat_dec, py, rows, eff_cut):
     h = np.where(np.abs(g - 2.0) < 0.0001, 0.0, g)
     d = h - (2 * pf * (1 - pf))[:, None]
     py = np.asarray(py, dtype=float).reshape(-1)
+    table = np.asarray(eff_cut, dtype=float).reshape(-1)
     out = []
     for i in rows:
         js = np.arange(i + 1, m)
+        eff_cut = table[np.asarray(freq_i)[i] * 10 + np.asarray(freq_j)[js]] if freq_i is not None else table[0]
         if kind == "AA":
             eff = (a[js] * a[i]) @ py
             keep = np.abs(eff) > eff_cut
@@ -305,3 +308,47 @@ def epi_eff_screen(kind, snp_mat_dec, py, rows, eff_cut):
             out += [(j, i, e) for j, e in zip(js[k2], e2[k2])]
     out.sort(key=lambda t: (t[0], t[1]))
     return out
+
+
+def maf_classes(kind, snp_mat):
+    """Frequency classes of the _maf_approx pipelines from the (n, m) dosage matrix:
+    AA minor-allele frequency (remma_epiAA_maf_approx.py:38-41), DD heterozygosity
+    (remma_epiDD_maf_approx.py:39-44), AD both (remma_epiAD_maf_approx.py:39-50).
+    Returns (freq_i, freq_j) as int64 class arrays (value*20 truncated)."""
+    n = snp_mat.shape[0]
+    if kind == "AA":
+        f = 1 - np.sum(snp_mat, axis=0) / (2 * n)
+        f[f > 0.5] = 1 - f[f > 0.5]
+        c = np.array(list(map(np.longlong, f * 20)), dtype=np.int64)
+        return c, c
+    h = np.sum(np.absolute(snp_mat - 1.0) < 0.001, axis=0) / n
+    h[h > 0.5] = 1 - h[h > 0.5]
+    hc = np.array(h * 20, dtype=np.int64)
+    if kind == "DD":
+        return hc, hc
+    a = np.sum(snp_mat, axis=0) / (2 * n)
+    a[a > 0.5] = 1 - a[a > 0.5]
+    return np.array(a * 20, dtype=np.int64), hc
+
+
+def class_denominators(kind, random_rows, freq_i, freq_j):
+    """Per-class mean exact variance of random pairs (remma_epiAA_maf_approx.py:43-71; AD
+    one orientation, remma_epiAD_maf_approx.py:51-75).  random_rows: (i, j, var) tuples in
+    file order.  Returns the 111-entry denominator table."""
+    sums, counts = {}, {}
+    for i, j, v in random_rows:
+        keys = [(freq_i[i], freq_j[j])] if kind == "AD" else [(freq_i[i], freq_i[j]), (freq_i[j], freq_i[i])]
+        for k in keys:
+            counts[k] = counts.get(k, 0) + 1
+            sums[k] = sums.get(k, 0.0) + v
+    tot, cnt = 0, 0
+    for k in counts:
+        tot += sums[k]
+        cnt += counts[k]
+        sums[k] = sums[k] / counts[k]
+    mean = tot / cnt
+    deno = np.ones(111)
+    for k1 in set(freq_i.tolist()):
+        for k2 in set(freq_j.tolist()):
+            deno[k1 * 10 + k2] = sums.get((k1, k2), mean)
+    return deno

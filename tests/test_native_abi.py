@@ -8,14 +8,16 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "gmat_hip.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("gmat_hip.h", "gmat_remma_eff.h")]
 LIB = os.path.join(REPO, "gmat_amd", "libgmat_hip.so")
 
 
 def _header_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(gmat_[a-z0-9_]+)\s*\(", txt)))
+    names = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"^(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", txt, flags=re.M))
+    return sorted(names)
 
 
 def test_library_exports_every_header_symbol():

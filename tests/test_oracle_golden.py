@@ -133,3 +133,44 @@ def test_tiny_text_outputs_md5():
         p = os.path.join(d, "k")
         np.savetxt(p, ref["agmat"])  # np.savetxt default '%.18e', as gmatrix.py:12
         assert hashlib.md5(open(p, "rb").read()).hexdigest() == meta[".agrm0"]["md5"]
+
+
+def _eff_golden(name):
+    lines = open(os.path.join(MOUSE_DATA, name)).read().splitlines()
+    rows = [l.split() for l in lines[1:]]
+    return lines[0], {(int(a[0]), int(a[1])): a[2:] for a in rows}
+
+
+@pytest.fixture(scope="module")
+def mouse_eff_inputs():
+    prefix = os.path.join(MOUSE_DATA, "plink")
+    snp = O.read_plink(prefix)
+    n, m = snp.shape
+    with open(prefix + ".bed", "rb") as f:
+        dec = O.decode_bed(f.read(), n, m)
+    a, d = O.agmat(snp), O.dgmat_as(snp)
+    y, x, col, nid = O.design_matrix(os.path.join(MOUSE_DATA, "pheno"), prefix)
+    ref = np.load(os.path.join(MOUSE_DATA, "reml.npz"))
+    py2 = O.projection(y, x, col, nid, [a, a * a], ref["var2"])[1]
+    py5 = O.projection(y, x, col, nid, [a, d, a * a, a * d, d * d], ref["var5"])[1]
+    return dec, py2, py5
+
+
+@pytest.mark.parametrize("kind,var_app", [("AA", 1470.0), ("AD", 960.0), ("DD", 490.0)])
+def test_mouse_eff_screen_golden(mouse_eff_inputs, kind, var_app):
+    """The C effect screen (_remma_epi_eff_cpu.c) and its chi_app / p_app post-processing
+    (remma_epiAA_eff.py:85-95) on mouse rows 0..199 at a fixed threshold."""
+    from scipy.stats import chi2
+    dec, py2, py5 = mouse_eff_inputs
+    cut = np.sqrt(chi2.isf(1e-2, 1) * var_app)
+    got = O.epi_eff_screen(kind, dec, py2 if kind == "AA" else py5, range(200), cut)
+    hdr, exp = _eff_golden("epi%s_eff_rows200" % kind)
+    assert hdr == "snp_0 snp_1 eff chi_app p_app"
+    got_d = {(int(i), int(j)): e for i, j, e in got}
+    assert len(exp) > 1000
+    near = {k for k, e in got_d.items() if abs(abs(e) - cut) < 1e-9 * cut}
+    assert set(got_d) - near == set(exp) - near
+    for k, cols in exp.items():
+        assert abs(float(cols[0]) - got_d[k]) <= 5e-6 * abs(got_d[k]), (k, cols[0], got_d[k])
+        chi_app = float(cols[0]) * float(cols[0]) / var_app
+        assert cols[1] == repr(chi_app) and cols[2] == repr(float(chi2.sf(chi_app, 1)))

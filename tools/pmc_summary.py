@@ -9,6 +9,7 @@ d = sys.argv[1]
 key = sys.argv[2] if len(sys.argv) > 2 else "screen"
 agg = collections.defaultdict(float)
 dur = 0.0
+launches = 0
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         if key in r["Kernel_Name"]:
@@ -17,6 +18,7 @@ for f in sorted(glob.glob(os.path.join(d, "p1", "run_kernel_trace.csv"))):
     for r in csv.DictReader(open(f)):
         if key in r["Kernel_Name"]:
             dur += (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9
+            launches += 1
 print({k: "%.4g" % v for k, v in sorted(agg.items())})
 g = agg.get("GRBM_GUI_ACTIVE", 0) / 8
 if g:
@@ -35,3 +37,14 @@ if "TCC_HIT_sum" in agg:
     print("L2 hit %.3f" % (agg["TCC_HIT_sum"] / (agg["TCC_HIT_sum"] + agg["TCC_MISS_sum"])))
 if "FETCH_SIZE" in agg:
     print("FETCH_SIZE (KB, x2 gfx950 correction) %.4g -> %.4g GB" % (agg["FETCH_SIZE"], 2 * agg["FETCH_SIZE"] * 1024 / 1e9))
+
+if len(sys.argv) > 3 and "FETCH_SIZE" in agg:
+    import json
+    fetch = 2 * agg["FETCH_SIZE"] * 1024  # KB, gfx950 wide-read correction (MI355X_MICROARCH.md:298)
+    write = agg.get("WRITE_SIZE", 0.0) * 1024
+    rec = {"kernel": key, "launches": launches, "kernel_s": dur,
+           "fetch_bytes": fetch, "write_bytes": write,
+           "hbm_bytes_per_launch": (fetch + write) / max(launches, 1),
+           "source": os.path.relpath(d), "counters": {k: v for k, v in sorted(agg.items())}}
+    json.dump(rec, open(sys.argv[3], "w"), indent=1)
+    print("wrote", sys.argv[3], "bytes/launch %.4g" % rec["hbm_bytes_per_launch"])
