@@ -341,3 +341,46 @@ extern "C" int gmat_geno_decode(const gmat_geno *g, double *marker_mat) {
   GMAT_HIP(hipMemcpy(marker_mat, out.p, g->m * g->n * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }
+
+// Single-SNP random SNP-BLUP test quantities (remma_add.py:49-60, remma_dom.py:49-62): for every
+// SNP j, x_j = additive (g - 2p) or dominance ([g != 2] g - 2p(1-p)) coding with p = sum/(2n)
+// from the exact integer dosage sums; xpy[j] = x_j' py, xpx[j] = x_j' P x_j.  Chunks of SNPs:
+// X (C x n fp64, .fam order) from the packed panel, Y = X P (fp64 MFMA dgemm), row dots.
+extern "C" int gmat_snp_test(gmat_geno *g, int kind, const double *pvp, const double *py, double *xpy,
+                             double *xpx) {
+  GMAT_CHECK(g && pvp && py && xpy && xpx, GMAT_E_ARG, "gmat_snp_test: bad arguments");
+  GMAT_CHECK(kind == GMAT_GRM_ADD || kind == GMAT_GRM_DOM, GMAT_E_ARG, "gmat_snp_test: unknown kind %d", kind);
+  GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_snp_test: panel has %lld missing genotypes (impute first)",
+             (long long)g->total_missing);
+  const int64_t n = g->n, m = g->m;
+  std::vector<double> c(m);
+  for (int64_t j = 0; j < m; ++j) {
+    const double freq = (double)g->sum_dose[j] / (double)(2 * n);
+    c[j] = kind == GMAT_GRM_ADD ? 2 * freq : 2 * freq * (1 - freq);
+  }
+  const int64_t C = std::max<int64_t>(64, std::min<int64_t>(m, (int64_t)(1ll << 26) / std::max<int64_t>(n, 1)));
+  DBuf dc, dp, dpy, x, y, o1, o2;
+  GMAT_TRY(dc.alloc(m * sizeof(double)));
+  GMAT_TRY(dp.alloc(n * n * sizeof(double)));
+  GMAT_TRY(dpy.alloc(n * sizeof(double)));
+  GMAT_TRY(x.alloc(C * n * sizeof(double)));
+  GMAT_TRY(y.alloc(C * n * sizeof(double)));
+  GMAT_TRY(o1.alloc(m * sizeof(double)));
+  GMAT_TRY(o2.alloc(m * sizeof(double)));
+  GMAT_HIP(hipMemcpy(dc.p, c.data(), m * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(dp.p, pvp, n * n * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(dpy.p, py, n * sizeof(double), hipMemcpyHostToDevice));
+  for (int64_t j0 = 0; j0 < m; j0 += C) {
+    const int64_t nc = std::min(C, m - j0);
+    hipLaunchKernelGGL(eff_x_kernel, dim3((unsigned)nc), dim3(256), 0, 0, g->packed.as<uint8_t>() + j0 * g->nb, g->nb,
+                       n, dc.as<double>() + j0, kind == GMAT_GRM_DOM ? 1 : 0, x.as<double>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_TRY(dgemm(0, nc, n, n, 1.0, DView{x.as<double>(), n, 0}, DView{dp.as<double>(), n, 0}, 0.0, y.as<double>(),
+                   n));
+    GMAT_TRY(dot_rows(0, nc, n, x.as<double>(), n, y.as<double>(), n, o2.as<double>() + j0));
+    GMAT_TRY(dot_rows(0, nc, n, x.as<double>(), n, dpy.as<double>(), 0, o1.as<double>() + j0));
+  }
+  GMAT_HIP(hipMemcpy(xpy, o1.p, m * sizeof(double), hipMemcpyDeviceToHost));
+  GMAT_HIP(hipMemcpy(xpx, o2.p, m * sizeof(double), hipMemcpyDeviceToHost));
+  return GMAT_OK;
+}

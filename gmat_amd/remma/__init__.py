@@ -8,3 +8,5 @@ from gmat_amd.remma.remma_epiAD.remma_epiAD import remma_epiAD, remma_epiAD_para
 from gmat_amd.remma.remma_epiAD.remma_epiAD_pair import remma_epiAD_pair, _remma_epiAD_pair
 from gmat_amd.remma.remma_epiDD.remma_epiDD import remma_epiDD, remma_epiDD_parallel, _remma_epiDD
 from gmat_amd.remma.remma_epiDD.remma_epiDD_pair import remma_epiDD_pair, _remma_epiDD_pair
+from gmat_amd.remma.remma_add import remma_add, _remma_add
+from gmat_amd.remma.remma_dom import remma_dom, _remma_dom

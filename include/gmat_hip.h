@@ -120,6 +120,13 @@ int gmat_eff_scan(gmat_geno *g, int kind, const double *py, const int64_t *rows,
                   int64_t *n_hits);
 /* Last gmat_eff_scan on this process: pairs tested, hits, device seconds, text-writing seconds. */
 int gmat_eff_stats(double *out4);
+/* ---- single-SNP tests (remma_add / remma_dom) ----
+ * For every SNP j of the (imputed) panel: x_j = g_j - 2p_j (kind GMAT_GRM_ADD) or
+ * [g_j != 2] g_j - 2p_j(1-p_j) (GMAT_GRM_DOM), p_j = sum/(2n); xpy[j] = x_j' py and
+ * xpx[j] = x_j' P x_j with P (pvp, n x n) and py in .fam order.  Replaces the two dense
+ * products of remma_add.py:58-59 / remma_dom.py:60-61; the scaling by var_com and the
+ * chi2 test stay on the host. */
+int gmat_snp_test(gmat_geno *g, int kind, const double *pvp, const double *py, double *xpy, double *xpx);
 /* Decoded fp64 dosage (m x n, SNP-major, .fam order; (c^2+c)/6: missing = 1/3) -- the
  * reference's read_plink_bed (_read_plink_bed.c:5-51). */
 int gmat_geno_decode(const gmat_geno *g, double *marker_mat);

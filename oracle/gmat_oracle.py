@@ -352,3 +352,26 @@ def class_denominators(kind, random_rows, freq_i, freq_j):
         for k2 in set(freq_j.tolist()):
             deno[k1 * 10 + k2] = sums.get((k1, k2), mean)
     return deno
+
+
+def remma_single(kind, snp_mat, pvp, py, sigma):
+    """Single-SNP tests: remma_add.py:49-60 (kind "add") and remma_dom.py:49-64 ("dom") on an
+    (n, m) dosage matrix without missing values.  Returns (eff, chi, eff_to_fixed, p)."""
+    n, m = snp_mat.shape
+    freq = (np.sum(snp_mat, axis=0) / (2 * n)).reshape(1, m)
+    if kind == "add":
+        x = snp_mat - 2 * freq
+        scale = np.sum(2 * freq * (1 - freq))
+    else:
+        s = 2 * freq * (1 - freq)
+        scale = np.sum(s * (1 - s))
+        x = snp_mat.copy()
+        x[x > 1.5] = 0.0
+        x = x - s
+    py = np.asarray(py, dtype=float).reshape(-1, 1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        eff = np.dot(x.T, py)[:, -1] * sigma / scale
+        var = np.sum(x * np.dot(pvp, x), axis=0) * sigma * sigma / (scale * scale)
+        fixed = eff * sigma / (var * scale)
+        chi = eff * eff / var
+    return eff, chi, fixed, chi2.sf(chi, 1)

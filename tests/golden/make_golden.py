@@ -11,6 +11,8 @@ Fixtures ("reference code + its own C decoder in fp64"):
            epiAA_pair file, parallel parts, annotation, and the C effect screen.
   tiny/    a 150 x 200 related synthetic cohort (n % 4 == 2, two monomorphic SNPs and one
            all-heterozygous SNP) with full K/D and every testable pair for AA/AD/DD.
+  both:    remma_add / remma_dom result files (``python tests/golden/make_golden.py singles``
+           regenerates only these).
 """
 import gzip
 import hashlib
@@ -176,13 +178,42 @@ def tiny(gmat, work, out):
         os.remove(path)
 
 
+def singles(gmat, work, out_mouse, out_tiny):
+    """Single-SNP tests remma_add / remma_dom (remma_add.py:15-77, remma_dom.py:15-79) on mouse
+    ([A, AxA] and the 5-GRM variances) and on tiny (monomorphic SNPs -> NaN statistics)."""
+    from gmat.gmatrix import agmat, dgmat_as
+    from gmat.remma import remma_add, remma_dom
+    for f in ("plink.bed", "plink.bim", "plink.fam", "pheno"):
+        shutil.copy(os.path.join(MOUSE, f), work)
+    bed = os.path.join(work, "plink")
+    pheno = os.path.join(work, "pheno")
+    a, _ = agmat(bed)
+    d, _ = dgmat_as(bed)
+    ref = np.load(os.path.join(out_mouse, "reml.npz"))
+    remma_add(pheno, bed, [a, a * a], ref["var2"], out_file=os.path.join(out_mouse, "remma_add"))
+    remma_dom(pheno, bed, [a, d, a * a, a * d, d * d], ref["var5"], out_file=os.path.join(out_mouse, "remma_dom"))
+    for ext in (".bed", ".bim", ".fam", ".pheno"):
+        shutil.copy(os.path.join(out_tiny, "tiny" + ext), os.path.join(work, "tiny" + ext))
+    bed = os.path.join(work, "tiny")
+    tref = np.load(os.path.join(out_tiny, "tiny_ref.npz"))
+    a, d = tref["agmat"], tref["dgmat"]
+    remma_add(bed + ".pheno", bed, [a, a * a], tref["var"], out_file=os.path.join(out_tiny, "remma_add"))
+    remma_dom(bed + ".pheno", bed, [a, d], tref["var"], out_file=os.path.join(out_tiny, "remma_dom"))
+
+
 def main():
     gmat = import_reference()
     logging.getLogger().setLevel(logging.WARNING)
-    with tempfile.TemporaryDirectory() as work:
-        tiny(gmat, work, os.path.join(HERE, "tiny"))
-    with tempfile.TemporaryDirectory() as work:
-        mouse(gmat, work, os.path.join(HERE, "mouse"))
+    what = sys.argv[1:] or ["tiny", "mouse", "singles"]
+    if "tiny" in what:
+        with tempfile.TemporaryDirectory() as work:
+            tiny(gmat, work, os.path.join(HERE, "tiny"))
+    if "mouse" in what:
+        with tempfile.TemporaryDirectory() as work:
+            mouse(gmat, work, os.path.join(HERE, "mouse"))
+    if "singles" in what:
+        with tempfile.TemporaryDirectory() as work:
+            singles(gmat, work, os.path.join(HERE, "mouse"), os.path.join(HERE, "tiny"))
     print("golden fixtures written to", HERE)
 
 

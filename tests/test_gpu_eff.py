@@ -237,3 +237,45 @@ def test_mouse_approx_pipeline(mouse, kind, maf, tmp_path):
         e_txt = float("%g" % ed[(int(a[0]), int(a[1]))])
         p_app = chi2.sf(e_txt * e_txt / den_of(int(a[0]), int(a[1])), 1)
         assert float(a[5]) == pytest.approx(float(p_app), rel=1e-9)
+
+
+def _single(path):
+    lines = open(path).read().splitlines()
+    vals = np.array([[float(v) if v else np.nan for v in l.split(" ")[5:]] for l in lines[1:]])
+    return lines, vals
+
+
+@pytest.mark.parametrize("kind", ["add", "dom"])
+def test_single_snp_golden(mouse, kind, tmp_path):
+    """remma_add / remma_dom against the reference's files on mouse and
+    tiny (monomorphic SNPs: eff 0.0 and empty NaN fields; the all-heterozygous SNP of the
+    dominance test is rounding noise of an exact zero in the reference and is only checked
+    for eff ~ 0)."""
+    import gmat_amd.remma as R
+    fn = R.remma_add if kind == "add" else R.remma_dom
+    prefix, g2, g5, var2, var5 = mouse
+    out = str(tmp_path / "m")
+    df = fn(prefix.replace("plink", "pheno"), prefix, g2 if kind == "add" else g5, var2 if kind == "add" else var5,
+            out_file=out)
+    gl, gv = _single(out)
+    el, ev = _single(os.path.join(MOUSE, "remma_" + kind))
+    assert len(gl) == len(el) and gl[0] == el[0]
+    assert [l.split(" ")[:5] for l in gl] == [l.split(" ")[:5] for l in el]
+    np.testing.assert_allclose(gv, ev, rtol=1e-8, atol=1e-14)
+    assert df.shape == (len(gl) - 1, 9)
+    # tiny
+    d = tmp_path / "tiny"
+    d.mkdir()
+    for ext in (".bed", ".bim", ".fam", ".pheno"):
+        shutil.copy(os.path.join(GOLD, "tiny", "tiny" + ext), str(d))
+    tp = str(d / "tiny")
+    ref = np.load(os.path.join(GOLD, "tiny", "tiny_ref.npz"))
+    a, dm = ref["agmat"], ref["dgmat"]
+    fn(tp + ".pheno", tp, [a, a * a] if kind == "add" else [a, dm], ref["var"], out_file=tp + ".out")
+    gl, gv = _single(tp + ".out")
+    el, ev = _single(os.path.join(GOLD, "tiny", "remma_" + kind))
+    assert [l.split(" ")[:5] for l in gl] == [l.split(" ")[:5] for l in el]
+    noise = np.abs(ev[:, 0]) < 1e-12
+    assert np.all(np.abs(gv[noise, 0]) < 1e-12)
+    np.testing.assert_array_equal(np.isnan(gv[~noise]), np.isnan(ev[~noise]))
+    np.testing.assert_allclose(gv[~noise], ev[~noise], rtol=1e-8, atol=1e-14)

@@ -174,3 +174,43 @@ def test_mouse_eff_screen_golden(mouse_eff_inputs, kind, var_app):
         assert abs(float(cols[0]) - got_d[k]) <= 5e-6 * abs(got_d[k]), (k, cols[0], got_d[k])
         chi_app = float(cols[0]) * float(cols[0]) / var_app
         assert cols[1] == repr(chi_app) and cols[2] == repr(float(chi2.sf(chi_app, 1)))
+
+
+def _single_golden(path):
+    lines = open(path).read().splitlines()
+    assert lines[0] == "chro snp_ID pos allele1 allele2 eff_val chi_val eff_val_to_fixed p_val"
+    vals = np.array([[float(v) if v else np.nan for v in (l.split(" ")[5:])] for l in lines[1:]])
+    return lines, vals
+
+
+@pytest.mark.parametrize("kind", ["add", "dom"])
+def test_single_snp_golden(kind, tiny, mouse_eff_inputs):
+    """remma_add / remma_dom restatement vs the reference's files (tiny: monomorphic SNPs give
+    NaN statistics; the all-heterozygous SNP's dominance coding is a constant, so its numbers
+    are rounding noise of an exact zero and only eff ~ 0 is checked)."""
+    snp, ref, (y, x, col, nid) = tiny
+    a, d = ref["agmat"], ref["dgmat"]
+    g = [a, a * a] if kind == "add" else [a, d]
+    pvp, py = O.projection(y, x, col, nid, g, ref["var"])
+    sigma = ref["var"][0 if kind == "add" else 1]
+    got = np.column_stack(O.remma_single(kind, snp, pvp, py, sigma))
+    _, exp = _single_golden(os.path.join(TINY, "remma_" + kind))
+    noise = np.abs(got[:, 0]) < 1e-12
+    np.testing.assert_array_equal(np.isnan(got[~noise]), np.isnan(exp[~noise]))
+    np.testing.assert_allclose(got[~noise], exp[~noise], rtol=1e-8, atol=1e-14)
+    assert np.all(np.abs(exp[noise, 0]) < 1e-12)
+    # mouse
+    prefix = os.path.join(MOUSE_DATA, "plink")
+    msnp = O.read_plink(prefix)
+    ma, md = O.agmat(msnp), O.dgmat_as(msnp)
+    my, mx, mcol, mnid = O.design_matrix(os.path.join(MOUSE_DATA, "pheno"), prefix)
+    r = np.load(os.path.join(MOUSE_DATA, "reml.npz"))
+    if kind == "add":
+        pvp, py = O.projection(my, mx, mcol, mnid, [ma, ma * ma], r["var2"])
+        sigma = r["var2"][0]
+    else:
+        pvp, py = O.projection(my, mx, mcol, mnid, [ma, md, ma * ma, ma * md, md * md], r["var5"])
+        sigma = r["var5"][1]
+    got = np.column_stack(O.remma_single(kind, msnp, pvp, py, sigma))
+    _, exp = _single_golden(os.path.join(MOUSE_DATA, "remma_" + kind))
+    np.testing.assert_allclose(got, exp, rtol=1e-8, atol=1e-14)
