@@ -43,6 +43,7 @@ _PROTOS = {
     "gmat_eff_scan": (_INT, [_P, _INT, _P, _P, _I64, _P, _P, _P, ctypes.c_char_p, _P]),
     "gmat_eff_stats": (_INT, [_P]),
     "gmat_geno_decode": (_INT, [_P, _P]),
+    "gmat_blup": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
     # include/gmat_remma_eff.h: the reference's cffi prototypes (char*, long long, ...)
     "read_plink_bed": (_INT, [ctypes.c_char_p, _I64, _I64, _P]),

@@ -345,6 +345,67 @@ extern "C" int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n
   return GMAT_OK;
 }
 
+// Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-166), reproduced as
+// written there: the projection is built from V itself (vxmat = V X, pmat = V - VX (X'VX)^-1
+// X'V, :152-156) rather than from V^-1, then zpy = Z' pmat y and rand_eff[:, k] =
+// (G_k zpy) var_com[k].  rand_eff is n_id x n_gmat, row-major.
+extern "C" int gmat_blup(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y,
+                         const double *xmat, const int64_t *z_col, const double *const *gmat, const double *var_com,
+                         double *rand_eff) {
+  GMAT_CHECK(y && xmat && z_col && var_com && rand_eff && (gmat || n_gmat == 0), GMAT_E_ARG,
+             "gmat_blup: bad arguments");
+  Model md;
+  GMAT_TRY(md.setup(n_rec, n_fix, n_id, n_gmat, y, xmat, z_col, gmat));
+  const int64_t n = n_rec, p = n_fix;
+  const hipStream_t s = md.s;
+  Coefs k{};
+  k.c = n_gmat;
+  k.diag = var_com[n_gmat];
+  for (int t = 0; t < n_gmat; ++t) {
+    k.g[t] = md.zg[t].as<double>();
+    k.s[t] = var_com[t];
+  }
+  hipLaunchKernelGGL(combine_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s, n, k, md.v.as<double>());
+  GMAT_HIP(hipGetLastError());
+  // VX = V X ; XVX = X' VX (p x p, inverted on the host)
+  GMAT_TRY(dgemm(s, n, p, n, 1.0, DView{md.v.as<double>(), n, 0}, DView{md.x.as<double>(), p, 0}, 0.0,
+                 md.vx.as<double>(), p));
+  GMAT_CHECK(p * p <= 1024, GMAT_E_ARG, "too many fixed effects (%lld)", (long long)p);
+  double *dxvx = md.small.as<double>() + 8;
+  GMAT_TRY(dgemm(s, p, p, n, 1.0, DView{md.x.as<double>(), p, 1}, DView{md.vx.as<double>(), p, 0}, 0.0, dxvx, p));
+  std::vector<double> xvx(p * p), xvxi(p * p);
+  GMAT_HIP(hipMemcpyAsync(xvx.data(), dxvx, p * p * sizeof(double), hipMemcpyDeviceToHost, s));
+  GMAT_HIP(hipStreamSynchronize(s));
+  GMAT_CHECK(small_inverse((int)p, xvx.data(), xvxi.data(), nullptr), GMAT_E_NOTPD, "X'VX is singular");
+  double *dxi = md.small.as<double>() + 8 + 1024;
+  GMAT_HIP(hipMemcpyAsync(dxi, xvxi.data(), p * p * sizeof(double), hipMemcpyHostToDevice, s));
+  // pmat = V - (VX XVX^-1) VX' ; py = pmat y
+  GMAT_TRY(dgemm(s, n, p, p, 1.0, DView{md.vx.as<double>(), p, 0}, DView{dxi, p, 0}, 0.0, md.t.as<double>(), p));
+  GMAT_TRY(dgemm(s, n, n, p, -1.0, DView{md.t.as<double>(), p, 0}, DView{md.vx.as<double>(), p, 1}, 1.0,
+                 md.v.as<double>(), n));
+  GMAT_TRY(dgemm(s, n, 1, n, 1.0, DView{md.v.as<double>(), n, 0}, DView{md.y.as<double>(), 1, 0}, 0.0,
+                 md.py.as<double>(), 1));
+  std::vector<double> hpy(n), zpy(n_id, 0.0);
+  GMAT_HIP(hipMemcpyAsync(hpy.data(), md.py.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  GMAT_HIP(hipStreamSynchronize(s));
+  for (int64_t r = 0; r < n; ++r) zpy[z_col[r]] += hpy[r];  // Z' (records in order)
+  DBuf g, dz, de;
+  GMAT_TRY(g.alloc((size_t)n_id * n_id * sizeof(double)));
+  GMAT_TRY(dz.alloc((size_t)n_id * sizeof(double)));
+  GMAT_TRY(de.alloc((size_t)n_id * sizeof(double)));
+  GMAT_HIP(hipMemcpyAsync(dz.p, zpy.data(), n_id * sizeof(double), hipMemcpyHostToDevice, s));
+  std::vector<double> he(n_id);
+  for (int t = 0; t < n_gmat; ++t) {
+    GMAT_HIP(hipMemcpyAsync(g.p, gmat[t], (size_t)n_id * n_id * sizeof(double), hipMemcpyHostToDevice, s));
+    GMAT_TRY(dgemm(s, n_id, 1, n_id, 1.0, DView{g.as<double>(), n_id, 0}, DView{dz.as<double>(), 1, 0}, 0.0,
+                   de.as<double>(), 1));
+    GMAT_HIP(hipMemcpyAsync(he.data(), de.p, n_id * sizeof(double), hipMemcpyDeviceToHost, s));
+    GMAT_HIP(hipStreamSynchronize(s));
+    for (int64_t a = 0; a < n_id; ++a) rand_eff[a * n_gmat + t] = he[a] * var_com[t];
+  }
+  return GMAT_OK;
+}
+
 extern "C" int gmat_spd_inverse(int64_t n, const double *a, double *ainv, double *logdet) {
   GMAT_CHECK(n > 0 && a && ainv, GMAT_E_ARG, "gmat_spd_inverse: bad arguments");
   DBuf da, dinv, work, out, sm;

@@ -54,3 +54,45 @@ def z_columns(zmat, n_rec):
     if not (np.all(nnz == 1) and np.all(z.data == 1.0)):
         raise ValueError("Z must be an incidence matrix (exactly one 1.0 per record)")
     return np.ascontiguousarray(z.indices, dtype=np.int64), z.shape[1]
+
+
+def design_matrix_wemai_multi_gmat_pred(pheno_file, bed_file):
+    """As design_matrix_wemai_multi_gmat, but genotyped ids without a phenotype are allowed:
+    they keep a (record-less) column of Z so that their random effects are predicted
+    (design_matrix.py:60-113)."""
+    fam = []
+    with open(bed_file + ".fam") as f:
+        for line in f:
+            a = line.split()
+            fam.append(a[0] + " " + a[1])
+    recs = {}
+    with open(pheno_file) as f:
+        for line in f:
+            a = line.split()
+            if a[-1] in _NA:
+                continue
+            recs.setdefault(a[0] + " " + a[1], []).append(a)
+    y, x, iid = [], [], []
+    for key in fam:
+        if key in recs:
+            for a in recs[key]:
+                y.append(float(a[-1]))
+                x.append(a[2:-1])
+                iid.append(a[1])
+        else:
+            iid.append(None)
+    y = np.array(y).reshape(-1, 1)
+    xmat = np.array(x, dtype=float).reshape(y.shape[0], -1)
+    order, rows, col = {}, 0, []
+    n_col = 0
+    for v in iid:
+        if v is None:
+            n_col += 1
+            continue
+        if v not in order:
+            order[v] = n_col
+            n_col += 1
+        col.append(order[v])
+        rows += 1
+    zmat = csr_matrix((np.ones(rows), (np.arange(rows), col)), shape=(rows, n_col))
+    return y, xmat, zmat

@@ -10,7 +10,7 @@ import logging
 import numpy as np
 
 from .. import _native as N
-from .design_matrix import design_matrix_wemai_multi_gmat, z_columns
+from .design_matrix import design_matrix_wemai_multi_gmat, design_matrix_wemai_multi_gmat_pred, z_columns
 
 
 def _gmat_ptrs(gmat_lst, n_id):
@@ -54,6 +54,37 @@ def wemai_multi_gmat(pheno_file, bed_file, gmat_lst, init=None, maxiter=200, cc_
     y, xmat, zmat = design_matrix_wemai_multi_gmat(pheno_file, bed_file)
     var_com = _wemai_multi_gmat(y, xmat, zmat, gmat_lst, init=init, maxiter=maxiter, cc_par=cc_par, cc_gra=cc_gra)
     np.savetxt(out_file, var_com)
+    return var_com
+
+
+def predict_random(y, xmat, zmat, gmat_lst, var_com):
+    """rand_eff (n_id x len(gmat_lst)) of wemai_multi_gmat_pred (uvlmm_varcom.py:147-165), on the
+    device (gmat_blup), with the reference's formula as written there."""
+    lib = N.ensure_device()
+    y = N.f64(np.asarray(y).reshape(-1))
+    n = y.shape[0]
+    xmat = N.f64(np.asarray(xmat).reshape(n, -1))
+    col, n_id = z_columns(zmat, n)
+    mats, arr = _gmat_ptrs(gmat_lst, n_id)
+    var = N.f64(np.asarray(var_com, dtype=float).reshape(-1))
+    if var.size != len(mats) + 1:
+        raise ValueError("var_com must have %d values" % (len(mats) + 1))
+    out = np.zeros((n_id, len(mats)))
+    N.check(lib.gmat_blup(n, xmat.shape[1], n_id, len(mats), N.ptr(y), N.ptr(xmat), N.ptr(col), arr, N.ptr(var),
+                          N.ptr(out)), "gmat_blup")
+    return out
+
+
+def wemai_multi_gmat_pred(pheno_file, bed_file, gmat_lst, init=None, maxiter=200, cc_par=1.0e-8, cc_gra=1.0e-6,
+                          out_file='wemai_multi_gmat_pred'):
+    """uvlmm_varcom.py:129-167: REML with genotyped-but-unphenotyped ids kept in Z, then the
+    random-effect prediction; writes out_file + '.var' and out_file + '.rand_eff'."""
+    y, xmat, zmat = design_matrix_wemai_multi_gmat_pred(pheno_file, bed_file)
+    var_com = _wemai_multi_gmat(y, xmat, zmat, gmat_lst, init=init, maxiter=maxiter, cc_par=cc_par, cc_gra=cc_gra)
+    np.savetxt(out_file + '.var', var_com)
+    logging.info('Predict the random effects')
+    rand_eff = predict_random(y, xmat, zmat, gmat_lst, var_com)
+    np.savetxt(out_file + '.rand_eff', rand_eff)
     return var_com
 
 

@@ -105,6 +105,12 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
 int gmat_epi_stats(const gmat_epi *e, double *out10);
 int gmat_epi_destroy(gmat_epi *e);
 
+/* Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-166) at var_com, as
+ * the reference computes it (its projection uses V, not V^-1: vxmat = V X, pmat = V -
+ * VX (X'VX)^-1 X'V).  rand_eff[a * n_gmat + k] = (G_k Z' pmat y)[a] * var_com[k]. */
+int gmat_blup(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y, const double *xmat,
+              const int64_t *z_col, const double *const *gmat, const double *var_com, double *rand_eff);
+
 /* ---- effect-only screen (the approximate pipeline's first pass) ----
  * Replaces the OpenMP row loops of _remma_epi_eff_cpu.c (AA :61-137, AA maf :141-219,
  * AD :226-314, AD maf :318-410, DD :415-496, DD maf :500-574).  eff(i, j) =

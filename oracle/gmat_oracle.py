@@ -116,6 +116,58 @@ def design_matrix(pheno_file, bed_file):
             np.array(col, dtype=np.int64), len(order))
 
 
+def design_matrix_pred(pheno_file, bed_file):
+    """design_matrix_wemai_multi_gmat_pred (uvlmm/design_matrix.py:60-113): genotyped ids
+    without records keep an empty column of Z.  Same return convention as design_matrix."""
+    fam = []
+    with open(bed_file + ".fam") as f:
+        for line in f:
+            a = line.split()
+            fam.append(a[0] + " " + a[1])
+    recs = {}
+    with open(pheno_file) as f:
+        for line in f:
+            a = line.split()
+            if a[-1] in ("NA", "NaN", "nan", "na"):
+                continue
+            recs.setdefault(a[0] + " " + a[1], []).append(a)
+    y, x, iid = [], [], []
+    for key in fam:
+        if key in recs:
+            for a in recs[key]:
+                y.append(float(a[-1]))
+                x.append([float(v) for v in a[2:-1]])
+                iid.append(a[1])
+        else:
+            iid.append("NA")
+    order, col, ncol = {}, [], 0
+    for v in iid:
+        if v != "NA":
+            if v not in order:
+                order[v] = ncol
+                ncol += 1
+            col.append(order[v])
+        else:
+            ncol += 1
+    return (np.array(y).reshape(-1, 1), np.array(x, dtype=float).reshape(len(y), -1),
+            np.array(col, dtype=np.int64), ncol)
+
+
+def predict_random(y, xmat, col, n_id, gmat_lst, var_com):
+    """Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-165) exactly as
+    written there (its 'P' is built from V, not V^-1)."""
+    n = y.shape[0]
+    v = np.diag([var_com[-1]] * n)
+    for k, g in enumerate(gmat_lst):
+        v += zgz(col, n_id, g) * var_com[k]
+    vx = v @ xmat
+    p = v - vx @ np.linalg.inv(xmat.T @ vx) @ vx.T
+    zt = np.zeros((n_id, n))
+    zt[col, np.arange(n)] = 1.0
+    zpy = zt @ (p @ y)
+    return np.concatenate([(g @ zpy) * var_com[k] for k, g in enumerate(gmat_lst)], axis=1)
+
+
 def zgz(col, n_id, g):
     """Z G Z' for an incidence Z given as record->individual index (uvlmm_varcom.py:34)."""
     return g[np.ix_(col, col)]

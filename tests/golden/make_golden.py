@@ -11,6 +11,7 @@ Fixtures ("reference code + its own C decoder in fp64"):
            epiAA_pair file, parallel parts, annotation, and the C effect screen.
   tiny/    a 150 x 200 related synthetic cohort (n % 4 == 2, two monomorphic SNPs and one
            all-heterozygous SNP) with full K/D and every testable pair for AA/AD/DD.
+           rep*: repeated records (Z != I) REML + epiAA, and wemai_multi_gmat_pred.
   both:    remma_add / remma_dom result files (``python tests/golden/make_golden.py singles``
            regenerates only these).
 """
@@ -201,10 +202,47 @@ def singles(gmat, work, out_mouse, out_tiny):
     remma_dom(bed + ".pheno", bed, [a, d], tref["var"], out_file=os.path.join(out_tiny, "remma_dom"))
 
 
+def repeated(gmat, work, out_tiny):
+    """Repeated records (Z != I): 1-3 records per individual with a covariate, REML and an
+    exact AA scan; and the prediction workflow (wemai_multi_gmat_pred) with 15 genotyped
+    individuals lacking records (design_matrix.py:60-113, uvlmm_varcom.py:129-167)."""
+    from gmat.uvlmm import wemai_multi_gmat, wemai_multi_gmat_pred
+    from gmat.remma.remma_epiAA import remma_epiAA
+    for ext in (".bed", ".bim", ".fam"):
+        shutil.copy(os.path.join(out_tiny, "tiny" + ext), os.path.join(work, "tiny" + ext))
+    bed = os.path.join(work, "tiny")
+    tref = np.load(os.path.join(out_tiny, "tiny_ref.npz"))
+    a = tref["agmat"]
+    ids = [l.split()[:2] for l in open(bed + ".fam")]
+    rng = np.random.Generator(np.random.PCG64(8))
+    lines, lines_pred = [], []
+    skip = set(rng.choice(len(ids), 15, replace=False).tolist())
+    base = rng.standard_normal(len(ids))
+    for k, (fid, iid) in enumerate(ids):
+        for _ in range(int(rng.integers(1, 4))):
+            cov = rng.uniform(-1, 1)
+            yv = 1.0 + 0.5 * cov + base[k] + 0.7 * rng.standard_normal()
+            row = "%s %s 1 %.6f %.6f" % (fid, iid, cov, yv)
+            lines.append(row)
+            if k not in skip:
+                lines_pred.append(row)
+    rng.shuffle(lines)  # records need not be grouped or ordered
+    with open(os.path.join(out_tiny, "rep.pheno"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with open(os.path.join(out_tiny, "rep_pred.pheno"), "w") as f:
+        f.write("\n".join(lines_pred) + "\nF0 I0 1 0.0 NA\n")
+    g = [a, a * a]
+    var = wemai_multi_gmat(os.path.join(out_tiny, "rep.pheno"), bed, g, out_file=os.path.join(work, "v"))
+    remma_epiAA(os.path.join(out_tiny, "rep.pheno"), bed, g, var, p_cut=0.05, out_file=os.path.join(out_tiny, "rep_epiAA"))
+    wemai_multi_gmat_pred(os.path.join(out_tiny, "rep_pred.pheno"), bed, g, out_file=os.path.join(work, "pred"))
+    np.savez(os.path.join(out_tiny, "rep_ref.npz"), var=var, pred_var=np.loadtxt(os.path.join(work, "pred.var")),
+             rand_eff=np.loadtxt(os.path.join(work, "pred.rand_eff")))
+
+
 def main():
     gmat = import_reference()
     logging.getLogger().setLevel(logging.WARNING)
-    what = sys.argv[1:] or ["tiny", "mouse", "singles"]
+    what = sys.argv[1:] or ["tiny", "mouse", "singles", "repeated"]
     if "tiny" in what:
         with tempfile.TemporaryDirectory() as work:
             tiny(gmat, work, os.path.join(HERE, "tiny"))
@@ -214,6 +252,9 @@ def main():
     if "singles" in what:
         with tempfile.TemporaryDirectory() as work:
             singles(gmat, work, os.path.join(HERE, "mouse"), os.path.join(HERE, "tiny"))
+    if "repeated" in what:
+        with tempfile.TemporaryDirectory() as work:
+            repeated(gmat, work, os.path.join(HERE, "tiny"))
     print("golden fixtures written to", HERE)
 
 

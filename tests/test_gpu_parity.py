@@ -269,3 +269,25 @@ def test_scan_deterministic_and_row_split(synth_cohort):
         order = np.lexsort((cat[1], cat[0]))
         for a, b in zip(full, cat):
             np.testing.assert_array_equal(a, b[order])
+
+
+def test_repeated_records_and_prediction(tiny_dir, tmp_path):
+    """Z != I: REML and the exact AA scan on repeated, unordered
+    records; wemai_multi_gmat_pred with record-less genotyped ids (.var and .rand_eff)."""
+    import gmat_amd.remma as R
+    from gmat_amd.uvlmm import wemai_multi_gmat, wemai_multi_gmat_pred
+    ref = np.load(os.path.join(TINY, "tiny_ref.npz"))
+    rep = np.load(os.path.join(TINY, "rep_ref.npz"))
+    a = ref["agmat"]
+    pheno = os.path.join(TINY, "rep.pheno")
+    var = wemai_multi_gmat(pheno, tiny_dir, [a, a * a], out_file=str(tmp_path / "v"))
+    np.testing.assert_allclose(var, rep["var"], rtol=1e-6)
+    R.remma_epiAA(pheno, tiny_dir, [a, a * a], rep["var"], p_cut=0.05, out_file=str(tmp_path / "aa"))
+    _cmp_hits(str(tmp_path / "aa"), os.path.join(TINY, "rep_epiAA"))
+    out = str(tmp_path / "pred")
+    pv = wemai_multi_gmat_pred(os.path.join(TINY, "rep_pred.pheno"), tiny_dir, [a, a * a], out_file=out)
+    np.testing.assert_allclose(pv, rep["pred_var"], rtol=1e-6)
+    np.testing.assert_allclose(np.loadtxt(out + ".var"), rep["pred_var"], rtol=1e-6)
+    re = np.loadtxt(out + ".rand_eff")
+    assert re.shape == (150, 2)
+    np.testing.assert_allclose(re, rep["rand_eff"], rtol=1e-5, atol=1e-10)

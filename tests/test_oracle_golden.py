@@ -214,3 +214,29 @@ def test_single_snp_golden(kind, tiny, mouse_eff_inputs):
     got = np.column_stack(O.remma_single(kind, msnp, pvp, py, sigma))
     _, exp = _single_golden(os.path.join(MOUSE_DATA, "remma_" + kind))
     np.testing.assert_allclose(got, exp, rtol=1e-8, atol=1e-14)
+
+
+def test_repeated_records_golden(tiny):
+    """Z != I: repeated, unordered records with a covariate (REML, exact AA scan) and the
+    prediction workflow with record-less genotyped ids, against the reference's outputs."""
+    _, ref, _ = tiny
+    a = ref["agmat"]
+    rep = np.load(os.path.join(TINY, "rep_ref.npz"))
+    prefix = os.path.join(TINY, "tiny")
+    y, x, col, nid = O.design_matrix(os.path.join(TINY, "rep.pheno"), prefix)
+    assert y.shape[0] > nid and x.shape[1] == 2
+    var = O.wemai_multi_gmat(y, x, col, nid, [a, a * a])
+    np.testing.assert_allclose(var, rep["var"], rtol=1e-7)
+    pvp, py = O.projection(y, x, col, nid, [a, a * a], rep["var"])
+    snp = O.read_plink(prefix)
+    got = O.epi_scan("AA", snp, pvp, py, p_cut=0.05)
+    hdr, exp = _load_hits(os.path.join(TINY, "rep_epiAA"))
+    assert got.shape == exp.shape
+    np.testing.assert_array_equal(got[:, :2], exp[:, :2])
+    np.testing.assert_allclose(got[:, 2:], exp[:, 2:], rtol=1e-8, atol=1e-300)
+    y, x, col, nid = O.design_matrix_pred(os.path.join(TINY, "rep_pred.pheno"), prefix)
+    assert nid == 150 and len(set(col.tolist())) == 135
+    var = O.wemai_multi_gmat(y, x, col, nid, [a, a * a])
+    np.testing.assert_allclose(var, rep["pred_var"], rtol=1e-7)
+    re = O.predict_random(y, x, col, nid, [a, a * a], rep["pred_var"])
+    np.testing.assert_allclose(re, rep["rand_eff"], rtol=1e-6, atol=1e-12)
