@@ -44,6 +44,8 @@ _PROTOS = {
     "gmat_eff_stats": (_INT, [_P]),
     "gmat_geno_decode": (_INT, [_P, _P]),
     "gmat_blup": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P]),
+    "gmat_write_grm_text": (_INT, [ctypes.c_char_p, _P, _I64, _INT, ctypes.c_char_p, _INT]),
+    "gmat_float_repr": (_INT, [_D, ctypes.c_char_p, _INT]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
     # include/gmat_remma_eff.h: the reference's cffi prototypes (char*, long long, ...)
     "read_plink_bed": (_INT, [ctypes.c_char_p, _I64, _I64, _P]),

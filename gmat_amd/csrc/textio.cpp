@@ -1,0 +1,148 @@
+// Multi-threaded writers of the relationship-matrix text formats (gmatrix.py:10-31).
+//
+// 'mat' is np.savetxt's default ("%.18e", ' ' between values, '\n' per row): glibc's
+// printf and CPython's '%' formatting both round correctly, so the bytes are identical.
+// 'row_col_val' / 'id_id_val' are pandas DataFrame.to_csv rows whose float column is the
+// shortest round-trip repr of each value (CPython float_repr_style 'short'): digits from
+// std::to_chars (shortest round trip), laid out with CPython's rules -- fixed notation for
+// decimal exponents -4 <= e < 16, otherwise d[.ddd]e(+|-)XX.
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+// CPython repr(float) of v into out; returns the length.
+int py_repr(double v, char *out) {
+  if (std::isnan(v)) return (int)(strcpy(out, "nan"), 3);
+  if (std::isinf(v)) {
+    if (v < 0) return (int)(strcpy(out, "-inf"), 4);
+    return (int)(strcpy(out, "inf"), 3);
+  }
+  char sci[64];
+  auto r = std::to_chars(sci, sci + sizeof(sci), v, std::chars_format::scientific);
+  *r.ptr = 0;
+  // sci = [-]d[.ddd]e(+|-)XX
+  const char *p = sci;
+  int len = 0;
+  if (*p == '-') {
+    out[len++] = '-';
+    ++p;
+  }
+  char dig[32];
+  int nd = 0;
+  for (; *p && *p != 'e'; ++p)
+    if (*p != '.') dig[nd++] = *p;
+  const int e10 = atoi(p + 1);  // value = d.ddd x 10^e10
+  if (nd == 1 && dig[0] == '0') {
+    memcpy(out + len, "0.0", 3);
+    return len + 3;
+  }
+  const int decpt = e10 + 1;  // value = 0.ddd x 10^decpt
+  if (decpt > -4 && decpt <= 16) {
+    if (decpt <= 0) {
+      out[len++] = '0';
+      out[len++] = '.';
+      for (int k = 0; k < -decpt; ++k) out[len++] = '0';
+      memcpy(out + len, dig, nd);
+      len += nd;
+    } else if (decpt >= nd) {
+      memcpy(out + len, dig, nd);
+      len += nd;
+      for (int k = nd; k < decpt; ++k) out[len++] = '0';
+      out[len++] = '.';
+      out[len++] = '0';
+    } else {
+      memcpy(out + len, dig, decpt);
+      len += decpt;
+      out[len++] = '.';
+      memcpy(out + len, dig + decpt, nd - decpt);
+      len += nd - decpt;
+    }
+    return len;
+  }
+  out[len++] = dig[0];
+  if (nd > 1) {
+    out[len++] = '.';
+    memcpy(out + len, dig + 1, nd - 1);
+    len += nd - 1;
+  }
+  len += snprintf(out + len, 16, "e%c%02d", e10 < 0 ? '-' : '+', e10 < 0 ? -e10 : e10);
+  return len;
+}
+
+// Format rows [r0, r1) of the chosen layout into buf.
+void format_rows(int fmt, const double *mat, int64_t n, const std::vector<std::string> &ids, int64_t r0, int64_t r1,
+                 std::string *buf) {
+  char tmp[96];
+  for (int64_t r = r0; r < r1; ++r) {
+    if (fmt == 0) {
+      for (int64_t c = 0; c < n; ++c) {
+        const int l = snprintf(tmp, sizeof(tmp), c + 1 < n ? "%.18e " : "%.18e\n", mat[r * n + c]);
+        buf->append(tmp, l);
+      }
+    } else {
+      for (int64_t c = 0; c <= r; ++c) {
+        if (fmt == 1) {
+          buf->append(std::to_string(r + 1)).push_back(' ');
+          buf->append(std::to_string(c + 1)).push_back(' ');
+        } else {
+          buf->append(ids[r]).push_back(' ');
+          buf->append(ids[c]).push_back(' ');
+        }
+        const int l = py_repr(mat[r * n + c], tmp);
+        buf->append(tmp, l).push_back('\n');
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int gmat_float_repr(double v, char *out, int cap) {
+  GMAT_CHECK(out && cap >= 32, GMAT_E_ARG, "gmat_float_repr: buffer");
+  const int l = py_repr(v, out);
+  out[l] = 0;
+  return l;
+}
+
+extern "C" int gmat_write_grm_text(const char *path, const double *mat, int64_t n, int fmt, const char *ids_blob,
+                                   int n_threads) {
+  GMAT_CHECK(path && mat && n > 0 && fmt >= 0 && fmt <= 2 && (fmt != 2 || ids_blob), GMAT_E_ARG,
+             "gmat_write_grm_text: bad arguments");
+  std::vector<std::string> ids;
+  if (fmt == 2) {  // n NUL-terminated strings back to back
+    const char *p = ids_blob;
+    for (int64_t k = 0; k < n; ++k) {
+      ids.emplace_back(p);
+      p += ids.back().size() + 1;
+    }
+  }
+  FILE *f = fopen(path, "wb");
+  GMAT_CHECK(f, GMAT_E_ARG, "gmat_write_grm_text: cannot open %s", path);
+  const int T = n_threads > 0 ? n_threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // row blocks of roughly equal output size, written in order
+  const int64_t R = 64;
+  int rc = GMAT_OK;
+  for (int64_t base = 0; base < n && rc == GMAT_OK; base += R * T) {
+    std::vector<std::string> bufs(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) {
+      const int64_t r0 = std::min(n, base + t * R), r1 = std::min(n, r0 + R);
+      if (r0 >= r1) break;
+      th.emplace_back(format_rows, fmt, mat, n, std::cref(ids), r0, r1, &bufs[t]);
+    }
+    for (auto &x : th) x.join();
+    for (auto &b : bufs)
+      if (!b.empty() && fwrite(b.data(), 1, b.size(), f) != b.size()) rc = GMAT_E_ARG;
+  }
+  if (fclose(f) != 0) rc = GMAT_E_ARG;
+  GMAT_CHECK(rc == GMAT_OK, rc, "gmat_write_grm_text: write to %s failed", path);
+  return GMAT_OK;
+}

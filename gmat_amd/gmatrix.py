@@ -25,26 +25,25 @@ def _fam_ids_as_pandas(bed_file):
 
 
 def output_mat(mat, id, out_file, out_fmt):
-    """Text output of gmatrix.py:10-31: 'mat' (np.savetxt '%.18e', suffix 0),
-    'row_col_val' (1-based lower triangle, suffix 1), 'id_id_val' (suffix 2)."""
-    if out_fmt == "mat":
-        np.savetxt(out_file + "0", mat)
-    elif out_fmt in ("row_col_val", "id_id_val"):
-        r, c = np.tril_indices_from(mat)
-        vals = mat[r, c]
-        if out_fmt == "row_col_val":
-            a, b, suffix = r + 1, c + 1, "1"
-        else:
-            a, b, suffix = id[r], id[c], "2"
-        with open(out_file + suffix, "w") as f:
-            f.write("".join("%s %s %r\n" % (x, y, float(v)) for x, y, v in zip(a, b, vals)))
-    else:
+    """Output of gmatrix.py:10-31: 'mat' (np.savetxt '%.18e', suffix 0), 'row_col_val' (1-based
+    lower triangle, suffix 1), 'id_id_val' (suffix 2), byte-identical to the reference's
+    writers but formatted by the library's multi-threaded C++ writer (gmat_write_grm_text).
+    Addition: 'npy' writes the binary float64 matrix to out_file + '0.npy' (np.load-able)."""
+    mat = N.f64(mat)
+    fmt = {"mat": 0, "row_col_val": 1, "id_id_val": 2}.get(out_fmt)
+    if out_fmt == "npy":
+        np.save(out_file + "0.npy", mat)
+        return 1
+    if fmt is None:
         return 0
+    blob = b"".join(str(v).encode() + b"\0" for v in id) if fmt == 2 else None
+    N.check(N.load().gmat_write_grm_text((out_file + str(fmt)).encode(), N.ptr(mat), mat.shape[0], fmt, blob, 0),
+            "gmat_write_grm_text")
     return 1
 
 
 def _grm(bed_file, kind, inv, small_val, out_fmt, suffix, inv_suffix):
-    if out_fmt not in ("mat", "row_col_val", "id_id_val"):
+    if out_fmt not in ("mat", "row_col_val", "id_id_val", "npy"):
         raise ValueError("Not Recognized output format: " + str(out_fmt))
     lib = N.ensure_device()
     with Geno(bed_file) as g:

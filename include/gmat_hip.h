@@ -126,6 +126,15 @@ int gmat_eff_scan(gmat_geno *g, int kind, const double *py, const int64_t *rows,
                   int64_t *n_hits);
 /* Last gmat_eff_scan on this process: pairs tested, hits, device seconds, text-writing seconds. */
 int gmat_eff_stats(double *out4);
+/* ---- relationship-matrix text output (gmatrix.py:10-31), multi-threaded ----
+ * fmt 0 'mat': np.savetxt layout ("%.18e", ' ', '\n'); fmt 1 'row_col_val' and fmt 2
+ * 'id_id_val': lower triangle row by row, "<row> <col> <value>" with 1-based indices or the
+ * ids (ids_blob: n NUL-terminated strings back to back) and the value as CPython
+ * repr(float), as pandas to_csv writes it.  n_threads <= 0: up to 16. */
+int gmat_write_grm_text(const char *path, const double *mat, int64_t n, int fmt, const char *ids_blob, int n_threads);
+/* CPython repr(float) of v (the value text of fmt 1/2); returns its length (cap >= 32). */
+int gmat_float_repr(double v, char *out, int cap);
+
 /* ---- single-SNP tests (remma_add / remma_dom) ----
  * For every SNP j of the (imputed) panel: x_j = g_j - 2p_j (kind GMAT_GRM_ADD) or
  * [g_j != 2] g_j - 2p_j(1-p_j) (GMAT_GRM_DOM), p_j = sum/(2n); xpy[j] = x_j' py and

@@ -52,3 +52,40 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("a GPU is visible")
     with pytest.raises(_native.GmatNativeError):
         _native.ensure_device()
+
+
+def test_text_writers_match_numpy_and_pandas(tmp_path):
+    """The host-side text writers (no GPU needed) are byte-identical to np.savetxt and to
+    pandas to_csv (CPython float repr) -- the formats of gmatrix.py:10-31."""
+    if not os.path.exists(LIB):
+        pytest.skip("libgmat_hip.so not built")
+    import numpy as np
+    import pandas as pd
+    from gmat_amd import _native as N
+    lib = N.load()
+    rng = np.random.default_rng(1)
+    vals = np.concatenate([rng.standard_normal(50000) * 10.0 ** rng.integers(-30, 30, 50000),
+                           rng.random(20000), np.round(rng.random(5000), 3), [0.0, -0.0, 1e16, 1e15, 1e-4, 1e-5,
+                           123456789012345678.0, 5e-324, 1.7976931348623157e308, 0.1, 2.0, -3.5, np.nan, np.inf,
+                           -np.inf, 1234567890123456.0, 0.001, 1e22]])
+    buf = ctypes.create_string_buffer(64)
+    for v in vals.tolist():
+        n = lib.gmat_float_repr(v, buf, 64)
+        assert buf.value.decode() == repr(v), (v, buf.value)
+        assert n == len(repr(v))
+    n = 37
+    mat = rng.standard_normal((n, n)) * 10.0 ** rng.integers(-8, 8, (n, n))
+    mat[3, 2] = 0.0
+    p0 = str(tmp_path / "m0")
+    assert lib.gmat_write_grm_text(p0.encode(), N.ptr(mat), n, 0, None, 3) == 0
+    np.savetxt(str(tmp_path / "e0"), mat)
+    assert open(p0, "rb").read() == open(str(tmp_path / "e0"), "rb").read()
+    ind = np.tril_indices_from(mat)
+    ids = np.array(["id%d" % k for k in range(n)], dtype=object)
+    blob = b"".join(s.encode() + b"\0" for s in ids)
+    for fmt, a, b in ((1, ind[0] + 1, ind[1] + 1), (2, ids[ind[0]], ids[ind[1]])):
+        p = str(tmp_path / ("m%d" % fmt))
+        assert lib.gmat_write_grm_text(p.encode(), N.ptr(mat), n, fmt, blob if fmt == 2 else None, 0) == 0
+        e = str(tmp_path / ("e%d" % fmt))
+        pd.DataFrame({"a": a, "b": b, "v": mat[ind]}).to_csv(e, sep=" ", index=False, header=False)
+        assert open(p, "rb").read() == open(e, "rb").read()
