@@ -601,6 +601,11 @@ struct gmat_epi {
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
   double stats[10] = {0};
   hipStream_t s = 0;
+  hipStream_t s1 = nullptr, s2 = nullptr;  // scan pipeline: screen / side-term streams
+  ~gmat_epi() {
+    if (s1) (void)hipStreamDestroy(s1);
+    if (s2) (void)hipStreamDestroy(s2);
+  }
 };
 
 namespace {
@@ -645,13 +650,13 @@ int build_coding(gmat_epi *e, int which) {
 }
 
 // exact statistics for device pair lists (pi, pj) of length np -> device eff/var/chi/p
-int refine(gmat_epi *e, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp, const int64_t *pi,
-           const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
+int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp,
+           const int64_t *pi, const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
   if (np <= 0) return GMAT_OK;
-  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, QT)), dim3(256), 0, e->s, e->n_pad, e->Ps.as<double>(),
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, QT)), dim3(256), 0, st, e->n_pad, e->Ps.as<double>(),
                      e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var);
   GMAT_HIP(hipGetLastError());
-  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, e->s, np, eff, var, chi, p);
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
   GMAT_HIP(hipGetLastError());
   return GMAT_OK;
 }
@@ -784,7 +789,7 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
     const int64_t np = std::min(chunk, n_pairs - t0);
     GMAT_HIP(hipMemcpy(di.p, hi.data() + t0, np * 8, hipMemcpyHostToDevice));
     GMAT_HIP(hipMemcpy(dj.p, hj.data() + t0, np * 8, hipMemcpyHostToDevice));
-    GMAT_TRY(refine(e, e->code[lc], e->code[rc], lp, rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(),
+    GMAT_TRY(refine(e, e->s, e->code[lc], e->code[rc], lp, rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(),
                     dv.as<double>(), dc.as<double>(), dpv.as<double>()));
     GMAT_HIP(hipMemcpy(eff + t0, de.p, np * 8, hipMemcpyDeviceToHost));
     GMAT_HIP(hipMemcpy(var + t0, dv.p, np * 8, hipMemcpyDeviceToHost));
@@ -839,12 +844,19 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const double scale_main = e->pmax / 127.0 * std::pow(128.0, -(S - 1));
   const double delta = e->rho[S];
 
-  DBuf drows, dtiles, bl, ba, e13, e2;
-  GMAT_TRY(drows.alloc(ROWS_PER_LAUNCH * 8));
-  GMAT_TRY(bl.alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad * sizeof(double)));
-  GMAT_TRY(ba.alloc((size_t)ROWS_PER_LAUNCH * n_pad));
-  GMAT_TRY(e13.alloc((size_t)2 * ROWS_PER_LAUNCH * m * sizeof(double)));
-  GMAT_TRY(e2.alloc((size_t)ROWS_PER_LAUNCH * m * sizeof(double)));
+  // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
+  // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
+  // read it has completed (event wait).
+  const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ);
+  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2];
+  for (int b = 0; b < 2; ++b) {
+    GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
+    GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
+    GMAT_TRY(bl[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad * sizeof(double)));
+    GMAT_TRY(ba[b].alloc((size_t)ROWS_PER_LAUNCH * n_pad));
+    GMAT_TRY(e13[b].alloc((size_t)2 * ROWS_PER_LAUNCH * m * sizeof(double)));
+    GMAT_TRY(e2[b].alloc((size_t)ROWS_PER_LAUNCH * m * sizeof(double)));
+  }
   if (e->cand_cap == 0) {
     e->cand_cap = 1 << 22;
     GMAT_TRY(e->cand_i.alloc(e->cand_cap * 8));
@@ -855,29 +867,56 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e->cp.alloc(e->cand_cap * 8));
     GMAT_TRY(e->counter.alloc(8));
   }
-  hipEvent_t ev[6];
-  for (auto &x : ev) GMAT_HIP(hipEventCreate(&x));
+  // scan-private streams (the null stream would serialise them): screen + refine on sm,
+  // side terms on S2; ordered after the coding setup by a device synchronisation
+  if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
+  if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
+  const hipStream_t sm = e->s1, S2 = e->s2;
+  GMAT_HIP(hipDeviceSynchronize());
+  struct Ev {
+    hipEvent_t e[8];
+    Ev() {
+      for (auto &x : e) x = nullptr;
+    }
+    ~Ev() {
+      for (auto &x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs;
+  for (auto &x : evs.e) GMAT_HIP(hipEventCreate(&x));
+  hipEvent_t *ev = evs.e;  // 0/1 side start/done (per buffer: 0,1 = buf 0; 5,6 = buf 1), 2 screen done,
+                           // 3/4 refine, 7 screen start
+  hipEvent_t side_beg[2] = {ev[0], ev[5]}, side_end[2] = {ev[1], ev[6]};
+  hipEvent_t screen_end[2];
+  GMAT_HIP(hipEventCreate(&screen_end[0]));
+  GMAT_HIP(hipEventCreate(&screen_end[1]));
+  struct EvPair {
+    hipEvent_t *p;
+    ~EvPair() {
+      (void)hipEventDestroy(p[0]);
+      (void)hipEventDestroy(p[1]);
+    }
+  } screen_end_guard{screen_end};
   double t_screen = 0, t_side = 0, t_ref = 0, pairs_tested = 0, ncand_total = 0, ops = 0;
   int64_t launches_done = 0;
-  std::vector<int> tiles;
   int64_t pending = 0;  // candidates waiting in the device buffer
-  GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+  GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
   // exact refine of candidates [0, count) and collection of the hits
   auto flush = [&](int64_t count) -> int {
     if (count <= 0) return GMAT_OK;
-    GMAT_HIP(hipEventRecord(ev[3], e->s));
-    GMAT_TRY(refine(e, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), count, e->ceff.as<double>(),
+    GMAT_HIP(hipEventRecord(ev[3], sm));
+    GMAT_TRY(refine(e, sm, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), count, e->ceff.as<double>(),
                     e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>()));
-    GMAT_HIP(hipEventRecord(ev[4], e->s));
+    GMAT_HIP(hipEventRecord(ev[4], sm));
     std::vector<int64_t> ci(count), cj(count);
     std::vector<double> ce(count), cv(count), cc(count), cp(count);
-    GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, count * 8, hipMemcpyDeviceToHost, e->s));
-    GMAT_HIP(hipStreamSynchronize(e->s));
+    GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, count * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipStreamSynchronize(sm));
     float ms34;
     GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
     t_ref += ms34 * 1e-3;
@@ -894,37 +933,64 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
     return GMAT_OK;
   };
+
+  // per-launch host plan (rows, tile list); empty launches dropped
+  struct Launch {
+    std::vector<int64_t> rows;
+    std::vector<int> tiles;
+    int64_t j_lo = 0;
+  };
+  std::vector<Launch> plan;
   for (auto &rws : launches) {
     const int Rn = (int)rws.size();
     if (Rn == 0) continue;
-    // pairs tested and tile list
-    tiles.clear();
     const int64_t j_lo = tri ? rws[0] + 1 : 0;
     if (tri && j_lo >= m) continue;
+    Launch ln;
+    ln.rows = rws;
+    ln.j_lo = j_lo;
     for (int r0 = 0; r0 < Rn; r0 += BI) {
       const int64_t imin = rws[r0];
       const int64_t jb0 = tri ? (imin + 1) / BJ : 0;
       for (int64_t J = jb0; J * BJ < m; ++J) {
-        tiles.push_back(r0);
-        tiles.push_back((int)J);
+        ln.tiles.push_back(r0);
+        ln.tiles.push_back((int)J);
       }
     }
     for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
-    const int64_t ntiles = (int64_t)tiles.size() / 2;
-    GMAT_TRY(dtiles.alloc(tiles.size() * sizeof(int)));
-    GMAT_HIP(hipMemcpyAsync(drows.p, rws.data(), Rn * 8, hipMemcpyHostToDevice, e->s));
-    GMAT_HIP(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(int), hipMemcpyHostToDevice, e->s));
-    const int64_t ncol = m - j_lo;
-    GMAT_HIP(hipEventRecord(ev[0], e->s));
-    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, e->s, n_pad, Rn, drows.as<int64_t>(),
-                       L.Lp.as<double>(), L.L3.as<double>(), lp, bl.as<double>(), ba.as<int8_t>());
+    plan.push_back(std::move(ln));
+  }
+
+  // side terms of launch `li` into buffer set b (stream s2)
+  auto enqueue_side = [&](size_t li, int b) -> int {
+    const Launch &ln = plan[li];
+    const int Rn = (int)ln.rows.size();
+    const int64_t ncol = m - ln.j_lo;
+    GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+    GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
+    GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
+                            S2));
+    GMAT_HIP(hipEventRecord(side_beg[b], S2));
+    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, drows[b].as<int64_t>(),
+                       L.Lp.as<double>(), L.L3.as<double>(), lp, bl[b].as<double>(), ba[b].as<int8_t>());
     GMAT_HIP(hipGetLastError());
     // E1/E3 = [L'; L3]_band . b_j ;  E2 = a_band . R'_j
-    GMAT_TRY(dgemm_i8b(e->s, 2 * Rn, ncol, n_pad, 1.0, DView{bl.as<double>(), n_pad, 0},
-                       I8View{rp + j_lo * n_pad, n_pad, 1}, 0.0, e13.as<double>(), m));
-    GMAT_TRY(dgemm_i8a(e->s, Rn, ncol, n_pad, 1.0, I8View{ba.as<int8_t>(), n_pad, 0},
-                       DView{R.Rp.as<double>() + j_lo * n_pad, n_pad, 1}, 0.0, e2.as<double>(), m));
-    GMAT_HIP(hipEventRecord(ev[1], e->s));
+    GMAT_TRY(dgemm_i8b(S2, 2 * Rn, ncol, n_pad, 1.0, DView{bl[b].as<double>(), n_pad, 0},
+                       I8View{rp + ln.j_lo * n_pad, n_pad, 1}, 0.0, e13[b].as<double>(), m));
+    GMAT_TRY(dgemm_i8a(S2, Rn, ncol, n_pad, 1.0, I8View{ba[b].as<int8_t>(), n_pad, 0},
+                       DView{R.Rp.as<double>() + ln.j_lo * n_pad, n_pad, 1}, 0.0, e2[b].as<double>(), m));
+    GMAT_HIP(hipEventRecord(side_end[b], S2));
+    return GMAT_OK;
+  };
+  // the first screen launches wait on never-recorded events: record them once up front
+  GMAT_HIP(hipEventRecord(screen_end[0], sm));
+  GMAT_HIP(hipEventRecord(screen_end[1], sm));
+  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
+  for (size_t li = 0; li < plan.size(); ++li) {
+    const Launch &ln = plan[li];
+    const int b = (int)(li & 1);
+    const int Rn = (int)ln.rows.size();
+    const int64_t ntiles = (int64_t)ln.tiles.size() / 2;
     ScreenArgs sa;
     sa.slices = e->slices.as<int8_t>();
     sa.slices_bytes = (int64_t)e->n_slice * n_pad * n_pad;
@@ -937,14 +1003,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.left = lp;
     sa.right = rp;
     sa.m = m;
-    sa.rows = drows.as<int64_t>();
+    sa.rows = drows[b].as<int64_t>();
     sa.n_rows = Rn;
-    sa.tiles = dtiles.as<int>();
+    sa.tiles = dtiles[b].as<int>();
     sa.tri = tri;
-    sa.e13 = e13.as<double>();
-    sa.e2 = e2.as<double>();
+    sa.e13 = e13[b].as<double>();
+    sa.e2 = e2[b].as<double>();
     sa.ld_e = m;
-    sa.j_lo = j_lo;
+    sa.j_lo = ln.j_lo;
     sa.alpha = L.off.as<double>();
     sa.qa = L.qa.as<double>();
     sa.ra = L.ra.as<double>();
@@ -966,18 +1032,23 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cand_j = e->cand_j.as<int64_t>();
     unsigned long long count = 0;
     for (int attempt = 0;; ++attempt) {
+      GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
+      GMAT_HIP(hipEventRecord(ev[7], sm));
       switch (variant) {
-        case 0: hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
-        case 1: hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
-        case 2: hipLaunchKernelGGL(screen_kernel<2>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
-        case 3: hipLaunchKernelGGL(screen_kernel<3>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
-        case 4: hipLaunchKernelGGL(screen_kernel<4>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
-        default: hipLaunchKernelGGL(screen_kernel<5>, dim3((unsigned)ntiles), dim3(256), 0, e->s, sa); break;
+        case 0: hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
+        case 1: hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
+        case 2: hipLaunchKernelGGL(screen_kernel<2>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
+        case 3: hipLaunchKernelGGL(screen_kernel<3>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
+        case 4: hipLaunchKernelGGL(screen_kernel<4>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
+        default: hipLaunchKernelGGL(screen_kernel<5>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
       }
       GMAT_HIP(hipGetLastError());
-      GMAT_HIP(hipEventRecord(ev[2], e->s));
-      GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, e->s));
-      GMAT_HIP(hipStreamSynchronize(e->s));
+      GMAT_HIP(hipEventRecord(ev[2], sm));
+      GMAT_HIP(hipEventRecord(screen_end[b], sm));
+      GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+      // next launch's side terms overlap this screen
+      if (attempt == 0 && li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1));
+      GMAT_HIP(hipStreamSynchronize(sm));
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left, then redo this one
       GMAT_CHECK(attempt == 0 && pending > 0, GMAT_E_OVERFLOW,
@@ -985,25 +1056,26 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
                  "use the pair test", count, (long long)e->cand_cap);
       GMAT_TRY(flush(pending));
       pending = 0;
-      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
     pending = (int64_t)count;
-    float ms01, ms12;
-    GMAT_HIP(hipEventElapsedTime(&ms01, ev[0], ev[1]));
-    GMAT_HIP(hipEventElapsedTime(&ms12, ev[1], ev[2]));
-    t_side += ms01 * 1e-3;
-    t_screen += ms12 * 1e-3;
+    float ms_side, ms_screen;
+    GMAT_HIP(hipEventSynchronize(side_end[b]));
+    GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
+    GMAT_HIP(hipEventElapsedTime(&ms_screen, ev[7], ev[2]));
+    t_side += ms_side * 1e-3;
+    t_screen += ms_screen * 1e-3;
     // int8 MFMA ops: per tile and slice, sum over K-blocks of (n_pad-K)/32 k-steps x 32 MFMAs x 65536
     ops += (double)ntiles * S * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
     ++launches_done;
     if (pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));
       pending = 0;
-      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, e->s));
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
   }
+  GMAT_HIP(hipStreamSynchronize(S2));
   GMAT_TRY(flush(pending));
-  for (auto &x : ev) (void)hipEventDestroy(x);
   // sort hits by (i, j)
   std::vector<int64_t> ord(e->hit_i.size());
   std::iota(ord.begin(), ord.end(), 0);
