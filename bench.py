@@ -121,6 +121,41 @@ def grm_bench(n, m_grm, seed, reps=5):
             "int8_tops": st[1] / kern / 1e12}
 
 
+def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
+    """Effect-only screen (the remma_epiAA_eff_cpu replacement) over the
+    same cohort, threshold from the exact variance median of 20,000 random pairs as
+    remma_epiAA_approx does.  Algorithmic 2n flop per pair; f64 MFMA roof."""
+    import ctypes
+    import tempfile
+    from scipy.stats import chi2
+    from gmat_amd import _native as N
+    lib = N.ensure_device()
+    rng = np.random.Generator(np.random.PCG64(seed + 5))
+    i = rng.integers(0, m - 1, 40000)
+    j = rng.integers(0, m, 40000)
+    keep = i < j
+    pr = np.column_stack([i[keep], j[keep]])[:20000]
+    _, var, _, _ = plan.pairs("AA", pr)
+    eff_cut = np.array([np.sqrt(chi2.isf(p_cut, 1) * np.median(var))])
+    rows = np.arange(m - 1, dtype=np.int64)
+    pyn = N.f64(py)
+    nh = ctypes.c_int64()
+    st = np.zeros(4)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "eff").encode()
+        t0 = time.perf_counter()
+        N.check(lib.gmat_eff_scan(g.handle, N.GMAT_AA, N.ptr(pyn), N.ptr(rows), rows.size, N.ptr(eff_cut), None, None,
+                                  out, ctypes.byref(nh)), "gmat_eff_scan")
+        wall = time.perf_counter() - t0
+    N.check(lib.gmat_eff_stats(N.ptr(st)), "gmat_eff_stats")
+    pairs = st[0]
+    return {"config": "remma_epiAA_eff over all %d pairs, eff_cut from the median var (p_cut=%g)" % (pairs, p_cut),
+            "pairs_per_s_device": pairs / st[2], "pairs_per_s_end_to_end": pairs / wall, "device_s": st[2],
+            "text_s": st[3], "hits": int(nh.value),
+            "fp64_tflops_algorithmic": pairs * 2.0 * n / st[2] / 1e12,
+            "reference_c_8_threads_pairs_per_s": 3.3e6}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +168,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-grm", action="store_true")
+    ap.add_argument("--no-eff", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
 
@@ -210,6 +246,9 @@ def main():
     grm = None
     if rank == 0 and not args.no_grm:
         grm = grm_bench(n, 20000, args.seed)
+    eff = None
+    if rank == 0 and ws == 1 and not args.no_eff:
+        eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed)
     if rank == 0:
         value = total_pairs * args.steps / t_max
         out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,
@@ -220,7 +259,7 @@ def main():
                           "n_id": n, "n_snp": m, "p_cut": args.p_cut, "kind": "AA",
                           "parallelism": "rows folded over %d rank(s) (parallel=[N,k] split), backend %s"
                                          % (ws, backend or "single")},
-               "roofline": roofline, "cpu_baseline": cpu, "grm": grm,
+               "roofline": roofline, "cpu_baseline": cpu, "grm": grm, "eff_screen": eff,
                "scan": {"hits_per_step": hits_all, "candidates_per_step": cands_all,
                         "screen_s_per_step_rank0": screen_s / args.steps, "side_s_per_step_rank0": side_s / args.steps,
                         "refine_s_per_step_rank0": ref_s / args.steps}}

@@ -291,3 +291,26 @@ def test_repeated_records_and_prediction(tiny_dir, tmp_path):
     re = np.loadtxt(out + ".rand_eff")
     assert re.shape == (150, 2)
     np.testing.assert_allclose(re, rep["rand_eff"], rtol=1e-5, atol=1e-10)
+
+
+def test_scan_large_n(tmp_path):
+    """n = 4,133 (n_pad 4,224 > 4,096: deeper K-loops, larger epilogue sums) on a 400-SNP
+    cohort: every kind on stratified rows vs the oracle; also the plan's pair kernel."""
+    from oracle import gmat_oracle as O
+    from gmat_amd import synth
+    from gmat_amd.remma._scan import EpiPlan
+    from gmat_amd.plink import Geno
+    prefix = str(tmp_path / "big")
+    synth.make_cohort(prefix, 4133, 400, seed=17)
+    snp = O.read_plink(prefix)
+    ka = O.agmat(snp)
+    y, x, col, nid = O.design_matrix(prefix + ".pheno", prefix)
+    pvp, py = O.projection(y, x, col, nid, [ka, ka * ka], [0.4, 0.2, 0.4])
+    rows = np.array([0, 3, 150, 398])
+    with Geno(prefix) as g, EpiPlan(g, pvp, py[:, 0]) as plan:
+        for kind in ("AA", "DD", "AD"):
+            hi, hj, eff, var_, chi, p = plan.scan(kind, rows, 0.2)
+            exp = O.epi_scan(kind, snp, pvp, py, snp_lst_0=rows, p_cut=0.2)
+            assert hi.size == exp.shape[0] and hi.size > 20, (kind, hi.size, exp.shape)
+            np.testing.assert_array_equal(np.column_stack([hi, hj]), exp[:, :2].astype(np.int64))
+            np.testing.assert_allclose(np.column_stack([eff, chi, p]), exp[:, 2:], rtol=1e-8, atol=1e-300)
