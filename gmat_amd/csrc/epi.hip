@@ -965,7 +965,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   auto enqueue_side = [&](size_t li, int b) -> int {
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
-    const int64_t ncol = m - ln.j_lo;
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
     GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -974,11 +973,22 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, drows[b].as<int64_t>(),
                        L.Lp.as<double>(), L.L3.as<double>(), lp, bl[b].as<double>(), ba[b].as<int8_t>());
     GMAT_HIP(hipGetLastError());
-    // E1/E3 = [L'; L3]_band . b_j ;  E2 = a_band . R'_j
-    GMAT_TRY(dgemm_i8b(S2, 2 * Rn, ncol, n_pad, 1.0, DView{bl[b].as<double>(), n_pad, 0},
-                       I8View{rp + ln.j_lo * n_pad, n_pad, 1}, 0.0, e13[b].as<double>(), m));
-    GMAT_TRY(dgemm_i8a(S2, Rn, ncol, n_pad, 1.0, I8View{ba[b].as<int8_t>(), n_pad, 0},
-                       DView{R.Rp.as<double>() + ln.j_lo * n_pad, n_pad, 1}, 0.0, e2[b].as<double>(), m));
+    // E1/E3 = [L'; L3]_band . b_j ;  E2 = a_band . R'_j, per group of 64 rows (one GEMM tile
+    // row) from the group's first needed column: a folded launch's second chunk needs far
+    // fewer columns than its first (triangle), so this skips ~1/3 of the side work.
+    for (int g0 = 0; g0 < Rn; g0 += 64) {
+      const int gn = std::min(64, Rn - g0);
+      const int64_t jg = tri ? std::max<int64_t>(ln.j_lo, ln.rows[g0] + 1) : ln.j_lo;
+      const int64_t nc = m - jg, coff = jg - ln.j_lo;
+      if (nc <= 0) continue;
+      for (int part = 0; part < 2; ++part)  // L' rows, then L3 rows
+        GMAT_TRY(dgemm_i8b(S2, gn, nc, n_pad, 1.0, DView{bl[b].as<double>() + (int64_t)(part * Rn + g0) * n_pad, n_pad, 0},
+                           I8View{rp + jg * n_pad, n_pad, 1}, 0.0, e13[b].as<double>() + (int64_t)(part * Rn + g0) * m + coff,
+                           m));
+      GMAT_TRY(dgemm_i8a(S2, gn, nc, n_pad, 1.0, I8View{ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0},
+                         DView{R.Rp.as<double>() + jg * n_pad, n_pad, 1}, 0.0, e2[b].as<double>() + (int64_t)g0 * m + coff,
+                         m));
+    }
     GMAT_HIP(hipEventRecord(side_end[b], S2));
     return GMAT_OK;
   };
