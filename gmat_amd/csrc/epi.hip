@@ -39,6 +39,7 @@ constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b1
 constexpr int BI = 8;    // first-SNP rows per screen tile
 constexpr int BJ = 32;   // second-SNP columns per screen tile
 constexpr int ROWS_PER_LAUNCH = 128;
+constexpr int SIDE_T = 3;  // int8 slices of the O(n)-per-pair side vectors (21 bits)
 
 // w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
 // j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
@@ -61,7 +62,13 @@ struct ScreenArgs {
   int n_rows;
   const int *tiles;  // (row offset, J) pairs
   int tri;           // 1: only j > i
-  const double *e13, *e2;
+  // side terms as int32 products of int8 slices (SIDE_T slices, slice stride in elements):
+  // E1 = sL[i] sum_t 128^-t c13[t][ri], E3 = sL3[i] sum_t 128^-t c13[t][R+ri],
+  // E2 = sR[j] sum_t 128^-t c2[t][ri]; slicing error bounds side_eps * scale * code sum
+  const int *c13, *c2;
+  int64_t c13_stride, c2_stride;
+  const double *sL, *sL3, *sR, *csum_l, *csum_r;
+  double side_eps;
   int64_t ld_e, j_lo;
   const double *alpha, *qa, *ra, *sa;
   const double *beta, *qb, *rb, *sb;
@@ -294,9 +301,17 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const int ri = roff + 2 * w + t;
     const double M = (double)(tot[t] + other) * a.scale_main;
     const double sumw2 = (double)(sw[t] + osw);
-    const double E1 = a.e13[(int64_t)ri * a.ld_e + (j - a.j_lo)];
-    const double E3 = a.e13[(int64_t)(a.n_rows + ri) * a.ld_e + (j - a.j_lo)];
-    const double E2 = a.e2[(int64_t)ri * a.ld_e + (j - a.j_lo)];
+    const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+    double c1 = 0.0, c3 = 0.0, c2 = 0.0;
+#pragma unroll
+    for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
+      c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
+      c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+      c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
+    }
+    const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, E2 = a.sR[j] * c2;
+    const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
+                 dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
     const double al = a.alpha[i], be = a.beta[j];
     const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
                  t5 = al * al * a.qb[j], t6 = -2.0 * al * al * be * a.rb[j], t7 = al * al * be * be * a.zz;
@@ -304,8 +319,9 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
     const double slack = 1e-12 * (fabs(M) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
     // |w'(P - P~)w| <= ||P - P~||_2 * |w|^2  (a.delta = rigorous upper bound of the spectral norm)
-    const double var_lo = var - a.delta * sumw2 - slack;
-    const bool cand = !(var_lo > 0.0) || eff * eff * (1.0 + 1e-9) >= a.chi_cut * var_lo;
+    const double var_lo = var - a.delta * sumw2 - slack - 2.0 * fabs(be) * dE1 - 2.0 * fabs(al) * dE2;
+    const double eff_hi = fabs(eff) + dE3;
+    const bool cand = !(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * var_lo;
     if (cand) {
       const unsigned long long k = atomicAdd(a.counter, 1ULL);
       if ((int64_t)k < a.cap) {
@@ -547,16 +563,105 @@ __global__ __launch_bounds__(256) void right_side_kernel(int64_t n_pad, const in
   }
 }
 
-// gather band rows: BL[t] = Lp[rows[t]], BL[R+t] = L3[rows[t]], BA[t] = panel[rows[t]]
-__global__ void gather_band_kernel(int64_t n_pad, int R, const int64_t *rows, const double *Lp, const double *L3,
-                                   const int8_t *panel, double *BL, int8_t *BA) {
-  const int t = blockIdx.x;
-  const int64_t src = rows[t];
-  for (int64_t q = threadIdx.x; q < n_pad; q += blockDim.x) {
-    BL[(int64_t)t * n_pad + q] = Lp[src * n_pad + q];
-    BL[(int64_t)(R + t) * n_pad + q] = L3[src * n_pad + q];
-    BA[(int64_t)t * n_pad + q] = panel[src * n_pad + q];
+// Per-row int8 slices of an fp64 [rows][n_pad] matrix: v = s (sum_{t<T} 128^-t Q_t + r) with
+// s = max|v|/127, |Q_0| <= 127, |Q_t| <= 64, |r| <= 0.5 * 128^-(T-1) (+ fp64 rounding).
+__global__ __launch_bounds__(256) void quantize_rows_kernel(int64_t n_pad, int64_t slice_stride, const double *v,
+                                                            int8_t *q, double *scale) {
+  const int64_t j = blockIdx.x;
+  const double *row = v + j * n_pad;
+  double mx = 0.0;
+  for (int64_t k = threadIdx.x; k < n_pad; k += 256) mx = fmax(mx, fabs(row[k]));
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  const double s = mx / 127.0, inv = mx > 0.0 ? 127.0 / mx : 0.0;
+  for (int64_t k = threadIdx.x; k < n_pad; k += 256) {
+    double r = row[k] * inv;
+#pragma unroll
+    for (int t = 0; t < SIDE_T; ++t) {
+      const double qv = rint(r);
+      q[t * slice_stride + j * n_pad + k] = (int8_t)qv;
+      r = (r - qv) * 128.0;
+    }
   }
+  if (threadIdx.x == 0) scale[j] = s;
+}
+
+// gather band rows of the int8 side slices: BL[t][r] = Lq[t][rows[r]], BL[t][R+r] = L3q[t][rows[r]],
+// BA[r] = panel[rows[r]]
+__global__ void gather_band_kernel(int64_t n_pad, int R, int64_t slice_stride, const int64_t *rows, const int8_t *Lq,
+                                   const int8_t *L3q, const int8_t *panel, int8_t *BL, int8_t *BA) {
+  const int r = blockIdx.x;
+  const int64_t src = rows[r];
+  for (int64_t q = threadIdx.x * 16; q < n_pad; q += blockDim.x * 16) {
+#pragma unroll
+    for (int t = 0; t < SIDE_T; ++t) {
+      *(v4i *)&BL[((int64_t)t * 2 * R + r) * n_pad + q] = *(const v4i *)&Lq[t * slice_stride + src * n_pad + q];
+      *(v4i *)&BL[((int64_t)t * 2 * R + R + r) * n_pad + q] = *(const v4i *)&L3q[t * slice_stride + src * n_pad + q];
+    }
+    *(v4i *)&BA[(int64_t)r * n_pad + q] = *(const v4i *)&panel[src * n_pad + q];
+  }
+}
+
+// C[z] (M x N int32, ldc) = A[z] (M x K int8, lda) . B[z]^T (N x K int8, ldb) for z = blockIdx.z;
+// K a multiple of 64.  64 x 128 tile per workgroup, each wave 32 x 64 (two 32x32x32 i8 MFMAs
+// per k-step), 64-deep LDS stages with the 80-byte pitch.  Exact int32 accumulation.
+constexpr int GM = 64, GN = 128, GKK = 64, GPI = 80;
+__global__ __launch_bounds__(256) void i8gemm_nt_kernel(int M, int N, int K, const int8_t *__restrict__ A, int64_t lda,
+                                                        int64_t za, const int8_t *__restrict__ B, int64_t ldb,
+                                                        int64_t zb, int *__restrict__ C, int64_t ldc, int64_t zc) {
+  A += blockIdx.z * za;
+  B += blockIdx.z * zb;
+  C += blockIdx.z * zc;
+  const int m0 = blockIdx.y * GM, n0 = blockIdx.x * GN;
+  __shared__ __attribute__((aligned(16))) int8_t sa[GM * GPI];
+  __shared__ __attribute__((aligned(16))) int8_t sb[GN * GPI];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+  v16i acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0;
+  const int ar = tid >> 2, c16 = (tid & 3) * 16;
+  const v4i zero = {0, 0, 0, 0};
+  for (int k0 = 0; k0 < K; k0 += GKK) {
+    *(v4i *)&sa[ar * GPI + c16] = (m0 + ar < M) ? *(const v4i *)&A[(int64_t)(m0 + ar) * lda + k0 + c16] : zero;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int br = ar + 64 * u;
+      *(v4i *)&sb[br * GPI + c16] = (n0 + br < N) ? *(const v4i *)&B[(int64_t)(n0 + br) * ldb + k0 + c16] : zero;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v4i fa = *(const v4i *)&sa[(wr * 32 + (lane & 31)) * GPI + kk * 32 + (lane >> 5) * 16];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const v4i fb = *(const v4i *)&sb[(wc * 64 + t * 32 + (lane & 31)) * GPI + kk * 32 + (lane >> 5) * 16];
+        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = m0 + wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      const int col = n0 + wc * 64 + t * 32 + (lane & 31);
+      if (row < M && col < N) C[(int64_t)row * ldc + col] = acc[t][e];
+    }
+}
+
+int i8gemm_nt(hipStream_t st, int Z, int M, int N, int K, const int8_t *A, int64_t lda, int64_t za, const int8_t *B,
+              int64_t ldb, int64_t zb, int *C, int64_t ldc, int64_t zc) {
+  if (M <= 0 || N <= 0) return GMAT_OK;
+  hipLaunchKernelGGL(i8gemm_nt_kernel, dim3((unsigned)cdiv(N, GN), (unsigned)cdiv(M, GM), (unsigned)Z), dim3(256), 0,
+                     st, M, N, K, A, lda, za, B, ldb, zb, C, ldc, zc);
+  GMAT_HIP(hipGetLastError());
+  return GMAT_OK;
 }
 
 __global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
@@ -581,7 +686,8 @@ struct Coding {
   bool ready = false;
   DBuf U;                      // P * code panel  [m][n_pad]
   DBuf off;                    // alpha/beta (centring offsets) [m]
-  DBuf Lp, L3, Rp;             // side vectors [m][n_pad]
+  DBuf Lq, L3q, Rq;            // side vectors L', L3, R' as int8 slices [SIDE_T][m][n_pad]
+  DBuf sL, sL3, sR, csum;       // their per-SNP scales; per-SNP code sums
   DBuf qa, ra, sa, qb, rb, sb;  // per-SNP scalars
   DBuf mono;                   // uint8 [m]
 };
@@ -625,11 +731,17 @@ int build_coding(gmat_epi *e, int which) {
     mono[j] = which == 0 ? (sd == 0 || sd == 2 * n || e->g->n_het[j] == n) : (sd == 0 || sd == 2 * n);
   }
   const size_t vb = (size_t)m * n_pad * sizeof(double);
+  DBuf Lp, L3, Rp;  // fp64 side vectors, sliced to int8 below
   GMAT_TRY(cd.U.alloc(vb));
-  GMAT_TRY(cd.Lp.alloc(vb));
-  GMAT_TRY(cd.L3.alloc(vb));
-  GMAT_TRY(cd.Rp.alloc(vb));
-  for (DBuf *b : {&cd.off, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb}) GMAT_TRY(b->alloc(m * sizeof(double)));
+  GMAT_TRY(Lp.alloc(vb));
+  GMAT_TRY(L3.alloc(vb));
+  GMAT_TRY(Rp.alloc(vb));
+  for (DBuf *b : {&cd.off, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb, &cd.sL, &cd.sL3, &cd.sR, &cd.csum})
+    GMAT_TRY(b->alloc(m * sizeof(double)));
+  for (DBuf *b : {&cd.Lq, &cd.L3q, &cd.Rq}) GMAT_TRY(b->alloc((size_t)SIDE_T * m * n_pad));
+  std::vector<double> csum(m);
+  for (int64_t j = 0; j < m; ++j) csum[j] = (double)(which == 0 ? e->g->sum_dose[j] : e->g->n_het[j]);
+  GMAT_HIP(hipMemcpy(cd.csum.p, csum.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_TRY(cd.mono.alloc(m));
   GMAT_HIP(hipMemcpy(cd.off.p, off.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.mono.p, mono.data(), m, hipMemcpyHostToDevice));
@@ -637,13 +749,22 @@ int build_coding(gmat_epi *e, int which) {
   GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
                      cd.U.as<double>(), n_pad));
   hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), cd.Lp.as<double>(),
-                     cd.L3.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
+                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), Lp.as<double>(),
+                     L3.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
   GMAT_HIP(hipGetLastError());
   hipLaunchKernelGGL(right_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), cd.Rp.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), Rp.as<double>(),
                      cd.qb.as<double>(), cd.rb.as<double>(), cd.sb.as<double>());
   GMAT_HIP(hipGetLastError());
+  const int64_t ss = m * n_pad;
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Lp.as<double>(),
+                     cd.Lq.as<int8_t>(), cd.sL.as<double>());
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, L3.as<double>(),
+                     cd.L3q.as<int8_t>(), cd.sL3.as<double>());
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
+                     cd.Rq.as<int8_t>(), cd.sR.as<double>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipStreamSynchronize(e->s));
   cd.U.release();
   cd.ready = true;
   return GMAT_OK;
@@ -852,10 +973,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
-    GMAT_TRY(bl[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad * sizeof(double)));
+    GMAT_TRY(bl[b].alloc((size_t)SIDE_T * 2 * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)ROWS_PER_LAUNCH * n_pad));
-    GMAT_TRY(e13[b].alloc((size_t)2 * ROWS_PER_LAUNCH * m * sizeof(double)));
-    GMAT_TRY(e2[b].alloc((size_t)ROWS_PER_LAUNCH * m * sizeof(double)));
+    GMAT_TRY(e13[b].alloc((size_t)SIDE_T * 2 * ROWS_PER_LAUNCH * m * sizeof(int)));
+    GMAT_TRY(e2[b].alloc((size_t)SIDE_T * ROWS_PER_LAUNCH * m * sizeof(int)));
   }
   if (e->cand_cap == 0) {
     e->cand_cap = 1 << 22;
@@ -970,24 +1091,25 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
                             S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
-    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, drows[b].as<int64_t>(),
-                       L.Lp.as<double>(), L.L3.as<double>(), lp, bl[b].as<double>(), ba[b].as<int8_t>());
+    const int64_t ss = m * n_pad;  // slice stride of the side vectors
+    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, ss, drows[b].as<int64_t>(),
+                       L.Lq.as<int8_t>(), L.L3q.as<int8_t>(), lp, bl[b].as<int8_t>(), ba[b].as<int8_t>());
     GMAT_HIP(hipGetLastError());
-    // E1/E3 = [L'; L3]_band . b_j ;  E2 = a_band . R'_j, per group of 64 rows (one GEMM tile
-    // row) from the group's first needed column: a folded launch's second chunk needs far
-    // fewer columns than its first (triangle), so this skips ~1/3 of the side work.
+    // int32 slice products (int8 MFMA, exact): C13[t] = [L'q_t; L3q_t]_band . b_j,
+    // C2[t] = a_band . R'q_t,j; per group of 64 rows from the group's first needed column (a
+    // folded launch's second chunk needs far fewer columns than its first)
+    const int64_t z13 = (int64_t)2 * Rn * m, z2 = (int64_t)Rn * m;
     for (int g0 = 0; g0 < Rn; g0 += 64) {
       const int gn = std::min(64, Rn - g0);
       const int64_t jg = tri ? std::max<int64_t>(ln.j_lo, ln.rows[g0] + 1) : ln.j_lo;
       const int64_t nc = m - jg, coff = jg - ln.j_lo;
       if (nc <= 0) continue;
       for (int part = 0; part < 2; ++part)  // L' rows, then L3 rows
-        GMAT_TRY(dgemm_i8b(S2, gn, nc, n_pad, 1.0, DView{bl[b].as<double>() + (int64_t)(part * Rn + g0) * n_pad, n_pad, 0},
-                           I8View{rp + jg * n_pad, n_pad, 1}, 0.0, e13[b].as<double>() + (int64_t)(part * Rn + g0) * m + coff,
-                           m));
-      GMAT_TRY(dgemm_i8a(S2, gn, nc, n_pad, 1.0, I8View{ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0},
-                         DView{R.Rp.as<double>() + jg * n_pad, n_pad, 1}, 0.0, e2[b].as<double>() + (int64_t)g0 * m + coff,
-                         m));
+        GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
+                           n_pad, (int64_t)2 * Rn * n_pad, rp + jg * n_pad, n_pad, 0,
+                           e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
+      GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
+                         R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
     }
     GMAT_HIP(hipEventRecord(side_end[b], S2));
     return GMAT_OK;
@@ -1017,8 +1139,17 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.n_rows = Rn;
     sa.tiles = dtiles[b].as<int>();
     sa.tri = tri;
-    sa.e13 = e13[b].as<double>();
-    sa.e2 = e2[b].as<double>();
+    sa.c13 = e13[b].as<int>();
+    sa.c2 = e2[b].as<int>();
+    sa.c13_stride = (int64_t)2 * Rn * m;
+    sa.c2_stride = (int64_t)Rn * m;
+    sa.sL = L.sL.as<double>();
+    sa.sL3 = L.sL3.as<double>();
+    sa.sR = R.sR.as<double>();
+    sa.csum_l = L.csum.as<double>();
+    sa.csum_r = R.csum.as<double>();
+    // per element |v - s sum_t 128^-t Q_t| <= s (0.5 * 128^-(T-1) + fp64 rounding)
+    sa.side_eps = 0.5 * std::pow(128.0, -(SIDE_T - 1)) + 1e-12;
     sa.ld_e = m;
     sa.j_lo = ln.j_lo;
     sa.alpha = L.off.as<double>();
