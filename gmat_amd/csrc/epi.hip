@@ -369,12 +369,15 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
-    for (int64_t k0 = 0; k0 < n_pad; k0 += QK) {
-      // A: P[rb + r][k0 + k], contiguous along k
+    // symmetric P: only column blocks k0 >= rb, the off-diagonal ones counted twice (x2 is
+    // exact); the rb == 0 pass covers every k and also accumulates the eff partials
+    for (int64_t k0 = rb; k0 < n_pad; k0 += QK) {
+      // A: P[rb + r][k0 + k] (x2 beyond the diagonal block), contiguous along k
       {
         const int k = tid & 15, r = tid >> 4;
+        const double f = k0 >= rb + QT ? 2.0 : 1.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) As[k][r + 16 * q] = P[(rb + r + 16 * q) * n_pad + k0 + k];
+        for (int q = 0; q < 4; ++q) As[k][r + 16 * q] = f * P[(rb + r + 16 * q) * n_pad + k0 + k];
       }
       // B: E[k0 + k][col]
       {
