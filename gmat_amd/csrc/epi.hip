@@ -33,13 +33,12 @@ using namespace gmat;
 
 namespace {
 
-constexpr int MT = 128;  // rows of P per K-block
 constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
-constexpr int BI = 8;    // first-SNP rows per screen tile
 constexpr int BJ = 32;   // second-SNP columns per screen tile
 constexpr int ROWS_PER_LAUNCH = 128;
-constexpr int SIDE_T = 3;  // int8 slices of the O(n)-per-pair side vectors (21 bits)
+constexpr int SIDE_T = 3;
+constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)  // int8 slices of the O(n)-per-pair side vectors (21 bits)
 
 // w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
 // j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
@@ -79,16 +78,6 @@ struct ScreenArgs {
   int64_t *cand_i, *cand_j;
 };
 
-// One workgroup = one tile of BI first-SNP rows x BJ second-SNP columns (256 pairs); wave w
-// owns the col tiles of rows 2w, 2w+1 (4 row tiles x 2 col tiles of 32 x 32).
-// Loop nest per tile: slice s -> K-block (MT rows of A_s) -> stage pairs (2 x LK individuals,
-// static LDS double-buffer parity).  The next stage's A band and genotype chunks are fetched
-// with buffer loads (per-lane constant voffset, scalar soffset) while the current stage
-// multiplies, including across K-block and slice boundaries.  The diagonal stage pair is
-// peeled: its MFMAs start from a zero C operand and its genotype chunks are also kept in a
-// ping-pong LDS region (eI/eJ) from which the K-block epilogue rebuilds w[row].
-constexpr int EP = MT + 16;  // epilogue-region pitch (128 individuals + pad)
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
   const uint64_t b = (uint64_t)base;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
@@ -96,11 +85,35 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, in
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)nb, 0x00020000);
 }
 
-// VAR selects tuning variants for in-process A/B runs (GMAT_SCREEN_VARIANT):
-//   bit 0: staging lane map (0 = 4 lanes per row, 1 = 8 rows per 8-lane group)
-//   bit 1: s_setprio(1) around the MFMA clusters
-template <int VAR>
+// Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
+// PB per wave.  SH 0: MT 128, PB 2 -> 8 first SNPs x 32 second SNPs per workgroup; each
+//   generated B fragment feeds 4 MFMAs.
+// SH 1: MT 256, PB 1 -> 4 x 32 per workgroup; each B fragment feeds 8 MFMAs (half the
+//   B-generation VALU per MFMA), same 128 accumulator registers.
+template <int SH>
+struct Shape {
+  static constexpr int MT = SH ? 256 : 128;
+  static constexpr int PB = SH ? 1 : 2;
+  static constexpr int BI = 4 * PB;      // first-SNP rows per tile
+  static constexpr int RB = MT / 32;     // 32-row accumulator blocks per wave
+  static constexpr int EP = MT + 16;     // epilogue-region pitch
+  static constexpr int NA = MT / 64;     // 16-byte A chunks per thread per stage
+  static constexpr int DS = MT / LK;     // diagonal-block stages per K-block
+};
+
+// One workgroup = one tile of BI first-SNP rows x BJ second-SNP columns; wave w owns the 32-wide
+// column tiles of first-SNP rows PB*w .. PB*w+PB-1 (RB row tiles x PB col tiles of 32 x 32).
+// Loop nest per tile: slice s -> K-block (MT rows of A_s) -> stage pairs (2 x LK individuals,
+// static LDS double-buffer parity).  The next stage's A band and genotype chunks are fetched
+// with buffer loads (per-lane constant voffset, scalar soffset) while the current stage
+// multiplies, including across K-block and slice boundaries.  The first stage pair of a K-block
+// is peeled (its MFMAs start from a zero C operand); the genotype chunks of the diagonal-block
+// stages are also kept in a ping-pong LDS region (eI/eJ) from which the K-block epilogue
+// rebuilds w[row].
+template <int SH>
 __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
+  using S_ = Shape<SH>;
+  constexpr int MT = S_::MT, PB = S_::PB, BI = S_::BI, RB = S_::RB, EP = S_::EP, NA = S_::NA, DS = S_::DS;
   __shared__ __attribute__((aligned(16))) int8_t sA[2][MT * AP];
   __shared__ __attribute__((aligned(16))) int8_t sI[2][BI * AP];
   __shared__ __attribute__((aligned(16))) int8_t sJ[2][BJ * AP];
@@ -115,97 +128,94 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(a.slices, a.slices_bytes);
   const __amdgpu_buffer_rsrc_t rsP = make_rsrc(a.panels, a.panels_bytes);
 
-  int64_t ti[2];
+  int64_t ti[PB];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int r = roff + 2 * w + t;
+  for (int t = 0; t < PB; ++t) {
+    const int r = roff + PB * w + t;
     ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
   }
-  // staging roles: two 16-byte A chunks per thread, one genotype chunk for tid < 160
-  // staging lanes: each group of 8 consecutive lanes writes 8 different rows at one 16-byte
-  // column (conflict-free ds_write_b128 with the 80-byte pitch) and 4 such groups read 8
-  // rows x 64 contiguous bytes from global memory
-  const int arow0 = (VAR & 1) ? (lane & 7) + 8 * (lane >> 5) + 16 * w : tid >> 2;
-  const int acol0 = (VAR & 1) ? ((lane >> 3) & 3) * 16 : (tid & 3) * 16;
-  const int arow1 = arow0 + 64;
-  const int voffA0 = arow0 * n_pad + acol0, voffA1 = arow1 * n_pad + acol0;
-  int prow = 0, pcol = 0, pside = 0;  // 1 = i-panel (offset coded), 2 = j-panel
-  unsigned voffP = 0xFFFFFFF0u;       // out of range -> the buffer load returns zeros
-  if (tid < 32) {
+  // staging roles: NA 16-byte A chunks per thread (rows tid/4 + 64u), one genotype chunk for
+  // the first 4*(BI+BJ) threads (i-side rows first, offset-coded when stored)
+  const int arow0 = tid >> 2, acol0 = (tid & 3) * 16;
+  int voffA[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) voffA[u] = (arow0 + 64 * u) * n_pad + acol0;
+  int prow = 0, pcol = (tid & 3) * 16, pside = 0;  // 1 = i-panel (offset coded), 2 = j-panel
+  unsigned voffP = 0xFFFFFFF0u;                     // out of range -> the buffer load returns zeros
+  if (tid < 4 * BI) {
     pside = 1;
-    prow = (VAR & 1) ? tid & 7 : tid >> 2;
-    pcol = (VAR & 1) ? ((tid >> 3) & 3) * 16 : (tid & 3) * 16;
+    prow = tid >> 2;
     const int r = roff + prow;
     if (r < a.n_rows) voffP = (unsigned)(a.left_off + a.rows[r] * n_pad + pcol);
-  } else if (tid < 160) {
+  } else if (tid < 4 * (BI + BJ)) {
     pside = 2;
-    const int u = tid - 32;
-    prow = (VAR & 1) ? (u & 7) + 8 * (u >> 5) : u >> 2;
-    pcol = (VAR & 1) ? ((u >> 3) & 3) * 16 : (u & 3) * 16;
+    prow = (tid - 4 * BI) >> 2;
     if (J0 + prow < a.m) voffP = (unsigned)(a.right_off + (J0 + prow) * n_pad + pcol);
   }
 
-  v4i ra0, ra1, rp = {0, 0, 0, 0};
+  v4i ra[NA], rp = {0, 0, 0, 0};
   // fetch stage (A band at scalar byte offset soffA, genotype chunk at individual L)
   auto load = [&](int soffA, int L) __attribute__((always_inline)) {
-    ra0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA0, soffA, 0);
-    ra1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA1, soffA, 0);
+#pragma unroll
+    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA[u], soffA, 0);
     if (pside) rp = __builtin_amdgcn_raw_buffer_load_b128(rsP, voffP, L, 0);
   };
   // write the fetched stage into buffer b; epi >= 0: also into epilogue region at column epi
-  auto store_set = [&](int b, int epi, int region, const v4i &x0, const v4i &x1, const v4i &xp)
-                       __attribute__((always_inline)) {
-    *(v4i *)&sA[b][arow0 * AP + acol0] = x0;
-    *(v4i *)&sA[b][arow1 * AP + acol0] = x1;
+  auto store = [&](int b, int epi, int region) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][(arow0 + 64 * u) * AP + acol0] = ra[u];
     if (pside == 1) {
       v4i o;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)xp[q]);
+      for (int q = 0; q < 4; ++q) o[q] = (int)to_offset((unsigned)rp[q]);
       *(v4i *)&sI[b][prow * AP + pcol] = o;
       if (epi >= 0) *(v4i *)&eI[region][prow * EP + epi + pcol] = o;
     } else if (pside == 2) {
-      *(v4i *)&sJ[b][prow * AP + pcol] = xp;
-      if (epi >= 0) *(v4i *)&eJ[region][prow * EP + epi + pcol] = xp;
+      *(v4i *)&sJ[b][prow * AP + pcol] = rp;
+      if (epi >= 0) *(v4i *)&eJ[region][prow * EP + epi + pcol] = rp;
     }
   };
-  auto store = [&](int b, int epi, int region) __attribute__((always_inline)) { store_set(b, epi, region, ra0, ra1, rp); };
 
-  v16i acc[4][2];
+  v16i acc[RB][PB];
   // one 32-deep k-step on buffer b: B fragments w = a_i*b_j generated from the staged
   // genotype chunks, A fragments from the staged band
   auto kstep = [&](int b, int kk, bool diag, bool zero) __attribute__((always_inline)) {
     const unsigned tlo = diag ? T_LO : T2_LO, thi = diag ? T_HI : T2_HI;
-    v4i fb[2];
+    v4i fb[PB];
+    const v4i v = *(const v4i *)&sJ[b][c * AP + kk * 32 + 16 * h];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const v4i o = *(const v4i *)&sI[b][(2 * w + t) * AP + kk * 32 + 16 * h];
-      const v4i v = *(const v4i *)&sJ[b][c * AP + kk * 32 + 16 * h];
+    for (int t = 0; t < PB; ++t) {
+      const v4i o = *(const v4i *)&sI[b][(PB * w + t) * AP + kk * 32 + 16 * h];
 #pragma unroll
       for (int q = 0; q < 4; ++q) fb[t][q] = (int)__builtin_amdgcn_perm(thi, tlo, (unsigned)o[q] + (unsigned)v[q]);
     }
     const v16i z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (VAR & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < RB; ++r) {
       const v4i fa = *(const v4i *)&sA[b][(r * 32 + c) * AP + kk * 32 + 16 * h];
-      acc[r][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[0], zero ? z : acc[r][0], 0, 0, 0);
-      acc[r][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[1], zero ? z : acc[r][1], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < PB; ++t)
+        acc[r][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[t], zero ? z : acc[r][t], 0, 0, 0);
     }
-    if (VAR & 2) __builtin_amdgcn_s_setprio(0);
   };
 
-  int64_t tot[2] = {0, 0};
-  unsigned sw[2] = {0, 0};
+  int64_t tot[PB];
+  unsigned sw[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    tot[t] = 0;
+    sw[t] = 0;
+  }
   // epilogue: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage slot 16h+e of
   // each 32-row tile, whose genotype bytes sit in the LDS epilogue region (24-bit products:
   // |acc| <= 127 * 8 * n_pad < 2^23 for n_pad <= 8192)
   auto epilogue = [&](int region, int shift, bool first_slice) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < PB; ++t) {
       int64_t part64 = 0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const v4i o = *(const v4i *)&eI[region][(2 * w + t) * EP + r * 32 + 16 * h];
+      for (int r = 0; r < RB; ++r) {
+        const v4i o = *(const v4i *)&eI[region][(PB * w + t) * EP + r * 32 + 16 * h];
         const v4i v = *(const v4i *)&eJ[region][c * EP + r * 32 + 16 * h];
         int part = 0;
 #pragma unroll
@@ -221,26 +231,16 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     }
   };
 
-  // second staging register set for two-stage-deep prefetch (VAR & 4)
-  v4i rb0 = {0, 0, 0, 0}, rb1 = {0, 0, 0, 0}, rq = {0, 0, 0, 0};
-  auto loadB = [&](int soffA, int L) __attribute__((always_inline)) {
-    rb0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA0, soffA, 0);
-    rb1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA1, soffA, 0);
-    if (pside) rq = __builtin_amdgcn_raw_buffer_load_b128(rsP, voffP, L, 0);
-  };
-  constexpr bool DEEP = (VAR & 4) != 0;
-
   int gk = 0;  // K-blocks done (epilogue region parity)
   load(0, 0);
   store(0, 0, 0);
-  if (DEEP) loadB(LK, LK);  // stage 1 (the first K-block always has >= 2 stages)
   __syncthreads();
   for (int s = 0; s < a.n_slice; ++s) {
     const int shift = 7 * (a.n_slice - 1 - s);
     for (int kb = 0; kb < nK; ++kb) {
       const int K = kb * MT;
       const int row0 = s * nn + K * n_pad;  // byte offset of row K of A_s
-      const int nst = 2 * (nK - kb);
+      const int nst = (nK - kb) * DS;
       int nxtA = -1, nxtL = 0;  // first stage of the next K-block (or slice)
       if (kb + 1 < nK) {
         nxtA = row0 + MT * n_pad + K + MT;
@@ -249,30 +249,18 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
         nxtA = (s + 1) * nn;
         nxtL = 0;
       }
-      // stage pair (st, st+1): st in LDS buffer 0, st+1 in buffer 1.
-      // DEEP: set A (ra*) carries even stages, set B (rb*) odd stages, each issued two
-      // stages before its LDS store; otherwise set A carries every stage, one ahead.
+      // stage pair (st, st+1): st in LDS buffer 0, st+1 in buffer 1; stages < DS are the
+      // diagonal block (table T, epilogue copies), later ones count twice (table 2T)
       auto pair = [&](int st, bool diag, bool zero) __attribute__((always_inline)) {
         const int L0 = K + st * LK;
         const bool last = (st + 2 == nst);
-        if (DEEP) {
-          if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
-          else if (nxtA >= 0) load(nxtA, nxtL);
-        } else {
-          load(row0 + L0 + LK, L0 + LK);
-        }
+        load(row0 + L0 + LK, L0 + LK);
         kstep(0, 0, diag, zero);
         kstep(0, 1, diag, false);
-        if (DEEP) store_set(1, (st + 1 < 2) ? (st + 1) * LK : -1, gk & 1, rb0, rb1, rq);
-        else store(1, (st + 1 < 2) ? (st + 1) * LK : -1, gk & 1);
+        store(1, (st + 1 < DS) ? (st + 1) * LK : -1, gk & 1);
         __syncthreads();
-        if (DEEP) {
-          if (!last) loadB(row0 + L0 + 3 * LK, L0 + 3 * LK);
-          else if (nxtA >= 0) loadB(nxtA + LK, nxtL + LK);
-        } else {
-          if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
-          else if (nxtA >= 0) load(nxtA, nxtL);
-        }
+        if (!last) load(row0 + L0 + 2 * LK, L0 + 2 * LK);
+        else if (nxtA >= 0) load(nxtA, nxtL);
         kstep(1, 0, diag, false);
         kstep(1, 1, diag, false);
         if (last) {
@@ -280,25 +268,27 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
           ++gk;
           if (nxtA >= 0) store(0, 0, gk & 1);
         } else {
-          store(0, -1, 0);
+          store(0, (st + 2 < DS) ? (st + 2) * LK : -1, gk & 1);
         }
         __syncthreads();
       };
       pair(0, true, true);
+#pragma unroll
+      for (int st = 2; st < DS; st += 2) pair(st, true, false);
 #pragma unroll 1
-      for (int st = 2; st < nst; st += 2) pair(st, false, false);
+      for (int st = DS; st < nst; st += 2) pair(st, false, false);
     }
   }
   // combine the two lane halves (disjoint rows of the same column), then test
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < PB; ++t) {
     const int64_t other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
     const int64_t i = ti[t], j = J0 + c;
     if (j >= a.m || (a.tri && j <= i)) continue;
     if (a.mono_l[i] || a.mono_r[j]) continue;  // x == 0: the reference's statistic is NaN
-    const int ri = roff + 2 * w + t;
+    const int ri = roff + PB * w + t;
     const double M = (double)(tot[t] + other) * a.scale_main;
     const double sumw2 = (double)(sw[t] + osw);
     const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
@@ -942,7 +932,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int tri = (kind != GMAT_AD);
   const char *venv = getenv("GMAT_SCREEN_VARIANT");
-  const int variant = venv ? atoi(venv) : 0;
+  // tile shape of the screen (Shape<SH>); GMAT_SCREEN_VARIANT overrides for A/B runs
+  const int shape = venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE;
+  const int BI = shape ? Shape<1>::BI : Shape<0>::BI, MT = shape ? Shape<1>::MT : Shape<0>::MT;
+  GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   for (double &v : e->stats) v = 0.0;
   e->hit_i.clear();
   e->hit_j.clear();
@@ -1178,14 +1171,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     for (int attempt = 0;; ++attempt) {
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
-      switch (variant) {
-        case 0: hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-        case 1: hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-        case 2: hipLaunchKernelGGL(screen_kernel<2>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-        case 3: hipLaunchKernelGGL(screen_kernel<3>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-        case 4: hipLaunchKernelGGL(screen_kernel<4>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-        default: hipLaunchKernelGGL(screen_kernel<5>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa); break;
-      }
+      if (shape)
+        hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
+      else
+        hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ev[2], sm));
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
@@ -1209,8 +1198,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipEventElapsedTime(&ms_screen, ev[7], ev[2]));
     t_side += ms_side * 1e-3;
     t_screen += ms_screen * 1e-3;
-    // int8 MFMA ops: per tile and slice, sum over K-blocks of (n_pad-K)/32 k-steps x 32 MFMAs x 65536
-    ops += (double)ntiles * S * (double)n_pad * (double)(n_pad / MT + 1) * 32768.0;
+    // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
+    // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
+    ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
     if (pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));

@@ -12,7 +12,7 @@ __host__ __device__ inline int perm_nat(int q) { return (q & 3) + 8 * ((q & 15) 
 
 struct gmat_geno {
   int64_t n = 0, m = 0;  // individuals, SNPs
-  int64_t n_pad = 0;     // individuals padded to a multiple of 128 (zero genotypes)
+  int64_t n_pad = 0;     // individuals padded to a multiple of 256 (zero genotypes)
   int64_t nb = 0;        // packed bytes per SNP (ceil(n/4))
   gmat::DBuf packed;     // m * nb, PLINK order
   gmat::DBuf panels;     // int8 [2][m][n_pad]: dosage 0/1/2 (missing stored as 0), then the

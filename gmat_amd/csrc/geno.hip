@@ -169,7 +169,7 @@ extern "C" int gmat_geno_create(gmat_geno **out, const uint8_t *bed_body, int64_
   g->n = n_id;
   g->m = n_snp;
   g->nb = nb;
-  g->n_pad = round_up(n_id, 128);
+  g->n_pad = round_up(n_id, 256);
   int rc = g->packed.alloc(nb * n_snp);
   if (rc == GMAT_OK) rc = g->panels.alloc(2 * g->n_pad * n_snp);
   DBuf cnt;
