@@ -239,10 +239,54 @@ def repeated(gmat, work, out_tiny):
              rand_eff=np.loadtxt(os.path.join(work, "pred.rand_eff")))
 
 
+def maf_eff(gmat, work, out_mouse):
+    """Per-frequency-class effect screens (remma_epi{AA,AD,DD}_maf_eff, C print_out*_maf) on mouse
+    rows 0..199: classes computed as the _maf_approx pipelines do, a fixed 111-entry
+    denominator table (so the thresholds are known), p_cut 1e-2."""
+    from gmat.gmatrix import agmat, dgmat_as
+    from gmat.remma.remma_epiAA.remma_epiAA_maf_eff import remma_epiAA_maf_eff
+    from gmat.remma.remma_epiAD.remma_epiAD_maf_eff import remma_epiAD_maf_eff
+    from gmat.remma.remma_epiDD.remma_epiDD_maf_eff import remma_epiDD_maf_eff
+    from gmat.process_plink.process_plink import read_plink
+    for f in ("plink.bed", "plink.bim", "plink.fam", "pheno"):
+        shutil.copy(os.path.join(MOUSE, f), work)
+    bed = os.path.join(work, "plink")
+    pheno = os.path.join(work, "pheno")
+    a, _ = agmat(bed)
+    d, _ = dgmat_as(bed)
+    ref = np.load(os.path.join(out_mouse, "reml.npz"))
+    snp = read_plink(bed)
+    n = snp.shape[0]
+    f_aa = 1 - np.sum(snp, axis=0) / (2 * n)
+    f_aa[f_aa > 0.5] = 1 - f_aa[f_aa > 0.5]
+    f_aa = np.array(list(map(np.longlong, f_aa * 20)), dtype=np.longlong)
+    f_d = np.sum(np.absolute(snp - 1.0) < 0.001, axis=0) / n
+    f_d[f_d > 0.5] = 1 - f_d[f_d > 0.5]
+    f_d = np.array(f_d * 20, dtype=np.longlong)
+    f_a = np.sum(snp, axis=0) / (2 * n)
+    f_a[f_a > 0.5] = 1 - f_a[f_a > 0.5]
+    f_a = np.array(f_a * 20, dtype=np.longlong)
+    k = np.arange(111)
+    rows = list(range(200))
+    g2, g5 = [a, a * a], [a, d, a * a, a * d, d * d]
+    cwd = os.getcwd()
+    os.chdir(work)
+    try:
+        remma_epiAA_maf_eff(pheno, bed, g2, ref["var2"], snp_lst_0=rows, freq=f_aa, freq_deno=1470.0 * (0.8 + 0.004 * k),
+                            p_cut=1e-2, out_file=os.path.join(out_mouse, "epiAA_maf_eff_rows200"))
+        remma_epiDD_maf_eff(pheno, bed, g5, ref["var5"], snp_lst_0=rows, freq=f_d, freq_deno=490.0 * (0.8 + 0.004 * k),
+                            p_cut=1e-2, out_file=os.path.join(out_mouse, "epiDD_maf_eff_rows200"))
+        remma_epiAD_maf_eff(pheno, bed, g5, ref["var5"], snp_lst_0=rows, freqA=f_a, freqD=f_d,
+                            freq_deno=960.0 * (0.8 + 0.004 * k), p_cut=1e-2,
+                            out_file=os.path.join(out_mouse, "epiAD_maf_eff_rows200"))
+    finally:
+        os.chdir(cwd)
+
+
 def main():
     gmat = import_reference()
     logging.getLogger().setLevel(logging.WARNING)
-    what = sys.argv[1:] or ["tiny", "mouse", "singles", "repeated"]
+    what = sys.argv[1:] or ["tiny", "mouse", "singles", "repeated", "maf"]
     if "tiny" in what:
         with tempfile.TemporaryDirectory() as work:
             tiny(gmat, work, os.path.join(HERE, "tiny"))
@@ -252,6 +296,9 @@ def main():
     if "singles" in what:
         with tempfile.TemporaryDirectory() as work:
             singles(gmat, work, os.path.join(HERE, "mouse"), os.path.join(HERE, "tiny"))
+    if "maf" in what:
+        with tempfile.TemporaryDirectory() as work:
+            maf_eff(gmat, work, os.path.join(HERE, "mouse"))
     if "repeated" in what:
         with tempfile.TemporaryDirectory() as work:
             repeated(gmat, work, os.path.join(HERE, "tiny"))

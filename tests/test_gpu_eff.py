@@ -279,3 +279,38 @@ def test_single_snp_golden(mouse, kind, tmp_path):
     assert np.all(np.abs(gv[noise, 0]) < 1e-12)
     np.testing.assert_array_equal(np.isnan(gv[~noise]), np.isnan(ev[~noise]))
     np.testing.assert_allclose(gv[~noise], ev[~noise], rtol=1e-8, atol=1e-14)
+
+
+@pytest.mark.parametrize("kind,base", [("AA", 1470.0), ("AD", 960.0), ("DD", 490.0)])
+def test_mouse_maf_eff_golden(mouse, kind, base, tmp_path):
+    """remma_epiXX_maf_eff (per-class thresholds) on mouse rows 0..199 against the reference's
+    files: same pair sets, eff %g text, chi_app / p_app from each line's own classes."""
+    import importlib
+    from oracle import gmat_oracle as O
+    prefix, g2, g5, var2, var5 = mouse
+    fi, fj = O.maf_classes(kind, O.read_plink(prefix))
+    deno = base * (0.8 + 0.004 * np.arange(111))
+    mod = importlib.import_module("gmat_amd.remma.remma_epi%s" % kind)
+    fn = getattr(mod, "remma_epi%s_maf_eff" % kind)
+    out = str(tmp_path / kind)
+    kw = dict(freqA=fi, freqD=fj) if kind == "AD" else dict(freq=fi)
+    cwd = os.getcwd()
+    os.chdir(str(tmp_path))
+    try:
+        assert fn(prefix.replace("plink", "pheno"), prefix, g2 if kind == "AA" else g5, var2 if kind == "AA" else var5,
+                  snp_lst_0=list(range(200)), freq_deno=deno, p_cut=1e-2, out_file=out, **kw) == 0
+    finally:
+        os.chdir(cwd)
+    if kind != "AD":
+        assert os.path.exists(str(tmp_path / "eff_cut"))  # written to the working directory, as the reference
+    hdr, got = _read_eff(out)
+    ehdr, exp = _read_eff(os.path.join(MOUSE, "epi%s_maf_eff_rows200" % kind))
+    assert hdr == ehdr
+    gd = {(a[0], a[1]): a[2:] for a in got}
+    ed = {(a[0], a[1]): a[2:] for a in exp}
+    assert set(gd) == set(ed) and len(gd) > 1000
+    same = 0
+    for k, cols in gd.items():
+        assert float(cols[0]) == pytest.approx(float(ed[k][0]), rel=5e-6)
+        same += cols == ed[k]
+    assert same >= 0.99 * len(gd)

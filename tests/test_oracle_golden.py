@@ -240,3 +240,25 @@ def test_repeated_records_golden(tiny):
     np.testing.assert_allclose(var, rep["pred_var"], rtol=1e-7)
     re = O.predict_random(y, x, col, nid, [a, a * a], rep["pred_var"])
     np.testing.assert_allclose(re, rep["rand_eff"], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind,base", [("AA", 1470.0), ("AD", 960.0), ("DD", 490.0)])
+def test_mouse_maf_eff_screen_golden(mouse_eff_inputs, kind, base):
+    """The per-class effect screens (print_out*_maf, _remma_epi_eff_cpu.c:141-166, :318-348,
+    :500-522) and their post-processing (denominator of each written line from its own
+    columns, remma_epiAD_maf_eff.py:102) with the classes of the _maf_approx pipelines."""
+    from scipy.stats import chi2
+    dec, py2, py5 = mouse_eff_inputs
+    snp = O.read_plink(os.path.join(MOUSE_DATA, "plink"))
+    fi, fj = O.maf_classes(kind, snp)
+    deno = base * (0.8 + 0.004 * np.arange(111))
+    cut = np.sqrt(chi2.isf(1e-2, 1) * deno)
+    got = O.epi_eff_screen(kind, dec, py2 if kind == "AA" else py5, range(200), cut, freq_i=fi, freq_j=fj)
+    hdr, exp = _eff_golden("epi%s_maf_eff_rows200" % kind)
+    assert hdr == "snp_0 snp_1 eff chi_app p_app"
+    got_d = {(int(i), int(j)): e for i, j, e in got}
+    assert len(exp) > 1000 and set(got_d) == set(exp)
+    for (i, j), cols in exp.items():
+        assert abs(float(cols[0]) - got_d[(i, j)]) <= 5e-6 * abs(got_d[(i, j)])
+        chi_app = float(float(cols[0]) * float(cols[0]) / deno[fi[i] * 10 + fj[j]])
+        assert cols[1] == repr(chi_app) and cols[2] == repr(float(chi2.sf(chi_app, 1)))
