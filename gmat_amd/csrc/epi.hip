@@ -7,16 +7,21 @@
 // chi = eff^2/var, p = chi2.sf(chi, 1), and keeps p < p_cut.
 //
 // Here the scan runs in two passes:
-//  1. SCREEN.  With w = a_i o b_j (integers 0..4) the quadratic form expands into
-//       e'Pe = w'Pw - 2 beta L'_i.b_j - 2 alpha a_i.R'_j + (per-SNP and constant terms),
+//  1. SCREEN.  The screen codes count the MINOR allele (a~ = 2 - a when 2p > 1, which only
+//     flips the sign of x and leaves e'Pe unchanged), so w = a~_i o b~_j (integers 0..4)
+//     stays small.  The quadratic form expands into
+//       e'Pe = w'P_off w + sum_q P_qq w_q^2 - 2 beta L'_i.b_j - 2 alpha a_i.R'_j + (per-SNP
+//              and constant terms),
 //     L'_i = a_i o (P a_i - alpha_i P1),  R'_j = x_j o (P b_j).
-//     The O(n^2)-per-pair term w'Pw is evaluated EXACTLY for a sliced P:
-//       P ~ (pmax/127) sum_s 128^-s A_s,  A_s int8,
+//     The O(n^2)-per-pair term w'P_off w (P without its diagonal) is evaluated EXACTLY for a
+//     sliced P_off:
+//       P_off ~ (qmax/127) sum_s 128^-s A_s,  A_s int8,  qmax = max |P_kl| (k != l),
 //     as integer quadratic forms on v_mfma_i32_32x32x32_i8 (int32 accumulation, int64
 //     combination -- bit-deterministic), using the symmetry of A_s to visit only the
-//     block-upper half.  The O(n)-per-pair side terms are fp64 MFMA GEMMs.  The slicing
-//     error is bounded rigorously by delta * (sum w)^2, so every pair that COULD have
-//     p < p_cut becomes a candidate.
+//     block-upper half.  The O(n)-per-pair side terms (diagonal included) are int8-sliced
+//     MFMA GEMMs.  The slicing error is bounded rigorously by delta * sum w^2, so every pair
+//     that COULD have p < p_cut becomes a candidate.  Minor-allele codes and the diagonal
+//     split make the one-slice bound tight enough for small p_cut (half the MFMA work of two).
 //  2. REFINE.  Candidates are re-evaluated exactly as the reference does (fp64 e = x_i*x_j,
 //     var = e'Pe on f64 MFMA, p = erfc(sqrt(chi/2))) and the hits are kept.
 // The reported statistics therefore come from the same fp64 formula as the reference;
@@ -37,8 +42,9 @@ constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
 constexpr int ROWS_PER_LAUNCH = 128;
-constexpr int SIDE_T = 3;
-constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)  // int8 slices of the O(n)-per-pair side vectors (21 bits)
+constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
+constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
+constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)
 
 // w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
 // j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
@@ -63,10 +69,11 @@ struct ScreenArgs {
   int tri;           // 1: only j > i
   // side terms as int32 products of int8 slices (SIDE_T slices, slice stride in elements):
   // E1 = sL[i] sum_t 128^-t c13[t][ri], E3 = sL3[i] sum_t 128^-t c13[t][R+ri],
+  // Ed = sLd[i] sum_t 128^-t c13[t][2R+ri] (= sum_q P_qq a_q^2 b_q^2),
   // E2 = sR[j] sum_t 128^-t c2[t][ri]; slicing error bounds side_eps * scale * code sum
   const int *c13, *c2;
   int64_t c13_stride, c2_stride;
-  const double *sL, *sL3, *sR, *csum_l, *csum_r;
+  const double *sL, *sL3, *sLd, *sR, *csum_l, *csum_r, *csq_r;
   double side_eps;
   int64_t ld_e, j_lo;
   const double *alpha, *qa, *ra, *sa;
@@ -291,25 +298,28 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const int ri = roff + PB * w + t;
     const double M = (double)(tot[t] + other) * a.scale_main;
     const double sumw2 = (double)(sw[t] + osw);
-    const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-    double c1 = 0.0, c3 = 0.0, c2 = 0.0;
+    const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e,
+                  od = o3 + (int64_t)a.n_rows * a.ld_e;
+    double c1 = 0.0, c3 = 0.0, cd = 0.0, c2 = 0.0;
 #pragma unroll
     for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
       c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
       c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+      cd = cd * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + od];
       c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
     }
-    const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, E2 = a.sR[j] * c2;
+    const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, Ed = a.sLd[i] * cd, E2 = a.sR[j] * c2;
     const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
-                 dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
+                 dEd = a.side_eps * a.sLd[i] * a.csq_r[j], dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
     const double al = a.alpha[i], be = a.beta[j];
     const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
                  t5 = al * al * a.qb[j], t6 = -2.0 * al * al * be * a.rb[j], t7 = al * al * be * be * a.zz;
-    const double var = M + t1 + t2 + t3 + t4 + t5 + t6 + t7;
+    const double var = M + Ed + t1 + t2 + t3 + t4 + t5 + t6 + t7;
     const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-    const double slack = 1e-12 * (fabs(M) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
+    const double slack =
+        1e-12 * (fabs(M) + fabs(Ed) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
     // |w'(P - P~)w| <= ||P - P~||_2 * |w|^2  (a.delta = rigorous upper bound of the spectral norm)
-    const double var_lo = var - a.delta * sumw2 - slack - 2.0 * fabs(be) * dE1 - 2.0 * fabs(al) * dE2;
+    const double var_lo = var - a.delta * sumw2 - slack - 2.0 * fabs(be) * dE1 - 2.0 * fabs(al) * dE2 - dEd;
     const double eff_hi = fabs(eff) + dE3;
     const bool cand = !(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * var_lo;
     if (cand) {
@@ -460,14 +470,15 @@ __global__ void permute_vec_kernel(int64_t n, int64_t n_pad, const double *v, do
   const int64_t r = (q & ~31LL) + perm_nat((int)(q & 31));
   vs[q] = (r < n) ? v[r] : 0.0;
 }
-// slices A_s[rho][t] (rho natural row, t storage column) of P*127/pmax
+// slices A_s[rho][t] (rho natural row, t storage column) of P_off*127/qmax (zero diagonal:
+// the diagonal enters the screen exactly, as a side term)
 __global__ void slice_kernel(int64_t n, int64_t n_pad, const double *P, double inv_unit, int n_slice,
                              int8_t *slices) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n_pad * n_pad) return;
   const int64_t rho = idx / n_pad, t = idx % n_pad;
   const int64_t c = (t & ~31LL) + perm_nat((int)(t & 31));
-  double r = (rho < n && c < n) ? P[rho * n + c] * inv_unit : 0.0;
+  double r = (rho < n && c < n && rho != c) ? P[rho * n + c] * inv_unit : 0.0;
   for (int s = 0; s < n_slice; ++s) {
     const double q = rint(r);
     slices[(int64_t)s * n_pad * n_pad + idx] = (int8_t)q;
@@ -475,23 +486,23 @@ __global__ void slice_kernel(int64_t n, int64_t n_pad, const double *P, double i
   }
 }
 
-// residual of the slicing, R = P - P~ (natural order, zero padded), scaled by 1/rscale
+// residual of the slicing, R = P_off - P~ (natural order, zero padded and zero diagonal), scaled
 __global__ void residual_kernel(int64_t n, int64_t n_pad, const double *P, double inv_unit, int n_slice,
                                 double out_scale, double *R) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n_pad * n_pad) return;
   const int64_t r0 = idx / n_pad, c0 = idx % n_pad;
-  double r = (r0 < n && c0 < n) ? P[r0 * n + c0] * inv_unit : 0.0;
+  double r = (r0 < n && c0 < n && r0 != c0) ? P[r0 * n + c0] * inv_unit : 0.0;
   for (int s = 0; s < n_slice; ++s) r = (r - rint(r)) * 128.0;
   R[idx] = r * out_scale;
 }
 
-// per-SNP side vectors for the left coding: L' = a o (u - alpha z), L3 = a o py, and
-// scalars qa = a.u, ra = a.z, sa = a.py.  One workgroup per SNP.
+// per-SNP side vectors for the left coding: L' = a o (u - alpha z), L3 = a o py,
+// Ld = diag(P) o a o a, and scalars qa = a.u, ra = a.z, sa = a.py.  One workgroup per SNP.
 __global__ __launch_bounds__(256) void left_side_kernel(int64_t n_pad, const int8_t *panel, const double *U,
-                                                        const double *z, const double *py, const double *alpha,
-                                                        double *Lp, double *L3, double *qa, double *ra,
-                                                        double *sa) {
+                                                        const double *z, const double *py, const double *dg,
+                                                        const double *alpha, double *Lp, double *L3, double *Ld,
+                                                        double *qa, double *ra, double *sa) {
   const int64_t j = blockIdx.x;
   const double al = alpha[j];
   double s1 = 0, s2 = 0, s3 = 0;
@@ -500,6 +511,7 @@ __global__ __launch_bounds__(256) void left_side_kernel(int64_t n_pad, const int
     const double u = U[j * n_pad + q];
     Lp[j * n_pad + q] = av * (u - al * z[q]);
     L3[j * n_pad + q] = av * py[q];
+    Ld[j * n_pad + q] = av * av * dg[q];
     s1 += av * u;
     s2 += av * z[q];
     s3 += av * py[q];
@@ -583,16 +595,19 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(int64_t n_pad, int64
 }
 
 // gather band rows of the int8 side slices: BL[t][r] = Lq[t][rows[r]], BL[t][R+r] = L3q[t][rows[r]],
-// BA[r] = panel[rows[r]]
+// BL[t][2R+r] = Ldq[t][rows[r]], BA[r] = panel[rows[r]]
 __global__ void gather_band_kernel(int64_t n_pad, int R, int64_t slice_stride, const int64_t *rows, const int8_t *Lq,
-                                   const int8_t *L3q, const int8_t *panel, int8_t *BL, int8_t *BA) {
+                                   const int8_t *L3q, const int8_t *Ldq, const int8_t *panel, int8_t *BL,
+                                   int8_t *BA) {
   const int r = blockIdx.x;
   const int64_t src = rows[r];
   for (int64_t q = threadIdx.x * 16; q < n_pad; q += blockDim.x * 16) {
 #pragma unroll
     for (int t = 0; t < SIDE_T; ++t) {
-      *(v4i *)&BL[((int64_t)t * 2 * R + r) * n_pad + q] = *(const v4i *)&Lq[t * slice_stride + src * n_pad + q];
-      *(v4i *)&BL[((int64_t)t * 2 * R + R + r) * n_pad + q] = *(const v4i *)&L3q[t * slice_stride + src * n_pad + q];
+      const int64_t o = (int64_t)t * SIDE_P * R + r, so = t * slice_stride + src * n_pad + q;
+      *(v4i *)&BL[o * n_pad + q] = *(const v4i *)&Lq[so];
+      *(v4i *)&BL[(o + R) * n_pad + q] = *(const v4i *)&L3q[so];
+      *(v4i *)&BL[(o + 2 * R) * n_pad + q] = *(const v4i *)&Ldq[so];
     }
     *(v4i *)&BA[(int64_t)r * n_pad + q] = *(const v4i *)&panel[src * n_pad + q];
   }
@@ -657,6 +672,25 @@ int i8gemm_nt(hipStream_t st, int Z, int M, int N, int K, const int8_t *A, int64
   return GMAT_OK;
 }
 
+// screen panel of the additive coding: minor-allele dosage a~ = flip ? 2 - a : a (padding stays
+// 0), and its square a~^2 in {0, 1, 4}
+__global__ void flip_panel_kernel(int64_t n, int64_t n_pad, int64_t m, const int8_t *src, const uint8_t *flip,
+                                  int8_t *dst, int8_t *sq) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= m * n_pad) return;
+  const int64_t j = idx / n_pad, q = idx % n_pad;
+  const int64_t nat = (q & ~31LL) + perm_nat((int)(q & 31));
+  const int a = src[idx];
+  const int v = (flip[j] && nat < n) ? 2 - a : a;
+  dst[idx] = (int8_t)v;
+  sq[idx] = (int8_t)(v * v);
+}
+
+__global__ void diag_kernel(int64_t n_pad, const double *Ps, double *dg) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n_pad) dg[q] = Ps[q * n_pad + q];
+}
+
 __global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -677,21 +711,24 @@ double now() {
 
 struct Coding {
   bool ready = false;
-  DBuf U;                      // P * code panel  [m][n_pad]
-  DBuf off;                    // alpha/beta (centring offsets) [m]
-  DBuf Lq, L3q, Rq;            // side vectors L', L3, R' as int8 slices [SIDE_T][m][n_pad]
-  DBuf sL, sL3, sR, csum;       // their per-SNP scales; per-SNP code sums
-  DBuf qa, ra, sa, qb, rb, sb;  // per-SNP scalars
-  DBuf mono;                   // uint8 [m]
+  DBuf U;                         // P * screen code panel  [m][n_pad]
+  DBuf off;                       // alpha/beta of the reference codes (refine) [m]
+  DBuf soff;                      // centring offsets of the screen codes [m]
+  DBuf sq;                        // squared screen codes (additive coding only) [m][n_pad]
+  DBuf Lq, L3q, Ldq, Rq;          // side vectors L', L3, Ld, R' as int8 slices [SIDE_T][m][n_pad]
+  DBuf sL, sL3, sLd, sR, csum, csq;  // their per-SNP scales; per-SNP sums of codes / squared codes
+  DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
+  DBuf mono;                      // uint8 [m]
 };
 
 struct gmat_epi {
   gmat_geno *g = nullptr;
   int64_t n = 0, n_pad = 0, m = 0;
   int n_slice = 3;
-  double pmax = 0, zz = 0, spy = 0;
-  double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P - sum_{s<S} A_s 128^-s pmax/127||_2
-  DBuf Ps, py, z, slices;
+  double qmax = 0, zz = 0, spy = 0;
+  double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2
+  DBuf Ps, py, z, dg, slices;
+  DBuf spanels;  // screen codes, one allocation: [0] minor-allele dosage, [1] heterozygote [m][n_pad]
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
@@ -709,44 +746,75 @@ struct gmat_epi {
 
 namespace {
 
+// screen panel of a coding (inside e->spanels) and its squared codes (B operand of the Ld term)
+const int8_t *screen_panel(const gmat_epi *e, int which) { return e->spanels.as<int8_t>() + which * e->m * e->n_pad; }
+const int8_t *screen_sq(const gmat_epi *e, int which) {
+  return which == 0 ? e->code[0].sq.as<int8_t>() : screen_panel(e, 1);  // 0/1 codes: a^2 = a
+}
+
 int build_coding(gmat_epi *e, int which) {
   Coding &cd = e->code[which];
   if (cd.ready) return GMAT_OK;
   const int64_t m = e->m, n_pad = e->n_pad, n = e->n;
-  const int8_t *panel = which == 0 ? e->g->dose_ptr() : e->g->het_ptr();
-  // centring offsets exactly as the reference: freq = sum/(2n); A: 2*freq, D: 2*freq*(1-freq)
-  std::vector<double> off(m);
-  std::vector<uint8_t> mono(m);
+  // centring offsets exactly as the reference (for the refine): freq = sum/(2n); A: 2*freq,
+  // D: 2*freq*(1-freq).  Screen codes: the additive coding counts the minor allele
+  // (a~ = 2 - a, offset 2(1 - freq), when freq > 1/2); the heterozygote coding is unchanged.
+  std::vector<double> off(m), soff(m), csum(m), csq(m);
+  std::vector<uint8_t> mono(m), flip(m);
   for (int64_t j = 0; j < m; ++j) {
-    const double freq = (double)e->g->sum_dose[j] / (2.0 * (double)n);
+    const int64_t sd = e->g->sum_dose[j], nh = e->g->n_het[j], n2 = (sd - nh) / 2, n0 = n - nh - n2;
+    const double freq = (double)sd / (2.0 * (double)n);
     off[j] = which == 0 ? 2.0 * freq : 2.0 * freq * (1.0 - freq);
-    const int64_t sd = e->g->sum_dose[j];
-    mono[j] = which == 0 ? (sd == 0 || sd == 2 * n || e->g->n_het[j] == n) : (sd == 0 || sd == 2 * n);
+    mono[j] = which == 0 ? (sd == 0 || sd == 2 * n || nh == n) : (sd == 0 || sd == 2 * n);
+    if (which == 0) {
+      flip[j] = sd > n;
+      soff[j] = flip[j] ? 2.0 * ((double)(2 * n - sd) / (2.0 * (double)n)) : off[j];
+      csum[j] = (double)(flip[j] ? 2 * n - sd : sd);
+      csq[j] = (double)(nh + 4 * (flip[j] ? n0 : n2));
+    } else {
+      soff[j] = off[j];
+      csum[j] = csq[j] = (double)nh;
+    }
+  }
+  int8_t *panel = e->spanels.as<int8_t>() + which * m * n_pad;
+  if (which == 0) {
+    DBuf dflip;
+    GMAT_TRY(dflip.alloc(m));
+    GMAT_TRY(cd.sq.alloc((size_t)m * n_pad));
+    GMAT_HIP(hipMemcpy(dflip.p, flip.data(), m, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(flip_panel_kernel, dim3((unsigned)cdiv(m * n_pad, 256)), dim3(256), 0, e->s, n, n_pad, m,
+                       e->g->dose_ptr(), dflip.as<uint8_t>(), panel, cd.sq.as<int8_t>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipStreamSynchronize(e->s));
+  } else {
+    GMAT_HIP(hipMemcpyAsync(panel, e->g->het_ptr(), (size_t)m * n_pad, hipMemcpyDeviceToDevice, e->s));
   }
   const size_t vb = (size_t)m * n_pad * sizeof(double);
-  DBuf Lp, L3, Rp;  // fp64 side vectors, sliced to int8 below
+  DBuf Lp, L3, Ld, Rp;  // fp64 side vectors, sliced to int8 below
   GMAT_TRY(cd.U.alloc(vb));
   GMAT_TRY(Lp.alloc(vb));
   GMAT_TRY(L3.alloc(vb));
+  GMAT_TRY(Ld.alloc(vb));
   GMAT_TRY(Rp.alloc(vb));
-  for (DBuf *b : {&cd.off, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb, &cd.sL, &cd.sL3, &cd.sR, &cd.csum})
+  for (DBuf *b : {&cd.off, &cd.soff, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb, &cd.sL, &cd.sL3, &cd.sLd, &cd.sR,
+                  &cd.csum, &cd.csq})
     GMAT_TRY(b->alloc(m * sizeof(double)));
-  for (DBuf *b : {&cd.Lq, &cd.L3q, &cd.Rq}) GMAT_TRY(b->alloc((size_t)SIDE_T * m * n_pad));
-  std::vector<double> csum(m);
-  for (int64_t j = 0; j < m; ++j) csum[j] = (double)(which == 0 ? e->g->sum_dose[j] : e->g->n_het[j]);
+  for (DBuf *b : {&cd.Lq, &cd.L3q, &cd.Ldq, &cd.Rq}) GMAT_TRY(b->alloc((size_t)SIDE_T * m * n_pad));
   GMAT_HIP(hipMemcpy(cd.csum.p, csum.data(), m * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(cd.csq.p, csq.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_TRY(cd.mono.alloc(m));
   GMAT_HIP(hipMemcpy(cd.off.p, off.data(), m * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(cd.soff.p, soff.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.mono.p, mono.data(), m, hipMemcpyHostToDevice));
   // U[j][q] = sum_q' panel[j][q'] P[q'][q]
   GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
                      cd.U.as<double>(), n_pad));
   hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), Lp.as<double>(),
-                     L3.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
+                     e->z.as<double>(), e->py.as<double>(), e->dg.as<double>(), cd.soff.as<double>(), Lp.as<double>(),
+                     L3.as<double>(), Ld.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
   GMAT_HIP(hipGetLastError());
   hipLaunchKernelGGL(right_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), cd.off.as<double>(), Rp.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), cd.soff.as<double>(), Rp.as<double>(),
                      cd.qb.as<double>(), cd.rb.as<double>(), cd.sb.as<double>());
   GMAT_HIP(hipGetLastError());
   const int64_t ss = m * n_pad;
@@ -754,6 +822,8 @@ int build_coding(gmat_epi *e, int which) {
                      cd.Lq.as<int8_t>(), cd.sL.as<double>());
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, L3.as<double>(),
                      cd.L3q.as<int8_t>(), cd.sL3.as<double>());
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Ld.as<double>(),
+                     cd.Ldq.as<int8_t>(), cd.sLd.as<double>());
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
                      cd.Rq.as<int8_t>(), cd.sR.as<double>());
   GMAT_HIP(hipGetLastError());
@@ -784,7 +854,7 @@ void kind_codings(int kind, int *lc, int *rc) {
 
 extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
   GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
-  GMAT_CHECK(n_slice >= 2 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 2..4");
+  GMAT_CHECK(n_slice >= 1 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 1..4");
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
   GMAT_CHECK(g->n_pad <= 8192 && 2 * g->m * g->n_pad < (1LL << 32), GMAT_E_ARG,
              "gmat_epi_create: supports n_id <= 8192 and 2 * n_snp * n_pad < 2^32 (32-bit buffer offsets)");
@@ -795,9 +865,14 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   e->m = g->m;
   e->n_slice = n_slice;
   const int64_t n = e->n, n_pad = e->n_pad;
-  double pmax = 0.0;
-  for (int64_t i = 0; i < n * n; ++i) pmax = std::max(pmax, std::fabs(pvp[i]));
-  e->pmax = pmax;
+  double pmax = 0.0, qmax = 0.0;  // max |P|, max |P_kl| off the diagonal
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t k = 0; k < n; ++k) {
+      const double v = std::fabs(pvp[i * n + k]);
+      pmax = std::max(pmax, v);
+      if (k != i) qmax = std::max(qmax, v);
+    }
+  e->qmax = qmax;
   double spy = 0.0;
   for (int64_t i = 0; i < n; ++i) spy += py[i];
   e->spy = spy;
@@ -809,7 +884,8 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   };
   if ((rc = dp.alloc(n * n * sizeof(double))) || (rc = dv.alloc(n * sizeof(double))) ||
       (rc = e->Ps.alloc(n_pad * n_pad * sizeof(double))) || (rc = e->py.alloc(n_pad * sizeof(double))) ||
-      (rc = e->z.alloc(n_pad * sizeof(double))) || (rc = e->slices.alloc((size_t)n_slice * n_pad * n_pad)))
+      (rc = e->z.alloc(n_pad * sizeof(double))) || (rc = e->dg.alloc(n_pad * sizeof(double))) ||
+      (rc = e->slices.alloc((size_t)n_slice * n_pad * n_pad)) || (rc = e->spanels.alloc((size_t)2 * e->m * n_pad)))
     return fail(rc);
   if (hipMemcpy(dp.p, pvp, n * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(dv.p, py, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
@@ -820,18 +896,20 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   hipLaunchKernelGGL(permute_p_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), e->Ps.as<double>());
   hipLaunchKernelGGL(permute_vec_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n, n_pad, dv.as<double>(),
                      e->py.as<double>());
-  const double unit = pmax > 0 ? 127.0 / pmax : 1.0;
+  const double unit = qmax > 0 ? 127.0 / qmax : 1.0;
   hipLaunchKernelGGL(slice_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, n_slice,
                      e->slices.as<int8_t>());
   hipLaunchKernelGGL(zsum_kernel, dim3((unsigned)cdiv(n_pad, 4)), dim3(256), 0, 0, n_pad, e->Ps.as<double>(),
                      e->z.as<double>());
+  hipLaunchKernelGGL(diag_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n_pad, e->Ps.as<double>(),
+                     e->dg.as<double>());
   if (hipGetLastError() != hipSuccess) {
     set_error("gmat_epi_create: setup kernels failed");
     return fail(GMAT_E_HIP);
   }
   // ||R||_2 <= ||R^16||_F^(1/16) (R symmetric): four fp64 MFMA squarings of R scaled to
   // unit max entry (|R_kl| <= 0.5 * 128^-(S-1) / unit), for every usable slice count S
-  for (int S = 2; S <= n_slice; ++S) {
+  for (int S = 1; S <= n_slice; ++S) {
     const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
     DBuf r1, r2, rows;
     if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
@@ -928,8 +1006,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_TRY(build_coding(e, lc));
   GMAT_TRY(build_coding(e, rc));
   const Coding &L = e->code[lc], &R = e->code[rc];
-  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();  // reference codes (refine)
   const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc), *srq = screen_sq(e, rc);  // screen codes
   const int tri = (kind != GMAT_AD);
   const char *venv = getenv("GMAT_SCREEN_VARIANT");
   // tile shape of the screen (Shape<SH>); GMAT_SCREEN_VARIANT overrides for A/B runs
@@ -955,11 +1034,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) rws.push_back(rows[t]);
     launches.push_back(rws);
   }
-  // slices used: 2 when the candidate band of the 2-slice bound stays thin (small p_cut), else all
-  const int S = n_slice > 0 ? n_slice : (p_cut <= 1e-4 ? 2 : e->n_slice);
-  GMAT_CHECK(S >= 2 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [2, %d]", S, e->n_slice);
-  const double scale_main = e->pmax / 127.0 * std::pow(128.0, -(S - 1));
-  const double delta = e->rho[S];
+  // slices used: 1 when the candidate band of the one-slice bound stays thin (small p_cut), 2 up
+  // to p_cut 1e-2, else all; a launch whose candidates overflow the buffer is redone with one
+  // more slice (and the scan keeps it)
+  int S = n_slice > 0 ? n_slice : std::min(e->n_slice, p_cut <= 1e-4 ? 1 : (p_cut <= 1e-2 ? 2 : 4));
+  GMAT_CHECK(S >= 1 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
+  int S_max_used = S;
 
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
@@ -969,9 +1049,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
-    GMAT_TRY(bl[b].alloc((size_t)SIDE_T * 2 * ROWS_PER_LAUNCH * n_pad));
+    GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)ROWS_PER_LAUNCH * n_pad));
-    GMAT_TRY(e13[b].alloc((size_t)SIDE_T * 2 * ROWS_PER_LAUNCH * m * sizeof(int)));
+    GMAT_TRY(e13[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * m * sizeof(int)));
     GMAT_TRY(e2[b].alloc((size_t)SIDE_T * ROWS_PER_LAUNCH * m * sizeof(int)));
   }
   if (e->cand_cap == 0) {
@@ -1089,20 +1169,21 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
     const int64_t ss = m * n_pad;  // slice stride of the side vectors
     hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, ss, drows[b].as<int64_t>(),
-                       L.Lq.as<int8_t>(), L.L3q.as<int8_t>(), lp, bl[b].as<int8_t>(), ba[b].as<int8_t>());
+                       L.Lq.as<int8_t>(), L.L3q.as<int8_t>(), L.Ldq.as<int8_t>(), slp, bl[b].as<int8_t>(),
+                       ba[b].as<int8_t>());
     GMAT_HIP(hipGetLastError());
-    // int32 slice products (int8 MFMA, exact): C13[t] = [L'q_t; L3q_t]_band . b_j,
-    // C2[t] = a_band . R'q_t,j; per group of 64 rows from the group's first needed column (a
-    // folded launch's second chunk needs far fewer columns than its first)
-    const int64_t z13 = (int64_t)2 * Rn * m, z2 = (int64_t)Rn * m;
+    // int32 slice products (int8 MFMA, exact): C13[t] = [L'q_t; L3q_t]_band . b_j and
+    // Ldq_t,band . b_j^2, C2[t] = a_band . R'q_t,j; per group of 64 rows from the group's first
+    // needed column (a folded launch's second chunk needs far fewer columns than its first)
+    const int64_t z13 = (int64_t)SIDE_P * Rn * m, z2 = (int64_t)Rn * m;
     for (int g0 = 0; g0 < Rn; g0 += 64) {
       const int gn = std::min(64, Rn - g0);
       const int64_t jg = tri ? std::max<int64_t>(ln.j_lo, ln.rows[g0] + 1) : ln.j_lo;
       const int64_t nc = m - jg, coff = jg - ln.j_lo;
       if (nc <= 0) continue;
-      for (int part = 0; part < 2; ++part)  // L' rows, then L3 rows
+      for (int part = 0; part < SIDE_P; ++part)  // L' rows, L3 rows (x b), Ld rows (x b^2)
         GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
-                           n_pad, (int64_t)2 * Rn * n_pad, rp + jg * n_pad, n_pad, 0,
+                           n_pad, (int64_t)SIDE_P * Rn * n_pad, (part == 2 ? srq : srp) + jg * n_pad, n_pad, 0,
                            e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
       GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
                          R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
@@ -1122,14 +1203,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     ScreenArgs sa;
     sa.slices = e->slices.as<int8_t>();
     sa.slices_bytes = (int64_t)e->n_slice * n_pad * n_pad;
-    sa.panels = e->g->panels.as<int8_t>();
+    sa.panels = e->spanels.as<int8_t>();
     sa.panels_bytes = 2 * m * n_pad;
     sa.left_off = lc == 0 ? 0 : m * n_pad;
     sa.right_off = rc == 0 ? 0 : m * n_pad;
     sa.n_pad = n_pad;
-    sa.n_slice = S;
-    sa.left = lp;
-    sa.right = rp;
+    sa.left = slp;
+    sa.right = srp;
     sa.m = m;
     sa.rows = drows[b].as<int64_t>();
     sa.n_rows = Rn;
@@ -1137,22 +1217,24 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.tri = tri;
     sa.c13 = e13[b].as<int>();
     sa.c2 = e2[b].as<int>();
-    sa.c13_stride = (int64_t)2 * Rn * m;
+    sa.c13_stride = (int64_t)SIDE_P * Rn * m;
     sa.c2_stride = (int64_t)Rn * m;
     sa.sL = L.sL.as<double>();
     sa.sL3 = L.sL3.as<double>();
+    sa.sLd = L.sLd.as<double>();
     sa.sR = R.sR.as<double>();
     sa.csum_l = L.csum.as<double>();
     sa.csum_r = R.csum.as<double>();
+    sa.csq_r = R.csq.as<double>();
     // per element |v - s sum_t 128^-t Q_t| <= s (0.5 * 128^-(T-1) + fp64 rounding)
     sa.side_eps = 0.5 * std::pow(128.0, -(SIDE_T - 1)) + 1e-12;
     sa.ld_e = m;
     sa.j_lo = ln.j_lo;
-    sa.alpha = L.off.as<double>();
+    sa.alpha = L.soff.as<double>();
     sa.qa = L.qa.as<double>();
     sa.ra = L.ra.as<double>();
     sa.sa = L.sa.as<double>();
-    sa.beta = R.off.as<double>();
+    sa.beta = R.soff.as<double>();
     sa.qb = R.qb.as<double>();
     sa.rb = R.rb.as<double>();
     sa.sb = R.sb.as<double>();
@@ -1160,8 +1242,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.mono_r = R.mono.as<uint8_t>();
     sa.zz = e->zz;
     sa.spy = e->spy;
-    sa.scale_main = scale_main;
-    sa.delta = delta;
     sa.chi_cut = chi_cut;
     sa.counter = e->counter.as<unsigned long long>();
     sa.cap = e->cand_cap;
@@ -1169,6 +1249,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cand_j = e->cand_j.as<int64_t>();
     unsigned long long count = 0;
     for (int attempt = 0;; ++attempt) {
+      sa.n_slice = S;
+      sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
+      sa.delta = e->rho[S];
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
       if (shape)
@@ -1183,10 +1266,15 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       if (attempt == 0 && li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1));
       GMAT_HIP(hipStreamSynchronize(sm));
       if ((int64_t)count <= e->cand_cap) break;
-      // overflow in this launch: refine what earlier launches left, then redo this one
-      GMAT_CHECK(attempt == 0 && pending > 0, GMAT_E_OVERFLOW,
-                 "one screen launch produced %llu candidates (capacity %lld): p_cut too large for a scan; "
-                 "use the pair test", count, (long long)e->cand_cap);
+      // overflow in this launch: refine what earlier launches left and redo this one; if it
+      // overflowed on its own, redo it with one more slice (thinner candidate band)
+      if (pending == 0) {
+        GMAT_CHECK(S < e->n_slice, GMAT_E_OVERFLOW,
+                   "one screen launch produced %llu candidates (capacity %lld) with %d slices: p_cut too large "
+                   "for a scan; use the pair test", count, (long long)e->cand_cap, S);
+        ++S;
+        S_max_used = std::max(S_max_used, S);
+      }
       GMAT_TRY(flush(pending));
       pending = 0;
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
@@ -1235,8 +1323,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[5] = t_side;
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
-  e->stats[8] = S;
-  e->stats[9] = delta;
+  e->stats[8] = S_max_used;
+  e->stats[9] = e->rho[S_max_used];
   return GMAT_OK;
 }
 

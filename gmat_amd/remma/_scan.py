@@ -19,7 +19,7 @@ from ..uvlmm.uvlmm_varcom import projection
 KINDS = {"AA": N.GMAT_AA, "AD": N.GMAT_AD, "DD": N.GMAT_DD}
 SCAN_HEADER = "snp_0 snp_1 eff chi p_val"
 PAIR_HEADER = "snp_0 snp_1 eff var chi p"
-N_SLICE = 3  # slices kept; each scan uses 2 or 3 (gmat_epi_scan n_slice=0)
+N_SLICE = 3  # slices kept; each scan uses 1, 2 or 3 by p_cut (gmat_epi_scan n_slice=0)
 
 
 class EpiPlan:

@@ -84,13 +84,14 @@ int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, cons
 /* ---------------------------------------------------------------- epistasis scans
  * A scan plan keeps the genotype panel, P (= Z'PZ) and Py resident in HBM. */
 typedef struct gmat_epi gmat_epi;
-/* n_slice (2..4): int8 slices of P kept for the screen (see gmat_epi_scan). */
+/* n_slice (1..4): int8 slices of P (off the diagonal) kept for the screen (see gmat_epi_scan). */
 int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice);
 /* Exhaustive exact scan over first-SNP rows `rows` (sorted ascending): AA/DD test pairs
  * (i, j>i) (remma_epiAA.py:71-82, remma_epiDD.py:75-86), AD tests (i, all j) including i==j
  * (remma_epiAD.py:76-87).  A pair is a hit when p < p_cut with p = chi2.sf(eff^2/var, 1);
- * chi_cut must be chi2.isf(p_cut, 1).  n_slice: slices the screen uses (0 = automatic: 2 for
- * p_cut <= 1e-4, else all); the hit set does not depend on it.  *n_hits receives the number
+ * chi_cut must be chi2.isf(p_cut, 1).  n_slice: slices the screen uses (0 = automatic: 1 for
+ * p_cut <= 1e-4, 2 for p_cut <= 1e-2, else all kept; a launch whose candidates overflow is redone
+ * with one more); the hit set does not depend on it.  *n_hits receives the number
  * of hits, retrieved with gmat_epi_hits (sorted by (i, j)). */
 int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
                   int n_slice, int64_t *n_hits);

@@ -225,11 +225,12 @@ def test_scan_vs_oracle_rows(synth_cohort):
     pvp, py = O.projection(y, x, col, nid, [ka, ka * ka], var)
     rows = np.array([0, 1, 2, 500, 1499, 2001, 2990, 2998])
     with Geno(prefix) as g, EpiPlan(g, pvp, py[:, 0]) as plan:
-        for kind in ("AA", "DD", "AD"):
-            p_cut = 5e-2
-            hi, hj, eff, var_, chi, p = plan.scan(kind, rows, p_cut)
+        for kind, p_cut, ns in (("AA", 5e-2, 0), ("DD", 5e-2, 0), ("AD", 5e-2, 0), ("AA", 0.5, 1), ("DD", 0.3, 1),
+                                ("AD", 0.5, 1), ("AA", 1e-3, 1)):
+            # forced single-slice screens at large p_cut put most pairs inside the bound's band
+            hi, hj, eff, var_, chi, p = plan.scan(kind, rows, p_cut, n_slice=ns)
             exp = O.epi_scan(kind, snp, pvp, py, snp_lst_0=rows, p_cut=p_cut)
-            assert hi.size == exp.shape[0], (kind, hi.size, exp.shape)
+            assert hi.size == exp.shape[0], (kind, p_cut, ns, hi.size, exp.shape)
             np.testing.assert_array_equal(np.column_stack([hi, hj]), exp[:, :2].astype(np.int64))
             np.testing.assert_allclose(np.column_stack([eff, chi, p]), exp[:, 2:], rtol=1e-8, atol=1e-300)
             # the pair kernel gives the same numbers for the same pairs
@@ -259,7 +260,7 @@ def test_scan_deterministic_and_row_split(synth_cohort):
         for a, b in zip(full, again):
             np.testing.assert_array_equal(a, b)
         # the hit set does not depend on how many int8 slices the screen used
-        for ns in (2, 3):
+        for ns in (1, 2, 3):
             forced = plan.scan("AA", np.arange(m - 1), 1e-3, n_slice=ns)
             assert plan.stats()["n_slice"] == ns
             for a, b in zip(full, forced):
