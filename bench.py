@@ -27,6 +27,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "SNP-pairs tested/sec (whole node) + GRM GFLOP/s, mouse-sized cohort"
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x the 2.5 PF dense bf16), MI355X_MICROARCH.md
+MX_PEAK_TFLOPS = 10000.0  # dense block-scaled fp6/fp4 MFMA (4x bf16 per clock), MI355X_MICROARCH.md
 
 
 def log(*a):
@@ -219,25 +220,33 @@ def main():
     hits_all = dist.allreduce_sum(hits) / args.steps
     cands_all = dist.allreduce_sum(cands) / args.steps
 
-    # roofline of the dominant kernel (screen): algorithmic int8 ops per launch / avg launch time.
-    # per pair the sliced symmetric quadratic form needs S * n * (n + 128) / 2 int8 MACs
+    # roofline of the dominant kernel (screen): algorithmic ops per launch / avg launch time.
+    # Per pair the symmetric quadratic form w'P_off w needs n (n + 128) / 2 MACs per pass: one
+    # pass of fp6 x fp4 MX MFMA (level 0), or S passes of int8 MFMA (level S = slices)
     my_pairs = float(sum(m - 1 - int(i) for i in rows))
-    alg_ops_step = my_pairs * n_slice * n * (n + 128)
+    passes = max(n_slice, 1)
+    alg_ops_step = my_pairs * passes * n * (n + 128)
     avg_launch_s = screen_s / max(launches, 1)
     alg_ops_launch = alg_ops_step * args.steps / max(launches, 1)
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            if tj.get("screen_level", 1) == n_slice:
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TFLOP/s",
-                "frac": achieved / INT8_PEAK_TOPS, "traffic": traffic,
-                "kernel": "screen_kernel (v_mfma_i32_32x32x32_i8)",
-                "ops_note": "int8 ops (TOP/s); algorithmic = S slices x n(n+128)/2 MACs x 2 per pair",
-                "n_slice": n_slice,
-                "issued_int8_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
+    if n_slice == 0:
+        peak, kern = MX_PEAK_TFLOPS, "mx_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
+        note = "fp6 x fp4 ops (TFLOP/s); algorithmic = n(n+128)/2 MACs x 2 per pair, one pass"
+    else:
+        peak, kern = INT8_PEAK_TOPS, "screen_kernel (v_mfma_i32_32x32x32_i8)"
+        note = "int8 ops (TOP/s); algorithmic = S slices x n(n+128)/2 MACs x 2 per pair"
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": traffic, "kernel": kern, "ops_note": note,
+                "screen_level": n_slice,
+                "issued_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
                 "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
 
     cpu = None
@@ -253,7 +262,7 @@ def main():
         value = total_pairs * args.steps / t_max
         out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None, "dtype": "int8/fp64", "data": "synthetic",
+               "scaling": "strong", "vs_baseline": None, "dtype": "fp6xfp4/fp64" if n_slice == 0 else "int8/fp64", "data": "synthetic",
                "config": {"workload": "configs[2]/[3]: exhaustive exact remma_epiAA, synthetic related cohort "
                                       "%d ind x %d SNP, p_cut=%g, %d pairs per step" % (n, m, args.p_cut, total_pairs),
                           "n_id": n, "n_snp": m, "p_cut": args.p_cut, "kind": "AA",

@@ -92,6 +92,44 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, in
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)nb, 0x00020000);
 }
 
+// Candidate test of pair (i, j) (band row ri of the launch) given M = w'P~w (P~ the screen's
+// approximation of P_off) and sum w^2: every pair whose p-value could be below p_cut is kept.
+__device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i, int64_t j, double M, double sumw2) {
+  if (j >= a.m || (a.tri && j <= i)) return;
+  if (a.mono_l[i] || a.mono_r[j]) return;  // x == 0: the reference's statistic is NaN
+  const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e,
+                od = o3 + (int64_t)a.n_rows * a.ld_e;
+  double c1 = 0.0, c3 = 0.0, cd = 0.0, c2 = 0.0;
+#pragma unroll
+  for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
+    c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
+    c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+    cd = cd * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + od];
+    c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
+  }
+  const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, Ed = a.sLd[i] * cd, E2 = a.sR[j] * c2;
+  const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
+               dEd = a.side_eps * a.sLd[i] * a.csq_r[j], dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
+  const double al = a.alpha[i], be = a.beta[j];
+  const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
+               t5 = al * al * a.qb[j], t6 = -2.0 * al * al * be * a.rb[j], t7 = al * al * be * be * a.zz;
+  const double var = M + Ed + t1 + t2 + t3 + t4 + t5 + t6 + t7;
+  const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
+  const double slack =
+      1e-12 * (fabs(M) + fabs(Ed) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
+  // |w'(P_off - P~)w| <= a.delta * |w|^2 (a.delta: rigorous bound of the approximation error)
+  const double var_lo = var - a.delta * sumw2 - slack - 2.0 * fabs(be) * dE1 - 2.0 * fabs(al) * dE2 - dEd;
+  const double eff_hi = fabs(eff) + dE3;
+  const bool cand = !(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * var_lo;
+  if (cand) {
+    const unsigned long long k = atomicAdd(a.counter, 1ULL);
+    if ((int64_t)k < a.cap) {
+      a.cand_i[k] = i;
+      a.cand_j[k] = j;
+    }
+  }
+}
+
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
 // PB per wave.  SH 0: MT 128, PB 2 -> 8 first SNPs x 32 second SNPs per workgroup; each
 //   generated B fragment feeds 4 MFMAs.
@@ -292,43 +330,233 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
     const int64_t other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
-    const int64_t i = ti[t], j = J0 + c;
-    if (j >= a.m || (a.tri && j <= i)) continue;
-    if (a.mono_l[i] || a.mono_r[j]) continue;  // x == 0: the reference's statistic is NaN
-    const int ri = roff + PB * w + t;
-    const double M = (double)(tot[t] + other) * a.scale_main;
-    const double sumw2 = (double)(sw[t] + osw);
-    const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e,
-                  od = o3 + (int64_t)a.n_rows * a.ld_e;
-    double c1 = 0.0, c3 = 0.0, cd = 0.0, c2 = 0.0;
+    cand_test(a, roff + PB * w + t, ti[t], J0 + c, (double)(tot[t] + other) * a.scale_main, (double)(sw[t] + osw));
+  }
+}
+
+// ------------------------------------------------------------------ MX screen (fp6 x fp4)
+// The same screen on the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (fp6 e2m3 x fp4 e2m1,
+// twice the int8 rate).  A = P_off in fp6 with one e8m0 scale per (row, 32 storage columns)
+// (residual ~0.46x that of one int8 slice on relationship matrices: the per-block scale follows
+// the many small entries); B = w/2 in fp4 (w in {0,1,2,4} -> codes 0,1,2,4, so the code IS the
+// integer w), generated per 8 individuals with one v_and + one v_and_or from nibble planes:
+//   i side  M1 = [a == 1] 0xF, M2 = [a == 2] 0xF;  j side  S1 = b, S2 = 2b;
+//   code(w) = (M1 & S1) | (M2 & S2).
+// The B scale restores w (x2) on the diagonal block and 2w (x4) beyond it.  Accumulation is
+// fp32; its rounding is bounded rigorously (gmat_epi_create) and folded into delta.  The
+// epilogue sums w[row] * acc[row] with v_cvt_scalef32_pk_f32_fp4 (two w per instruction, from the
+// same nibble codes) and v_pk_fma_f32; sum w^2 comes from v_dot8_u32_u4.
+//
+// Layouts: A record per (natural row, 128-column stage) = 4 blocks of 24 bytes (32 fp6 codes,
+// code j at bits 6j) in the LDS order of block b at 24 * (2(b&1) + (b>>1)), scales likewise
+// ordered in one dword; genotype nibble records per (SNP, stage) = two 64-byte planes.
+constexpr int MXK = 128;    // individuals per MX stage (= K-block height)
+constexpr int MX_REC = 96;  // fp6 bytes per (row, stage)
+constexpr int MX_AP = 112;  // LDS pitch of an A row record (+ scale dword + pad): conflict-free reads
+constexpr int NB_REC = 128; // nibble bytes per (SNP, stage): two planes
+constexpr int NB_P = 144;   // LDS pitch of a staged nibble record
+constexpr int NB_E = 136;   // LDS pitch of the epilogue copies (8-byte reads)
+constexpr int MX_PB = 2, MX_BI = 4 * MX_PB, MX_RB = MXK / 32;
+
+typedef int v2i_ __attribute__((ext_vector_type(2)));
+typedef int v8i_ __attribute__((ext_vector_type(8)));
+typedef float v16f_ __attribute__((ext_vector_type(16)));
+typedef float v2f_ __attribute__((ext_vector_type(2)));
+
+struct MxArgs {
+  const uint8_t *data;     // [n_pad rows][nK][MX_REC]
+  const uint32_t *scale;   // [n_pad rows][nK]
+  const uint8_t *nib_i;    // i-side planes (M1, M2) of the left coding [m][nK][NB_REC]
+  const uint8_t *nib_j;    // j-side planes (S1, S2) of the right coding
+  int64_t data_bytes, scale_bytes, nib_bytes;
+  int nK;
+};
+
+template <int KK>
+__device__ __forceinline__ v16f_ mfma_mx(v8i_ fa, v8i_ fb, v16f_ c, unsigned sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb, c, 2, 4, KK, (int)sa, 0, sb);  // fp6 x fp4
+}
+template <int BB>
+__device__ __forceinline__ v2f_ fp4_pair(unsigned wd) {
+  return __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(wd, 2.0f, BB);
+}
+
+__global__ __launch_bounds__(256, 2) void mx_screen_kernel(ScreenArgs a, MxArgs x) {
+  constexpr int PB = MX_PB, RB = MX_RB;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[2][MXK * MX_AP];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_P];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][BJ * NB_P];
+  __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
+  __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  const int64_t J0 = (int64_t)J * BJ;
+  const int nK = x.nK;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.data, x.data_bytes);
+  const __amdgpu_buffer_rsrc_t rsS = make_rsrc(x.scale, x.scale_bytes);
+  const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
+  const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
+
+  int64_t ti[PB];
 #pragma unroll
-    for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
-      c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
-      c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
-      cd = cd * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + od];
-      c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
+  for (int t = 0; t < PB; ++t) {
+    const int r = roff + PB * w + t;
+    ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
+  }
+  // staging roles: 3 A chunks of 16 bytes (6 per row record), a scale dword (threads < 128),
+  // one j-side nibble chunk, one i-side chunk (threads < 64)
+  const int rowpitch = nK * MX_REC;
+  int voffA[3], ldsA[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int ch = tid + 256 * u, row = ch / 6, piece = ch % 6;
+    voffA[u] = row * rowpitch + piece * 16;
+    ldsA[u] = row * MX_AP + piece * 16;
+  }
+  const unsigned OOR = 0xFFFFFFF0u;  // out of range -> the buffer load returns zeros
+  const unsigned voffS = (tid < MXK) ? (unsigned)(tid * nK * 4) : OOR;
+  const int js = tid >> 3, jp = tid & 7;
+  const unsigned voffJ = (J0 + js < a.m) ? (unsigned)((J0 + js) * nK * NB_REC + jp * 16) : OOR;
+  unsigned voffI = OOR;
+  if (tid < 8 * MX_BI) {
+    const int r = roff + js;
+    if (r < a.n_rows) voffI = (unsigned)(a.rows[r] * nK * NB_REC + jp * 16);
+  }
+
+  v4i ra[3], rj, ri = {0, 0, 0, 0};
+  int rs = 0;
+  auto load = [&](int kb, int cs) __attribute__((always_inline)) {
+    const int soffA = kb * MXK * rowpitch + cs * MX_REC, soffS = (kb * MXK * nK + cs) * 4, soffN = cs * NB_REC;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA[u], soffA, 0);
+    if (tid < MXK) rs = (int)__builtin_amdgcn_raw_buffer_load_b32(rsS, voffS, soffS, 0);
+    rj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, soffN, 0);
+    if (tid < 8 * MX_BI) ri = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, soffN, 0);
+  };
+  auto store = [&](int b, int epi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) *(v4i *)&sA[b][ldsA[u]] = ra[u];
+    if (tid < MXK) *(int *)&sA[b][tid * MX_AP + MX_REC] = rs;
+    *(v4i *)&sJ[b][js * NB_P + jp * 16] = rj;
+    if (tid < 8 * MX_BI) *(v4i *)&sI[b][js * NB_P + jp * 16] = ri;
+    if (epi >= 0) {
+      *(v4i *)&eJ[epi][js * NB_E + jp * 16] = rj;
+      if (tid < 8 * MX_BI) *(v4i *)&eI[epi][js * NB_E + jp * 16] = ri;
     }
-    const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, Ed = a.sLd[i] * cd, E2 = a.sR[j] * c2;
-    const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
-                 dEd = a.side_eps * a.sLd[i] * a.csq_r[j], dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
-    const double al = a.alpha[i], be = a.beta[j];
-    const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
-                 t5 = al * al * a.qb[j], t6 = -2.0 * al * al * be * a.rb[j], t7 = al * al * be * be * a.zz;
-    const double var = M + Ed + t1 + t2 + t3 + t4 + t5 + t6 + t7;
-    const double eff = E3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-    const double slack =
-        1e-12 * (fabs(M) + fabs(Ed) + fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6) + fabs(t7));
-    // |w'(P - P~)w| <= ||P - P~||_2 * |w|^2  (a.delta = rigorous upper bound of the spectral norm)
-    const double var_lo = var - a.delta * sumw2 - slack - 2.0 * fabs(be) * dE1 - 2.0 * fabs(al) * dE2 - dEd;
-    const double eff_hi = fabs(eff) + dE3;
-    const bool cand = !(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * var_lo;
-    if (cand) {
-      const unsigned long long k = atomicAdd(a.counter, 1ULL);
-      if ((int64_t)k < a.cap) {
-        a.cand_i[k] = i;
-        a.cand_j[k] = j;
+  };
+
+  v16f_ acc[RB][PB];
+  // one stage (128 individuals = two 64-deep k-steps) from LDS buffer b
+  auto compute = [&](int b, bool diag) __attribute__((always_inline)) {
+    unsigned sc[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) sc[r] = *(const unsigned *)&sA[b][(32 * r + c) * MX_AP + MX_REC] >> (16 * h);
+    const int bscale = diag ? 128 : 129;  // x2 (fp4 codes hold w/2), x4 beyond the diagonal block
+    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v4i j1 = *(const v4i *)&sJ[b][c * NB_P + 32 * kk + 16 * h];
+      const v4i j2 = *(const v4i *)&sJ[b][c * NB_P + 64 + 32 * kk + 16 * h];
+      v8i_ fb[PB];
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        const v4i i1 = *(const v4i *)&sI[b][(PB * w + t) * NB_P + 32 * kk + 16 * h];
+        const v4i i2 = *(const v4i *)&sI[b][(PB * w + t) * NB_P + 64 + 32 * kk + 16 * h];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
+#pragma unroll
+        for (int q = 4; q < 8; ++q) fb[t][q] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const uint8_t *ar = &sA[b][(32 * r + c) * MX_AP + 48 * h];
+        v8i_ fa;
+        if (kk == 0) {
+          const v4i lo = *(const v4i *)ar;
+          const v2i_ hi = *(const v2i_ *)(ar + 16);
+          fa = v8i_{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], 0, 0};
+        } else {
+          const v2i_ lo = *(const v2i_ *)(ar + 24);
+          const v4i hi = *(const v4i *)(ar + 32);
+          fa = v8i_{lo[0], lo[1], hi[0], hi[1], hi[2], hi[3], 0, 0};
+        }
+#pragma unroll
+        for (int t = 0; t < PB; ++t)
+          acc[r][t] = kk == 0 ? mfma_mx<0>(fa, fb[t], diag ? z : acc[r][t], sc[r], bscale)
+                              : mfma_mx<1>(fa, fb[t], acc[r][t], sc[r], bscale);
       }
     }
+  };
+
+  double tot[PB];
+  unsigned sw[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    tot[t] = 0.0;
+    sw[t] = 0;
+  }
+  // epilogue of a K-block: sum_rows w[row] * acc[row]; acc register e of this lane <-> storage
+  // slot 16h + e of each 32-row tile <-> nibble e of the 8 bytes at 16r + 8h of the planes
+  auto epilogue = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < PB; ++t) {
+      v2f_ s2 = {0.f, 0.f};
+      unsigned sq = 0;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const v2i_ m1 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 16 * r + 8 * h];
+        const v2i_ m2 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 64 + 16 * r + 8 * h];
+        const v2i_ b1 = *(const v2i_ *)&eJ[q][c * NB_E + 16 * r + 8 * h];
+        const v2i_ b2 = *(const v2i_ *)&eJ[q][c * NB_E + 64 + 16 * r + 8 * h];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const unsigned wd = (unsigned)((m1[d] & b1[d]) | (m2[d] & b2[d]));
+          sq = __builtin_amdgcn_udot8(wd, wd, sq, false);  // codes are the integers w
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) {
+            const v2f_ wf = bb == 0 ? fp4_pair<0>(wd) : bb == 1 ? fp4_pair<1>(wd) : bb == 2 ? fp4_pair<2>(wd) : fp4_pair<3>(wd);
+            const v2f_ av = {acc[r][t][8 * d + 2 * bb], acc[r][t][8 * d + 2 * bb + 1]};
+            s2 = __builtin_elementwise_fma(wf, av, s2);
+          }
+        }
+      }
+      tot[t] += (double)s2[0] + (double)s2[1];
+      sw[t] += sq;
+    }
+  };
+
+  // one stage of K-block kb at column stage cs from buffer b: prefetch the next stage, multiply,
+  // epilogue after the last stage of the K-block, then write the next stage into buffer b^1
+  auto iter = [&](int kb, int cs, int b, bool diag) __attribute__((always_inline)) {
+    const bool last = (cs == nK - 1);
+    const int nkb = last ? kb + 1 : kb, ncs = last ? kb + 1 : cs + 1;
+    const bool more = nkb < nK;
+    if (more) load(nkb, ncs);
+    compute(b, diag);
+    if (last) epilogue(kb & 1);
+    if (more) store(b ^ 1, (ncs == nkb) ? (nkb & 1) : -1);
+    __syncthreads();
+  };
+
+  load(0, 0);
+  store(0, 0);
+  __syncthreads();
+  int b = 0;
+  for (int kb = 0; kb < nK; ++kb) {
+    iter(kb, kb, b, true);
+    b ^= 1;
+#pragma unroll 1
+    for (int cs = kb + 1; cs < nK; ++cs) {
+      iter(kb, cs, b, false);
+      b ^= 1;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const double other = __shfl_xor(tot[t], 32);
+    const unsigned osw = __shfl_xor(sw[t], 32);
+    if (h != 0 || ti[t] < 0) continue;
+    cand_test(a, roff + PB * w + t, ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
   }
 }
 
@@ -701,6 +929,107 @@ __global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
   if (lane == 0) z[q] = s;
 }
 
+// ---- MX setup.  fp6 e2m3 quantisation of P_off, one e8m0 scale per (natural row, 32 storage
+// columns): scale 2^e with e the least exponent giving |v| / 2^e <= 7.5, round to nearest even
+// on the e2m3 grid (steps 1/8 below 2, 1/4 below 4, 1/2 up to 7.5).  Also writes the dequantised
+// matrix Qn (natural order) for the rigorous residual bound.
+__global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *P, uint32_t *data, uint8_t *scale,
+                                double *Qn) {
+  const int64_t nblk = n_pad / 32;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * nblk) return;
+  const int64_t rho = idx / nblk, bI = idx % nblk;
+  const int64_t stage = bI >> 2;
+  const int b = (int)(bI & 3), pos = 2 * (b & 1) + (b >> 1);
+  double mx = 0.0;
+  for (int j = 0; j < 32; ++j) {
+    const int64_t c = bI * 32 + perm_nat(j);
+    const double v = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
+    mx = fmax(mx, fabs(v));
+  }
+  int e = -127;
+  if (mx > 0.0) {
+    e = (int)ceil(log2(mx / 7.5));
+    while (ldexp(7.5, e) < mx) ++e;
+    while (e > -127 && ldexp(7.5, e - 1) >= mx) --e;
+    e = e < -127 ? -127 : e;
+  }
+  uint32_t wds[6] = {0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < 32; ++j) {
+    const int64_t c = bI * 32 + perm_nat(j);
+    const double v = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
+    const double y = ldexp(v, -e), ay = fabs(y);
+    double q;
+    uint32_t code;
+    if (ay < 2.0) {
+      q = rint(ay * 8.0) / 8.0;
+      code = (uint32_t)(q * 8.0);  // 0..16 (16 = 2.0)
+    } else if (ay < 4.0) {
+      q = rint(ay * 4.0) / 4.0;
+      code = 16u + (uint32_t)((q - 2.0) * 4.0);
+    } else {
+      q = rint(ay * 2.0) / 2.0;
+      code = 24u + (uint32_t)((q - 4.0) * 2.0);
+    }
+    if (y < 0.0 && code) code |= 32u;
+    const int bit = 6 * j;
+    wds[bit >> 5] |= code << (bit & 31);
+    if ((bit & 31) > 26) wds[(bit >> 5) + 1] |= code >> (32 - (bit & 31));
+    Qn[rho * n_pad + c] = ldexp(y < 0.0 ? -q : q, e);
+  }
+  uint32_t *dst = data + ((rho * nK + stage) * MX_REC + 24 * pos) / 4;
+  for (int k = 0; k < 6; ++k) dst[k] = wds[k];
+  scale[(rho * nK + stage) * 4 + pos] = (uint8_t)(e + 127);
+}
+
+// R = (P_off - E) * out_scale with E the symmetric matrix the MX screen actually evaluates
+// (block-upper visit over 128-row K-blocks: off-diagonal blocks from the upper row's scales,
+// diagonal blocks symmetrised), natural order; rowabs[k] = sum_l |E_kl|.  One workgroup per row.
+__global__ __launch_bounds__(256) void mx_residual_kernel(int64_t n, int64_t n_pad, const double *P, const double *Qn,
+                                                          double out_scale, double *R, double *rowabs) {
+  const int64_t k = blockIdx.x, bk = k / MXK;
+  double s = 0.0;
+  for (int64_t l = threadIdx.x; l < n_pad; l += 256) {
+    const int64_t bl = l / MXK;
+    const double E = bl == bk ? 0.5 * (Qn[k * n_pad + l] + Qn[l * n_pad + k])
+                              : (bl > bk ? Qn[k * n_pad + l] : Qn[l * n_pad + k]);
+    const double po = (k < n && l < n && k != l) ? P[k * n + l] : 0.0;
+    R[k * n_pad + l] = (po - E) * out_scale;
+    s += fabs(E);
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) rowabs[k] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// nibble planes of a screen panel (storage order, codes 0..2): record (SNP, stage) = two 64-byte
+// planes, individual q of the stage at nibble q & 1 of byte q >> 1.  i side: M1 = [a==1] 0xF,
+// M2 = [a==2] 0xF; j side: S1 = b, S2 = 2b (fp4 codes of w/2 for w = 1*b, 2*b).
+__global__ void nibble_kernel(int64_t m, int64_t n_pad, int nK, const int8_t *panel, uint32_t *nib_i,
+                              uint32_t *nib_j) {
+  const int64_t per = n_pad / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= m * per) return;
+  const int64_t j = idx / per, d = idx % per;
+  const int64_t stage = d / 16, dd = d % 16;
+  const int8_t *src = panel + j * n_pad + 8 * d;
+  uint32_t m1 = 0, m2 = 0, s1 = 0, s2 = 0;
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t a = (uint32_t)src[e];
+    m1 |= (a == 1 ? 0xFu : 0u) << (4 * e);
+    m2 |= (a == 2 ? 0xFu : 0u) << (4 * e);
+    s1 |= a << (4 * e);
+    s2 |= (2 * a) << (4 * e);
+  }
+  const int64_t rec = (j * nK + stage) * (NB_REC / 4);
+  nib_i[rec + dd] = m1;
+  nib_i[rec + 16 + dd] = m2;
+  nib_j[rec + dd] = s1;
+  nib_j[rec + 16 + dd] = s2;
+}
+
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -719,6 +1048,7 @@ struct Coding {
   DBuf sL, sL3, sLd, sR, csum, csq;  // their per-SNP scales; per-SNP sums of codes / squared codes
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
+  DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
 };
 
 struct gmat_epi {
@@ -727,7 +1057,10 @@ struct gmat_epi {
   int n_slice = 3;
   double qmax = 0, zz = 0, spy = 0;
   double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2
+  double rho_mx = 0;                // the MX screen's bound: ||P_off - E||_2 + fp32 accumulation term
+  int nK = 0;                       // 128-individual stages
   DBuf Ps, py, z, dg, slices;
+  DBuf mx_data, mx_scale;           // fp6 P_off records and e8m0 scales (MX screen)
   DBuf spanels;  // screen codes, one allocation: [0] minor-allele dosage, [1] heterozygote [m][n_pad]
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
@@ -827,6 +1160,11 @@ int build_coding(gmat_epi *e, int which) {
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
                      cd.Rq.as<int8_t>(), cd.sR.as<double>());
   GMAT_HIP(hipGetLastError());
+  GMAT_TRY(cd.nibI.alloc((size_t)m * n_pad));
+  GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
+  hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
+                     panel, cd.nibI.as<uint32_t>(), cd.nibJ.as<uint32_t>());
+  GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipStreamSynchronize(e->s));
   cd.U.release();
   cd.ready = true;
@@ -864,6 +1202,7 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   e->n_pad = g->n_pad;
   e->m = g->m;
   e->n_slice = n_slice;
+  e->nK = (int)(g->n_pad / MXK);
   const int64_t n = e->n, n_pad = e->n_pad;
   double pmax = 0.0, qmax = 0.0;  // max |P|, max |P_kl| off the diagonal
   for (int64_t i = 0; i < n; ++i)
@@ -909,30 +1248,64 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   }
   // ||R||_2 <= ||R^16||_F^(1/16) (R symmetric): four fp64 MFMA squarings of R scaled to
   // unit max entry (|R_kl| <= 0.5 * 128^-(S-1) / unit), for every usable slice count S
-  for (int S = 1; S <= n_slice; ++S) {
-    const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
-    DBuf r1, r2, rows;
-    if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
-        (rc = rows.alloc(n_pad * sizeof(double))))
-      return fail(rc);
-    hipLaunchKernelGGL(residual_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, S,
-                       1.0 / 64.0, r1.as<double>());  // final residual in [-64, 64] scaled units
+  // ||R^16||_F from a residual already scaled to entries of order one (four fp64 squarings)
+  DBuf r1, r2, rrows;
+  if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
+      (rc = rrows.alloc(n_pad * sizeof(double))))
+    return fail(rc);
+  auto fro16 = [&](double *fro_root) -> int {
     double *src = r1.as<double>(), *dst = r2.as<double>();
     for (int q = 0; q < 4; ++q) {
-      if ((rc = dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad)))
-        return fail(rc);
+      GMAT_TRY(dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad));
       std::swap(src, dst);
     }
-    if ((rc = dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rows.as<double>()))) return fail(rc);
+    GMAT_TRY(dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rrows.as<double>()));
     std::vector<double> hr(n_pad);
-    if (hipMemcpy(hr.data(), rows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
-      set_error("gmat_epi_create: residual norm download failed");
-      return fail(GMAT_E_HIP);
-    }
+    GMAT_HIP(hipMemcpy(hr.data(), rrows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost));
     double fro2 = 0.0;
     for (double v : hr) fro2 += v;
+    *fro_root = std::pow(std::sqrt(fro2), 1.0 / 16.0);
+    return GMAT_OK;
+  };
+  for (int S = 1; S <= n_slice; ++S) {
+    const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
+    hipLaunchKernelGGL(residual_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, S,
+                       1.0 / 64.0, r1.as<double>());  // final residual in [-64, 64] scaled units
+    double fr;
+    if ((rc = fro16(&fr))) return fail(rc);
     // 5% margin for the fp64 rounding of the squarings, plus the rounding of P*unit itself
-    e->rho[S] = 1.05 * rmax * std::pow(std::sqrt(fro2), 1.0 / 16.0) + 1e-15 * pmax * (double)n;
+    e->rho[S] = 1.05 * rmax * fr + 1e-15 * pmax * (double)n;
+  }
+  // MX screen: fp6 records + scales, the residual of the matrix it evaluates, and the fp32
+  // accumulation bound: every acc_k is a sum of at most n_pad products (each exact in fp32)
+  // accumulated with at most one rounding per product (x2 margin for the MFMA's internal
+  // order), the epilogue adds 32 roundings; all are bounded by u * w'|E|w <= u * max_k
+  // sum_l |E_kl| * |w|^2 (|E| symmetric non-negative).
+  {
+    DBuf qn, rabs;
+    if ((rc = e->mx_data.alloc((size_t)n_pad * e->nK * MX_REC)) || (rc = e->mx_scale.alloc((size_t)n_pad * e->nK * 4)) ||
+        (rc = qn.alloc(n_pad * n_pad * sizeof(double))) || (rc = rabs.alloc(n_pad * sizeof(double))))
+      return fail(rc);
+    hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)cdiv(n_pad * (n_pad / 32), 256)), dim3(256), 0, 0, n, n_pad,
+                       e->nK, dp.as<double>(), e->mx_data.as<uint32_t>(), e->mx_scale.as<uint8_t>(), qn.as<double>());
+    const double os = qmax > 0 ? 15.0 / qmax : 1.0;
+    hipLaunchKernelGGL(mx_residual_kernel, dim3((unsigned)n_pad), dim3(256), 0, 0, n, n_pad, dp.as<double>(),
+                       qn.as<double>(), os, r1.as<double>(), rabs.as<double>());
+    if (hipGetLastError() != hipSuccess) {
+      set_error("gmat_epi_create: MX setup kernels failed");
+      return fail(GMAT_E_HIP);
+    }
+    double fr;
+    if ((rc = fro16(&fr))) return fail(rc);
+    std::vector<double> ha(n_pad);
+    if (hipMemcpy(ha.data(), rabs.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("gmat_epi_create: MX row sums download failed");
+      return fail(GMAT_E_HIP);
+    }
+    double amax = 0.0;
+    for (double v : ha) amax = std::max(amax, v);
+    const double u = std::ldexp(1.0, -24);
+    e->rho_mx = 1.05 * fr / os + 1e-15 * pmax * (double)n + 1.01 * (2.0 * (double)n_pad + 64.0) * u * amax;
   }
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
@@ -1012,7 +1385,15 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int tri = (kind != GMAT_AD);
   const char *venv = getenv("GMAT_SCREEN_VARIANT");
   // tile shape of the screen (Shape<SH>); GMAT_SCREEN_VARIANT overrides for A/B runs
-  const int shape = venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE;
+  // screen level S: 0 = MX (fp6 x fp4, one pass, tighter than one int8 slice), 1..n_slice = int8
+  // slices.  Automatic: MX when the candidate band stays thin (p_cut <= 1e-4), 2 slices up to
+  // p_cut 1e-2, else all; n_slice > 0 forces S slices, n_slice < 0 forces MX.  A launch whose
+  // candidates overflow the buffer is redone one level finer (and the scan keeps that level).
+  int S = n_slice > 0 ? n_slice
+                      : (n_slice < 0 ? 0 : (p_cut <= 1e-4 ? 0 : std::min(e->n_slice, p_cut <= 1e-2 ? 2 : 4)));
+  GMAT_CHECK(S >= 0 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
+  int S_max_used = S;
+  const int shape = (S == 0) ? 0 : (venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE);  // MX tiles are Shape<0>'s
   const int BI = shape ? Shape<1>::BI : Shape<0>::BI, MT = shape ? Shape<1>::MT : Shape<0>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   for (double &v : e->stats) v = 0.0;
@@ -1034,12 +1415,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) rws.push_back(rows[t]);
     launches.push_back(rws);
   }
-  // slices used: 1 when the candidate band of the one-slice bound stays thin (small p_cut), 2 up
-  // to p_cut 1e-2, else all; a launch whose candidates overflow the buffer is redone with one
-  // more slice (and the scan keeps it)
-  int S = n_slice > 0 ? n_slice : std::min(e->n_slice, p_cut <= 1e-4 ? 1 : (p_cut <= 1e-2 ? 2 : 4));
-  GMAT_CHECK(S >= 1 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
-  int S_max_used = S;
 
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
@@ -1248,13 +1623,24 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cand_i = e->cand_i.as<int64_t>();
     sa.cand_j = e->cand_j.as<int64_t>();
     unsigned long long count = 0;
+    MxArgs mx;
+    mx.data = e->mx_data.as<uint8_t>();
+    mx.scale = e->mx_scale.as<uint32_t>();
+    mx.nib_i = L.nibI.as<uint8_t>();
+    mx.nib_j = R.nibJ.as<uint8_t>();
+    mx.data_bytes = (int64_t)e->mx_data.bytes;
+    mx.scale_bytes = (int64_t)e->mx_scale.bytes;
+    mx.nib_bytes = m * n_pad;
+    mx.nK = e->nK;
     for (int attempt = 0;; ++attempt) {
       sa.n_slice = S;
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
-      sa.delta = e->rho[S];
+      sa.delta = S == 0 ? e->rho_mx : e->rho[S];
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
-      if (shape)
+      if (S == 0)
+        hipLaunchKernelGGL(mx_screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, sm, sa, mx);
+      else if (shape)
         hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       else
         hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
@@ -1272,7 +1658,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         GMAT_CHECK(S < e->n_slice, GMAT_E_OVERFLOW,
                    "one screen launch produced %llu candidates (capacity %lld) with %d slices: p_cut too large "
                    "for a scan; use the pair test", count, (long long)e->cand_cap, S);
-        ++S;
+        S = S == 0 ? std::min(2, e->n_slice) : S + 1;
         S_max_used = std::max(S_max_used, S);
       }
       GMAT_TRY(flush(pending));
@@ -1288,7 +1674,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     t_screen += ms_screen * 1e-3;
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
     // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
-    ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
+    ops += (double)ntiles * std::max(S, 1) * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
     if (pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));
@@ -1324,7 +1710,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
   e->stats[8] = S_max_used;
-  e->stats[9] = e->rho[S_max_used];
+  e->stats[9] = S_max_used == 0 ? e->rho_mx : e->rho[S_max_used];
   return GMAT_OK;
 }
 

@@ -1,6 +1,11 @@
+# GPU-box quick check: parity tests (-k filter optional), then a short headline bench.
 set -o pipefail
-mkdir -p gpurun_out/s1
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/s1/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/s1/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/s1/pytest_gpu.log
-timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff > gpurun_out/s1/bench.json 2> gpurun_out/s1/bench.log || { tail -20 gpurun_out/s1/bench.log; exit 1; }
-cat gpurun_out/s1/bench.json
+TAG=${1:-q}
+K=${2:-}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+if [ -n "$K" ]; then KARG="-k $K"; else KARG=""; fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider $KARG > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff > $OUT/bench.json 2> $OUT/bench.log || { tail -20 $OUT/bench.log; exit 1; }
+cat $OUT/bench.json
