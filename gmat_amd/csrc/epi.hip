@@ -45,6 +45,7 @@ constexpr int ROWS_PER_LAUNCH = 128;
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
 constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)
+constexpr int MX_SHAPE = 0;      // default workgroup shape of the MX screen (MxShape<V> below)
 
 // w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
 // j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
@@ -347,16 +348,24 @@ __global__ __launch_bounds__(256, 2) void screen_kernel(ScreenArgs a) {
 // epilogue sums w[row] * acc[row] with v_cvt_scalef32_pk_f32_fp4 (two w per instruction, from the
 // same nibble codes) and v_pk_fma_f32; sum w^2 comes from v_dot8_u32_u4.
 //
-// Layouts: A record per (natural row, 128-column stage) = 4 blocks of 24 bytes (32 fp6 codes,
-// code j at bits 6j) in the LDS order of block b at 24 * (2(b&1) + (b>>1)), scales likewise
-// ordered in one dword; genotype nibble records per (SNP, stage) = two 64-byte planes.
-constexpr int MXK = 128;    // individuals per MX stage (= K-block height)
-constexpr int MX_REC = 96;  // fp6 bytes per (row, stage)
-constexpr int MX_AP = 112;  // LDS pitch of an A row record (+ scale dword + pad): conflict-free reads
-constexpr int NB_REC = 128; // nibble bytes per (SNP, stage): two planes
-constexpr int NB_P = 144;   // LDS pitch of a staged nibble record
-constexpr int NB_E = 136;   // LDS pitch of the epilogue copies (8-byte reads)
-constexpr int MX_PB = 2, MX_BI = 4 * MX_PB, MX_RB = MXK / 32;
+// A is stored as tile images, one per (K-block of 128 natural rows, 128-column stage), laid out
+// exactly as the LDS stage: four planes (block (kk, h) = columns 64kk + 32h .. +32) of 128 rows x
+// a 32-byte slot = 6 dwords of fp6 codes (code j at bits 6j), the row's e8m0 scale in dword 6,
+// dword 7 zero; rows with (row >> 3) & 1 store the two 16-byte halves swapped, which makes the
+// two ds_read_b128 per fragment bank-conflict-free.  Genotype nibble records per (SNP, stage) =
+// two 64-byte planes (individual 2q + e at nibble e of byte q); in LDS the j side's 16-byte slots
+// are XOR-swizzled with (snp >> 1) & 7 (conflict-free), the i side is read as a broadcast.
+constexpr int MXK = 128;          // individuals per MX stage (= K-block height)
+constexpr int MX_TILE = 16384;    // bytes per A tile image
+constexpr int NB_REC = 128;       // nibble bytes per (SNP, stage): two planes
+constexpr int NB_E = 136;         // LDS pitch of the epilogue copies (8-byte reads)
+constexpr int MX_BI = 16, MX_RB = MXK / 32;  // first SNPs per workgroup; 32-row tiles per K-block
+// workgroup shapes (MxShape<V>): V 0 = 4 waves x 4 pair blocks (one wave per SIMD, 256
+// accumulator registers), V 1 = 8 waves x 2 pair blocks (two waves per SIMD)
+template <int V>
+struct MxShape {
+  static constexpr int NW = V ? 8 : 4, PB = MX_BI / NW, T = 64 * NW, MINB = 1;
+};
 
 typedef int v2i_ __attribute__((ext_vector_type(2)));
 typedef int v8i_ __attribute__((ext_vector_type(8)));
@@ -364,36 +373,42 @@ typedef float v16f_ __attribute__((ext_vector_type(16)));
 typedef float v2f_ __attribute__((ext_vector_type(2)));
 
 struct MxArgs {
-  const uint8_t *data;     // [n_pad rows][nK][MX_REC]
-  const uint32_t *scale;   // [n_pad rows][nK]
+  const uint8_t *tiles;    // [nK][nK] A tile images (upper ones used)
   const uint8_t *nib_i;    // i-side planes (M1, M2) of the left coding [m][nK][NB_REC]
   const uint8_t *nib_j;    // j-side planes (S1, S2) of the right coding
-  int64_t data_bytes, scale_bytes, nib_bytes;
+  int64_t tiles_bytes, nib_bytes;
   int nK;
 };
 
-template <int KK>
-__device__ __forceinline__ v16f_ mfma_mx(v8i_ fa, v8i_ fb, v16f_ c, unsigned sa, int sb) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb, c, 2, 4, KK, (int)sa, 0, sb);  // fp6 x fp4
+__device__ __forceinline__ v16f_ mfma_mx(v8i_ fa, v8i_ fb, v16f_ c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb, c, 2, 4, 0, sa, 0, sb);  // fp6 x fp4
 }
 template <int BB>
 __device__ __forceinline__ v2f_ fp4_pair(unsigned wd) {
   return __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(wd, 2.0f, BB);
 }
 
-__global__ __launch_bounds__(256, 2) void mx_screen_kernel(ScreenArgs a, MxArgs x) {
-  constexpr int PB = MX_PB, RB = MX_RB;
-  __shared__ __attribute__((aligned(16))) uint8_t sA[2][MXK * MX_AP];
-  __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_P];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][BJ * NB_P];
+// One workgroup = MX_BI first SNPs x BJ second SNPs; wave w owns first-SNP rows PB*w .. +PB
+// (MX_RB row tiles x PB column tiles of 32 x 32 per K-block).  Loop nest: K-block kb -> column
+// stage cs >= kb (one 128-deep stage = two 64-deep k-steps), LDS double buffer, one barrier per
+// stage; the next stage is fetched into registers while this one multiplies.  The diagonal
+// stage's genotype records are also copied to eI/eJ for the K-block's epilogue.
+// DBG (timing experiments only, results invalid): bit 0 no stage fetch after the first, bit 1 no
+// epilogue, bit 2 no MFMA, bit 3 no B-fragment generation, bit 4 no A reads, bit 5 no i/j reads
+template <int V, int DBG = 0>
+__global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_kernel(ScreenArgs a, MxArgs x) {
+  constexpr int PB = MxShape<V>::PB, RB = MX_RB, MX_T = MxShape<V>::T, NA = MX_TILE / 16 / MX_T;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[2][MX_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][BJ * NB_REC];
   __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
   __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  if (roff < 0) return;  // padding of the XCD deal
   const int64_t J0 = (int64_t)J * BJ;
   const int nK = x.nK;
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.data, x.data_bytes);
-  const __amdgpu_buffer_rsrc_t rsS = make_rsrc(x.scale, x.scale_bytes);
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
   const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
   const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
 
@@ -403,87 +418,74 @@ __global__ __launch_bounds__(256, 2) void mx_screen_kernel(ScreenArgs a, MxArgs 
     const int r = roff + PB * w + t;
     ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
   }
-  // staging roles: 3 A chunks of 16 bytes (6 per row record), a scale dword (threads < 128),
-  // one j-side nibble chunk, one i-side chunk (threads < 64)
-  const int rowpitch = nK * MX_REC;
-  int voffA[3], ldsA[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int ch = tid + 256 * u, row = ch / 6, piece = ch % 6;
-    voffA[u] = row * rowpitch + piece * 16;
-    ldsA[u] = row * MX_AP + piece * 16;
-  }
+  // staging roles (branch-free): NA 16-byte A chunks per thread (a straight copy of the tile
+  // image); one j-side chunk (SNP js, physical slot jq <- logical slot jq ^ f(js)) and one i-side
+  // chunk per thread, threads beyond the 256 / 128 chunks repeating them (identical stores)
   const unsigned OOR = 0xFFFFFFF0u;  // out of range -> the buffer load returns zeros
-  const unsigned voffS = (tid < MXK) ? (unsigned)(tid * nK * 4) : OOR;
-  const int js = tid >> 3, jp = tid & 7;
-  const unsigned voffJ = (J0 + js < a.m) ? (unsigned)((J0 + js) * nK * NB_REC + jp * 16) : OOR;
-  unsigned voffI = OOR;
-  if (tid < 8 * MX_BI) {
-    const int r = roff + js;
-    if (r < a.n_rows) voffI = (unsigned)(a.rows[r] * nK * NB_REC + jp * 16);
-  }
+  const int js = (tid >> 3) & 31, jq = tid & 7, jl = jq ^ ((js >> 1) & 7);
+  const int is = (tid >> 3) & 15;
+  unsigned voffJ = OOR, voffI = OOR;
+  if (J0 + js < a.m) voffJ = (unsigned)((J0 + js) * nK * NB_REC + jl * 16);
+  if (roff + is < a.n_rows) voffI = (unsigned)(a.rows[roff + is] * nK * NB_REC + jq * 16);
 
-  v4i ra[3], rj, ri = {0, 0, 0, 0};
-  int rs = 0;
+  v4i ra[NA], rnj, rni;
   auto load = [&](int kb, int cs) __attribute__((always_inline)) {
-    const int soffA = kb * MXK * rowpitch + cs * MX_REC, soffS = (kb * MXK * nK + cs) * 4, soffN = cs * NB_REC;
+    const int soffA = (kb * nK + cs) * MX_TILE;
 #pragma unroll
-    for (int u = 0; u < 3; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, voffA[u], soffA, 0);
-    if (tid < MXK) rs = (int)__builtin_amdgcn_raw_buffer_load_b32(rsS, voffS, soffS, 0);
-    rj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, soffN, 0);
-    if (tid < 8 * MX_BI) ri = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, soffN, 0);
+    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * MX_T) * 16, soffA, 0);
+    rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
+    rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
   };
-  auto store = [&](int b, int epi) __attribute__((always_inline)) {
+  auto store = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < 3; ++u) *(v4i *)&sA[b][ldsA[u]] = ra[u];
-    if (tid < MXK) *(int *)&sA[b][tid * MX_AP + MX_REC] = rs;
-    *(v4i *)&sJ[b][js * NB_P + jp * 16] = rj;
-    if (tid < 8 * MX_BI) *(v4i *)&sI[b][js * NB_P + jp * 16] = ri;
-    if (epi >= 0) {
-      *(v4i *)&eJ[epi][js * NB_E + jp * 16] = rj;
-      if (tid < 8 * MX_BI) *(v4i *)&eI[epi][js * NB_E + jp * 16] = ri;
-    }
+    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][(tid + u * MX_T) * 16] = ra[u];
+    *(v4i *)&sJ[b][js * NB_REC + jq * 16] = rnj;
+    *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
+  };
+  // the genotype records of a K-block's diagonal stage (in buffer b) kept for its epilogue
+  auto keep_diag = [&](int b, int q) __attribute__((always_inline)) {
+    const v4i vj = *(const v4i *)&sJ[b][js * NB_REC + jq * 16];
+    const v4i vi = *(const v4i *)&sI[b][is * NB_REC + jq * 16];
+    *(v4i *)&eJ[q][js * NB_E + jl * 16] = vj;
+    *(v4i *)&eI[q][is * NB_E + jq * 16] = vi;
   };
 
   v16f_ acc[RB][PB];
+  const int sw16 = 16 * ((c >> 3) & 1);  // half swap of this lane's A rows
+  const int jf = (c >> 1) & 7;           // j-side slot swizzle of this lane's SNP
   // one stage (128 individuals = two 64-deep k-steps) from LDS buffer b
   auto compute = [&](int b, bool diag) __attribute__((always_inline)) {
-    unsigned sc[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) sc[r] = *(const unsigned *)&sA[b][(32 * r + c) * MX_AP + MX_REC] >> (16 * h);
     const int bscale = diag ? 128 : 129;  // x2 (fp4 codes hold w/2), x4 beyond the diagonal block
     const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const v4i j1 = *(const v4i *)&sJ[b][c * NB_P + 32 * kk + 16 * h];
-      const v4i j2 = *(const v4i *)&sJ[b][c * NB_P + 64 + 32 * kk + 16 * h];
+      const v4i j1 = (DBG & 32) ? v4i{kk, 1, 2, 3} : *(const v4i *)&sJ[b][c * NB_REC + 16 * ((2 * kk + h) ^ jf)];
+      const v4i j2 = (DBG & 32) ? v4i{kk, 5, 2, 3} : *(const v4i *)&sJ[b][c * NB_REC + 16 * ((4 + 2 * kk + h) ^ jf)];
       v8i_ fb[PB];
 #pragma unroll
       for (int t = 0; t < PB; ++t) {
-        const v4i i1 = *(const v4i *)&sI[b][(PB * w + t) * NB_P + 32 * kk + 16 * h];
-        const v4i i2 = *(const v4i *)&sI[b][(PB * w + t) * NB_P + 64 + 32 * kk + 16 * h];
+        const v4i i1 = (DBG & 32) ? v4i{t, 1, 2, 3} : *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+        const v4i i2 = (DBG & 32) ? v4i{t, 7, 2, 3} : *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
+        for (int q = 0; q < 4; ++q) fb[t][q] = (DBG & 8) ? i1[q] : (i1[q] & j1[q]) | (i2[q] & j2[q]);
 #pragma unroll
         for (int q = 4; q < 8; ++q) fb[t][q] = 0;
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
-        const uint8_t *ar = &sA[b][(32 * r + c) * MX_AP + 48 * h];
-        v8i_ fa;
-        if (kk == 0) {
-          const v4i lo = *(const v4i *)ar;
-          const v2i_ hi = *(const v2i_ *)(ar + 16);
-          fa = v8i_{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], 0, 0};
-        } else {
-          const v2i_ lo = *(const v2i_ *)(ar + 24);
-          const v4i hi = *(const v4i *)(ar + 32);
-          fa = v8i_{lo[0], lo[1], hi[0], hi[1], hi[2], hi[3], 0, 0};
-        }
+        const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
+        const v4i lo = (DBG & 16) ? v4i{kk, r, 3, 4} : *(const v4i *)(ar + sw16);
+        const v4i hi = (DBG & 16) ? v4i{5, 6, 120, 8} : *(const v4i *)(ar + (16 - sw16));
+        const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int t = 0; t < PB; ++t)
-          acc[r][t] = kk == 0 ? mfma_mx<0>(fa, fb[t], diag ? z : acc[r][t], sc[r], bscale)
-                              : mfma_mx<1>(fa, fb[t], acc[r][t], sc[r], bscale);
+        for (int t = 0; t < PB; ++t) {
+          if (DBG & 4) {
+            acc[r][t][0] += __int_as_float(fa[0] ^ fb[t][0] ^ hi[2]);
+            continue;
+          }
+          acc[r][t] = kk == 0 ? mfma_mx(fa, fb[t], diag ? z : acc[r][t], hi[2], bscale)
+                              : mfma_mx(fa, fb[t], acc[r][t], hi[2], bscale);
+        }
       }
     }
   };
@@ -519,36 +521,46 @@ __global__ __launch_bounds__(256, 2) void mx_screen_kernel(ScreenArgs a, MxArgs 
             s2 = __builtin_elementwise_fma(wf, av, s2);
           }
         }
+        __builtin_amdgcn_sched_barrier(0);  // consume the accumulators a tile at a time
       }
       tot[t] += (double)s2[0] + (double)s2[1];
       sw[t] += sq;
     }
   };
 
-  // one stage of K-block kb at column stage cs from buffer b: prefetch the next stage, multiply,
-  // epilogue after the last stage of the K-block, then write the next stage into buffer b^1
-  auto iter = [&](int kb, int cs, int b, bool diag) __attribute__((always_inline)) {
-    const bool last = (cs == nK - 1);
-    const int nkb = last ? kb + 1 : kb, ncs = last ? kb + 1 : cs + 1;
-    const bool more = nkb < nK;
-    if (more) load(nkb, ncs);
+  // one stage from buffer b with the next stage (nkb, ncs) fetched meanwhile into buffer b^1
+  auto iter = [&](int b, bool diag, int nkb, int ncs) __attribute__((always_inline)) {
+    if (!(DBG & 1)) load(nkb, ncs);
     compute(b, diag);
-    if (last) epilogue(kb & 1);
-    if (more) store(b ^ 1, (ncs == nkb) ? (nkb & 1) : -1);
+    store(b ^ 1);
     __syncthreads();
   };
 
   load(0, 0);
-  store(0, 0);
+  store(0);
   __syncthreads();
+  keep_diag(0, 0);
   int b = 0;
   for (int kb = 0; kb < nK; ++kb) {
-    iter(kb, kb, b, true);
+    // stages (kb, kb) .. (kb, nK-1); the last one prefetches (kb+1, kb+1) (clamped at the end)
+    const int nb = kb + 1 < nK ? kb + 1 : kb;
+    if (kb + 1 < nK) iter(b, true, kb, kb + 1);
+    else iter(b, true, nb, nb);
     b ^= 1;
 #pragma unroll 1
     for (int cs = kb + 1; cs < nK; ++cs) {
-      iter(kb, cs, b, false);
+      const bool lastc = cs + 1 == nK;
+      iter(b, false, lastc ? nb : kb, lastc ? nb : cs + 1);
       b ^= 1;
+    }
+    if (kb + 1 < nK) keep_diag(b, (kb + 1) & 1);  // buffer b now holds stage (kb+1, kb+1)
+    if (!(DBG & 2)) {
+      epilogue(kb & 1);
+    } else {
+#pragma unroll
+      for (int t = 0; t < PB; ++t)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) tot[t] += acc[r][t][0] + acc[r][t][15];
     }
   }
 #pragma unroll
@@ -933,14 +945,11 @@ __global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
 // columns): scale 2^e with e the least exponent giving |v| / 2^e <= 7.5, round to nearest even
 // on the e2m3 grid (steps 1/8 below 2, 1/4 below 4, 1/2 up to 7.5).  Also writes the dequantised
 // matrix Qn (natural order) for the rigorous residual bound.
-__global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *P, uint32_t *data, uint8_t *scale,
-                                double *Qn) {
+__global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *P, uint32_t *tiles, double *Qn) {
   const int64_t nblk = n_pad / 32;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n_pad * nblk) return;
   const int64_t rho = idx / nblk, bI = idx % nblk;
-  const int64_t stage = bI >> 2;
-  const int b = (int)(bI & 3), pos = 2 * (b & 1) + (b >> 1);
   double mx = 0.0;
   for (int j = 0; j < 32; ++j) {
     const int64_t c = bI * 32 + perm_nat(j);
@@ -954,7 +963,7 @@ __global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *
     while (e > -127 && ldexp(7.5, e - 1) >= mx) --e;
     e = e < -127 ? -127 : e;
   }
-  uint32_t wds[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t wds[8] = {0, 0, 0, 0, 0, 0, (uint32_t)(e + 127), 0};
   for (int j = 0; j < 32; ++j) {
     const int64_t c = bI * 32 + perm_nat(j);
     const double v = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
@@ -977,9 +986,12 @@ __global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *
     if ((bit & 31) > 26) wds[(bit >> 5) + 1] |= code >> (32 - (bit & 31));
     Qn[rho * n_pad + c] = ldexp(y < 0.0 ? -q : q, e);
   }
-  uint32_t *dst = data + ((rho * nK + stage) * MX_REC + 24 * pos) / 4;
-  for (int k = 0; k < 6; ++k) dst[k] = wds[k];
-  scale[(rho * nK + stage) * 4 + pos] = (uint8_t)(e + 127);
+  // tile (K-block of rho, stage of the block), plane = block within the stage, 32-byte slot of
+  // the row, halves swapped on rows with (row >> 3) & 1
+  const int64_t kb = rho / MXK, row = rho % MXK, cs = bI >> 2, plane = bI & 3;
+  uint32_t *dst = tiles + ((kb * nK + cs) * MX_TILE + plane * 4096 + row * 32) / 4;
+  const int sw = (int)((row >> 3) & 1) * 4;
+  for (int k = 0; k < 8; ++k) dst[(k + sw) & 7] = wds[k];
 }
 
 // R = (P_off - E) * out_scale with E the symmetric matrix the MX screen actually evaluates
@@ -1060,7 +1072,7 @@ struct gmat_epi {
   double rho_mx = 0;                // the MX screen's bound: ||P_off - E||_2 + fp32 accumulation term
   int nK = 0;                       // 128-individual stages
   DBuf Ps, py, z, dg, slices;
-  DBuf mx_data, mx_scale;           // fp6 P_off records and e8m0 scales (MX screen)
+  DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
   DBuf spanels;  // screen codes, one allocation: [0] minor-allele dosage, [1] heterozygote [m][n_pad]
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
@@ -1283,11 +1295,11 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   // sum_l |E_kl| * |w|^2 (|E| symmetric non-negative).
   {
     DBuf qn, rabs;
-    if ((rc = e->mx_data.alloc((size_t)n_pad * e->nK * MX_REC)) || (rc = e->mx_scale.alloc((size_t)n_pad * e->nK * 4)) ||
-        (rc = qn.alloc(n_pad * n_pad * sizeof(double))) || (rc = rabs.alloc(n_pad * sizeof(double))))
+    if ((rc = e->mx_tiles.alloc((size_t)e->nK * e->nK * MX_TILE)) || (rc = qn.alloc(n_pad * n_pad * sizeof(double))) ||
+        (rc = rabs.alloc(n_pad * sizeof(double))))
       return fail(rc);
     hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)cdiv(n_pad * (n_pad / 32), 256)), dim3(256), 0, 0, n, n_pad,
-                       e->nK, dp.as<double>(), e->mx_data.as<uint32_t>(), e->mx_scale.as<uint8_t>(), qn.as<double>());
+                       e->nK, dp.as<double>(), e->mx_tiles.as<uint32_t>(), qn.as<double>());
     const double os = qmax > 0 ? 15.0 / qmax : 1.0;
     hipLaunchKernelGGL(mx_residual_kernel, dim3((unsigned)n_pad), dim3(256), 0, 0, n, n_pad, dp.as<double>(),
                        qn.as<double>(), os, r1.as<double>(), rabs.as<double>());
@@ -1393,7 +1405,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
                       : (n_slice < 0 ? 0 : (p_cut <= 1e-4 ? 0 : std::min(e->n_slice, p_cut <= 1e-2 ? 2 : 4)));
   GMAT_CHECK(S >= 0 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
   int S_max_used = S;
-  const int shape = (S == 0) ? 0 : (venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE);  // MX tiles are Shape<0>'s
+  const int shape = venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE;
+  const char *mxenv = getenv("GMAT_MX_VARIANT");  // MxShape<V> of the MX screen (A/B runs)
+  const int mxv = mxenv ? atoi(mxenv) : MX_SHAPE;
   const int BI = shape ? Shape<1>::BI : Shape<0>::BI, MT = shape ? Shape<1>::MT : Shape<0>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   for (double &v : e->stats) v = 0.0;
@@ -1419,11 +1433,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
   // read it has completed (event wait).
-  const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ);
+  const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ) + 16;  // (+ MX padding)
   DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2];
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
-    GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
+    GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 4 * sizeof(int)));  // int8 tile list, then the MX one
     GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(e13[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * m * sizeof(int)));
@@ -1509,8 +1523,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // per-launch host plan (rows, tile list); empty launches dropped
   struct Launch {
     std::vector<int64_t> rows;
-    std::vector<int> tiles;
-    int64_t j_lo = 0;
+    std::vector<int> tiles, tiles_mx;  // (row offset, J) per workgroup of the int8 / MX screen
+    int64_t j_lo = 0, n_mx = 0;        // n_mx: MX tiles without the padding
   };
   std::vector<Launch> plan;
   for (auto &rws : launches) {
@@ -1529,6 +1543,26 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         ln.tiles.push_back((int)J);
       }
     }
+    // MX tiles J-major (the row groups of one J run back to back, so its j-side records are
+    // re-read from L2), dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous
+    // chunks; padding entries (-1) exit at once
+    {
+      std::vector<int> lst;
+      for (int64_t J = 0; J * BJ < m; ++J)
+        for (int r0 = 0; r0 < Rn; r0 += MX_BI)
+          if (!tri || J >= (rws[r0] + 1) / BJ) {
+            lst.push_back(r0);
+            lst.push_back((int)J);
+          }
+      const int64_t N = (int64_t)lst.size() / 2, C = cdiv(N, 8);
+      ln.n_mx = N;
+      ln.tiles_mx.assign((size_t)16 * C, -1);
+      for (int64_t p = 0; p < N; ++p) {
+        const int64_t b = 8 * (p % C) + p / C;
+        ln.tiles_mx[2 * b] = lst[2 * p];
+        ln.tiles_mx[2 * b + 1] = lst[2 * p + 1];
+      }
+    }
     for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
     plan.push_back(std::move(ln));
   }
@@ -1541,6 +1575,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
                             S2));
+    GMAT_HIP(hipMemcpyAsync(dtiles[b].as<int>() + max_tiles * 2, ln.tiles_mx.data(), ln.tiles_mx.size() * sizeof(int),
+                            hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
     const int64_t ss = m * n_pad;  // slice stride of the side vectors
     hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, ss, drows[b].as<int64_t>(),
@@ -1624,12 +1660,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cand_j = e->cand_j.as<int64_t>();
     unsigned long long count = 0;
     MxArgs mx;
-    mx.data = e->mx_data.as<uint8_t>();
-    mx.scale = e->mx_scale.as<uint32_t>();
+    mx.tiles = e->mx_tiles.as<uint8_t>();
     mx.nib_i = L.nibI.as<uint8_t>();
     mx.nib_j = R.nibJ.as<uint8_t>();
-    mx.data_bytes = (int64_t)e->mx_data.bytes;
-    mx.scale_bytes = (int64_t)e->mx_scale.bytes;
+    mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
     mx.nib_bytes = m * n_pad;
     mx.nK = e->nK;
     for (int attempt = 0;; ++attempt) {
@@ -1638,8 +1672,26 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
+      sa.tiles = dtiles[b].as<int>() + (S == 0 ? max_tiles * 2 : 0);
       if (S == 0)
-        hipLaunchKernelGGL(mx_screen_kernel, dim3((unsigned)ntiles), dim3(256), 0, sm, sa, mx);
+      {
+        const unsigned g = (unsigned)(ln.tiles_mx.size() / 2);
+        const dim3 T1(MxShape<1>::T);
+        switch (mxv) {
+          case 0: hipLaunchKernelGGL(mx_screen_kernel<0>, dim3(g), dim3(MxShape<0>::T), 0, sm, sa, mx); break;
+          case 3: hipLaunchKernelGGL((mx_screen_kernel<1, 1>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 5: hipLaunchKernelGGL((mx_screen_kernel<1, 2>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 9: hipLaunchKernelGGL((mx_screen_kernel<1, 4>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 17: hipLaunchKernelGGL((mx_screen_kernel<1, 8>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 7: hipLaunchKernelGGL((mx_screen_kernel<1, 3>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 33: hipLaunchKernelGGL((mx_screen_kernel<1, 16>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 65: hipLaunchKernelGGL((mx_screen_kernel<1, 32>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 97: hipLaunchKernelGGL((mx_screen_kernel<1, 48>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 99: hipLaunchKernelGGL((mx_screen_kernel<1, 49>), dim3(g), T1, 0, sm, sa, mx); break;
+          case 103: hipLaunchKernelGGL((mx_screen_kernel<1, 51>), dim3(g), T1, 0, sm, sa, mx); break;
+          default: hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), T1, 0, sm, sa, mx);
+        }
+      }
       else if (shape)
         hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       else
@@ -1674,7 +1726,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     t_screen += ms_screen * 1e-3;
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
     // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
-    ops += (double)ntiles * std::max(S, 1) * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
+    if (S == 0)
+      ops += (double)ln.n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;
+    else
+      ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
     if (pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));

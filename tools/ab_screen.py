@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--n-id", type=int, default=2000)
     ap.add_argument("--n-snp", type=int, default=12000)
     ap.add_argument("--p-cut", type=float, default=1e-5)
+    ap.add_argument("--env", default="GMAT_SCREEN_VARIANT", help="variant selector (GMAT_MX_VARIANT for the MX screen)")
     args = ap.parse_args()
     import bench
     from gmat_amd import _native as N
@@ -32,7 +33,7 @@ def main():
     ref = None
     for r in range(args.rounds + 1):
         for v in variants:
-            os.environ["GMAT_SCREEN_VARIANT"] = str(v)
+            os.environ[args.env] = str(v)
             out = plan.scan("AA", rows, args.p_cut)
             st = plan.stats()
             if ref is None:
