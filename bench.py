@@ -220,15 +220,16 @@ def main():
     hits_all = dist.allreduce_sum(hits) / args.steps
     cands_all = dist.allreduce_sum(cands) / args.steps
 
-    # roofline of the dominant kernel (screen): algorithmic ops per launch / avg launch time.
-    # Per pair the symmetric quadratic form w'P_off w needs n (n + 128) / 2 MACs per pass: one
-    # pass of fp6 x fp4 MX MFMA (level 0), or S passes of int8 MFMA (level S = slices)
+    # roofline of the dominant kernel (the quadratic-form screen): its ops per launch / average
+    # launch time.  The spectral prefilter clears most 32-pair blocks before the
+    # screen, so the screen's work is counted over the blocks it actually multiplies: per
+    # processed block of BI x 32 pairs, n_pad (n_pad + 128) / 2 MACs x 2 per pair and pass
+    # (gmat_epi_stats[2]); the per-pair dense figure would exceed the peak and mean nothing.
     my_pairs = float(sum(m - 1 - int(i) for i in rows))
-    passes = max(n_slice, 1)
-    alg_ops_step = my_pairs * passes * n * (n + 128)
     avg_launch_s = screen_s / max(launches, 1)
-    alg_ops_launch = alg_ops_step * args.steps / max(launches, 1)
+    alg_ops_launch = ops / max(launches, 1)
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
+    dense_ops_step = my_pairs * max(n_slice, 1) * n * (n + 128)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -239,10 +240,12 @@ def main():
             traffic = None
     if n_slice == 0:
         peak, kern = MX_PEAK_TFLOPS, "mx_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
-        note = "fp6 x fp4 ops (TFLOP/s); algorithmic = n(n+128)/2 MACs x 2 per pair, one pass"
+        note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: n_pad(n_pad+128)/2 MACs x 2 per pair, one pass; "
+                "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
     else:
         peak, kern = INT8_PEAK_TOPS, "screen_kernel (v_mfma_i32_32x32x32_i8)"
-        note = "int8 ops (TOP/s); algorithmic = S slices x n(n+128)/2 MACs x 2 per pair"
+        note = ("int8 ops (TOP/s) of the screened blocks: S slices x n_pad(n_pad+128)/2 MACs x 2 per pair; "
+                "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
     roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": achieved / peak, "traffic": traffic, "kernel": kern, "ops_note": note,
                 "screen_level": n_slice,

@@ -66,7 +66,8 @@ struct ScreenArgs {
   int64_t m;
   const int64_t *rows;
   int n_rows;
-  const int *tiles;  // (row offset, J) pairs
+  const int *tiles;  // (row offset, J) pairs; MX screens: (row-list index, J)
+  const int *tile_rows;  // MX screens: MX_BI band rows per tile (-1 = none)
   int tri;           // 1: only j > i
   // side terms as int32 products of int8 slices (SIDE_T slices, slice stride in elements):
   // E1 = sL[i] sum_t 128^-t c13[t][ri], E3 = sL3[i] sum_t 128^-t c13[t][R+ri],
@@ -74,7 +75,7 @@ struct ScreenArgs {
   // E2 = sR[j] sum_t 128^-t c2[t][ri]; slicing error bounds side_eps * scale * code sum
   const int *c13, *c2;
   int64_t c13_stride, c2_stride;
-  const double *sL, *sL3, *sLd, *sR, *csum_l, *csum_r, *csq_r;
+  const double *sL, *sL3, *sLd, *sR, *csum_l, *csum_r, *csq_l, *csq_r;
   double side_eps;
   int64_t ld_e, j_lo;
   const double *alpha, *qa, *ra, *sa;
@@ -84,6 +85,13 @@ struct ScreenArgs {
   unsigned long long *counter;
   int64_t cap;
   int64_t *cand_i, *cand_j;
+  // spectral prefilter: exact code products Sab, Sa2b, Sab2, Sa2b2 ([4][R][ld_e] int32, z-stride
+  // pfc_stride), the certificate (pf_mu, pf_eps), n, and per (band row, 32-column block) flags
+  const int *pfc;
+  int64_t pfc_stride;
+  double pf_mu, pf_tau, pf_eps, n_id;
+  uint8_t *flags;
+  int nJ;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -129,6 +137,48 @@ __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i
       a.cand_j[k] = j;
     }
   }
+}
+
+// Spectral prefilter (one thread per band row r and 32-column block J): flags[r][J] = 1 unless
+// every pair (i = rows[r], j in block J) provably has p >= p_cut by
+//   var = e'Pe >= pf_mu (|e|^2 - (1'e)^2 / n) - pf_eps |e|^2,
+// with |e|^2 and 1'e exact from the int8 code products (e = (a - alpha) o (b - beta) expanded)
+// and eff from the sliced side term (bound dE3), as in cand_test.
+__global__ void prefilter_kernel(ScreenArgs a) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)a.n_rows * a.nJ) return;
+  const int r = (int)(idx / a.nJ), J = (int)(idx % a.nJ);
+  const int64_t i = a.rows[r];
+  uint8_t flag = 0;
+  if (!a.mono_l[i]) {
+    const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
+    for (int jj = 0; jj < 32 && !flag; ++jj) {
+      const int64_t j = (int64_t)J * 32 + jj;
+      if (j >= a.m || j < a.j_lo || (a.tri && j <= i) || a.mono_r[j]) continue;
+      const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+      double c3 = 0.0;
+#pragma unroll
+      for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+      const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
+      const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
+      const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * a.csum_r[j];
+      const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
+                   sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+      const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
+                              -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
+      double ee = 0.0, mag = 0.0;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        ee += t_ee[k];
+        mag += fabs(t_ee[k]);
+      }
+      const double se = sab - be * ca - al * cb + n * al * be;
+      const double pe = ee - se * se / n;
+      const double vlo = a.pf_mu * pe - a.pf_tau * se * se / n - a.pf_eps * ee - 1e-12 * a.pf_mu * (mag + se * se / n);
+      if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) flag = 1;
+    }
+  }
+  a.flags[idx] = flag;
 }
 
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
@@ -404,8 +454,9 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
   __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
-  const int roff = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
-  if (roff < 0) return;  // padding of the XCD deal
+  const int tl = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  if (tl < 0) return;  // padding of the XCD deal
+  const int *trow = a.tile_rows + (int64_t)tl * MX_BI;  // band rows of this tile (-1 = none)
   const int64_t J0 = (int64_t)J * BJ;
   const int nK = x.nK;
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
@@ -415,8 +466,8 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   int64_t ti[PB];
 #pragma unroll
   for (int t = 0; t < PB; ++t) {
-    const int r = roff + PB * w + t;
-    ti[t] = (r < a.n_rows) ? a.rows[r] : -1;
+    const int r = trow[PB * w + t];
+    ti[t] = (r >= 0) ? a.rows[r] : -1;
   }
   // staging roles (branch-free): NA 16-byte A chunks per thread (a straight copy of the tile
   // image); one j-side chunk (SNP js, physical slot jq <- logical slot jq ^ f(js)) and one i-side
@@ -426,7 +477,7 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   const int is = (tid >> 3) & 15;
   unsigned voffJ = OOR, voffI = OOR;
   if (J0 + js < a.m) voffJ = (unsigned)((J0 + js) * nK * NB_REC + jl * 16);
-  if (roff + is < a.n_rows) voffI = (unsigned)(a.rows[roff + is] * nK * NB_REC + jq * 16);
+  if (trow[is] >= 0) voffI = (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16);
 
   v4i ra[NA], rnj, rni;
   auto load = [&](int kb, int cs) __attribute__((always_inline)) {
@@ -460,7 +511,7 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const v4i j1 = (DBG & 32) ? v4i{kk, 1, 2, 3} : *(const v4i *)&sJ[b][c * NB_REC + 16 * ((2 * kk + h) ^ jf)];
-      const v4i j2 = (DBG & 32) ? v4i{kk, 5, 2, 3} : *(const v4i *)&sJ[b][c * NB_REC + 16 * ((4 + 2 * kk + h) ^ jf)];
+      const v4i j2 = j1 << 1;  // S2 = 2b = S1 << 1 (nibbles <= 4: no carry)
       v8i_ fb[PB];
 #pragma unroll
       for (int t = 0; t < PB; ++t) {
@@ -531,6 +582,7 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   // one stage from buffer b with the next stage (nkb, ncs) fetched meanwhile into buffer b^1
   auto iter = [&](int b, bool diag, int nkb, int ncs) __attribute__((always_inline)) {
     if (!(DBG & 1)) load(nkb, ncs);
+    __builtin_amdgcn_sched_barrier(0);  // keep the next stage's fetch ahead of this stage's work
     compute(b, diag);
     store(b ^ 1);
     __syncthreads();
@@ -568,7 +620,244 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
     const double other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
-    cand_test(a, roff + PB * w + t, ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
+    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
+  }
+}
+
+// Software-pipelined MX screen (4 waves, one per SIMD, 4 x 4 accumulator tiles of 32 x 32 per
+// wave = 256 accumulator registers).  Three LDS stage buffers: stage g+2 is fetched from global
+// memory during stage g and written at its end, so the operands of stage g+1's first k-step can
+// be read while stage g's second k-step multiplies (that buffer was completed before the
+// previous barrier).  Each k-step's operands are read in two groups during the previous k-step's
+// MFMAs (13 + 4 ds_reads: a wait for the first group never has to count past 15), A rows at a
+// 48-byte pitch (one 32-byte fragment = two contiguous ds_read_b128, conflict-free), the j-side
+// second plane derived (S2 = S1 << 1).  Register-only MFMAs are pinned between the memory ops by
+// laundering values through empty asm statements (no instructions).
+constexpr int M3_T = 256, M3_PB = 4, M3_NA = MX_TILE / 16 / M3_T, M3_AP = 48, M3_PL = MXK * M3_AP;
+
+// DBG (timing experiments only, results invalid): bit 0 no global fetch / LDS stores in the
+// loop, bit 1 no barrier, bit 2 no operand reads in the loop, bit 3 no epilogue
+template <int DBG = 0>
+__global__ __launch_bounds__(M3_T, 1) void mx3_screen_kernel(ScreenArgs a, MxArgs x) {
+  constexpr int PB = M3_PB, RB = MX_RB, NA = M3_NA;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[3][4 * M3_PL];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[3][MX_BI * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[3][BJ * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
+  __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int tl = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  if (tl < 0) return;  // padding of the XCD deal
+  const int *trow = a.tile_rows + (int64_t)tl * MX_BI;  // band rows of this tile (-1 = none)
+  const int64_t J0 = (int64_t)J * BJ;
+  const int nK = x.nK;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
+  const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
+  const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
+  int64_t ti[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const int r = trow[PB * w + t];
+    ti[t] = (r >= 0) ? a.rows[r] : -1;
+  }
+  // staging: NA 16-byte chunks of the tile image per thread (un-swapping the halves into the
+  // 48-byte pitch); one j-side chunk (SNP js, physical slot jq <- logical jl); threads < 128 an
+  // i-side chunk
+  const unsigned OOR = 0xFFFFFFF0u;
+  const int js = tid >> 3, jq = tid & 7, jl = jq ^ ((js >> 1) & 7), is = (tid >> 3) & 15;
+  const bool irole = tid < 8 * MX_BI;
+  const unsigned voffJ = (J0 + js < a.m) ? (unsigned)((J0 + js) * nK * NB_REC + jl * 16) : OOR;
+  const unsigned voffI = (trow[is] >= 0) ? (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16) : OOR;
+  int ldsA[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int q = tid + u * M3_T, pl = q >> 8, row = (q & 255) >> 1, half = (q & 1) ^ ((row >> 3) & 1);
+    ldsA[u] = pl * M3_PL + row * M3_AP + half * 16;
+  }
+  v4i ra[NA], rnj, rni = {0, 0, 0, 0};
+  auto load = [&](int kb, int cs) __attribute__((always_inline)) {
+    const int soffA = (kb * nK + cs) * MX_TILE;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * M3_T) * 16, soffA, 0);
+    rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
+    if (irole) rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][ldsA[u]] = ra[u];
+    *(v4i *)&sJ[b][js * NB_REC + jq * 16] = rnj;
+    if (irole) *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
+  };
+  auto keep_diag = [&](int b, int q) __attribute__((always_inline)) {
+    *(v4i *)&eJ[q][js * NB_E + jl * 16] = *(const v4i *)&sJ[b][js * NB_REC + jq * 16];
+    if (irole) *(v4i *)&eI[q][is * NB_E + jq * 16] = *(const v4i *)&sI[b][is * NB_REC + jq * 16];
+  };
+
+  const int jf = (c >> 1) & 7;
+  v16f_ acc[RB][PB];
+  // operands of one k-step (A fragments incl. the scale in dword 6; raw genotype chunks)
+  struct Ops {
+    v8i_ fa[RB];
+    v4i j1, i1[PB], i2[PB];
+  };
+  auto read1 = [&](Ops &o, int b, int kk) __attribute__((always_inline)) {  // j, i(t0, t1), A
+    o.j1 = *(const v4i *)&sJ[b][c * NB_REC + 16 * ((2 * kk + h) ^ jf)];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      o.i1[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+      o.i2[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) o.fa[r] = *(const v8i_ *)&sA[b][(2 * kk + h) * M3_PL + (32 * r + c) * M3_AP];
+  };
+  auto read2 = [&](Ops &o, int b, int kk) __attribute__((always_inline)) {  // i(t2, t3)
+#pragma unroll
+    for (int t = 2; t < PB; ++t) {
+      o.i1[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+      o.i2[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+    }
+  };
+  v4i fb[2][PB];
+  auto build_b = [&](const Ops &o, int q, int t0, int t1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = t0; t < t1; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) fb[q][t][e] = (o.i1[t][e] & o.j1[e]) | (o.i2[t][e] & (o.j1[e] << 1));
+  };
+  auto mfmas = [&](const Ops &o, int q, int t0, int t1, int bscale, bool zero) __attribute__((always_inline)) {
+    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = t0; t < t1; ++t) {
+      const v8i_ bb = {fb[q][t][0], fb[q][t][1], fb[q][t][2], fb[q][t][3], 0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < RB; ++r) acc[r][t] = mfma_mx(o.fa[r], bb, zero ? z : acc[r][t], o.fa[r][6], bscale);
+    }
+  };
+  // order pins (empty asm): after_mem launders a value for the MFMAs that follow the preceding
+  // memory ops; after_lo / after_hi launder a value for memory ops that follow the MFMAs of
+  // accumulator columns 0-1 / 2-3
+  auto after_mem = [&](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(v) : : "memory");
+    return v;
+  };
+  auto after_lo = [&](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v)
+                 : "a"(acc[0][0]), "a"(acc[1][0]), "a"(acc[2][0]), "a"(acc[3][0]), "a"(acc[0][1]), "a"(acc[1][1]),
+                   "a"(acc[2][1]), "a"(acc[3][1])
+                 : "memory");
+    return v;
+  };
+  auto after_hi = [&](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v)
+                 : "a"(acc[0][2]), "a"(acc[1][2]), "a"(acc[2][2]), "a"(acc[3][2]), "a"(acc[0][3]), "a"(acc[1][3]),
+                   "a"(acc[2][3]), "a"(acc[3][3])
+                 : "memory");
+    return v;
+  };
+
+  double tot[PB];
+  unsigned sw[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    tot[t] = 0.0;
+    sw[t] = 0;
+  }
+  auto epilogue = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < PB; ++t) {
+      v2f_ s2 = {0.f, 0.f};
+      unsigned sq = 0;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const v2i_ m1 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 16 * r + 8 * h];
+        const v2i_ m2 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 64 + 16 * r + 8 * h];
+        const v2i_ b1 = *(const v2i_ *)&eJ[q][c * NB_E + 16 * r + 8 * h];
+        const v2i_ b2 = *(const v2i_ *)&eJ[q][c * NB_E + 64 + 16 * r + 8 * h];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const unsigned wd = (unsigned)((m1[d] & b1[d]) | (m2[d] & b2[d]));
+          sq = __builtin_amdgcn_udot8(wd, wd, sq, false);
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) {
+            const v2f_ wf = bb == 0 ? fp4_pair<0>(wd) : bb == 1 ? fp4_pair<1>(wd) : bb == 2 ? fp4_pair<2>(wd) : fp4_pair<3>(wd);
+            const v2f_ av = {acc[r][t][8 * d + 2 * bb], acc[r][t][8 * d + 2 * bb + 1]};
+            s2 = __builtin_elementwise_fma(wf, av, s2);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      tot[t] += (double)s2[0] + (double)s2[1];
+      sw[t] += sq;
+    }
+  };
+
+  // stage sequence (kb, cs), cs = kb .. nK-1; clamped at the end
+  auto advance = [&](int &kb, int &cs) __attribute__((always_inline)) {
+    if (cs + 1 < nK) {
+      ++cs;
+    } else if (kb + 1 < nK) {
+      ++kb;
+      cs = kb;
+    }
+  };
+  int kb1 = 0, cs1 = 0;
+  advance(kb1, cs1);
+  int kb2 = kb1, cs2 = cs1;
+  advance(kb2, cs2);
+  load(0, 0);
+  store(0);
+  load(kb1, cs1);
+  store(1);
+  __syncthreads();
+  keep_diag(0, 0);
+  Ops oc, on;
+  read1(oc, 0, 0);
+  read2(oc, 0, 0);
+  build_b(oc, 0, 0, PB);
+  int b0 = 0, b1 = 1, b2 = 2;
+  // one stage from buffer b0 (its first k-step's operands in oc / fb[0])
+  auto stage = [&](bool diag) __attribute__((always_inline)) {
+    const int bscale = diag ? 128 : 129;  // x2 (fp4 codes hold w/2), x4 beyond the diagonal block
+    if (!(DBG & 1)) load(kb2, cs2);
+    if (!(DBG & 4)) read1(on, b0, 1);
+    mfmas(oc, 0, 0, 2, after_mem(bscale), diag);
+    if (!(DBG & 4)) read2(on, after_lo(b0), 1);
+    mfmas(oc, 0, 2, PB, after_mem(bscale), diag);
+    build_b(on, 1, 0, PB);
+    if (!(DBG & 4)) read1(oc, after_hi(b1), 0);
+    mfmas(on, 1, 0, 2, after_mem(bscale), false);
+    if (!(DBG & 4)) read2(oc, after_lo(b1), 0);
+    mfmas(on, 1, 2, PB, after_mem(bscale), false);
+    build_b(oc, 0, 0, PB);
+    if (!(DBG & 1)) store(after_hi(b2));
+    if (!(DBG & 2)) __syncthreads();
+    else asm volatile("" ::: "memory");
+    const int t0 = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = t0;
+    advance(kb2, cs2);
+  };
+  for (int kb = 0; kb < nK; ++kb) {
+    stage(true);
+#pragma unroll 1
+    for (int cs = kb + 1; cs < nK; ++cs) stage(false);
+    if (kb + 1 < nK) keep_diag(b0, (kb + 1) & 1);  // buffer b0 holds stage (kb+1, kb+1)
+    if (!(DBG & 8)) {
+      epilogue(kb & 1);
+    } else {
+#pragma unroll
+      for (int t = 0; t < PB; ++t)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) tot[t] += acc[r][t][0] + acc[r][t][15];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const double other = __shfl_xor(tot[t], 32);
+    const unsigned osw = __shfl_xor(sw[t], 32);
+    if (h != 0 || ti[t] < 0) continue;
+    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
   }
 }
 
@@ -835,10 +1124,10 @@ __global__ __launch_bounds__(256) void quantize_rows_kernel(int64_t n_pad, int64
 }
 
 // gather band rows of the int8 side slices: BL[t][r] = Lq[t][rows[r]], BL[t][R+r] = L3q[t][rows[r]],
-// BL[t][2R+r] = Ldq[t][rows[r]], BA[r] = panel[rows[r]]
+// BL[t][2R+r] = Ldq[t][rows[r]], BA[r] = panel[rows[r]], BA[R+r] = sqpanel[rows[r]] (squared codes)
 __global__ void gather_band_kernel(int64_t n_pad, int R, int64_t slice_stride, const int64_t *rows, const int8_t *Lq,
-                                   const int8_t *L3q, const int8_t *Ldq, const int8_t *panel, int8_t *BL,
-                                   int8_t *BA) {
+                                   const int8_t *L3q, const int8_t *Ldq, const int8_t *panel, const int8_t *sqpanel,
+                                   int8_t *BL, int8_t *BA) {
   const int r = blockIdx.x;
   const int64_t src = rows[r];
   for (int64_t q = threadIdx.x * 16; q < n_pad; q += blockDim.x * 16) {
@@ -850,6 +1139,7 @@ __global__ void gather_band_kernel(int64_t n_pad, int R, int64_t slice_stride, c
       *(v4i *)&BL[(o + 2 * R) * n_pad + q] = *(const v4i *)&Ldq[so];
     }
     *(v4i *)&BA[(int64_t)r * n_pad + q] = *(const v4i *)&panel[src * n_pad + q];
+    *(v4i *)&BA[(int64_t)(R + r) * n_pad + q] = *(const v4i *)&sqpanel[src * n_pad + q];
   }
 }
 
@@ -1042,6 +1332,14 @@ __global__ void nibble_kernel(int64_t m, int64_t n_pad, int nK, const int8_t *pa
   nib_j[rec + 16 + dd] = s2;
 }
 
+// A = P + (mu + tau) 11'/n - mu I (natural order, n x n) for the prefilter's Cholesky certificate
+__global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double tau, double *A) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * n) return;
+  const int64_t r = idx / n, c = idx % n;
+  A[idx] = P[idx] + (mu + tau) / (double)n - (r == c ? mu : 0.0);
+}
+
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1070,6 +1368,9 @@ struct gmat_epi {
   double qmax = 0, zz = 0, spy = 0;
   double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2
   double rho_mx = 0;                // the MX screen's bound: ||P_off - E||_2 + fp32 accumulation term
+  // spectral prefilter: e'Pe >= pf_mu * (|e|^2 - (1'e)^2 / n) - pf_eps * |e|^2 for every e,
+  // certified by a Cholesky factorisation of P + pf_mu (11'/n - I); pf_mu = 0: disabled
+  double pf_mu = 0, pf_tau = 0, pf_eps = 0;
   int nK = 0;                       // 128-individual stages
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
@@ -1319,6 +1620,47 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
     const double u = std::ldexp(1.0, -24);
     e->rho_mx = 1.05 * fr / os + 1e-15 * pmax * (double)n + 1.01 * (2.0 * (double)n_pad + 64.0) * u * amax;
   }
+  // Spectral prefilter certificate.  If the fp64 Cholesky of A = P + (mu + tau) 11'/n - mu I
+  // completes with positive pivots, A + E = LL' with |E| <= gamma_{n+1} |L||L'|, so lambda_min(A)
+  // >= -||E||_2 >= -gamma_{n+1} trace(A) (||L||_F^2 = trace(LL')), i.e. for every e
+  //   e'Pe >= mu (|e|^2 - (1'e)^2/n) - tau (1'e)^2/n - eps |e|^2,
+  // eps = 2 gamma_{n+1} trace(A) (x2 margin for the blocked MFMA order).  P 1 = 0 for an
+  // intercept-only model, so tau (a small lift of that direction) keeps A definite; mu is bisected.
+  {
+    DBuf A, dinv, ld, info;
+    if ((rc = A.alloc(n * n * sizeof(double))) || (rc = dinv.alloc(n * 64 * sizeof(double))) ||
+        (rc = ld.alloc(sizeof(double))) || (rc = info.alloc(sizeof(int))))
+      return fail(rc);
+    double trP = 0.0;
+    for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+    const double tau0 = 1e-8 * trP / (double)n;
+    auto ok = [&](double mu) -> int {  // 1 = certified, 0 = not, < 0 error
+      hipLaunchKernelGGL(pf_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dp.as<double>(), mu,
+                         tau0 + 1e-6 * mu, A.as<double>());
+      if (hipGetLastError() != hipSuccess) return -1;
+      if (cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), info.as<int>()) != GMAT_OK) return -1;
+      int hinfo = 1;
+      if (hipMemcpy(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      return hinfo == 0 ? 1 : 0;
+    };
+    double lo = 0.0, hi = 2.0 * trP / (double)n;  // mu above the mean eigenvalue cannot pass
+    for (int it = 0; it < 24; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      const int r = ok(mid);
+      if (r < 0) {
+        set_error("gmat_epi_create: prefilter certificate failed");
+        return fail(GMAT_E_HIP);
+      }
+      (r ? lo : hi) = mid;
+    }
+    const double eps = 2.0 * (double)(n + 1) * std::ldexp(1.0, -53) * (trP + tau0 + 1e-6 * lo + lo * (1.0 - (double)n)) * 1.01;
+    if (lo > 0.0 && lo > 1e3 * eps) {
+      e->pf_mu = lo;
+      e->pf_tau = tau0 + 1e-6 * lo;
+      e->pf_eps = eps + 1e-15 * lo;
+    }
+    if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: prefilter mu %.6g eps %.3g (trace/n %.4g)\n", lo, eps, trP / n);
+  }
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
     set_error("gmat_epi_create: z download failed");
@@ -1394,6 +1736,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();  // reference codes (refine)
   const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
   const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc), *srq = screen_sq(e, rc);  // screen codes
+  const int8_t *slq = screen_sq(e, lc);
   const int tri = (kind != GMAT_AD);
   const char *venv = getenv("GMAT_SCREEN_VARIANT");
   // tile shape of the screen (Shape<SH>); GMAT_SCREEN_VARIANT overrides for A/B runs
@@ -1433,13 +1776,21 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
   // read it has completed (event wait).
-  const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ) + 16;  // (+ MX padding)
-  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2];
+  const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ);
+  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
+  const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
+  const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
-    GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 4 * sizeof(int)));  // int8 tile list, then the MX one
+    GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
     GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
-    GMAT_TRY(ba[b].alloc((size_t)ROWS_PER_LAUNCH * n_pad));
+    GMAT_TRY(ba[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad));
+    GMAT_TRY(mxt[b].alloc((size_t)max_mx * 2 * sizeof(int)));
+    GMAT_TRY(mxr[b].alloc((size_t)max_mx * MX_BI * sizeof(int)));
+    if (use_pf) {
+      GMAT_TRY(pfc[b].alloc((size_t)4 * ROWS_PER_LAUNCH * m * sizeof(int)));
+      GMAT_TRY(flags[b].alloc((size_t)ROWS_PER_LAUNCH * nJ));
+    }
     GMAT_TRY(e13[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * m * sizeof(int)));
     GMAT_TRY(e2[b].alloc((size_t)SIDE_T * ROWS_PER_LAUNCH * m * sizeof(int)));
   }
@@ -1523,8 +1874,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // per-launch host plan (rows, tile list); empty launches dropped
   struct Launch {
     std::vector<int64_t> rows;
-    std::vector<int> tiles, tiles_mx;  // (row offset, J) per workgroup of the int8 / MX screen
-    int64_t j_lo = 0, n_mx = 0;        // n_mx: MX tiles without the padding
+    std::vector<int> tiles;  // (row offset, J) per workgroup of the int8 screen
+    int64_t j_lo = 0;
   };
   std::vector<Launch> plan;
   for (auto &rws : launches) {
@@ -1543,75 +1894,15 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         ln.tiles.push_back((int)J);
       }
     }
-    // MX tiles J-major (the row groups of one J run back to back, so its j-side records are
-    // re-read from L2), dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous
-    // chunks; padding entries (-1) exit at once
-    {
-      std::vector<int> lst;
-      for (int64_t J = 0; J * BJ < m; ++J)
-        for (int r0 = 0; r0 < Rn; r0 += MX_BI)
-          if (!tri || J >= (rws[r0] + 1) / BJ) {
-            lst.push_back(r0);
-            lst.push_back((int)J);
-          }
-      const int64_t N = (int64_t)lst.size() / 2, C = cdiv(N, 8);
-      ln.n_mx = N;
-      ln.tiles_mx.assign((size_t)16 * C, -1);
-      for (int64_t p = 0; p < N; ++p) {
-        const int64_t b = 8 * (p % C) + p / C;
-        ln.tiles_mx[2 * b] = lst[2 * p];
-        ln.tiles_mx[2 * b + 1] = lst[2 * p + 1];
-      }
-    }
     for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
     plan.push_back(std::move(ln));
   }
 
-  // side terms of launch `li` into buffer set b (stream s2)
-  auto enqueue_side = [&](size_t li, int b) -> int {
-    const Launch &ln = plan[li];
-    const int Rn = (int)ln.rows.size();
-    GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-    GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
-    GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
-                            S2));
-    GMAT_HIP(hipMemcpyAsync(dtiles[b].as<int>() + max_tiles * 2, ln.tiles_mx.data(), ln.tiles_mx.size() * sizeof(int),
-                            hipMemcpyHostToDevice, S2));
-    GMAT_HIP(hipEventRecord(side_beg[b], S2));
-    const int64_t ss = m * n_pad;  // slice stride of the side vectors
-    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, ss, drows[b].as<int64_t>(),
-                       L.Lq.as<int8_t>(), L.L3q.as<int8_t>(), L.Ldq.as<int8_t>(), slp, bl[b].as<int8_t>(),
-                       ba[b].as<int8_t>());
-    GMAT_HIP(hipGetLastError());
-    // int32 slice products (int8 MFMA, exact): C13[t] = [L'q_t; L3q_t]_band . b_j and
-    // Ldq_t,band . b_j^2, C2[t] = a_band . R'q_t,j; per group of 64 rows from the group's first
-    // needed column (a folded launch's second chunk needs far fewer columns than its first)
-    const int64_t z13 = (int64_t)SIDE_P * Rn * m, z2 = (int64_t)Rn * m;
-    for (int g0 = 0; g0 < Rn; g0 += 64) {
-      const int gn = std::min(64, Rn - g0);
-      const int64_t jg = tri ? std::max<int64_t>(ln.j_lo, ln.rows[g0] + 1) : ln.j_lo;
-      const int64_t nc = m - jg, coff = jg - ln.j_lo;
-      if (nc <= 0) continue;
-      for (int part = 0; part < SIDE_P; ++part)  // L' rows, L3 rows (x b), Ld rows (x b^2)
-        GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
-                           n_pad, (int64_t)SIDE_P * Rn * n_pad, (part == 2 ? srq : srp) + jg * n_pad, n_pad, 0,
-                           e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
-      GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
-                         R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
-    }
-    GMAT_HIP(hipEventRecord(side_end[b], S2));
-    return GMAT_OK;
-  };
-  // the first screen launches wait on never-recorded events: record them once up front
-  GMAT_HIP(hipEventRecord(screen_end[0], sm));
-  GMAT_HIP(hipEventRecord(screen_end[1], sm));
-  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
-  for (size_t li = 0; li < plan.size(); ++li) {
-    const Launch &ln = plan[li];
-    const int b = (int)(li & 1);
-    const int Rn = (int)ln.rows.size();
-    const int64_t ntiles = (int64_t)ln.tiles.size() / 2;
+  // kernel arguments of launch li on buffer set b
+  auto make_args = [&](size_t li, int b) -> ScreenArgs {
     ScreenArgs sa;
+    const Launch &ln = plan[li];
+    const int Rn = (int)ln.rows.size();
     sa.slices = e->slices.as<int8_t>();
     sa.slices_bytes = (int64_t)e->n_slice * n_pad * n_pad;
     sa.panels = e->spanels.as<int8_t>();
@@ -1636,7 +1927,17 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.sR = R.sR.as<double>();
     sa.csum_l = L.csum.as<double>();
     sa.csum_r = R.csum.as<double>();
+    sa.csq_l = L.csq.as<double>();
     sa.csq_r = R.csq.as<double>();
+    sa.tile_rows = mxr[b].as<int>();
+    sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
+    sa.pfc_stride = (int64_t)Rn * m;
+    sa.pf_mu = e->pf_mu;
+    sa.pf_eps = e->pf_eps;
+    sa.pf_tau = e->pf_tau;
+    sa.n_id = (double)e->n;
+    sa.flags = use_pf ? flags[b].as<uint8_t>() : nullptr;
+    sa.nJ = (int)nJ;
     // per element |v - s sum_t 128^-t Q_t| <= s (0.5 * 128^-(T-1) + fp64 rounding)
     sa.side_eps = 0.5 * std::pow(128.0, -(SIDE_T - 1)) + 1e-12;
     sa.ld_e = m;
@@ -1658,6 +1959,65 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.cap = e->cand_cap;
     sa.cand_i = e->cand_i.as<int64_t>();
     sa.cand_j = e->cand_j.as<int64_t>();
+    sa.n_slice = 0;
+    sa.scale_main = 0.0;
+    sa.delta = 0.0;
+    return sa;
+  };
+  // side terms of launch `li` into buffer set b (stream s2)
+  auto enqueue_side = [&](size_t li, int b) -> int {
+    const Launch &ln = plan[li];
+    const int Rn = (int)ln.rows.size();
+    GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+    GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
+    GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
+                            S2));
+    GMAT_HIP(hipEventRecord(side_beg[b], S2));
+    const int64_t ss = m * n_pad;  // slice stride of the side vectors
+    hipLaunchKernelGGL(gather_band_kernel, dim3(Rn), dim3(256), 0, S2, n_pad, Rn, ss, drows[b].as<int64_t>(),
+                       L.Lq.as<int8_t>(), L.L3q.as<int8_t>(), L.Ldq.as<int8_t>(), slp, slq, bl[b].as<int8_t>(),
+                       ba[b].as<int8_t>());
+    GMAT_HIP(hipGetLastError());
+    // int32 slice products (int8 MFMA, exact): C13[t] = [L'q_t; L3q_t]_band . b_j and
+    // Ldq_t,band . b_j^2, C2[t] = a_band . R'q_t,j; per group of 64 rows from the group's first
+    // needed column (a folded launch's second chunk needs far fewer columns than its first)
+    const int64_t z13 = (int64_t)SIDE_P * Rn * m, z2 = (int64_t)Rn * m;
+    for (int g0 = 0; g0 < Rn; g0 += 64) {
+      const int gn = std::min(64, Rn - g0);
+      const int64_t jg = tri ? std::max<int64_t>(ln.j_lo, ln.rows[g0] + 1) : ln.j_lo;
+      const int64_t nc = m - jg, coff = jg - ln.j_lo;
+      if (nc <= 0) continue;
+      for (int part = 0; part < SIDE_P; ++part)  // L' rows, L3 rows (x b), Ld rows (x b^2)
+        GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
+                           n_pad, (int64_t)SIDE_P * Rn * n_pad, (part == 2 ? srq : srp) + jg * n_pad, n_pad, 0,
+                           e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
+      GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
+                         R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
+      if (use_pf) {  // exact code products [Sab; Sa2b] (x b) and [Sab2; Sa2b2] (x b^2)
+        for (int bq = 0; bq < 2; ++bq)
+          GMAT_TRY(i8gemm_nt(S2, 2, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad,
+                             (int64_t)Rn * n_pad, (bq ? srq : srp) + jg * n_pad, n_pad, 0,
+                             pfc[b].as<int>() + (int64_t)(2 * bq) * Rn * m + (int64_t)g0 * m + coff, m, (int64_t)Rn * m));
+      }
+    }
+    if (use_pf) {
+      const ScreenArgs pa = make_args(li, b);
+      hipLaunchKernelGGL(prefilter_kernel, dim3((unsigned)cdiv((int64_t)Rn * nJ, 256)), dim3(256), 0, S2, pa);
+      GMAT_HIP(hipGetLastError());
+    }
+    GMAT_HIP(hipEventRecord(side_end[b], S2));
+    return GMAT_OK;
+  };
+  // the first screen launches wait on never-recorded events: record them once up front
+  GMAT_HIP(hipEventRecord(screen_end[0], sm));
+  GMAT_HIP(hipEventRecord(screen_end[1], sm));
+  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
+  for (size_t li = 0; li < plan.size(); ++li) {
+    const Launch &ln = plan[li];
+    const int b = (int)(li & 1);
+    const int Rn = (int)ln.rows.size();
+    const int64_t ntiles = (int64_t)ln.tiles.size() / 2;
+    ScreenArgs sa = make_args(li, b);
     unsigned long long count = 0;
     MxArgs mx;
     mx.tiles = e->mx_tiles.as<uint8_t>();
@@ -1666,19 +2026,75 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
     mx.nib_bytes = m * n_pad;
     mx.nK = e->nK;
+    // MX tiles: per 32-column block J the band rows with work in it (all rows whose block holds
+    // a pair j > i; with the prefilter only flagged (row, block) pairs), MX_BI rows per tile,
+    // J-major, dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous chunks so a
+    // J's j-side records are re-read from one L2; padding entries (-1) exit at once
+    std::vector<int> mx_tiles, mx_rows;
+    int64_t n_mx = 0;
+    auto build_mx = [&]() -> int {
+      std::vector<uint8_t> fl;
+      if (use_pf) {
+        fl.resize((size_t)Rn * nJ);
+        GMAT_HIP(hipEventSynchronize(side_end[b]));
+        GMAT_HIP(hipMemcpy(fl.data(), flags[b].p, fl.size(), hipMemcpyDeviceToHost));
+      }
+      std::vector<int> lst, rl;
+      for (int64_t J = 0; J < nJ; ++J) {
+        int cnt = 0;
+        for (int r = 0; r < Rn; ++r) {
+          const bool live = use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
+          if (!live) continue;
+          if (cnt % MX_BI == 0) {
+            lst.push_back((int)(rl.size() / MX_BI));
+            lst.push_back((int)J);
+            rl.insert(rl.end(), MX_BI, -1);
+          }
+          rl[rl.size() - MX_BI + cnt % MX_BI] = r;
+          ++cnt;
+        }
+      }
+      n_mx = (int64_t)lst.size() / 2;
+      if (getenv("GMAT_DEBUG") && li < 3) {
+        int64_t live = 0;
+        for (auto f : fl) live += f;
+        fprintf(stderr, "launch %zu: %lld MX tiles, flagged blocks %lld of %lld\n", li, (long long)n_mx, (long long)live,
+                (long long)fl.size());
+      }
+      const int64_t C = cdiv(n_mx, 8);
+      mx_tiles.assign((size_t)16 * C, -1);
+      for (int64_t p = 0; p < n_mx; ++p) {
+        const int64_t bb = 8 * (p % C) + p / C;
+        mx_tiles[2 * bb] = lst[2 * p];
+        mx_tiles[2 * bb + 1] = lst[2 * p + 1];
+      }
+      mx_rows.swap(rl);
+      if (!mx_tiles.empty()) {
+        GMAT_HIP(hipMemcpyAsync(mxt[b].p, mx_tiles.data(), mx_tiles.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+        GMAT_HIP(hipMemcpyAsync(mxr[b].p, mx_rows.data(), mx_rows.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+      }
+      return GMAT_OK;
+    };
     for (int attempt = 0;; ++attempt) {
+      if (S == 0 && attempt == 0) GMAT_TRY(build_mx());
       sa.n_slice = S;
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
-      sa.tiles = dtiles[b].as<int>() + (S == 0 ? max_tiles * 2 : 0);
-      if (S == 0)
-      {
-        const unsigned g = (unsigned)(ln.tiles_mx.size() / 2);
+      sa.tiles = S == 0 ? mxt[b].as<int>() : dtiles[b].as<int>();
+      if (S == 0 && !mx_tiles.empty()) {
+        const unsigned g = (unsigned)(mx_tiles.size() / 2);
         const dim3 T1(MxShape<1>::T);
         switch (mxv) {
           case 0: hipLaunchKernelGGL(mx_screen_kernel<0>, dim3(g), dim3(MxShape<0>::T), 0, sm, sa, mx); break;
+          case 2: hipLaunchKernelGGL(mx3_screen_kernel<0>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 4: hipLaunchKernelGGL(mx3_screen_kernel<1>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 6: hipLaunchKernelGGL(mx3_screen_kernel<3>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 8: hipLaunchKernelGGL(mx3_screen_kernel<4>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 10: hipLaunchKernelGGL(mx3_screen_kernel<8>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 12: hipLaunchKernelGGL(mx3_screen_kernel<7>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
+          case 14: hipLaunchKernelGGL(mx3_screen_kernel<15>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
           case 3: hipLaunchKernelGGL((mx_screen_kernel<1, 1>), dim3(g), T1, 0, sm, sa, mx); break;
           case 5: hipLaunchKernelGGL((mx_screen_kernel<1, 2>), dim3(g), T1, 0, sm, sa, mx); break;
           case 9: hipLaunchKernelGGL((mx_screen_kernel<1, 4>), dim3(g), T1, 0, sm, sa, mx); break;
@@ -1692,7 +2108,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
           default: hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), T1, 0, sm, sa, mx);
         }
       }
-      else if (shape)
+      else if (S == 0) {
+      } else if (shape)
         hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       else
         hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
@@ -1727,7 +2144,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
     // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
     if (S == 0)
-      ops += (double)ln.n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;
+      ops += (double)n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;
     else
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
