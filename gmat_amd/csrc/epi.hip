@@ -41,7 +41,7 @@ namespace {
 constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
-constexpr int ROWS_PER_LAUNCH = 128;
+constexpr int ROWS_PER_LAUNCH = 256;
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
 constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)
@@ -68,6 +68,7 @@ struct ScreenArgs {
   int n_rows;
   const int *tiles;  // (row offset, J) pairs; MX screens: (row-list index, J)
   const int *tile_rows;  // MX screens: MX_BI band rows per tile (-1 = none)
+  const int *tile_side;  // MX screens: per tile [3][SIDE_T][MX_TS] E1 / Ed / E2 slice products
   int tri;           // 1: only j > i
   // side terms as int32 products of int8 slices (SIDE_T slices, slice stride in elements):
   // E1 = sL[i] sum_t 128^-t c13[t][ri], E3 = sL3[i] sum_t 128^-t c13[t][R+ri],
@@ -103,18 +104,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, in
 
 // Candidate test of pair (i, j) (band row ri of the launch) given M = w'P~w (P~ the screen's
 // approximation of P_off) and sum w^2: every pair whose p-value could be below p_cut is kept.
-__device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i, int64_t j, double M, double sumw2) {
+// ts (MX screens): the tile's E1 / Ed / E2 slice products ([3][SIDE_T][MX_TS] int32 at slot * 32 +
+// col, tile_side_kernel); otherwise they come from the launch's band arrays like E3.
+constexpr int MX_TS = 16 * 32;
+__device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i, int64_t j, double M, double sumw2,
+                                          const int *ts = nullptr, int slot = 0, int col = 0) {
   if (j >= a.m || (a.tri && j <= i)) return;
   if (a.mono_l[i] || a.mono_r[j]) return;  // x == 0: the reference's statistic is NaN
   const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e,
                 od = o3 + (int64_t)a.n_rows * a.ld_e;
   double c1 = 0.0, c3 = 0.0, cd = 0.0, c2 = 0.0;
+  const int so = slot * 32 + col;
 #pragma unroll
   for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
-    c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
     c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
-    cd = cd * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + od];
-    c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
+    if (ts) {
+      c1 = c1 * (1.0 / 128.0) + (double)ts[(0 * SIDE_T + t) * MX_TS + so];
+      cd = cd * (1.0 / 128.0) + (double)ts[(1 * SIDE_T + t) * MX_TS + so];
+      c2 = c2 * (1.0 / 128.0) + (double)ts[(2 * SIDE_T + t) * MX_TS + so];
+    } else {
+      c1 = c1 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o1];
+      cd = cd * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + od];
+      c2 = c2 * (1.0 / 128.0) + (double)a.c2[t * a.c2_stride + o1];
+    }
   }
   const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, Ed = a.sLd[i] * cd, E2 = a.sR[j] * c2;
   const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
@@ -144,24 +156,24 @@ __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i
 //   var = e'Pe >= pf_mu (|e|^2 - (1'e)^2 / n) - pf_eps |e|^2,
 // with |e|^2 and 1'e exact from the int8 code products (e = (a - alpha) o (b - beta) expanded)
 // and eff from the sliced side term (bound dE3), as in cand_test.
-__global__ void prefilter_kernel(ScreenArgs a) {
+__global__ __launch_bounds__(256) void prefilter_kernel(ScreenArgs a) {
+  // one thread per (band row r, column j), j fastest; a 32-lane half-wave covers one block
+  const int64_t nb = (int64_t)a.nJ * 32;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)a.n_rows * a.nJ) return;
-  const int r = (int)(idx / a.nJ), J = (int)(idx % a.nJ);
-  const int64_t i = a.rows[r];
-  uint8_t flag = 0;
-  if (!a.mono_l[i]) {
-    const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
-    for (int jj = 0; jj < 32 && !flag; ++jj) {
-      const int64_t j = (int64_t)J * 32 + jj;
-      if (j >= a.m || j < a.j_lo || (a.tri && j <= i) || a.mono_r[j]) continue;
+  const int r = (int)(idx / nb);
+  const int64_t j = idx % nb;
+  bool live = false;
+  if (r < a.n_rows) {
+    const int64_t i = a.rows[r];
+    if (!a.mono_l[i] && j < a.m && j >= a.j_lo && !(a.tri && j <= i) && !a.mono_r[j]) {
+      const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
       const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
       double c3 = 0.0;
 #pragma unroll
       for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
       const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
       const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-      const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * a.csum_r[j];
+      const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
       const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
                    sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
       const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
@@ -175,10 +187,12 @@ __global__ void prefilter_kernel(ScreenArgs a) {
       const double se = sab - be * ca - al * cb + n * al * be;
       const double pe = ee - se * se / n;
       const double vlo = a.pf_mu * pe - a.pf_tau * se * se / n - a.pf_eps * ee - 1e-12 * a.pf_mu * (mag + se * se / n);
-      if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) flag = 1;
+      live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
     }
   }
-  a.flags[idx] = flag;
+  const unsigned long long bal = __ballot(live);
+  const int lane = threadIdx.x & 63;
+  if ((lane & 31) == 0 && r < a.n_rows) a.flags[idx >> 5] = ((bal >> lane) & 0xFFFFFFFFull) != 0;
 }
 
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
@@ -620,7 +634,8 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
     const double other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
-    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
+    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw),
+              a.tile_side + (int64_t)tl * (3 * SIDE_T * MX_TS), PB * w + t, c);
   }
 }
 
@@ -857,8 +872,44 @@ __global__ __launch_bounds__(M3_T, 1) void mx3_screen_kernel(ScreenArgs a, MxArg
     const double other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
-    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
+    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw),
+              a.tile_side + (int64_t)tl * (3 * SIDE_T * MX_TS), PB * w + t, c);
   }
+}
+
+// Side terms of the MX screen's tiles only: E1 = L'q_t[i].b_j, Ed = Ldq_t[i].b_j^2, E2 =
+// a_i.R'q_t[j] (t < SIDE_T slices, exact int32 on v_mfma_i32_32x32x32_i8) for the tile's
+// MX_BI band rows x 32 columns; one wave per (tile, product).
+// A rows 16..31 and invalid rows / columns read valid dummy data: their results are never used.
+struct TileSideArgs {
+  const int *tiles, *tile_rows;
+  const int64_t *rows;
+  const int8_t *Lq, *Ldq, *a, *b, *b2, *Rq;
+  int64_t slice_stride, n_pad, m;
+  int *out;
+};
+__global__ __launch_bounds__(64) void tile_side_kernel(TileSideArgs x) {
+  const int p = blockIdx.y;  // product: term p / SIDE_T, slice p % SIDE_T
+  const int tl = x.tiles[2 * blockIdx.x], J = x.tiles[2 * blockIdx.x + 1];
+  if (tl < 0) return;
+  const int lane = threadIdx.x, h = lane >> 5, c = lane & 31;
+  const int rr = x.tile_rows[(int64_t)tl * MX_BI + (c & 15)];
+  const int64_t i = rr >= 0 ? x.rows[rr] : 0;
+  int64_t j = (int64_t)J * BJ + c;
+  j = j < x.m ? j : x.m - 1;
+  const int term = p / SIDE_T, t = p % SIDE_T;
+  const int8_t *ap = term == 0 ? x.Lq + t * x.slice_stride + i * x.n_pad
+                               : term == 1 ? x.Ldq + t * x.slice_stride + i * x.n_pad : x.a + i * x.n_pad;
+  const int8_t *bp = term == 0 ? x.b + j * x.n_pad : term == 1 ? x.b2 + j * x.n_pad : x.Rq + t * x.slice_stride + j * x.n_pad;
+  ap += 16 * h;
+  bp += 16 * h;
+  v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 16
+  for (int64_t k0 = 0; k0 < x.n_pad; k0 += 32)
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const v4i *)(ap + k0), *(const v4i *)(bp + k0), acc, 0, 0, 0);
+  int *out = x.out + (int64_t)tl * (3 * SIDE_T * MX_TS) + p * MX_TS;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[((e & 3) + 8 * (e >> 2) + 4 * h) * 32 + c] = acc[e];  // rows < 16
 }
 
 // ------------------------------------------------------------------ exact fp64 refine
@@ -1777,7 +1828,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
   // read it has completed (event wait).
   const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ);
-  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
+  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2], tside;
+  bool side_full[2] = {false, false};  // band arrays hold E1 / Ed / E2 too (int8 screens need them)
   const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
   const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
   for (int b = 0; b < 2; ++b) {
@@ -1786,6 +1838,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(mxt[b].alloc((size_t)max_mx * 2 * sizeof(int)));
+    if (b == 0) GMAT_TRY(tside.alloc((size_t)max_mx * 3 * SIDE_T * MX_TS * sizeof(int)));
     GMAT_TRY(mxr[b].alloc((size_t)max_mx * MX_BI * sizeof(int)));
     if (use_pf) {
       GMAT_TRY(pfc[b].alloc((size_t)4 * ROWS_PER_LAUNCH * m * sizeof(int)));
@@ -1930,6 +1983,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.csq_l = L.csq.as<double>();
     sa.csq_r = R.csq.as<double>();
     sa.tile_rows = mxr[b].as<int>();
+    sa.tile_side = tside.as<int>();
     sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
     sa.pfc_stride = (int64_t)Rn * m;
     sa.pf_mu = e->pf_mu;
@@ -1965,7 +2019,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     return sa;
   };
   // side terms of launch `li` into buffer set b (stream s2)
-  auto enqueue_side = [&](size_t li, int b) -> int {
+  auto enqueue_side = [&](size_t li, int b, bool full) -> int {
+    side_full[b] = full;
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
@@ -1988,11 +2043,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const int64_t nc = m - jg, coff = jg - ln.j_lo;
       if (nc <= 0) continue;
       for (int part = 0; part < SIDE_P; ++part)  // L' rows, L3 rows (x b), Ld rows (x b^2)
-        GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
-                           n_pad, (int64_t)SIDE_P * Rn * n_pad, (part == 2 ? srq : srp) + jg * n_pad, n_pad, 0,
-                           e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
-      GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
-                         R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
+        if (full || part == 1)
+          GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, bl[b].as<int8_t>() + (int64_t)(part * Rn + g0) * n_pad,
+                             n_pad, (int64_t)SIDE_P * Rn * n_pad, (part == 2 ? srq : srp) + jg * n_pad, n_pad, 0,
+                             e13[b].as<int>() + (int64_t)(part * Rn + g0) * m + coff, m, z13));
+      if (full)
+        GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
+                           R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
       if (use_pf) {  // exact code products [Sab; Sa2b] (x b) and [Sab2; Sa2b2] (x b^2)
         for (int bq = 0; bq < 2; ++bq)
           GMAT_TRY(i8gemm_nt(S2, 2, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad,
@@ -2002,7 +2059,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
     if (use_pf) {
       const ScreenArgs pa = make_args(li, b);
-      hipLaunchKernelGGL(prefilter_kernel, dim3((unsigned)cdiv((int64_t)Rn * nJ, 256)), dim3(256), 0, S2, pa);
+      hipLaunchKernelGGL(prefilter_kernel, dim3((unsigned)cdiv((int64_t)Rn * nJ * 32, 256)), dim3(256), 0, S2, pa);
       GMAT_HIP(hipGetLastError());
     }
     GMAT_HIP(hipEventRecord(side_end[b], S2));
@@ -2011,7 +2068,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // the first screen launches wait on never-recorded events: record them once up front
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
-  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
+  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0, S != 0));
   for (size_t li = 0; li < plan.size(); ++li) {
     const Launch &ln = plan[li];
     const int b = (int)(li & 1);
@@ -2083,8 +2140,29 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
       GMAT_HIP(hipEventRecord(ev[7], sm));
       sa.tiles = S == 0 ? mxt[b].as<int>() : dtiles[b].as<int>();
+      if (S != 0 && !side_full[b]) {  // escalated from the MX screen: the int8 screen needs E1 / Ed / E2
+        GMAT_HIP(hipStreamSynchronize(S2));
+        GMAT_TRY(enqueue_side(li, b, true));
+        GMAT_HIP(hipStreamSynchronize(S2));
+      }
       if (S == 0 && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / 2);
+        TileSideArgs tsa;
+        tsa.tiles = mxt[b].as<int>();
+        tsa.tile_rows = mxr[b].as<int>();
+        tsa.rows = drows[b].as<int64_t>();
+        tsa.Lq = L.Lq.as<int8_t>();
+        tsa.Ldq = L.Ldq.as<int8_t>();
+        tsa.a = slp;
+        tsa.b = srp;
+        tsa.b2 = srq;
+        tsa.Rq = R.Rq.as<int8_t>();
+        tsa.slice_stride = m * n_pad;
+        tsa.n_pad = n_pad;
+        tsa.m = m;
+        tsa.out = tside.as<int>();
+        hipLaunchKernelGGL(tile_side_kernel, dim3(g, 3 * SIDE_T), dim3(64), 0, sm, tsa);
+        GMAT_HIP(hipGetLastError());
         const dim3 T1(MxShape<1>::T);
         switch (mxv) {
           case 0: hipLaunchKernelGGL(mx_screen_kernel<0>, dim3(g), dim3(MxShape<0>::T), 0, sm, sa, mx); break;
@@ -2118,7 +2196,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
       GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
       // next launch's side terms overlap this screen
-      if (attempt == 0 && li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1));
+      if (attempt == 0 && li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
       GMAT_HIP(hipStreamSynchronize(sm));
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
