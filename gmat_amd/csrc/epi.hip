@@ -41,11 +41,10 @@ namespace {
 constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
-constexpr int ROWS_PER_LAUNCH = 256;
+constexpr int ROWS_PER_LAUNCH = 512;
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
 constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)
-constexpr int MX_SHAPE = 0;      // default workgroup shape of the MX screen (MxShape<V> below)
 
 // w = a*b via one v_perm_b32 per 4 bytes: the i-side byte holds o(a) = {0,2,5}[a], the
 // j-side byte b in {0,1,2}; T[o(a)+b] = a*b with T = {0,0,0,1,2,0,2,4}.  Off-diagonal
@@ -193,6 +192,147 @@ __global__ __launch_bounds__(256) void prefilter_kernel(ScreenArgs a) {
   const unsigned long long bal = __ballot(live);
   const int lane = threadIdx.x & 63;
   if ((lane & 31) == 0 && r < a.n_rows) a.flags[idx >> 5] = ((bal >> lane) & 0xFFFFFFFFull) != 0;
+}
+
+// ------------------------------------------------------------------ fused side pass
+// Multi-product int8 GEMMs over a launch's band rows x all columns, 64 x 64 (band row, column)
+// tiles, exact int32 on v_mfma_i32_32x32x32_i8 from double-buffered LDS stages of 64 individuals.
+// Row-side operand sets are read straight from the per-SNP arrays through rows[] (no band
+// gather), column-side sets by column.
+//   PASS 1: products E3_t = L3q_t[i].b_j (t < SIDE_T) and the code products a.b, a^2.b, a.b^2,
+//           a^2.b^2; the epilogue evaluates the spectral prefilter per pair (in registers), sets
+//           flags[r][J] for 32-column blocks that may hold a hit, and writes E3 for those blocks.
+//   PASS 2: products E1_t = L'q_t[i].b_j, Ed_t = Ldq_t[i].b_j^2, E2_t = a_i.R'q_t[j], written only
+//           for flagged blocks (the screen reads nothing else).
+constexpr int SG_T = 64, SG_K = 64, SG_P = 80;  // tile edge, individuals per stage, LDS pitch
+struct SideArgs {
+  ScreenArgs a;  // rows, tri, j_lo, ld_e, scalars, prefilter constants, flags, c13 / c2 outputs
+  const int8_t *rs[7];  // row-side sets [m][n_pad] (slices: stride slice_stride)
+  const int8_t *cs[5];  // column-side sets
+  int64_t n_pad;
+  int n_rt;             // row tiles
+};
+template <int PASS>
+__global__ __launch_bounds__(256) void side_gemm_kernel(SideArgs x) {
+  constexpr int NR = PASS == 1 ? 5 : 7, NC = PASS == 1 ? 2 : 5, NPR = PASS == 1 ? 7 : 9;
+  const ScreenArgs &a = x.a;
+  const int rt = blockIdx.x % x.n_rt, ct = blockIdx.x / x.n_rt;
+  const int r0 = rt * SG_T;
+  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * SG_T;  // 32-aligned: a half-wave = one block
+  if (r0 >= a.n_rows || c0 >= a.m) return;
+  {  // tiles entirely on or left of the diagonal hold no pair (AA / DD)
+    if (a.tri && c0 + SG_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
+  }
+  __shared__ __attribute__((aligned(16))) int8_t sR[2][NR][SG_T * SG_P];
+  __shared__ __attribute__((aligned(16))) int8_t sC[2][NC][SG_T * SG_P];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
+  // staging: chunk q of a set = (tile row q >> 2, 16-byte piece q & 3); 256 chunks per set
+  const int srow = tid >> 2, spc = (tid & 3) * 16;
+  const int rr = min(r0 + srow, a.n_rows - 1);
+  const int64_t si = a.rows[rr];
+  const int64_t sj = min(c0 + srow, a.m - 1);
+  v4i rv[NR], cv[NC];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) rv[u] = *(const v4i *)(x.rs[u] + si * x.n_pad + k0 + spc);
+#pragma unroll
+    for (int u = 0; u < NC; ++u) cv[u] = *(const v4i *)(x.cs[u] + sj * x.n_pad + k0 + spc);
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) *(v4i *)&sR[b][u][srow * SG_P + spc] = rv[u];
+#pragma unroll
+    for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
+  };
+  // product p: (row set, column set)
+  constexpr int PR[2][9] = {{0, 1, 2, 3, 4, 3, 4, 0, 0}, {0, 1, 2, 3, 4, 5, 6, 6, 6}};
+  constexpr int PC[2][9] = {{0, 0, 0, 0, 0, 1, 1, 0, 0}, {0, 0, 0, 1, 1, 1, 2, 3, 4}};
+  v16i acc[NPR];
+#pragma unroll
+  for (int p = 0; p < NPR; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[p][e] = 0;
+  load(0);
+  store(0);
+  __syncthreads();
+  int b = 0;
+  for (int k0 = 0; k0 < x.n_pad; k0 += SG_K) {
+    const bool more = k0 + SG_K < x.n_pad;
+    if (more) load(k0 + SG_K);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v4i fr[NR], fc[NC];
+#pragma unroll
+      for (int u = 0; u < NR; ++u) fr[u] = *(const v4i *)&sR[b][u][(32 * wr + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) fc[u] = *(const v4i *)&sC[b][u][(32 * wc + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+      for (int p = 0; p < NPR; ++p)
+        acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[PR[PASS - 1][p]], fc[PC[PASS - 1][p]], acc[p], 0, 0, 0);
+    }
+    if (more) store(b ^ 1);
+    __syncthreads();
+    b ^= 1;
+  }
+  // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 32 wc + c; the 32
+  // columns of a block are the 32 lanes of one half-wave
+  const int64_t j = c0 + 32 * wc + c;
+  const int J = (int)(j / 32);
+  const bool jok = j < a.m && j >= a.j_lo;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const bool rok = r < a.n_rows;
+    const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
+    if (PASS == 1) {
+      bool live = false;
+      if (rok && jok) {
+        const int64_t i = a.rows[r];
+        if (!a.mono_l[i] && !(a.tri && j <= i) && !a.mono_r[j]) {
+          const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
+          double c3 = 0.0;
+#pragma unroll
+          for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
+          const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
+          const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
+          const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
+          const double sab = (double)acc[3][e], sa2b = (double)acc[4][e], sab2 = (double)acc[5][e],
+                       sa2b2 = (double)acc[6][e];
+          const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
+                                  -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
+          double ee = 0.0, mag = 0.0;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) {
+            ee += t_ee[q];
+            mag += fabs(t_ee[q]);
+          }
+          const double se = sab - be * ca - al * cb + n * al * be;
+          const double pe = ee - se * se / n;
+          const double vlo =
+              a.pf_mu * pe - a.pf_tau * se * se / n - a.pf_eps * ee - 1e-12 * a.pf_mu * (mag + se * se / n);
+          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
+        }
+      }
+      const unsigned long long bal = __ballot(live);
+      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
+      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+      if (blk && rok && jok) {
+        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+        for (int t = 0; t < SIDE_T; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
+      }
+    } else {
+      if (rok && jok && a.flags[(int64_t)r * a.nJ + J]) {
+        const int64_t od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+        for (int t = 0; t < SIDE_T; ++t) {
+          ((int *)a.c13)[t * a.c13_stride + o1] = acc[t][e];
+          ((int *)a.c13)[t * a.c13_stride + od] = acc[SIDE_T + t][e];
+          ((int *)a.c2)[t * a.c2_stride + o1] = acc[2 * SIDE_T + t][e];
+        }
+      }
+    }
+  }
 }
 
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
@@ -424,11 +564,13 @@ constexpr int MX_TILE = 16384;    // bytes per A tile image
 constexpr int NB_REC = 128;       // nibble bytes per (SNP, stage): two planes
 constexpr int NB_E = 136;         // LDS pitch of the epilogue copies (8-byte reads)
 constexpr int MX_BI = 16, MX_RB = MXK / 32;  // first SNPs per workgroup; 32-row tiles per K-block
-// workgroup shapes (MxShape<V>): V 0 = 4 waves x 4 pair blocks (one wave per SIMD, 256
-// accumulator registers), V 1 = 8 waves x 2 pair blocks (two waves per SIMD)
+// workgroup shape (MxShape<1>): 8 waves x 2 pair blocks, two waves per SIMD (a 4-wave x 4-block
+// shape with 256 accumulator registers per wave measured slower: one wave per SIMD exposes the
+// LDS and barrier latency)
 template <int V>
 struct MxShape {
-  static constexpr int NW = V ? 8 : 4, PB = MX_BI / NW, T = 64 * NW, MINB = 1;
+  static_assert(V == 1, "only the 8-wave shape is built");
+  static constexpr int NW = 8, PB = MX_BI / NW, T = 64 * NW, MINB = 1;
 };
 
 typedef int v2i_ __attribute__((ext_vector_type(2)));
@@ -452,26 +594,31 @@ __device__ __forceinline__ v2f_ fp4_pair(unsigned wd) {
   return __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(wd, 2.0f, BB);
 }
 
-// One workgroup = MX_BI first SNPs x BJ second SNPs; wave w owns first-SNP rows PB*w .. +PB
-// (MX_RB row tiles x PB column tiles of 32 x 32 per K-block).  Loop nest: K-block kb -> column
-// stage cs >= kb (one 128-deep stage = two 64-deep k-steps), LDS double buffer, one barrier per
-// stage; the next stage is fetched into registers while this one multiplies.  The diagonal
-// stage's genotype records are also copied to eI/eJ for the K-block's epilogue.
-// DBG (timing experiments only, results invalid): bit 0 no stage fetch after the first, bit 1 no
-// epilogue, bit 2 no MFMA, bit 3 no B-fragment generation, bit 4 no A reads, bit 5 no i/j reads
-template <int V, int DBG = 0>
+// One workgroup = MX_BI (band row, 32-column block) slots in two halves: slots 0 .. MX_BI/2-1
+// pair with column block J0 of the tile, the rest with J1 (rows flagged by the prefilter are
+// packed in half-tiles, so partly filled column blocks share a workgroup).  Wave w owns slots
+// PB*w .. +PB (one half, so its column block is wave-uniform): MX_RB row tiles x PB column
+// tiles of 32 x 32 per K-block.  Loop nest: K-block kb -> column stage cs >= kb (one 128-deep
+// stage = two 64-deep k-steps), LDS double buffer, one barrier per stage; the next stage is
+// fetched into registers while this one multiplies.  The diagonal stage's genotype records are
+// also copied to eI/eJ for the K-block's epilogue.  Tile entries are (row-list index, J0, J1).
+constexpr int MX_TE = 3;  // ints per tile entry
+template <int V>
 __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_kernel(ScreenArgs a, MxArgs x) {
   constexpr int PB = MxShape<V>::PB, RB = MX_RB, MX_T = MxShape<V>::T, NA = MX_TILE / 16 / MX_T;
+  constexpr int NJC = 2 * 8 * BJ;  // j-side chunks per stage (two column blocks)
   __shared__ __attribute__((aligned(16))) uint8_t sA[2][MX_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][BJ * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][2 * BJ * NB_REC];
   __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
-  __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
+  __shared__ __attribute__((aligned(16))) uint8_t eJ[2][2 * BJ * NB_E];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
-  const int tl = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
+  const int tl = a.tiles[MX_TE * blockIdx.x];
   if (tl < 0) return;  // padding of the XCD deal
+  const int Jt[2] = {a.tiles[MX_TE * blockIdx.x + 1], a.tiles[MX_TE * blockIdx.x + 2]};
   const int *trow = a.tile_rows + (int64_t)tl * MX_BI;  // band rows of this tile (-1 = none)
-  const int64_t J0 = (int64_t)J * BJ;
+  const int half = (PB * w) / (MX_BI / 2);             // this wave's column block
+  const int64_t J0 = (int64_t)Jt[half] * BJ;
   const int nK = x.nK;
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
   const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
@@ -484,13 +631,17 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
     ti[t] = (r >= 0) ? a.rows[r] : -1;
   }
   // staging roles (branch-free): NA 16-byte A chunks per thread (a straight copy of the tile
-  // image); one j-side chunk (SNP js, physical slot jq <- logical slot jq ^ f(js)) and one i-side
-  // chunk per thread, threads beyond the 256 / 128 chunks repeating them (identical stores)
+  // image); j-side chunks (column block jh, SNP js, physical slot jq <- logical slot jq ^ f(js)) and
+  // one i-side chunk per thread, threads beyond the 512 / 128 chunks repeating them (identical
+  // stores)
   const unsigned OOR = 0xFFFFFFF0u;  // out of range -> the buffer load returns zeros
-  const int js = (tid >> 3) & 31, jq = tid & 7, jl = jq ^ ((js >> 1) & 7);
+  const int jc = tid % NJC, jh = jc >> 8, js = (jc >> 3) & 31, jq = jc & 7, jl = jq ^ ((js >> 1) & 7);
   const int is = (tid >> 3) & 15;
   unsigned voffJ = OOR, voffI = OOR;
-  if (J0 + js < a.m) voffJ = (unsigned)((J0 + js) * nK * NB_REC + jl * 16);
+  {
+    const int64_t jj = (int64_t)Jt[jh] * BJ + js;
+    if (Jt[jh] >= 0 && jj < a.m) voffJ = (unsigned)(jj * nK * NB_REC + jl * 16);
+  }
   if (trow[is] >= 0) voffI = (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16);
 
   v4i ra[NA], rnj, rni;
@@ -504,53 +655,47 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   auto store = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][(tid + u * MX_T) * 16] = ra[u];
-    *(v4i *)&sJ[b][js * NB_REC + jq * 16] = rnj;
+    *(v4i *)&sJ[b][(jh * BJ + js) * NB_REC + jq * 16] = rnj;
     *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
   };
   // the genotype records of a K-block's diagonal stage (in buffer b) kept for its epilogue
   auto keep_diag = [&](int b, int q) __attribute__((always_inline)) {
-    const v4i vj = *(const v4i *)&sJ[b][js * NB_REC + jq * 16];
+    const v4i vj = *(const v4i *)&sJ[b][(jh * BJ + js) * NB_REC + jq * 16];
     const v4i vi = *(const v4i *)&sI[b][is * NB_REC + jq * 16];
-    *(v4i *)&eJ[q][js * NB_E + jl * 16] = vj;
+    *(v4i *)&eJ[q][(jh * BJ + js) * NB_E + jl * 16] = vj;
     *(v4i *)&eI[q][is * NB_E + jq * 16] = vi;
   };
 
   v16f_ acc[RB][PB];
   const int sw16 = 16 * ((c >> 3) & 1);  // half swap of this lane's A rows
   const int jf = (c >> 1) & 7;           // j-side slot swizzle of this lane's SNP
+  const int jrow = (half * BJ + c) * NB_REC, erow = (half * BJ + c) * NB_E;
   // one stage (128 individuals = two 64-deep k-steps) from LDS buffer b
   auto compute = [&](int b, bool diag) __attribute__((always_inline)) {
     const int bscale = diag ? 128 : 129;  // x2 (fp4 codes hold w/2), x4 beyond the diagonal block
     const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const v4i j1 = (DBG & 32) ? v4i{kk, 1, 2, 3} : *(const v4i *)&sJ[b][c * NB_REC + 16 * ((2 * kk + h) ^ jf)];
+      const v4i j1 = *(const v4i *)&sJ[b][jrow + 16 * ((2 * kk + h) ^ jf)];
       const v4i j2 = j1 << 1;  // S2 = 2b = S1 << 1 (nibbles <= 4: no carry)
       v8i_ fb[PB];
 #pragma unroll
       for (int t = 0; t < PB; ++t) {
-        const v4i i1 = (DBG & 32) ? v4i{t, 1, 2, 3} : *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
-        const v4i i2 = (DBG & 32) ? v4i{t, 7, 2, 3} : *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+        const v4i i1 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+        const v4i i2 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fb[t][q] = (DBG & 8) ? i1[q] : (i1[q] & j1[q]) | (i2[q] & j2[q]);
+        for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
 #pragma unroll
         for (int q = 4; q < 8; ++q) fb[t][q] = 0;
       }
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
-        const v4i lo = (DBG & 16) ? v4i{kk, r, 3, 4} : *(const v4i *)(ar + sw16);
-        const v4i hi = (DBG & 16) ? v4i{5, 6, 120, 8} : *(const v4i *)(ar + (16 - sw16));
+        const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
         const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int t = 0; t < PB; ++t) {
-          if (DBG & 4) {
-            acc[r][t][0] += __int_as_float(fa[0] ^ fb[t][0] ^ hi[2]);
-            continue;
-          }
-          acc[r][t] = kk == 0 ? mfma_mx(fa, fb[t], diag ? z : acc[r][t], hi[2], bscale)
-                              : mfma_mx(fa, fb[t], acc[r][t], hi[2], bscale);
-        }
+        for (int t = 0; t < PB; ++t)
+          acc[r][t] = mfma_mx(fa, fb[t], (diag && kk == 0) ? z : acc[r][t], hi[2], bscale);
       }
     }
   };
@@ -573,8 +718,8 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
       for (int r = 0; r < RB; ++r) {
         const v2i_ m1 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 16 * r + 8 * h];
         const v2i_ m2 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 64 + 16 * r + 8 * h];
-        const v2i_ b1 = *(const v2i_ *)&eJ[q][c * NB_E + 16 * r + 8 * h];
-        const v2i_ b2 = *(const v2i_ *)&eJ[q][c * NB_E + 64 + 16 * r + 8 * h];
+        const v2i_ b1 = *(const v2i_ *)&eJ[q][erow + 16 * r + 8 * h];
+        const v2i_ b2 = *(const v2i_ *)&eJ[q][erow + 64 + 16 * r + 8 * h];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           const unsigned wd = (unsigned)((m1[d] & b1[d]) | (m2[d] & b2[d]));
@@ -595,7 +740,7 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
 
   // one stage from buffer b with the next stage (nkb, ncs) fetched meanwhile into buffer b^1
   auto iter = [&](int b, bool diag, int nkb, int ncs) __attribute__((always_inline)) {
-    if (!(DBG & 1)) load(nkb, ncs);
+    load(nkb, ncs);
     __builtin_amdgcn_sched_barrier(0);  // keep the next stage's fetch ahead of this stage's work
     compute(b, diag);
     store(b ^ 1);
@@ -620,266 +765,21 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
       b ^= 1;
     }
     if (kb + 1 < nK) keep_diag(b, (kb + 1) & 1);  // buffer b now holds stage (kb+1, kb+1)
-    if (!(DBG & 2)) {
-      epilogue(kb & 1);
-    } else {
-#pragma unroll
-      for (int t = 0; t < PB; ++t)
-#pragma unroll
-        for (int r = 0; r < RB; ++r) tot[t] += acc[r][t][0] + acc[r][t][15];
-    }
+    epilogue(kb & 1);
   }
 #pragma unroll
   for (int t = 0; t < PB; ++t) {
     const double other = __shfl_xor(tot[t], 32);
     const unsigned osw = __shfl_xor(sw[t], 32);
     if (h != 0 || ti[t] < 0) continue;
-    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw),
-              a.tile_side + (int64_t)tl * (3 * SIDE_T * MX_TS), PB * w + t, c);
-  }
-}
-
-// Software-pipelined MX screen (4 waves, one per SIMD, 4 x 4 accumulator tiles of 32 x 32 per
-// wave = 256 accumulator registers).  Three LDS stage buffers: stage g+2 is fetched from global
-// memory during stage g and written at its end, so the operands of stage g+1's first k-step can
-// be read while stage g's second k-step multiplies (that buffer was completed before the
-// previous barrier).  Each k-step's operands are read in two groups during the previous k-step's
-// MFMAs (13 + 4 ds_reads: a wait for the first group never has to count past 15), A rows at a
-// 48-byte pitch (one 32-byte fragment = two contiguous ds_read_b128, conflict-free), the j-side
-// second plane derived (S2 = S1 << 1).  Register-only MFMAs are pinned between the memory ops by
-// laundering values through empty asm statements (no instructions).
-constexpr int M3_T = 256, M3_PB = 4, M3_NA = MX_TILE / 16 / M3_T, M3_AP = 48, M3_PL = MXK * M3_AP;
-
-// DBG (timing experiments only, results invalid): bit 0 no global fetch / LDS stores in the
-// loop, bit 1 no barrier, bit 2 no operand reads in the loop, bit 3 no epilogue
-template <int DBG = 0>
-__global__ __launch_bounds__(M3_T, 1) void mx3_screen_kernel(ScreenArgs a, MxArgs x) {
-  constexpr int PB = M3_PB, RB = MX_RB, NA = M3_NA;
-  __shared__ __attribute__((aligned(16))) uint8_t sA[3][4 * M3_PL];
-  __shared__ __attribute__((aligned(16))) uint8_t sI[3][MX_BI * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[3][BJ * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t eI[2][MX_BI * NB_E];
-  __shared__ __attribute__((aligned(16))) uint8_t eJ[2][BJ * NB_E];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
-  const int tl = a.tiles[2 * blockIdx.x], J = a.tiles[2 * blockIdx.x + 1];
-  if (tl < 0) return;  // padding of the XCD deal
-  const int *trow = a.tile_rows + (int64_t)tl * MX_BI;  // band rows of this tile (-1 = none)
-  const int64_t J0 = (int64_t)J * BJ;
-  const int nK = x.nK;
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
-  const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
-  const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
-  int64_t ti[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    const int r = trow[PB * w + t];
-    ti[t] = (r >= 0) ? a.rows[r] : -1;
-  }
-  // staging: NA 16-byte chunks of the tile image per thread (un-swapping the halves into the
-  // 48-byte pitch); one j-side chunk (SNP js, physical slot jq <- logical jl); threads < 128 an
-  // i-side chunk
-  const unsigned OOR = 0xFFFFFFF0u;
-  const int js = tid >> 3, jq = tid & 7, jl = jq ^ ((js >> 1) & 7), is = (tid >> 3) & 15;
-  const bool irole = tid < 8 * MX_BI;
-  const unsigned voffJ = (J0 + js < a.m) ? (unsigned)((J0 + js) * nK * NB_REC + jl * 16) : OOR;
-  const unsigned voffI = (trow[is] >= 0) ? (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16) : OOR;
-  int ldsA[NA];
-#pragma unroll
-  for (int u = 0; u < NA; ++u) {
-    const int q = tid + u * M3_T, pl = q >> 8, row = (q & 255) >> 1, half = (q & 1) ^ ((row >> 3) & 1);
-    ldsA[u] = pl * M3_PL + row * M3_AP + half * 16;
-  }
-  v4i ra[NA], rnj, rni = {0, 0, 0, 0};
-  auto load = [&](int kb, int cs) __attribute__((always_inline)) {
-    const int soffA = (kb * nK + cs) * MX_TILE;
-#pragma unroll
-    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * M3_T) * 16, soffA, 0);
-    rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
-    if (irole) rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
-  };
-  auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][ldsA[u]] = ra[u];
-    *(v4i *)&sJ[b][js * NB_REC + jq * 16] = rnj;
-    if (irole) *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
-  };
-  auto keep_diag = [&](int b, int q) __attribute__((always_inline)) {
-    *(v4i *)&eJ[q][js * NB_E + jl * 16] = *(const v4i *)&sJ[b][js * NB_REC + jq * 16];
-    if (irole) *(v4i *)&eI[q][is * NB_E + jq * 16] = *(const v4i *)&sI[b][is * NB_REC + jq * 16];
-  };
-
-  const int jf = (c >> 1) & 7;
-  v16f_ acc[RB][PB];
-  // operands of one k-step (A fragments incl. the scale in dword 6; raw genotype chunks)
-  struct Ops {
-    v8i_ fa[RB];
-    v4i j1, i1[PB], i2[PB];
-  };
-  auto read1 = [&](Ops &o, int b, int kk) __attribute__((always_inline)) {  // j, i(t0, t1), A
-    o.j1 = *(const v4i *)&sJ[b][c * NB_REC + 16 * ((2 * kk + h) ^ jf)];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      o.i1[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
-      o.i2[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r) o.fa[r] = *(const v8i_ *)&sA[b][(2 * kk + h) * M3_PL + (32 * r + c) * M3_AP];
-  };
-  auto read2 = [&](Ops &o, int b, int kk) __attribute__((always_inline)) {  // i(t2, t3)
-#pragma unroll
-    for (int t = 2; t < PB; ++t) {
-      o.i1[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
-      o.i2[t] = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
-    }
-  };
-  v4i fb[2][PB];
-  auto build_b = [&](const Ops &o, int q, int t0, int t1) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = t0; t < t1; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) fb[q][t][e] = (o.i1[t][e] & o.j1[e]) | (o.i2[t][e] & (o.j1[e] << 1));
-  };
-  auto mfmas = [&](const Ops &o, int q, int t0, int t1, int bscale, bool zero) __attribute__((always_inline)) {
-    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int t = t0; t < t1; ++t) {
-      const v8i_ bb = {fb[q][t][0], fb[q][t][1], fb[q][t][2], fb[q][t][3], 0, 0, 0, 0};
-#pragma unroll
-      for (int r = 0; r < RB; ++r) acc[r][t] = mfma_mx(o.fa[r], bb, zero ? z : acc[r][t], o.fa[r][6], bscale);
-    }
-  };
-  // order pins (empty asm): after_mem launders a value for the MFMAs that follow the preceding
-  // memory ops; after_lo / after_hi launder a value for memory ops that follow the MFMAs of
-  // accumulator columns 0-1 / 2-3
-  auto after_mem = [&](int v) __attribute__((always_inline)) {
-    asm volatile("" : "+s"(v) : : "memory");
-    return v;
-  };
-  auto after_lo = [&](int v) __attribute__((always_inline)) {
-    asm volatile("" : "+v"(v)
-                 : "a"(acc[0][0]), "a"(acc[1][0]), "a"(acc[2][0]), "a"(acc[3][0]), "a"(acc[0][1]), "a"(acc[1][1]),
-                   "a"(acc[2][1]), "a"(acc[3][1])
-                 : "memory");
-    return v;
-  };
-  auto after_hi = [&](int v) __attribute__((always_inline)) {
-    asm volatile("" : "+v"(v)
-                 : "a"(acc[0][2]), "a"(acc[1][2]), "a"(acc[2][2]), "a"(acc[3][2]), "a"(acc[0][3]), "a"(acc[1][3]),
-                   "a"(acc[2][3]), "a"(acc[3][3])
-                 : "memory");
-    return v;
-  };
-
-  double tot[PB];
-  unsigned sw[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    tot[t] = 0.0;
-    sw[t] = 0;
-  }
-  auto epilogue = [&](int q) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < PB; ++t) {
-      v2f_ s2 = {0.f, 0.f};
-      unsigned sq = 0;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const v2i_ m1 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 16 * r + 8 * h];
-        const v2i_ m2 = *(const v2i_ *)&eI[q][(PB * w + t) * NB_E + 64 + 16 * r + 8 * h];
-        const v2i_ b1 = *(const v2i_ *)&eJ[q][c * NB_E + 16 * r + 8 * h];
-        const v2i_ b2 = *(const v2i_ *)&eJ[q][c * NB_E + 64 + 16 * r + 8 * h];
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const unsigned wd = (unsigned)((m1[d] & b1[d]) | (m2[d] & b2[d]));
-          sq = __builtin_amdgcn_udot8(wd, wd, sq, false);
-#pragma unroll
-          for (int bb = 0; bb < 4; ++bb) {
-            const v2f_ wf = bb == 0 ? fp4_pair<0>(wd) : bb == 1 ? fp4_pair<1>(wd) : bb == 2 ? fp4_pair<2>(wd) : fp4_pair<3>(wd);
-            const v2f_ av = {acc[r][t][8 * d + 2 * bb], acc[r][t][8 * d + 2 * bb + 1]};
-            s2 = __builtin_elementwise_fma(wf, av, s2);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      tot[t] += (double)s2[0] + (double)s2[1];
-      sw[t] += sq;
-    }
-  };
-
-  // stage sequence (kb, cs), cs = kb .. nK-1; clamped at the end
-  auto advance = [&](int &kb, int &cs) __attribute__((always_inline)) {
-    if (cs + 1 < nK) {
-      ++cs;
-    } else if (kb + 1 < nK) {
-      ++kb;
-      cs = kb;
-    }
-  };
-  int kb1 = 0, cs1 = 0;
-  advance(kb1, cs1);
-  int kb2 = kb1, cs2 = cs1;
-  advance(kb2, cs2);
-  load(0, 0);
-  store(0);
-  load(kb1, cs1);
-  store(1);
-  __syncthreads();
-  keep_diag(0, 0);
-  Ops oc, on;
-  read1(oc, 0, 0);
-  read2(oc, 0, 0);
-  build_b(oc, 0, 0, PB);
-  int b0 = 0, b1 = 1, b2 = 2;
-  // one stage from buffer b0 (its first k-step's operands in oc / fb[0])
-  auto stage = [&](bool diag) __attribute__((always_inline)) {
-    const int bscale = diag ? 128 : 129;  // x2 (fp4 codes hold w/2), x4 beyond the diagonal block
-    if (!(DBG & 1)) load(kb2, cs2);
-    if (!(DBG & 4)) read1(on, b0, 1);
-    mfmas(oc, 0, 0, 2, after_mem(bscale), diag);
-    if (!(DBG & 4)) read2(on, after_lo(b0), 1);
-    mfmas(oc, 0, 2, PB, after_mem(bscale), diag);
-    build_b(on, 1, 0, PB);
-    if (!(DBG & 4)) read1(oc, after_hi(b1), 0);
-    mfmas(on, 1, 0, 2, after_mem(bscale), false);
-    if (!(DBG & 4)) read2(oc, after_lo(b1), 0);
-    mfmas(on, 1, 2, PB, after_mem(bscale), false);
-    build_b(oc, 0, 0, PB);
-    if (!(DBG & 1)) store(after_hi(b2));
-    if (!(DBG & 2)) __syncthreads();
-    else asm volatile("" ::: "memory");
-    const int t0 = b0;
-    b0 = b1;
-    b1 = b2;
-    b2 = t0;
-    advance(kb2, cs2);
-  };
-  for (int kb = 0; kb < nK; ++kb) {
-    stage(true);
-#pragma unroll 1
-    for (int cs = kb + 1; cs < nK; ++cs) stage(false);
-    if (kb + 1 < nK) keep_diag(b0, (kb + 1) & 1);  // buffer b0 holds stage (kb+1, kb+1)
-    if (!(DBG & 8)) {
-      epilogue(kb & 1);
-    } else {
-#pragma unroll
-      for (int t = 0; t < PB; ++t)
-#pragma unroll
-        for (int r = 0; r < RB; ++r) tot[t] += acc[r][t][0] + acc[r][t][15];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    const double other = __shfl_xor(tot[t], 32);
-    const unsigned osw = __shfl_xor(sw[t], 32);
-    if (h != 0 || ti[t] < 0) continue;
-    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw),
-              a.tile_side + (int64_t)tl * (3 * SIDE_T * MX_TS), PB * w + t, c);
+    cand_test(a, trow[PB * w + t], ti[t], J0 + c, tot[t] + other, (double)(sw[t] + osw));
   }
 }
 
 // Side terms of the MX screen's tiles only: E1 = L'q_t[i].b_j, Ed = Ldq_t[i].b_j^2, E2 =
 // a_i.R'q_t[j] (t < SIDE_T slices, exact int32 on v_mfma_i32_32x32x32_i8) for the tile's
-// MX_BI band rows x 32 columns; one wave per (tile, product).
+// MX_BI band rows x 32 columns; one workgroup per tile, its 4 waves sharing the 2 x 9 (slot half,
+// product) combinations.
 // A rows 16..31 and invalid rows / columns read valid dummy data: their results are never used.
 struct TileSideArgs {
   const int *tiles, *tile_rows;
@@ -888,28 +788,47 @@ struct TileSideArgs {
   int64_t slice_stride, n_pad, m;
   int *out;
 };
-__global__ __launch_bounds__(64) void tile_side_kernel(TileSideArgs x) {
-  const int p = blockIdx.y;  // product: term p / SIDE_T, slice p % SIDE_T
-  const int tl = x.tiles[2 * blockIdx.x], J = x.tiles[2 * blockIdx.x + 1];
+__global__ __launch_bounds__(256) void tile_side_kernel(TileSideArgs x) {
+  const int tl = x.tiles[MX_TE * blockIdx.x];
   if (tl < 0) return;
-  const int lane = threadIdx.x, h = lane >> 5, c = lane & 31;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c = lane & 31;
   const int rr = x.tile_rows[(int64_t)tl * MX_BI + (c & 15)];
   const int64_t i = rr >= 0 ? x.rows[rr] : 0;
-  int64_t j = (int64_t)J * BJ + c;
-  j = j < x.m ? j : x.m - 1;
-  const int term = p / SIDE_T, t = p % SIDE_T;
-  const int8_t *ap = term == 0 ? x.Lq + t * x.slice_stride + i * x.n_pad
-                               : term == 1 ? x.Ldq + t * x.slice_stride + i * x.n_pad : x.a + i * x.n_pad;
-  const int8_t *bp = term == 0 ? x.b + j * x.n_pad : term == 1 ? x.b2 + j * x.n_pad : x.Rq + t * x.slice_stride + j * x.n_pad;
-  ap += 16 * h;
-  bp += 16 * h;
-  v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 16
-  for (int64_t k0 = 0; k0 < x.n_pad; k0 += 32)
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const v4i *)(ap + k0), *(const v4i *)(bp + k0), acc, 0, 0, 0);
-  int *out = x.out + (int64_t)tl * (3 * SIDE_T * MX_TS) + p * MX_TS;
+  int *out0 = x.out + (int64_t)tl * (3 * SIDE_T * MX_TS);
+  // 2 slot halves x 3 * SIDE_T products, dealt to the 4 waves
+  for (int q = w; q < 2 * 3 * SIDE_T; q += 4) {
+    const int hf = q / (3 * SIDE_T), p = q % (3 * SIDE_T);
+    const int J = x.tiles[MX_TE * blockIdx.x + 1 + hf];
+    if (J < 0) continue;
+    int64_t j = (int64_t)J * BJ + c;
+    j = j < x.m ? j : x.m - 1;
+    const int term = p / SIDE_T, t = p % SIDE_T;
+    const int8_t *ap = term == 0 ? x.Lq + t * x.slice_stride + i * x.n_pad
+                                 : term == 1 ? x.Ldq + t * x.slice_stride + i * x.n_pad : x.a + i * x.n_pad;
+    const int8_t *bp = term == 0 ? x.b + j * x.n_pad : term == 1 ? x.b2 + j * x.n_pad : x.Rq + t * x.slice_stride + j * x.n_pad;
+    // k order permuted (the sum does not care, A and B agree): lane half h takes bytes
+    // 64h .. 64h+63 of each 128-byte block as four k-steps, so each lane reads whole 64-byte lines
+    ap += 64 * h;
+    bp += 64 * h;
+    v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
+    for (int64_t k0 = 0; k0 < x.n_pad; k0 += 128) {
+      v4i fa[4], fb[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) out[((e & 3) + 8 * (e >> 2) + 4 * h) * 32 + c] = acc[e];  // rows < 16
+      for (int u = 0; u < 4; ++u) {
+        fa[u] = *(const v4i *)(ap + k0 + 16 * u);
+        fb[u] = *(const v4i *)(bp + k0 + 16 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[u], fb[u], acc, 0, 0, 0);
+    }
+    int *out = out0 + p * MX_TS;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {  // rows (slots) < 16; keep this half's slots
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (row / (MX_BI / 2) == hf) out[row * 32 + c] = acc[e];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ exact fp64 refine
@@ -1800,8 +1719,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_CHECK(S >= 0 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
   int S_max_used = S;
   const int shape = venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE;
-  const char *mxenv = getenv("GMAT_MX_VARIANT");  // MxShape<V> of the MX screen (A/B runs)
-  const int mxv = mxenv ? atoi(mxenv) : MX_SHAPE;
   const int BI = shape ? Shape<1>::BI : Shape<0>::BI, MT = shape ? Shape<1>::MT : Shape<0>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   for (double &v : e->stats) v = 0.0;
@@ -1837,7 +1754,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
     GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad));
-    GMAT_TRY(mxt[b].alloc((size_t)max_mx * 2 * sizeof(int)));
+    GMAT_TRY(mxt[b].alloc((size_t)max_mx * MX_TE * sizeof(int)));
     if (b == 0) GMAT_TRY(tside.alloc((size_t)max_mx * 3 * SIDE_T * MX_TS * sizeof(int)));
     GMAT_TRY(mxr[b].alloc((size_t)max_mx * MX_BI * sizeof(int)));
     if (use_pf) {
@@ -2021,6 +1938,38 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // side terms of launch `li` into buffer set b (stream s2)
   auto enqueue_side = [&](size_t li, int b, bool full) -> int {
     side_full[b] = full;
+    if (!full && use_pf) {  // fused passes: prefilter flags + E3, then E1 / Ed / E2 for flagged blocks
+      const Launch &ln = plan[li];
+      const int Rn = (int)ln.rows.size();
+      GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+      GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
+      GMAT_HIP(hipEventRecord(side_beg[b], S2));
+      GMAT_HIP(hipMemsetAsync(flags[b].p, 0, (size_t)Rn * nJ, S2));
+      SideArgs x;
+      x.a = make_args(li, b);
+      x.n_pad = n_pad;
+      x.n_rt = (int)cdiv(Rn, SG_T);
+      const int64_t ss = m * n_pad;
+      const int64_t ncols = m - (ln.j_lo / 32) * 32;
+      const unsigned grid = (unsigned)(x.n_rt * cdiv(ncols, SG_T));
+      for (int t = 0; t < SIDE_T; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
+      x.rs[3] = slp;
+      x.rs[4] = slq;
+      x.cs[0] = srp;
+      x.cs[1] = srq;
+      hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
+      GMAT_HIP(hipGetLastError());
+      for (int t = 0; t < SIDE_T; ++t) {
+        x.rs[t] = L.Lq.as<int8_t>() + t * ss;
+        x.rs[SIDE_T + t] = L.Ldq.as<int8_t>() + t * ss;
+        x.cs[2 + t] = R.Rq.as<int8_t>() + t * ss;
+      }
+      x.rs[6] = slp;
+      hipLaunchKernelGGL(side_gemm_kernel<2>, dim3(grid), dim3(256), 0, S2, x);
+      GMAT_HIP(hipGetLastError());
+      GMAT_HIP(hipEventRecord(side_end[b], S2));
+      return GMAT_OK;
+    }
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
@@ -2065,6 +2014,70 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipEventRecord(side_end[b], S2));
     return GMAT_OK;
   };
+    // MX tiles: per 32-column block J the band rows with work in it (all rows whose block holds
+    // a pair j > i; with the prefilter only flagged (row, block) pairs), MX_BI rows per tile,
+    // J-major, dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous chunks so a
+    // J's j-side records are re-read from one L2; padding entries (-1) exit at once
+  std::vector<int> mxT[2], mxR[2];
+  int64_t nMX[2] = {0, 0};
+  size_t built_for[2] = {SIZE_MAX, SIZE_MAX};
+  auto build_mx = [&](size_t li, int b) -> int {
+    const Launch &ln = plan[li];
+    const int Rn = (int)ln.rows.size();
+    std::vector<int> &mx_tiles = mxT[b], &mx_rows = mxR[b];
+    int64_t &n_mx = nMX[b];
+    built_for[b] = li;
+    {
+      std::vector<uint8_t> fl;
+      if (use_pf) {
+        fl.resize((size_t)Rn * nJ);
+        GMAT_HIP(hipEventSynchronize(side_end[b]));
+        GMAT_HIP(hipMemcpy(fl.data(), flags[b].p, fl.size(), hipMemcpyDeviceToHost));
+      }
+      // half-tiles: up to MX_BI/2 rows of one column block; consecutive half-tiles pair up
+      std::vector<int> lst, rl;  // lst: (row-list index, J0, J1) per tile
+      int halves = 0;
+      for (int64_t J = 0; J < nJ; ++J) {
+        int cnt = 0;
+        for (int r = 0; r < Rn; ++r) {
+          const bool live = use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
+          if (!live) continue;
+          if (cnt % (MX_BI / 2) == 0) {  // open a half-tile
+            if (halves % 2 == 0) {
+              lst.push_back((int)(rl.size() / MX_BI));
+              lst.push_back((int)J);
+              lst.push_back(-1);
+              rl.insert(rl.end(), MX_BI, -1);
+            } else {
+              lst.back() = (int)J;
+            }
+            ++halves;
+          }
+          rl[rl.size() - MX_BI + ((halves - 1) % 2) * (MX_BI / 2) + cnt % (MX_BI / 2)] = r;
+          ++cnt;
+        }
+      }
+      n_mx = (int64_t)lst.size() / MX_TE;
+      if (getenv("GMAT_DEBUG") && li < 3) {
+        int64_t live = 0;
+        for (auto f : fl) live += f;
+        fprintf(stderr, "launch %zu: %lld MX tiles, flagged blocks %lld of %lld\n", li, (long long)n_mx, (long long)live,
+                (long long)fl.size());
+      }
+      const int64_t C = cdiv(n_mx, 8);
+      mx_tiles.assign((size_t)MX_TE * 8 * C, -1);
+      for (int64_t p = 0; p < n_mx; ++p) {
+        const int64_t bb = 8 * (p % C) + p / C;
+        for (int k = 0; k < MX_TE; ++k) mx_tiles[MX_TE * bb + k] = lst[MX_TE * p + k];
+      }
+      mx_rows.swap(rl);
+      if (!mx_tiles.empty()) {
+        GMAT_HIP(hipMemcpyAsync(mxt[b].p, mx_tiles.data(), mx_tiles.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+        GMAT_HIP(hipMemcpyAsync(mxr[b].p, mx_rows.data(), mx_rows.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+      }
+    }
+    return GMAT_OK;
+  };
   // the first screen launches wait on never-recorded events: record them once up front
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
@@ -2083,57 +2096,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
     mx.nib_bytes = m * n_pad;
     mx.nK = e->nK;
-    // MX tiles: per 32-column block J the band rows with work in it (all rows whose block holds
-    // a pair j > i; with the prefilter only flagged (row, block) pairs), MX_BI rows per tile,
-    // J-major, dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous chunks so a
-    // J's j-side records are re-read from one L2; padding entries (-1) exit at once
-    std::vector<int> mx_tiles, mx_rows;
-    int64_t n_mx = 0;
-    auto build_mx = [&]() -> int {
-      std::vector<uint8_t> fl;
-      if (use_pf) {
-        fl.resize((size_t)Rn * nJ);
-        GMAT_HIP(hipEventSynchronize(side_end[b]));
-        GMAT_HIP(hipMemcpy(fl.data(), flags[b].p, fl.size(), hipMemcpyDeviceToHost));
-      }
-      std::vector<int> lst, rl;
-      for (int64_t J = 0; J < nJ; ++J) {
-        int cnt = 0;
-        for (int r = 0; r < Rn; ++r) {
-          const bool live = use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
-          if (!live) continue;
-          if (cnt % MX_BI == 0) {
-            lst.push_back((int)(rl.size() / MX_BI));
-            lst.push_back((int)J);
-            rl.insert(rl.end(), MX_BI, -1);
-          }
-          rl[rl.size() - MX_BI + cnt % MX_BI] = r;
-          ++cnt;
-        }
-      }
-      n_mx = (int64_t)lst.size() / 2;
-      if (getenv("GMAT_DEBUG") && li < 3) {
-        int64_t live = 0;
-        for (auto f : fl) live += f;
-        fprintf(stderr, "launch %zu: %lld MX tiles, flagged blocks %lld of %lld\n", li, (long long)n_mx, (long long)live,
-                (long long)fl.size());
-      }
-      const int64_t C = cdiv(n_mx, 8);
-      mx_tiles.assign((size_t)16 * C, -1);
-      for (int64_t p = 0; p < n_mx; ++p) {
-        const int64_t bb = 8 * (p % C) + p / C;
-        mx_tiles[2 * bb] = lst[2 * p];
-        mx_tiles[2 * bb + 1] = lst[2 * p + 1];
-      }
-      mx_rows.swap(rl);
-      if (!mx_tiles.empty()) {
-        GMAT_HIP(hipMemcpyAsync(mxt[b].p, mx_tiles.data(), mx_tiles.size() * sizeof(int), hipMemcpyHostToDevice, sm));
-        GMAT_HIP(hipMemcpyAsync(mxr[b].p, mx_rows.data(), mx_rows.size() * sizeof(int), hipMemcpyHostToDevice, sm));
-      }
-      return GMAT_OK;
-    };
+    if (S == 0 && built_for[b] != li) GMAT_TRY(build_mx(li, b));
+    const std::vector<int> &mx_tiles = mxT[b];
+    const int64_t n_mx = nMX[b];
     for (int attempt = 0;; ++attempt) {
-      if (S == 0 && attempt == 0) GMAT_TRY(build_mx());
       sa.n_slice = S;
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
@@ -2146,45 +2112,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         GMAT_HIP(hipStreamSynchronize(S2));
       }
       if (S == 0 && !mx_tiles.empty()) {
-        const unsigned g = (unsigned)(mx_tiles.size() / 2);
-        TileSideArgs tsa;
-        tsa.tiles = mxt[b].as<int>();
-        tsa.tile_rows = mxr[b].as<int>();
-        tsa.rows = drows[b].as<int64_t>();
-        tsa.Lq = L.Lq.as<int8_t>();
-        tsa.Ldq = L.Ldq.as<int8_t>();
-        tsa.a = slp;
-        tsa.b = srp;
-        tsa.b2 = srq;
-        tsa.Rq = R.Rq.as<int8_t>();
-        tsa.slice_stride = m * n_pad;
-        tsa.n_pad = n_pad;
-        tsa.m = m;
-        tsa.out = tside.as<int>();
-        hipLaunchKernelGGL(tile_side_kernel, dim3(g, 3 * SIDE_T), dim3(64), 0, sm, tsa);
-        GMAT_HIP(hipGetLastError());
-        const dim3 T1(MxShape<1>::T);
-        switch (mxv) {
-          case 0: hipLaunchKernelGGL(mx_screen_kernel<0>, dim3(g), dim3(MxShape<0>::T), 0, sm, sa, mx); break;
-          case 2: hipLaunchKernelGGL(mx3_screen_kernel<0>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 4: hipLaunchKernelGGL(mx3_screen_kernel<1>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 6: hipLaunchKernelGGL(mx3_screen_kernel<3>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 8: hipLaunchKernelGGL(mx3_screen_kernel<4>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 10: hipLaunchKernelGGL(mx3_screen_kernel<8>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 12: hipLaunchKernelGGL(mx3_screen_kernel<7>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 14: hipLaunchKernelGGL(mx3_screen_kernel<15>, dim3(g), dim3(M3_T), 0, sm, sa, mx); break;
-          case 3: hipLaunchKernelGGL((mx_screen_kernel<1, 1>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 5: hipLaunchKernelGGL((mx_screen_kernel<1, 2>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 9: hipLaunchKernelGGL((mx_screen_kernel<1, 4>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 17: hipLaunchKernelGGL((mx_screen_kernel<1, 8>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 7: hipLaunchKernelGGL((mx_screen_kernel<1, 3>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 33: hipLaunchKernelGGL((mx_screen_kernel<1, 16>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 65: hipLaunchKernelGGL((mx_screen_kernel<1, 32>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 97: hipLaunchKernelGGL((mx_screen_kernel<1, 48>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 99: hipLaunchKernelGGL((mx_screen_kernel<1, 49>), dim3(g), T1, 0, sm, sa, mx); break;
-          case 103: hipLaunchKernelGGL((mx_screen_kernel<1, 51>), dim3(g), T1, 0, sm, sa, mx); break;
-          default: hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), T1, 0, sm, sa, mx);
-        }
+        const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
+        hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, mx);
       }
       else if (S == 0) {
       } else if (shape)
@@ -2196,7 +2125,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
       GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
       // next launch's side terms overlap this screen
-      if (attempt == 0 && li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
+      if (attempt == 0 && li + 1 < plan.size()) {
+        GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
+        // the next launch's tile list is built on the host while this screen runs
+        if (S == 0) GMAT_TRY(build_mx(li + 1, b ^ 1));
+      }
       GMAT_HIP(hipStreamSynchronize(sm));
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
@@ -2222,7 +2155,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
     // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
     if (S == 0)
-      ops += (double)n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;
+      ops += (double)n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;  // incl. empty slots
     else
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
