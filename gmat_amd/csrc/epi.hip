@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 
 #include "dla.h"
@@ -213,9 +214,13 @@ struct SideArgs {
   int n_rt;             // row tiles
 };
 template <int PASS>
-__global__ __launch_bounds__(256) void side_gemm_kernel(SideArgs x) {
-  constexpr int NR = PASS == 1 ? 5 : 7, NC = PASS == 1 ? 2 : 5, NPR = PASS == 1 ? 7 : 9;
+__global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
+  // PASS 1: row sets L3q_0..2, a, a^2 x column sets b, b^2 (7 products); PASS 2: E1 (L'q_t x b),
+  // PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three products each
+  constexpr int NR = PASS == 1 ? 5 : PASS == 4 ? 1 : 3, NC = PASS == 1 ? 2 : PASS == 4 ? 3 : 1;
+  constexpr int NPR = PASS == 1 ? 7 : 3;
   const ScreenArgs &a = x.a;
+  static_assert(NR <= 7 && NC <= 5, "operand sets");
   const int rt = blockIdx.x % x.n_rt, ct = blockIdx.x / x.n_rt;
   const int r0 = rt * SG_T;
   const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * SG_T;  // 32-aligned: a half-wave = one block
@@ -245,8 +250,8 @@ __global__ __launch_bounds__(256) void side_gemm_kernel(SideArgs x) {
     for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
   };
   // product p: (row set, column set)
-  constexpr int PR[2][9] = {{0, 1, 2, 3, 4, 3, 4, 0, 0}, {0, 1, 2, 3, 4, 5, 6, 6, 6}};
-  constexpr int PC[2][9] = {{0, 0, 0, 0, 0, 1, 1, 0, 0}, {0, 0, 0, 1, 1, 1, 2, 3, 4}};
+  constexpr int PR[4][7] = {{0, 1, 2, 3, 4, 3, 4}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
+  constexpr int PC[4][7] = {{0, 0, 0, 0, 0, 1, 1}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
   v16i acc[NPR];
 #pragma unroll
   for (int p = 0; p < NPR; ++p)
@@ -326,12 +331,13 @@ __global__ __launch_bounds__(256) void side_gemm_kernel(SideArgs x) {
         const int64_t od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
         for (int t = 0; t < SIDE_T; ++t) {
-          ((int *)a.c13)[t * a.c13_stride + o1] = acc[t][e];
-          ((int *)a.c13)[t * a.c13_stride + od] = acc[SIDE_T + t][e];
-          ((int *)a.c2)[t * a.c2_stride + o1] = acc[2 * SIDE_T + t][e];
+          if (PASS == 2) ((int *)a.c13)[t * a.c13_stride + o1] = acc[t][e];
+          if (PASS == 3) ((int *)a.c13)[t * a.c13_stride + od] = acc[t][e];
+          if (PASS == 4) ((int *)a.c2)[t * a.c2_stride + o1] = acc[t][e];
         }
       }
     }
+    if (PASS == 1) __builtin_amdgcn_sched_barrier(0);  // one element's prefilter at a time
   }
 }
 
@@ -1688,6 +1694,29 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
   return GMAT_OK;
 }
 
+namespace {
+struct Pinned {
+  void *p = nullptr;
+  size_t cap = 0;
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+  int reserve(size_t n) {
+    if (n <= cap) return GMAT_OK;
+    if (p) GMAT_HIP(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
+    GMAT_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
+    cap = n;
+    return GMAT_OK;
+  }
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+}  // namespace
+
 extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
                              int n_slice, int64_t *n_hits) {
   GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
@@ -1936,13 +1965,23 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     return sa;
   };
   // side terms of launch `li` into buffer set b (stream s2)
+  // pinned host staging: asynchronous copies from / to pageable memory block the host until the
+  // stream drains, which would serialise the side passes of launch li+1 behind screen li
+  Pinned pin_count, pin_rows[2], pin_flags[2], pin_mxt[2], pin_mxr[2];
+  GMAT_TRY(pin_count.reserve(8));
+  auto stage_rows = [&](const Launch &ln, int b) -> int {
+    GMAT_TRY(pin_rows[b].reserve(ln.rows.size() * 8));
+    std::memcpy(pin_rows[b].p, ln.rows.data(), ln.rows.size() * 8);
+    return GMAT_OK;
+  };
   auto enqueue_side = [&](size_t li, int b, bool full) -> int {
     side_full[b] = full;
     if (!full && use_pf) {  // fused passes: prefilter flags + E3, then E1 / Ed / E2 for flagged blocks
       const Launch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
       GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-      GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
+      GMAT_TRY(stage_rows(ln, b));
+      GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
       GMAT_HIP(hipEventRecord(side_beg[b], S2));
       GMAT_HIP(hipMemsetAsync(flags[b].p, 0, (size_t)Rn * nJ, S2));
       SideArgs x;
@@ -1959,21 +1998,26 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.cs[1] = srq;
       hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
       GMAT_HIP(hipGetLastError());
-      for (int t = 0; t < SIDE_T; ++t) {
-        x.rs[t] = L.Lq.as<int8_t>() + t * ss;
-        x.rs[SIDE_T + t] = L.Ldq.as<int8_t>() + t * ss;
-        x.cs[2 + t] = R.Rq.as<int8_t>() + t * ss;
-      }
-      x.rs[6] = slp;
+      for (int t = 0; t < SIDE_T; ++t) x.rs[t] = L.Lq.as<int8_t>() + t * ss;  // E1
+      x.cs[0] = srp;
       hipLaunchKernelGGL(side_gemm_kernel<2>, dim3(grid), dim3(256), 0, S2, x);
+      for (int t = 0; t < SIDE_T; ++t) x.rs[t] = L.Ldq.as<int8_t>() + t * ss;  // Ed
+      x.cs[0] = srq;
+      hipLaunchKernelGGL(side_gemm_kernel<3>, dim3(grid), dim3(256), 0, S2, x);
+      x.rs[0] = slp;  // E2
+      for (int t = 0; t < SIDE_T; ++t) x.cs[t] = R.Rq.as<int8_t>() + t * ss;
+      hipLaunchKernelGGL(side_gemm_kernel<4>, dim3(grid), dim3(256), 0, S2, x);
       GMAT_HIP(hipGetLastError());
+      GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
+      GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, flags[b].p, (size_t)Rn * nJ, hipMemcpyDeviceToHost, S2));
       GMAT_HIP(hipEventRecord(side_end[b], S2));
       return GMAT_OK;
     }
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-    GMAT_HIP(hipMemcpyAsync(drows[b].p, ln.rows.data(), Rn * 8, hipMemcpyHostToDevice, S2));
+    GMAT_TRY(stage_rows(ln, b));
+    GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
                             S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
@@ -2028,20 +2072,33 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     int64_t &n_mx = nMX[b];
     built_for[b] = li;
     {
-      std::vector<uint8_t> fl;
+      const uint8_t *fl = nullptr;  // flags of launch li (copied to pinned memory by its side pass)
       if (use_pf) {
-        fl.resize((size_t)Rn * nJ);
         GMAT_HIP(hipEventSynchronize(side_end[b]));
-        GMAT_HIP(hipMemcpy(fl.data(), flags[b].p, fl.size(), hipMemcpyDeviceToHost));
+        fl = pin_flags[b].as<uint8_t>();
       }
       // half-tiles: up to MX_BI/2 rows of one column block; consecutive half-tiles pair up
       std::vector<int> lst, rl;  // lst: (row-list index, J0, J1) per tile
       int halves = 0;
+      // live rows per column block, bucketed in one row-major sweep of the flags
+      std::vector<int> jcnt(nJ + 1, 0), jrow;
+      auto live = [&](int r, int64_t J) {
+        return use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
+      };
+      for (int r = 0; r < Rn; ++r)
+        for (int64_t J = 0; J < nJ; ++J) jcnt[J + 1] += live(r, J);
+      for (int64_t J = 0; J < nJ; ++J) jcnt[J + 1] += jcnt[J];
+      jrow.resize(jcnt[nJ]);
+      {
+        std::vector<int> fill(jcnt.begin(), jcnt.end() - 1);
+        for (int r = 0; r < Rn; ++r)
+          for (int64_t J = 0; J < nJ; ++J)
+            if (live(r, J)) jrow[fill[J]++] = r;
+      }
       for (int64_t J = 0; J < nJ; ++J) {
         int cnt = 0;
-        for (int r = 0; r < Rn; ++r) {
-          const bool live = use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
-          if (!live) continue;
+        for (int q = jcnt[J]; q < jcnt[J + 1]; ++q) {
+          const int r = jrow[q];
           if (cnt % (MX_BI / 2) == 0) {  // open a half-tile
             if (halves % 2 == 0) {
               lst.push_back((int)(rl.size() / MX_BI));
@@ -2060,9 +2117,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       n_mx = (int64_t)lst.size() / MX_TE;
       if (getenv("GMAT_DEBUG") && li < 3) {
         int64_t live = 0;
-        for (auto f : fl) live += f;
+        for (int64_t q = 0; fl && q < (int64_t)Rn * nJ; ++q) live += fl[q];
         fprintf(stderr, "launch %zu: %lld MX tiles, flagged blocks %lld of %lld\n", li, (long long)n_mx, (long long)live,
-                (long long)fl.size());
+                (long long)Rn * nJ);
       }
       const int64_t C = cdiv(n_mx, 8);
       mx_tiles.assign((size_t)MX_TE * 8 * C, -1);
@@ -2071,9 +2128,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         for (int k = 0; k < MX_TE; ++k) mx_tiles[MX_TE * bb + k] = lst[MX_TE * p + k];
       }
       mx_rows.swap(rl);
-      if (!mx_tiles.empty()) {
-        GMAT_HIP(hipMemcpyAsync(mxt[b].p, mx_tiles.data(), mx_tiles.size() * sizeof(int), hipMemcpyHostToDevice, sm));
-        GMAT_HIP(hipMemcpyAsync(mxr[b].p, mx_rows.data(), mx_rows.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+      if (!mx_tiles.empty()) {  // sm is past screen li-1, the last reader of mxt[b] / mxr[b]
+        GMAT_TRY(pin_mxt[b].reserve(mx_tiles.size() * sizeof(int)));
+        GMAT_TRY(pin_mxr[b].reserve(mx_rows.size() * sizeof(int)));
+        std::memcpy(pin_mxt[b].p, mx_tiles.data(), mx_tiles.size() * sizeof(int));
+        std::memcpy(pin_mxr[b].p, mx_rows.data(), mx_rows.size() * sizeof(int));
+        GMAT_HIP(hipMemcpyAsync(mxt[b].p, pin_mxt[b].p, mx_tiles.size() * sizeof(int), hipMemcpyHostToDevice, sm));
+        GMAT_HIP(hipMemcpyAsync(mxr[b].p, pin_mxr[b].p, mx_rows.size() * sizeof(int), hipMemcpyHostToDevice, sm));
       }
     }
     return GMAT_OK;
@@ -2123,7 +2184,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ev[2], sm));
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
-      GMAT_HIP(hipMemcpyAsync(&count, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+      GMAT_HIP(hipMemcpyAsync(pin_count.p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
       // next launch's side terms overlap this screen
       if (attempt == 0 && li + 1 < plan.size()) {
         GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
@@ -2131,6 +2192,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         if (S == 0) GMAT_TRY(build_mx(li + 1, b ^ 1));
       }
       GMAT_HIP(hipStreamSynchronize(sm));
+      count = *pin_count.as<unsigned long long>();
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
       // overflowed on its own, redo it with one more slice (thinner candidate band)
