@@ -229,7 +229,8 @@ def main():
     avg_launch_s = screen_s / max(launches, 1)
     alg_ops_launch = ops / max(launches, 1)
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
-    dense_ops_step = my_pairs * max(n_slice, 1) * n * (n + 128)
+    dense_ops_step = (my_pairs * 2 * plan.lowrank_rank() * n if n_slice == -1
+                      else my_pairs * max(n_slice, 1) * n * (n + 128))
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -238,7 +239,12 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    if n_slice == 0:
+    if n_slice == -1:
+        peak, kern = MX_PEAK_TFLOPS, "lr_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
+        note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: R x n_pad MACs x 2 per pair (R = %d bottom "
+                "eigen-directions of P); screened share of the dense work %.4f"
+                % (plan.lowrank_rank(), ops / args.steps / max(dense_ops_step, 1.0)))
+    elif n_slice == 0:
         peak, kern = MX_PEAK_TFLOPS, "mx_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
         note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: n_pad(n_pad+128)/2 MACs x 2 per pair, one pass; "
                 "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
@@ -265,7 +271,7 @@ def main():
         value = total_pairs * args.steps / t_max
         out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None, "dtype": "fp6xfp4/fp64" if n_slice == 0 else "int8/fp64", "data": "synthetic",
+               "scaling": "strong", "vs_baseline": None, "dtype": "fp6xfp4/fp64" if n_slice <= 0 else "int8/fp64", "data": "synthetic",
                "config": {"workload": "configs[2]/[3]: exhaustive exact remma_epiAA, synthetic related cohort "
                                       "%d ind x %d SNP, p_cut=%g, %d pairs per step" % (n, m, args.p_cut, total_pairs),
                           "n_id": n, "n_snp": m, "p_cut": args.p_cut, "kind": "AA",

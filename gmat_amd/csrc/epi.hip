@@ -32,6 +32,8 @@
 #include <cstring>
 #include <numeric>
 
+#include <rocsolver/rocsolver.h>
+
 #include "dla.h"
 #include "geno.h"
 
@@ -93,6 +95,7 @@ struct ScreenArgs {
   double pf_mu, pf_tau, pf_eps, n_id;
   uint8_t *flags;
   int nJ;
+  int pf_store;  // side pass 1 also writes the code products of flagged blocks to pfc
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -325,6 +328,9 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
         const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
         for (int t = 0; t < SIDE_T; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
+        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = acc[3 + q][e];
       }
     } else {
       if (rok && jok && a.flags[(int64_t)r * a.nJ + J]) {
@@ -782,60 +788,264 @@ __global__ __launch_bounds__(MxShape<V>::T, MxShape<V>::MINB) void mx_screen_ker
   }
 }
 
-// Side terms of the MX screen's tiles only: E1 = L'q_t[i].b_j, Ed = Ldq_t[i].b_j^2, E2 =
-// a_i.R'q_t[j] (t < SIDE_T slices, exact int32 on v_mfma_i32_32x32x32_i8) for the tile's
-// MX_BI band rows x 32 columns; one workgroup per tile, its 4 waves sharing the 2 x 9 (slot half,
-// product) combinations.
-// A rows 16..31 and invalid rows / columns read valid dummy data: their results are never used.
-struct TileSideArgs {
-  const int *tiles, *tile_rows;
-  const int64_t *rows;
-  const int8_t *Lq, *Ldq, *a, *b, *b2, *Rq;
-  int64_t slice_stride, n_pad, m;
-  int *out;
+// ------------------------------------------------------------------ low-rank screen (LR)
+// A certified lower bound of var = e'Pe from the bottom of P's spectrum.  With B (n x R) the
+// fp6-quantised bottom eigenvectors of P (as the MFMA reads them) and D = diag(d) >= 0,
+// gmat_epi_create certifies by an fp64 Cholesky that
+//   P - lam (I - 11'/n) + tau 11'/n + B D B' - eps I  is positive semi-definite,
+// so for every e
+//   e'Pe >= lam (|e|^2 - (1'e)^2/n) - tau (1'e)^2/n - eps |e|^2 - sum_r d_r (B_r'e)^2.
+// The per-pair cost is R x n MACs instead of the quadratic form's n^2/2: for relationship-
+// structured P the few hundred smallest eigen-directions carry the bound (lam approaches the
+// (R+1)-th eigenvalue).  c_r = B_r'e expands with e = (a - alpha) o (b - beta) (screen codes):
+//   c_r = B_r'w - beta G_r(i) - alpha H_r(j) + alpha beta q1_r,   w = a o b,
+// B_r'w on v_mfma_scale_f32_32x32x64_f8f6f4 (A = B' in fp6 tile images, B = w/2 in fp4, the
+// MX screen's operands), G = panel x B per coding (fp32), q1 = B'1.  eta_r bounds the fp32
+// accumulation and the fp32 G / H / combination rounding, |c_r - c~_r| <= eta_r, so
+//   sum_r d_r c_r^2 <= sum_r d_r (|c~_r| + eta_r)^2.
+// |e|^2 and 1'e are exact from the prefilter pass's int8 code products (pfc), eff from E3.
+struct LrArgs {
+  const uint8_t *tiles;    // [nC][nK] B' tile images (MX_TILE bytes each)
+  const uint8_t *nib_i, *nib_j;
+  int64_t tiles_bytes, nib_bytes;
+  int nK, nC, R;           // stages, 128-row chunks, padded rank
+  const float *G, *H;      // [m][R] left / right coding projections B'a
+  const float *q1, *d, *eta;
+  double lam, tau, eps;
+  unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0, 1, 4, 5 per workgroup
 };
-__global__ __launch_bounds__(256) void tile_side_kernel(TileSideArgs x) {
-  const int tl = x.tiles[MX_TE * blockIdx.x];
-  if (tl < 0) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, c = lane & 31;
-  const int rr = x.tile_rows[(int64_t)tl * MX_BI + (c & 15)];
-  const int64_t i = rr >= 0 ? x.rows[rr] : 0;
-  int *out0 = x.out + (int64_t)tl * (3 * SIDE_T * MX_TS);
-  // 2 slot halves x 3 * SIDE_T products, dealt to the 4 waves
-  for (int q = w; q < 2 * 3 * SIDE_T; q += 4) {
-    const int hf = q / (3 * SIDE_T), p = q % (3 * SIDE_T);
-    const int J = x.tiles[MX_TE * blockIdx.x + 1 + hf];
-    if (J < 0) continue;
-    int64_t j = (int64_t)J * BJ + c;
-    j = j < x.m ? j : x.m - 1;
-    const int term = p / SIDE_T, t = p % SIDE_T;
-    const int8_t *ap = term == 0 ? x.Lq + t * x.slice_stride + i * x.n_pad
-                                 : term == 1 ? x.Ldq + t * x.slice_stride + i * x.n_pad : x.a + i * x.n_pad;
-    const int8_t *bp = term == 0 ? x.b + j * x.n_pad : term == 1 ? x.b2 + j * x.n_pad : x.Rq + t * x.slice_stride + j * x.n_pad;
-    // k order permuted (the sum does not care, A and B agree): lane half h takes bytes
-    // 64h .. 64h+63 of each 128-byte block as four k-steps, so each lane reads whole 64-byte lines
-    ap += 64 * h;
-    bp += 64 * h;
-    v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-    for (int64_t k0 = 0; k0 < x.n_pad; k0 += 128) {
-      v4i fa[4], fb[4];
+
+__device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, int ri, int64_t i, int64_t j,
+                                        double lowrank) {
+  if (j >= a.m || (a.tri && j <= i)) return;
+  if (a.mono_l[i] || a.mono_r[j]) return;
+  const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+  double c3 = 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        fa[u] = *(const v4i *)(ap + k0 + 16 * u);
-        fb[u] = *(const v4i *)(bp + k0 + 16 * u);
-      }
+  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+  const double al = a.alpha[i], be = a.beta[j], ca = a.csum_l[i], ca2 = a.csq_l[i], cb = a.csum_r[j],
+               cb2 = a.csq_r[j], n = a.n_id;
+  const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
+  const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
+  const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
+               sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+  const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
+                          -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
+  double ee = 0.0, mag = 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[u], fb[u], acc, 0, 0, 0);
-    }
-    int *out = out0 + p * MX_TS;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {  // rows (slots) < 16; keep this half's slots
-      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (row / (MX_BI / 2) == hf) out[row * 32 + c] = acc[e];
+  for (int q = 0; q < 9; ++q) {
+    ee += t_ee[q];
+    mag += fabs(t_ee[q]);
+  }
+  const double se = sab - be * ca - al * cb + n * al * be;
+  const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - lowrank * (1.0 + 1e-4) -
+                     1e-12 * (x.lam + x.tau) * (mag + se * se / n);
+  if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) {
+    const unsigned long long k = atomicAdd(a.counter, 1ULL);
+    if ((int64_t)k < a.cap) {
+      a.cand_i[k] = i;
+      a.cand_j[k] = j;
     }
   }
 }
+
+// Workgroup / wave layout, tile list, staging and LDS images as mx_screen_kernel (MxShape<1>);
+// the loop is chunk ch (128 eigen-directions) -> stage cs (128 individuals), every stage a full
+// K-sweep step (no symmetry), with the chunk's epilogue after its last stage.
+__global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
+  constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
+  constexpr int NJC = 2 * 8 * BJ;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[2][MX_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][2 * BJ * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sE[42 * 1024];  // chunk epilogue operands (LDS-DMA)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int tl = a.tiles[MX_TE * blockIdx.x];
+  if (tl < 0) return;
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (x.stamp && tid == 0) x.stamp[6 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  const int Jt[2] = {a.tiles[MX_TE * blockIdx.x + 1], a.tiles[MX_TE * blockIdx.x + 2]};
+  const int *trow = a.tile_rows + (int64_t)tl * MX_BI;
+  const int half = (PB * w) / (MX_BI / 2);
+  const int64_t J0 = (int64_t)Jt[half] * BJ;
+  const int nK = x.nK, nC = x.nC;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
+  const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
+  const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
+
+  int64_t ti[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const int r = trow[PB * w + t];
+    ti[t] = (r >= 0) ? a.rows[r] : -1;
+  }
+  const unsigned OOR = 0xFFFFFFF0u;
+  const int jc = tid % NJC, jh = jc >> 8, js = (jc >> 3) & 31, jq = jc & 7, jl = jq ^ ((js >> 1) & 7);
+  const int is = (tid >> 3) & 15;
+  unsigned voffJ = OOR, voffI = OOR;
+  {
+    const int64_t jj = (int64_t)Jt[jh] * BJ + js;
+    if (Jt[jh] >= 0 && jj < a.m) voffJ = (unsigned)(jj * nK * NB_REC + jl * 16);
+  }
+  if (trow[is] >= 0) voffI = (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16);
+
+  v4i ra[NA], rnj, rni;
+  auto load = [&](int ch, int cs) __attribute__((always_inline)) {
+    const int soffA = (ch * nK + cs) * MX_TILE;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * MX_T) * 16, soffA, 0);
+    rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
+    rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][(tid + u * MX_T) * 16] = ra[u];
+    *(v4i *)&sJ[b][(jh * BJ + js) * NB_REC + jq * 16] = rnj;
+    *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
+  };
+
+  v16f_ acc[RB][PB];
+  const int sw16 = 16 * ((c >> 3) & 1);
+  const int jf = (c >> 1) & 7;
+  const int jrow = (half * BJ + c) * NB_REC;
+  auto compute = [&](int b, bool first) __attribute__((always_inline)) {
+    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v4i j1 = *(const v4i *)&sJ[b][jrow + 16 * ((2 * kk + h) ^ jf)];
+      const v4i j2 = j1 << 1;
+      v8i_ fb[PB];
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        const v4i i1 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+        const v4i i2 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
+#pragma unroll
+        for (int q = 4; q < 8; ++q) fb[t][q] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
+        const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+        const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int t = 0; t < PB; ++t)
+          acc[r][t] = mfma_mx(fa, fb[t], (first && kk == 0) ? z : acc[r][t], hi[2], 128);  // x2: codes hold w/2
+      }
+    }
+  };
+  // Chunk epilogue operands staged in LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
+  // instruction q, written linearly at sE + q KB): q 0..7 = G rows of the 16 slots (512 B each),
+  // q 8..39 = H rows of the 64 columns (physical 16-byte chunk p of column row holds logical chunk
+  // p ^ (row & 15): conflict-free reads), q 40..41 = q1 | d | eta of the chunk.  Wave w issues q = w,
+  // 8+w, .., 32+w (and 40+w for w < 2); the per-lane source offsets are fixed per tile.
+  const int64_t jcol = max((int64_t)0, min(J0 + c, a.m - 1));  // J0 < 0 for an unused tile half
+  const float be = (float)a.beta[jcol];
+  float al[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) al[t] = (float)a.alpha[ti[t] < 0 ? 0 : ti[t]];
+  int offG, offH[4], offC;
+  {
+    const int sl = 2 * w + (lane >> 5), r = trow[sl];
+    offG = (int)((r >= 0 ? a.rows[r] : 0) * x.R) + 4 * (lane & 31);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = 2 * (w + 8 * u) + (lane >> 5);
+      const int Jh = Jt[row >> 5];
+      const int64_t jj = Jh < 0 ? 0 : min((int64_t)Jh * BJ + (row & 31), a.m - 1);
+      offH[u] = (int)(jj * x.R) + 4 * ((lane & 31) ^ (row & 15));
+    }
+    offC = (w * 256 + 4 * lane) & 511;  // float index in q1 | d | eta | (pad: re-reads q1)
+  }
+  auto fetch_epi = [&](int ch) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) void *lds_t;
+    __builtin_amdgcn_global_load_lds(x.G + offG + ch * MXK, (lds_t)&sE[w * 1024], 16, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_global_load_lds(x.H + offH[u] + ch * MXK, (lds_t)&sE[(8 + w + 8 * u) * 1024], 16, 0, 0);
+    if (w < 2) {
+      const float *src = offC < 128 ? x.q1 + offC : offC < 256 ? x.d + offC - 128 : offC < 384 ? x.eta + offC - 256 : x.q1;
+      __builtin_amdgcn_global_load_lds(src + ch * MXK, (lds_t)&sE[(40 + w) * 1024], 16, 0, 0);
+    }
+  };
+  double lowrank[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) lowrank[t] = 0.0;
+  const int hrow = half * BJ + c;
+  auto epilogue = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < PB; ++t) {
+      const float ab = al[t] * be;
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = 8 * r + 2 * q + h;  // logical 16-byte chunk of the chunk's 128 rows
+          const float4 g = *(const float4 *)&sE[(PB * w + t) * 512 + 16 * k];
+          const float4 hh = *(const float4 *)&sE[8192 + hrow * 512 + 16 * (k ^ (hrow & 15))];
+          const float4 qq = *(const float4 *)&sE[40960 + 16 * k], dd = *(const float4 *)&sE[40960 + 512 + 16 * k],
+                       et = *(const float4 *)&sE[40960 + 1024 + 16 * k];
+          const float gv[4] = {g.x, g.y, g.z, g.w}, hv[4] = {hh.x, hh.y, hh.z, hh.w}, qv[4] = {qq.x, qq.y, qq.z, qq.w},
+                      dv[4] = {dd.x, dd.y, dd.z, dd.w}, ev[4] = {et.x, et.y, et.z, et.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float cr = acc[r][t][4 * q + u] - be * gv[u] - al[t] * hv[u] + ab * qv[u];
+            const float y = fabsf(cr) + ev[u];
+            s = fmaf(dv[u] * y, y, s);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      lowrank[t] += (double)s;
+    }
+  };
+  auto iter = [&](int b, bool first, int nch, int ncs) __attribute__((always_inline)) {
+    load(nch, ncs);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(b, first);
+    store(b ^ 1);
+    __syncthreads();
+  };
+
+  load(0, 0);
+  store(0);
+  __syncthreads();
+  stamp(1);
+  int b = 0;
+  for (int ch = 0; ch < nC; ++ch) {
+    const bool lastch = ch + 1 == nC;
+    if (ch > 0) __syncthreads();  // every wave is past the previous chunk's epilogue reads of sE
+    fetch_epi(ch);                // lands during this chunk's stages
+    if (nK > 1) iter(b, true, ch, 1);
+    else iter(b, true, lastch ? ch : ch + 1, 0);
+    b ^= 1;
+#pragma unroll 1
+    for (int cs = 1; cs < nK; ++cs) {
+      const bool lastc = cs + 1 == nK;
+      iter(b, false, lastc ? (lastch ? ch : ch + 1) : ch, lastc ? 0 : cs + 1);
+      b ^= 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of sE has landed
+    __syncthreads();                                   // ... and every other wave's
+    epilogue();
+  }
+  stamp(4);
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const double other = __shfl_xor(lowrank[t], 32);
+    if (h != 0 || ti[t] < 0) continue;
+    lr_test(a, x, trow[PB * w + t], ti[t], J0 + c, lowrank[t] + other);
+  }
+  if (x.stamp) {
+    __syncthreads();
+    stamp(5);
+  }
+}
+
 
 // ------------------------------------------------------------------ exact fp64 refine
 // For pairs (pi[t], pj[t]): e = (a - alpha)(b - beta) in fp64 (storage order), var = e'Pe,
@@ -1211,17 +1421,9 @@ __global__ void zsum_kernel(int64_t n_pad, const double *Ps, double *z) {
 // columns): scale 2^e with e the least exponent giving |v| / 2^e <= 7.5, round to nearest even
 // on the e2m3 grid (steps 1/8 below 2, 1/4 below 4, 1/2 up to 7.5).  Also writes the dequantised
 // matrix Qn (natural order) for the rigorous residual bound.
-__global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *P, uint32_t *tiles, double *Qn) {
-  const int64_t nblk = n_pad / 32;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n_pad * nblk) return;
-  const int64_t rho = idx / nblk, bI = idx % nblk;
+__host__ __device__ inline void fp6_block(const double *v, uint32_t wds[8], double *dq) {
   double mx = 0.0;
-  for (int j = 0; j < 32; ++j) {
-    const int64_t c = bI * 32 + perm_nat(j);
-    const double v = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
-    mx = fmax(mx, fabs(v));
-  }
+  for (int j = 0; j < 32; ++j) mx = fmax(mx, fabs(v[j]));
   int e = -127;
   if (mx > 0.0) {
     e = (int)ceil(log2(mx / 7.5));
@@ -1229,11 +1431,10 @@ __global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *
     while (e > -127 && ldexp(7.5, e - 1) >= mx) --e;
     e = e < -127 ? -127 : e;
   }
-  uint32_t wds[8] = {0, 0, 0, 0, 0, 0, (uint32_t)(e + 127), 0};
+  for (int k = 0; k < 8; ++k) wds[k] = 0;
+  wds[6] = (uint32_t)(e + 127);
   for (int j = 0; j < 32; ++j) {
-    const int64_t c = bI * 32 + perm_nat(j);
-    const double v = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
-    const double y = ldexp(v, -e), ay = fabs(y);
+    const double y = ldexp(v[j], -e), ay = fabs(y);
     double q;
     uint32_t code;
     if (ay < 2.0) {
@@ -1250,14 +1451,31 @@ __global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *
     const int bit = 6 * j;
     wds[bit >> 5] |= code << (bit & 31);
     if ((bit & 31) > 26) wds[(bit >> 5) + 1] |= code >> (32 - (bit & 31));
-    Qn[rho * n_pad + c] = ldexp(y < 0.0 ? -q : q, e);
+    dq[j] = ldexp(y < 0.0 ? -q : q, e);
   }
-  // tile (K-block of rho, stage of the block), plane = block within the stage, 32-byte slot of
-  // the row, halves swapped on rows with (row >> 3) & 1
+}
+// tile image slot of (matrix row rho, 32-column storage block bI): tile (rho / MXK, bI / 4), plane
+// bI & 3, 32-byte slot of the row, halves swapped on rows with (row >> 3) & 1
+__host__ __device__ inline void fp6_store(uint32_t *tiles, int nK, int64_t rho, int64_t bI, const uint32_t wds[8]) {
   const int64_t kb = rho / MXK, row = rho % MXK, cs = bI >> 2, plane = bI & 3;
   uint32_t *dst = tiles + ((kb * nK + cs) * MX_TILE + plane * 4096 + row * 32) / 4;
   const int sw = (int)((row >> 3) & 1) * 4;
   for (int k = 0; k < 8; ++k) dst[(k + sw) & 7] = wds[k];
+}
+__global__ void mx_quant_kernel(int64_t n, int64_t n_pad, int nK, const double *P, uint32_t *tiles, double *Qn) {
+  const int64_t nblk = n_pad / 32;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * nblk) return;
+  const int64_t rho = idx / nblk, bI = idx % nblk;
+  double v[32], dq[32];
+  for (int j = 0; j < 32; ++j) {
+    const int64_t c = bI * 32 + perm_nat(j);
+    v[j] = (rho < n && c < n && rho != c) ? P[rho * n + c] : 0.0;
+  }
+  uint32_t wds[8];
+  fp6_block(v, wds, dq);
+  for (int j = 0; j < 32; ++j) Qn[rho * n_pad + bI * 32 + perm_nat(j)] = dq[j];
+  fp6_store(tiles, nK, rho, bI, wds);
 }
 
 // R = (P_off - E) * out_scale with E the symmetric matrix the MX screen actually evaluates
@@ -1316,6 +1534,18 @@ __global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double ta
   A[idx] = P[idx] + (mu + tau) / (double)n - (r == c ? mu : 0.0);
 }
 
+// A = P + C + (lam + tau) 11'/n - lam I (natural order) for the low-rank screen's certificate
+__global__ void lr_shift_kernel(int64_t n, const double *P, const double *C, double lam, double tau, double *A) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * n) return;
+  const int64_t r = idx / n, c = idx % n;
+  A[idx] = P[idx] + C[idx] + (lam + tau) / (double)n - (r == c ? lam : 0.0);
+}
+__global__ void f64_to_f32_kernel(int64_t count, const double *src, float *dst) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < count) dst[idx] = (float)src[idx];
+}
+
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1335,6 +1565,7 @@ struct Coding {
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
+  DBuf lrG;                       // low-rank screen: B' x screen codes, fp32 [m][lr_R]
 };
 
 struct gmat_epi {
@@ -1347,6 +1578,11 @@ struct gmat_epi {
   // spectral prefilter: e'Pe >= pf_mu * (|e|^2 - (1'e)^2 / n) - pf_eps * |e|^2 for every e,
   // certified by a Cholesky factorisation of P + pf_mu (11'/n - I); pf_mu = 0: disabled
   double pf_mu = 0, pf_tau = 0, pf_eps = 0;
+  // low-rank screen (lr_screen_kernel): e'Pe >= lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - sum_r d_r
+  // (B_r'e)^2 with B the fp6 bottom eigenvectors; lr_R = padded rank (0: disabled)
+  int lr_R = 0;
+  double lr_lam = 0, lr_tau = 0, lr_eps = 0;
+  DBuf lr_tiles, lr_Bs, lr_q1, lr_d, lr_eta;  // B' tile images; B fp64 [n_pad][lr_R] storage order
   int nK = 0;                       // 128-individual stages
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
@@ -1359,10 +1595,15 @@ struct gmat_epi {
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
   double stats[10] = {0};
   hipStream_t s = 0;
-  hipStream_t s1 = nullptr, s2 = nullptr;  // scan pipeline: screen / side-term streams
+  // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
+  struct ScanBufs {
+    DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
+  } sb;
+  hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
     if (s2) (void)hipStreamDestroy(s2);
+    if (s3) (void)hipStreamDestroy(s3);
   }
 };
 
@@ -1454,6 +1695,18 @@ int build_coding(gmat_epi *e, int which) {
   hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
                      panel, cd.nibI.as<uint32_t>(), cd.nibJ.as<uint32_t>());
   GMAT_HIP(hipGetLastError());
+  if (e->lr_R) {  // G = screen codes x B (exact in fp64: fp6 x small integers), kept in fp32
+    DBuf g64;
+    const int64_t Rp = e->lr_R;
+    GMAT_TRY(g64.alloc((size_t)m * Rp * sizeof(double)));
+    GMAT_TRY(cd.lrG.alloc((size_t)m * Rp * sizeof(float)));
+    GMAT_TRY(dgemm_i8a(e->s, m, Rp, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->lr_Bs.as<double>(), Rp, 0}, 0.0,
+                       g64.as<double>(), Rp));
+    hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)cdiv(m * Rp, 256)), dim3(256), 0, e->s, m * Rp,
+                       g64.as<double>(), cd.lrG.as<float>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipStreamSynchronize(e->s));
+  }
   GMAT_HIP(hipStreamSynchronize(e->s));
   cd.U.release();
   cd.ready = true;
@@ -1477,6 +1730,162 @@ void kind_codings(int kind, int *lc, int *rc) {
   *rc = (kind == GMAT_AA) ? 0 : 1;
 }
 
+
+// Low-rank screen setup: bottom eigenpairs of P (rocSOLVER syevd, the intercept direction lifted
+// out of the bottom by s 11'/n), fp6 quantisation of B (the exact values the MFMA multiplies),
+// and the certificate: the largest lam (bisection) for which an fp64 Cholesky of
+//   A = P - lam I + (lam + tau) 11'/n + B D(lam) B',  d_r = (lam - lam_r)_+ (1 + kappa)
+// completes.  As for the prefilter, A + E = LL' with ||E||_2 <= gamma_{n+1} trace(A); the fp64
+// rounding of A itself (at most (R + 4) u per entry of |P| + lam + 2(lam + tau)/n + |B|D|B'| <=
+// cmax) adds n (R + 4) u (...) in the spectral norm.  Returns GMAT_OK with lr_R = 0 when the
+// screen is disabled (GMAT_LR_RANK=0 / GMAT_NO_LR) or not applicable.
+int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
+  const int64_t n = e->n, n_pad = e->n_pad;
+  const char *renv = getenv("GMAT_LR_RANK"), *kenv = getenv("GMAT_LR_KAPPA");
+  const int R_req = renv ? atoi(renv) : 384;
+  if (R_req <= 0 || getenv("GMAT_NO_LR") || n < 8) return GMAT_OK;
+  const int Re = (int)std::min<int64_t>(R_req, n - 1);
+  const int Rp = (int)cdiv(Re, MXK) * MXK;
+  const int ne = (int)std::min<int64_t>(Re + 1, n);
+  const double kap = kenv ? atof(kenv) : 0.7;
+  double trP = 0.0;
+  for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+  const double t0 = now();
+  DBuf A, W, E, dinfo;
+  GMAT_TRY(A.alloc(n * n * sizeof(double)));
+  GMAT_TRY(W.alloc(n * sizeof(double)));
+  GMAT_TRY(E.alloc(n * sizeof(double)));
+  GMAT_TRY(dinfo.alloc(sizeof(int)));
+  hipLaunchKernelGGL(pf_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dP, 0.0, 4.0 * trP / (double)n,
+                     A.as<double>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipDeviceSynchronize());
+  {  // full symmetric eigendecomposition (ascending); column r of the column-major result =
+     // eigenvector r = row r of A read row-major
+    rocblas_handle hb = nullptr;
+    GMAT_CHECK(rocblas_create_handle(&hb) == rocblas_status_success, GMAT_E_HIP, "lr_setup: rocblas handle");
+    const rocblas_status st = rocsolver_dsyevd(hb, rocblas_evect_original, rocblas_fill_lower, (rocblas_int)n,
+                                               A.as<double>(), (rocblas_int)n, W.as<double>(), E.as<double>(),
+                                               dinfo.as<rocblas_int>());
+    GMAT_HIP(hipDeviceSynchronize());
+    rocblas_destroy_handle(hb);
+    GMAT_CHECK(st == rocblas_status_success, GMAT_E_HIP, "lr_setup: rocsolver_dsyevd status %d", (int)st);
+  }
+  int hinfo = 0;
+  GMAT_HIP(hipMemcpy(&hinfo, dinfo.p, sizeof(int), hipMemcpyDeviceToHost));
+  GMAT_CHECK(hinfo == 0, GMAT_E_HIP, "lr_setup: syevd info %d", hinfo);
+  std::vector<double> lam_r(ne), Zh((size_t)n * ne);
+  GMAT_HIP(hipMemcpy(lam_r.data(), W.p, ne * sizeof(double), hipMemcpyDeviceToHost));
+  GMAT_HIP(hipMemcpy(Zh.data(), A.p, Zh.size() * sizeof(double), hipMemcpyDeviceToHost));
+  const double t1 = now();
+  // fp6 B' (rows r, storage columns) -> tile images; dequantised B natural [k][r], storage [q][r]
+  const int nK = e->nK, nC = Rp / MXK;
+  std::vector<uint32_t> img((size_t)nC * nK * MX_TILE / 4, 0u);
+  std::vector<double> Bn((size_t)n * Rp, 0.0), Bs((size_t)n_pad * Rp, 0.0);
+  for (int r = 0; r < Rp; ++r)
+    for (int64_t bI = 0; bI < n_pad / 32; ++bI) {
+      double v[32], dq[32];
+      for (int j = 0; j < 32; ++j) {
+        const int64_t c = bI * 32 + perm_nat(j);
+        v[j] = (r < Re && c < n) ? Zh[(size_t)r * n + c] : 0.0;
+      }
+      uint32_t wds[8];
+      fp6_block(v, wds, dq);
+      fp6_store(img.data(), nK, r, bI, wds);
+      for (int j = 0; j < 32; ++j) {
+        const int64_t c = bI * 32 + perm_nat(j);
+        if (c < n) Bn[(size_t)c * Rp + r] = dq[j];
+        Bs[(size_t)(bI * 32 + j) * Rp + r] = dq[j];
+      }
+    }
+  std::vector<double> l1(Rp, 0.0), q1(Rp, 0.0);
+  for (int64_t k = 0; k < n; ++k)
+    for (int r = 0; r < Rp; ++r) {
+      l1[r] += std::fabs(Bn[(size_t)k * Rp + r]);
+      q1[r] += Bn[(size_t)k * Rp + r];
+    }
+  // certificate
+  DBuf dBn, dBD, C, dinv, ld, cinfo;
+  GMAT_TRY(dBn.alloc(Bn.size() * sizeof(double)));
+  GMAT_TRY(dBD.alloc(Bn.size() * sizeof(double)));
+  GMAT_TRY(C.alloc(n * n * sizeof(double)));
+  GMAT_TRY(dinv.alloc(n * 64 * sizeof(double)));
+  GMAT_TRY(ld.alloc(sizeof(double)));
+  GMAT_TRY(cinfo.alloc(sizeof(int)));
+  GMAT_HIP(hipMemcpy(dBn.p, Bn.data(), Bn.size() * sizeof(double), hipMemcpyHostToDevice));
+  const double lam_top = lam_r[ne - 1];
+  const double tau = 0.5 * lam_top;
+  std::vector<double> d(Rp, 0.0), BD(Bn.size());
+  auto dvec = [&](double lam) {
+    for (int r = 0; r < Rp; ++r) d[r] = r < Re ? std::max(lam - lam_r[r], 0.0) * (1.0 + kap) : 0.0;
+  };
+  auto eps_of = [&](double lam) {  // d must be dvec(lam)
+    double trC = 0.0, cmax = 0.0;
+    for (int64_t k = 0; k < n; ++k) {
+      double ck = 0.0;
+      for (int r = 0; r < Rp; ++r) ck += d[r] * Bn[(size_t)k * Rp + r] * Bn[(size_t)k * Rp + r];
+      trC += ck;
+      cmax = std::max(cmax, ck);
+    }
+    const double u = std::ldexp(1.0, -53);
+    const double trA = trP + trC + (lam + tau) - (double)n * lam;
+    return 2.0 * (double)(n + 1) * u * std::fabs(trA) * 1.01 +
+           (double)n * (Rp + 4) * u * (pmax + 2.0 * lam + 2.0 * (lam + tau) / (double)n + cmax);
+  };
+  auto ok = [&](double lam) -> int {
+    dvec(lam);
+    for (int64_t k = 0; k < n; ++k)
+      for (int r = 0; r < Rp; ++r) BD[(size_t)k * Rp + r] = Bn[(size_t)k * Rp + r] * d[r];
+    GMAT_HIP(hipMemcpy(dBD.p, BD.data(), BD.size() * sizeof(double), hipMemcpyHostToDevice));
+    GMAT_TRY(dgemm(0, n, n, Rp, 1.0, DView{dBD.as<double>(), Rp, 0}, DView{dBn.as<double>(), Rp, 1}, 0.0,
+                   C.as<double>(), n));
+    hipLaunchKernelGGL(lr_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dP, C.as<double>(), lam,
+                       tau, A.as<double>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_TRY(cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), cinfo.as<int>()));
+    int hi = 1;
+    GMAT_HIP(hipMemcpy(&hi, cinfo.p, sizeof(int), hipMemcpyDeviceToHost));
+    return hi == 0 ? 1 : 0;
+  };
+  double lo = 0.0, hi = 1.3 * std::max(lam_top, lam_r[Re - 1]);
+  for (int it = 0; it < 20; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    int r = ok(mid);
+    if (r < 0) return r;
+    (r ? lo : hi) = mid;
+  }
+  dvec(lo);
+  const double eps = eps_of(lo);
+  if (getenv("GMAT_DEBUG"))
+    fprintf(stderr, "lr_setup: R %d (padded %d) lam_0 %.4g lam_R %.4g -> lam %.4g tau %.3g eps %.3g (pf_mu %.4g); "
+                    "eigen %.2f s, certificate %.2f s\n",
+            Re, Rp, lam_r[0], lam_top, lo, tau, eps, e->pf_mu, t1 - t0, now() - t1);
+  if (!(lo > 0.0) || lo <= e->pf_mu || lo < 1e3 * eps) return GMAT_OK;  // no better than the prefilter
+  // kernel constants: d rounded up, eta = u32 |B_r|_1 (8 n_pad + 400) (fp32 accumulation over
+  // n_pad products with the MFMA-order margin, fp32 G / H / q1 and the 6-term combination)
+  std::vector<float> fd(Rp), feta(Rp), fq1(Rp);
+  const double u32 = std::ldexp(1.0, -24);
+  for (int r = 0; r < Rp; ++r) {
+    fd[r] = (float)(d[r] * (1.0 + 1e-6));
+    feta[r] = (float)(u32 * l1[r] * (8.0 * (double)n_pad + 400.0) * 1.01);
+    fq1[r] = (float)q1[r];
+  }
+  GMAT_TRY(e->lr_tiles.alloc(img.size() * 4));
+  GMAT_TRY(e->lr_Bs.alloc(Bs.size() * sizeof(double)));
+  GMAT_TRY(e->lr_q1.alloc(Rp * sizeof(float)));
+  GMAT_TRY(e->lr_d.alloc(Rp * sizeof(float)));
+  GMAT_TRY(e->lr_eta.alloc(Rp * sizeof(float)));
+  GMAT_HIP(hipMemcpy(e->lr_tiles.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_Bs.p, Bs.data(), Bs.size() * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_q1.p, fq1.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_d.p, fd.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_eta.p, feta.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
+  e->lr_lam = lo;
+  e->lr_tau = tau;
+  e->lr_eps = eps + 1e-15 * lo;
+  e->lr_R = Rp;
+  return GMAT_OK;
+}
 }  // namespace
 
 extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
@@ -1637,6 +2046,12 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
     }
     if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: prefilter mu %.6g eps %.3g (trace/n %.4g)\n", lo, eps, trP / n);
   }
+  if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax)) != GMAT_OK) {
+    // the low-rank screen is an accelerator: without it the MX screen runs
+    if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: low-rank screen unavailable: %s\n", gmat_last_error());
+    e->lr_R = 0;
+    rc = GMAT_OK;
+  }
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
     set_error("gmat_epi_create: z download failed");
@@ -1646,6 +2061,15 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   for (double v : hz) zz += v;
   e->zz = zz;
   *out = e;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_info(const gmat_epi *e, double *out4) {
+  GMAT_CHECK(e && out4, GMAT_E_ARG, "gmat_epi_info: bad arguments");
+  out4[0] = e->lr_R;
+  out4[1] = e->lr_lam;
+  out4[2] = e->pf_mu;
+  out4[3] = (double)e->n_pad;
   return GMAT_OK;
 }
 
@@ -1743,6 +2167,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // slices.  Automatic: MX when the candidate band stays thin (p_cut <= 1e-4), 2 slices up to
   // p_cut 1e-2, else all; n_slice > 0 forces S slices, n_slice < 0 forces MX.  A launch whose
   // candidates overflow the buffer is redone one level finer (and the scan keeps that level).
+  // Level 0 runs the low-rank screen when the plan has one (n_slice -1 forces the MX quadratic
+  // form, -2 the low-rank screen).
+  GMAT_CHECK(n_slice >= -2, GMAT_E_ARG, "n_slice %d < -2", n_slice);
+  GMAT_CHECK(n_slice != -2 || e->lr_R > 0, GMAT_E_ARG, "n_slice -2: this plan has no low-rank screen certificate");
   int S = n_slice > 0 ? n_slice
                       : (n_slice < 0 ? 0 : (p_cut <= 1e-4 ? 0 : std::min(e->n_slice, p_cut <= 1e-2 ? 2 : 4)));
   GMAT_CHECK(S >= 0 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
@@ -1774,17 +2202,18 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
   // read it has completed (event wait).
   const int64_t max_tiles = (ROWS_PER_LAUNCH / BI) * cdiv(m, BJ);
-  DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2], tside;
+  auto &drows = e->sb.drows, &dtiles = e->sb.dtiles, &bl = e->sb.bl, &ba = e->sb.ba, &e13 = e->sb.e13, &e2 = e->sb.e2,
+       &pfc = e->sb.pfc, &flags = e->sb.flags, &mxt = e->sb.mxt, &mxr = e->sb.mxr;
   bool side_full[2] = {false, false};  // band arrays hold E1 / Ed / E2 too (int8 screens need them)
   const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
   const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
+  const bool use_lr = use_pf && e->lr_R > 0 && n_slice != -1;  // level 0 = low-rank screen
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
     GMAT_TRY(bl[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(ba[b].alloc((size_t)2 * ROWS_PER_LAUNCH * n_pad));
     GMAT_TRY(mxt[b].alloc((size_t)max_mx * MX_TE * sizeof(int)));
-    if (b == 0) GMAT_TRY(tside.alloc((size_t)max_mx * 3 * SIDE_T * MX_TS * sizeof(int)));
     GMAT_TRY(mxr[b].alloc((size_t)max_mx * MX_BI * sizeof(int)));
     if (use_pf) {
       GMAT_TRY(pfc[b].alloc((size_t)4 * ROWS_PER_LAUNCH * m * sizeof(int)));
@@ -1838,25 +2267,43 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   int64_t pending = 0;  // candidates waiting in the device buffer
   GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
   // exact refine of candidates [0, count) and collection of the hits
+  // The exact refine runs on its own stream (s3) when the candidate buffer is flushed.  (Refining
+  // launch by launch beside the screens was measured 2.7x slower overall: refine waves occupy
+  // CUs that a screen workgroup, which needs a whole CU, then waits for.)  Candidates [0, issued)
+  // of the device buffer have their refine enqueued.
+  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  const hipStream_t S3 = e->s3;
+  int64_t issued = 0;
+  auto enqueue_refine = [&](int64_t upto) -> int {
+    if (upto <= issued) return GMAT_OK;
+    if (issued == 0) GMAT_HIP(hipEventRecord(ev[3], S3));
+    GMAT_TRY(refine(e, S3, L, R, lp, rp, e->cand_i.as<int64_t>() + issued, e->cand_j.as<int64_t>() + issued,
+                    upto - issued, e->ceff.as<double>() + issued, e->cvar.as<double>() + issued,
+                    e->cchi.as<double>() + issued, e->cp.as<double>() + issued));
+    GMAT_HIP(hipEventRecord(ev[4], S3));
+    issued = upto;
+    return GMAT_OK;
+  };
+  Pinned pin_res;
+  // refine what is left of [0, count), collect the hits; the buffer is free afterwards
   auto flush = [&](int64_t count) -> int {
     if (count <= 0) return GMAT_OK;
-    GMAT_HIP(hipEventRecord(ev[3], sm));
-    GMAT_TRY(refine(e, sm, L, R, lp, rp, e->cand_i.as<int64_t>(), e->cand_j.as<int64_t>(), count, e->ceff.as<double>(),
-                    e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>()));
-    GMAT_HIP(hipEventRecord(ev[4], sm));
-    std::vector<int64_t> ci(count), cj(count);
-    std::vector<double> ce(count), cv(count), cc(count), cp(count);
-    GMAT_HIP(hipMemcpyAsync(ci.data(), e->cand_i.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(cj.data(), e->cand_j.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(ce.data(), e->ceff.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(cv.data(), e->cvar.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(cc.data(), e->cchi.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(cp.data(), e->cp.p, count * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipStreamSynchronize(sm));
+    GMAT_TRY(enqueue_refine(count));
+    GMAT_TRY(pin_res.reserve((size_t)count * 48));
+    int64_t *ci = pin_res.as<int64_t>(), *cj = ci + count;
+    double *ce = (double *)(cj + count), *cv = ce + count, *cc = cv + count, *cp = cc + count;
+    GMAT_HIP(hipMemcpyAsync(ci, e->cand_i.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cj, e->cand_j.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cp, e->cp.p, count * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipStreamSynchronize(S3));
     float ms34;
     GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
-    t_ref += ms34 * 1e-3;
+    t_ref += ms34 * 1e-3;  // span of the refine stream's work (it shares the GPU with the screens)
     ncand_total += (double)count;
+    issued = 0;
     for (int64_t k = 0; k < count; ++k) {
       if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
         e->hit_i.push_back(ci[k]);
@@ -1885,18 +2332,23 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     Launch ln;
     ln.rows = rws;
     ln.j_lo = j_lo;
+    for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
+    plan.push_back(std::move(ln));
+  }
+
+  // the int8 screen's (row offset, J) tile list of a launch, built when a level >= 1 needs it
+  auto ensure_tiles = [&](size_t li) {
+    Launch &ln = plan[li];
+    if (!ln.tiles.empty()) return;
+    const int Rn = (int)ln.rows.size();
     for (int r0 = 0; r0 < Rn; r0 += BI) {
-      const int64_t imin = rws[r0];
-      const int64_t jb0 = tri ? (imin + 1) / BJ : 0;
+      const int64_t jb0 = tri ? (ln.rows[r0] + 1) / BJ : 0;
       for (int64_t J = jb0; J * BJ < m; ++J) {
         ln.tiles.push_back(r0);
         ln.tiles.push_back((int)J);
       }
     }
-    for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
-    plan.push_back(std::move(ln));
-  }
-
+  };
   // kernel arguments of launch li on buffer set b
   auto make_args = [&](size_t li, int b) -> ScreenArgs {
     ScreenArgs sa;
@@ -1929,7 +2381,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.csq_l = L.csq.as<double>();
     sa.csq_r = R.csq.as<double>();
     sa.tile_rows = mxr[b].as<int>();
-    sa.tile_side = tside.as<int>();
+    sa.tile_side = nullptr;
+    sa.pf_store = use_lr && S == 0;
     sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
     sa.pfc_stride = (int64_t)Rn * m;
     sa.pf_mu = e->pf_mu;
@@ -1974,12 +2427,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     std::memcpy(pin_rows[b].p, ln.rows.data(), ln.rows.size() * 8);
     return GMAT_OK;
   };
+  const bool side_serial = getenv("GMAT_SIDE_SERIAL") != nullptr;
   auto enqueue_side = [&](size_t li, int b, bool full) -> int {
     side_full[b] = full;
     if (!full && use_pf) {  // fused passes: prefilter flags + E3, then E1 / Ed / E2 for flagged blocks
       const Launch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
       GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+      if (side_serial) GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b ^ 1], 0));  // A/B: no overlap with the screen
       GMAT_TRY(stage_rows(ln, b));
       GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
       GMAT_HIP(hipEventRecord(side_beg[b], S2));
@@ -1998,6 +2453,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.cs[1] = srq;
       hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
       GMAT_HIP(hipGetLastError());
+      if (x.a.pf_store) {  // the low-rank screen needs nothing else
+        GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
+        GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, flags[b].p, (size_t)Rn * nJ, hipMemcpyDeviceToHost, S2));
+        GMAT_HIP(hipEventRecord(side_end[b], S2));
+        return GMAT_OK;
+      }
       for (int t = 0; t < SIDE_T; ++t) x.rs[t] = L.Lq.as<int8_t>() + t * ss;  // E1
       x.cs[0] = srp;
       hipLaunchKernelGGL(side_gemm_kernel<2>, dim3(grid), dim3(256), 0, S2, x);
@@ -2013,6 +2474,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipEventRecord(side_end[b], S2));
       return GMAT_OK;
     }
+    ensure_tiles(li);
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
@@ -2143,11 +2605,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
   if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0, S != 0));
+  const bool stamps_on = getenv("GMAT_LR_STAMPS") != nullptr;
+  DBuf dstamp;
+  if (stamps_on) GMAT_TRY(dstamp.alloc((size_t)max_mx * 8 * 6 * 8));
   for (size_t li = 0; li < plan.size(); ++li) {
     const Launch &ln = plan[li];
     const int b = (int)(li & 1);
     const int Rn = (int)ln.rows.size();
-    const int64_t ntiles = (int64_t)ln.tiles.size() / 2;
+    int64_t ntiles = 0;  // int8 screen workgroups (tile lists are built lazily)
     ScreenArgs sa = make_args(li, b);
     unsigned long long count = 0;
     MxArgs mx;
@@ -2157,6 +2622,24 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
     mx.nib_bytes = m * n_pad;
     mx.nK = e->nK;
+    LrArgs lx;
+    lx.tiles = e->lr_tiles.as<uint8_t>();
+    lx.nib_i = L.nibI.as<uint8_t>();
+    lx.nib_j = R.nibJ.as<uint8_t>();
+    lx.tiles_bytes = (int64_t)e->lr_tiles.bytes;
+    lx.nib_bytes = m * n_pad;
+    lx.nK = e->nK;
+    lx.nC = e->lr_R / MXK;
+    lx.R = e->lr_R;
+    lx.G = L.lrG.as<float>();
+    lx.H = R.lrG.as<float>();
+    lx.q1 = e->lr_q1.as<float>();
+    lx.d = e->lr_d.as<float>();
+    lx.eta = e->lr_eta.as<float>();
+    lx.lam = e->lr_lam;
+    lx.tau = e->lr_tau;
+    lx.eps = e->lr_eps;
+    lx.stamp = (stamps_on && li == 5) ? dstamp.as<unsigned long long>() : nullptr;
     if (S == 0 && built_for[b] != li) GMAT_TRY(build_mx(li, b));
     const std::vector<int> &mx_tiles = mxT[b];
     const int64_t n_mx = nMX[b];
@@ -2172,7 +2655,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         GMAT_TRY(enqueue_side(li, b, true));
         GMAT_HIP(hipStreamSynchronize(S2));
       }
-      if (S == 0 && !mx_tiles.empty()) {
+      ntiles = (int64_t)plan[li].tiles.size() / 2;
+      if (S == 0 && use_lr && !mx_tiles.empty()) {
+        const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
+        hipLaunchKernelGGL(lr_screen_kernel, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, lx);
+      } else if (S == 0 && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
         hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, mx);
       }
@@ -2208,6 +2695,31 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
     pending = (int64_t)count;
+    if (stamps_on && li == 5 && S == 0 && use_lr) {  // per-workgroup phase durations (diagnostics)
+      const size_t g = mx_tiles.size() / MX_TE;
+      std::vector<unsigned long long> hs(6 * g);
+      GMAT_HIP(hipMemcpy(hs.data(), dstamp.p, hs.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<double> ph[5];
+      unsigned long long t_min = ~0ull, t_max = 0;
+      for (size_t q = 0; q < g; ++q) {
+        if (mx_tiles[MX_TE * q] < 0) continue;
+        const unsigned long long *st = &hs[6 * q];
+        ph[0].push_back((double)(st[1] - st[0]) * 10.0);  // 100 MHz -> ns
+        ph[3].push_back((double)(st[4] - st[1]) * 10.0);
+        ph[4].push_back((double)(st[5] - st[4]) * 10.0);
+        t_min = std::min(t_min, st[0]);
+        t_max = std::max(t_max, st[5]);
+      }
+      const char *nm[5] = {"prologue", "-", "-", "chunks", "tests"};
+      for (int k = 0; k < 5; ++k) {
+        std::sort(ph[k].begin(), ph[k].end());
+        if (!ph[k].empty())
+          fprintf(stderr, "lr stamps %-16s median %8.0f ns  p10 %8.0f  p90 %8.0f\n", nm[k], ph[k][ph[k].size() / 2],
+                  ph[k][ph[k].size() / 10], ph[k][ph[k].size() * 9 / 10]);
+      }
+      fprintf(stderr, "lr stamps: %zu workgroups, first start -> last end %.0f us, %d chunks x %d stages\n", ph[0].size(),
+              (double)(t_max - t_min) * 0.01, (int)lx.nC, (int)lx.nK);
+    }
     float ms_side, ms_screen;
     GMAT_HIP(hipEventSynchronize(side_end[b]));
     GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
@@ -2216,7 +2728,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     t_screen += ms_screen * 1e-3;
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
     // pair = n_pad (n_pad + MT) / 2, x (BI x BJ) pairs x 2
-    if (S == 0)
+    if (S == 0 && use_lr)
+      ops += (double)n_mx * 2.0 * (double)e->lr_R * (double)n_pad * MX_BI * BJ;  // incl. empty slots
+    else if (S == 0)
       ops += (double)n_mx * (double)n_pad * (double)(n_pad + MXK) * MX_BI * BJ;  // incl. empty slots
     else
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
@@ -2254,8 +2768,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[5] = t_side;
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
-  e->stats[8] = S_max_used;
-  e->stats[9] = S_max_used == 0 ? e->rho_mx : e->rho[S_max_used];
+  const bool lr_only = use_lr && S_max_used == 0;
+  e->stats[8] = lr_only ? -1 : S_max_used;
+  e->stats[9] = lr_only ? e->lr_lam : (S_max_used == 0 ? e->rho_mx : e->rho[S_max_used]);
   return GMAT_OK;
 }
 

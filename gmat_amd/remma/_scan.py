@@ -66,6 +66,12 @@ class EpiPlan:
                 "n_slice", "bound_coef")
         return dict(zip(keys, s.tolist()))
 
+    def lowrank_rank(self):
+        """Rank of the plan's low-rank spectral screen (0: scans use the fp6 quadratic form)."""
+        s = np.zeros(4)
+        N.check(self._lib.gmat_epi_info(self._h, N.ptr(s)), "gmat_epi_info")
+        return int(s[0])
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.gmat_epi_destroy(self._h)

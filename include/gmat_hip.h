@@ -102,8 +102,13 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
                    double *chi, double *p);
 /* counters of the last scan: [0] pairs tested, [1] candidates refined, [2] int8 MFMA ops,
  * [3] screen kernel seconds, [4] refine kernel seconds, [5] side-term kernel seconds,
- * [6] total seconds, [7] screen kernel launches, [8] slices used, [9] bound coefficient */
+ * [6] total seconds, [7] screen kernel launches, [8] screen level (-1 low-rank, 0 MX, k int8 slices),
+ * [9] bound coefficient */
 int gmat_epi_stats(const gmat_epi *e, double *out10);
+/* screen certificates of the plan: [0] rank of the low-rank spectral screen (padded to 128; 0 =
+ * none, scans use the fp6 quadratic form), [1] its lam, [2] the prefilter's mu, [3] n_pad.  In
+ * gmat_epi_stats, [8] = -1 marks a scan screened by the low-rank bound. */
+int gmat_epi_info(const gmat_epi *e, double *out4);
 int gmat_epi_destroy(gmat_epi *e);
 
 /* Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-166) at var_com, as

@@ -227,7 +227,8 @@ def test_scan_vs_oracle_rows(synth_cohort):
     with Geno(prefix) as g, EpiPlan(g, pvp, py[:, 0]) as plan:
         for kind, p_cut, ns in (("AA", 5e-2, 0), ("DD", 5e-2, 0), ("AD", 5e-2, 0), ("AA", 0.5, 1), ("DD", 0.3, 1),
                                 ("AD", 0.5, 1), ("AA", 1e-3, 1), ("AA", 0.5, -1), ("DD", 0.3, -1), ("AD", 0.5, -1),
-                                ("AA", 1e-4, -1)):
+                                ("AA", 1e-4, -1), ("AA", 1e-4, -2), ("AA", 0.5, -2), ("DD", 0.3, -2), ("AD", 0.5, -2),
+                                ("DD", 1e-3, -2), ("AD", 1e-3, -2)):
             # forced single-slice screens at large p_cut put most pairs inside the bound's band
             hi, hj, eff, var_, chi, p = plan.scan(kind, rows, p_cut, n_slice=ns)
             exp = O.epi_scan(kind, snp, pvp, py, snp_lst_0=rows, p_cut=p_cut)
@@ -260,11 +261,11 @@ def test_scan_deterministic_and_row_split(synth_cohort):
         again = plan.scan("AA", np.arange(m - 1), 1e-3)
         for a, b in zip(full, again):
             np.testing.assert_array_equal(a, b)
-        # the hit set does not depend on the screen level (-1: fp6 x fp4 MX pass, reported as 0;
-        # 1-3: int8 slices)
-        for ns in (-1, 1, 2, 3):
+        # the hit set does not depend on the screen level (-2: low-rank spectral screen, reported
+        # as -1; -1: fp6 x fp4 MX quadratic form, reported as 0; 1-3: int8 slices)
+        for ns, level in ((-2, -1), (-1, 0), (1, 1), (2, 2), (3, 3)):
             forced = plan.scan("AA", np.arange(m - 1), 1e-3, n_slice=ns)
-            assert plan.stats()["n_slice"] == max(ns, 0)
+            assert plan.stats()["n_slice"] == level, (ns, plan.stats())
             for a, b in zip(full, forced):
                 np.testing.assert_array_equal(a, b)
         parts = [plan.scan("AA", np.array(sorted(parallel_rows(m, [4, k], "AA"))), 1e-3) for k in (1, 2, 3, 4)]
@@ -311,7 +312,7 @@ def test_scan_large_n(tmp_path):
     pvp, py = O.projection(y, x, col, nid, [ka, ka * ka], [0.4, 0.2, 0.4])
     rows = np.array([0, 3, 150, 398])
     with Geno(prefix) as g, EpiPlan(g, pvp, py[:, 0]) as plan:
-        for kind, ns in (("AA", 0), ("DD", 0), ("AD", 0), ("AA", -1), ("AD", -1)):
+        for kind, ns in (("AA", 0), ("DD", 0), ("AD", 0), ("AA", -1), ("AD", -1), ("AA", -2), ("DD", -2), ("AD", -2)):
             hi, hj, eff, var_, chi, p = plan.scan(kind, rows, 0.2, n_slice=ns)
             exp = O.epi_scan(kind, snp, pvp, py, snp_lst_0=rows, p_cut=0.2)
             assert hi.size == exp.shape[0] and hi.size > 20, (kind, hi.size, exp.shape)
