@@ -809,9 +809,8 @@ struct LrArgs {
   const uint8_t *nib_i, *nib_j;
   int64_t tiles_bytes, nib_bytes;
   int nK, nC, R;           // stages, 128-row chunks, padded rank
-  const float *G, *H;      // [m][R] left / right coding projections B'a
-  const float *q1, *d, *eta;
-  double lam, tau, eps;
+  const float *G, *H;      // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
+  double lam, tau, eps, E;  // E = sum_r eta_r^2
   unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0, 1, 4, 5 per workgroup
 };
 
@@ -838,7 +837,9 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
     mag += fabs(t_ee[q]);
   }
   const double se = sab - be * ca - al * cb + n * al * be;
-  const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - lowrank * (1.0 + 1e-4) -
+  // |Q'e|^2 <= (|c~| + |eta|)^2; fp32 sums of squares: relative error < 1e-4
+  const double qb = sqrt(lowrank * (1.0 + 1e-4)) + sqrt(x.E);
+  const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - qb * qb -
                      1e-12 * (x.lam + x.tau) * (mag + se * se / n);
   if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) {
     const unsigned long long k = atomicAdd(a.counter, 1ULL);
@@ -858,7 +859,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   __shared__ __attribute__((aligned(16))) uint8_t sA[2][MX_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_REC];
   __shared__ __attribute__((aligned(16))) uint8_t sJ[2][2 * BJ * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t sE[42 * 1024];  // chunk epilogue operands (LDS-DMA)
+  __shared__ __attribute__((aligned(16))) uint8_t sE[40 * 1024];  // chunk epilogue operands (LDS-DMA)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int tl = a.tiles[MX_TE * blockIdx.x];
   if (tl < 0) return;
@@ -938,16 +939,16 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
   };
   // Chunk epilogue operands staged in LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
-  // instruction q, written linearly at sE + q KB): q 0..7 = G rows of the 16 slots (512 B each),
+  // instruction q, written linearly at sE + q KB): q 0..7 = G' rows of the 16 slots (512 B each),
   // q 8..39 = H rows of the 64 columns (physical 16-byte chunk p of column row holds logical chunk
-  // p ^ (row & 15): conflict-free reads), q 40..41 = q1 | d | eta of the chunk.  Wave w issues q = w,
-  // 8+w, .., 32+w (and 40+w for w < 2); the per-lane source offsets are fixed per tile.
+  // p ^ (row & 15): conflict-free reads).  Wave w issues q = w, 8+w, .., 32+w; the per-lane source
+  // offsets are fixed per tile.
   const int64_t jcol = max((int64_t)0, min(J0 + c, a.m - 1));  // J0 < 0 for an unused tile half
   const float be = (float)a.beta[jcol];
   float al[PB];
 #pragma unroll
   for (int t = 0; t < PB; ++t) al[t] = (float)a.alpha[ti[t] < 0 ? 0 : ti[t]];
-  int offG, offH[4], offC;
+  int offG, offH[4];
   {
     const int sl = 2 * w + (lane >> 5), r = trow[sl];
     offG = (int)((r >= 0 ? a.rows[r] : 0) * x.R) + 4 * (lane & 31);
@@ -958,7 +959,6 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       const int64_t jj = Jh < 0 ? 0 : min((int64_t)Jh * BJ + (row & 31), a.m - 1);
       offH[u] = (int)(jj * x.R) + 4 * ((lane & 31) ^ (row & 15));
     }
-    offC = (w * 256 + 4 * lane) & 511;  // float index in q1 | d | eta | (pad: re-reads q1)
   }
   auto fetch_epi = [&](int ch) __attribute__((always_inline)) {
     typedef __attribute__((address_space(3))) void *lds_t;
@@ -966,20 +966,18 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       __builtin_amdgcn_global_load_lds(x.H + offH[u] + ch * MXK, (lds_t)&sE[(8 + w + 8 * u) * 1024], 16, 0, 0);
-    if (w < 2) {
-      const float *src = offC < 128 ? x.q1 + offC : offC < 256 ? x.d + offC - 128 : offC < 384 ? x.eta + offC - 256 : x.q1;
-      __builtin_amdgcn_global_load_lds(src + ch * MXK, (lds_t)&sE[(40 + w) * 1024], 16, 0, 0);
-    }
   };
+  // sum of c~_r^2 over the chunk's rows: c~ = acc - beta G' - alpha H, two rows per v_pk_fma_f32
   double lowrank[PB];
 #pragma unroll
   for (int t = 0; t < PB; ++t) lowrank[t] = 0.0;
   const int hrow = half * BJ + c;
   auto epilogue = [&]() __attribute__((always_inline)) {
+    const v2f_ nbe = {-be, -be};
 #pragma unroll
     for (int t = 0; t < PB; ++t) {
-      const float ab = al[t] * be;
-      float s = 0.f;
+      const v2f_ nal = {-al[t], -al[t]};
+      v2f_ s2 = {0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
 #pragma unroll
@@ -987,20 +985,18 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
           const int k = 8 * r + 2 * q + h;  // logical 16-byte chunk of the chunk's 128 rows
           const float4 g = *(const float4 *)&sE[(PB * w + t) * 512 + 16 * k];
           const float4 hh = *(const float4 *)&sE[8192 + hrow * 512 + 16 * (k ^ (hrow & 15))];
-          const float4 qq = *(const float4 *)&sE[40960 + 16 * k], dd = *(const float4 *)&sE[40960 + 512 + 16 * k],
-                       et = *(const float4 *)&sE[40960 + 1024 + 16 * k];
-          const float gv[4] = {g.x, g.y, g.z, g.w}, hv[4] = {hh.x, hh.y, hh.z, hh.w}, qv[4] = {qq.x, qq.y, qq.z, qq.w},
-                      dv[4] = {dd.x, dd.y, dd.z, dd.w}, ev[4] = {et.x, et.y, et.z, et.w};
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float cr = acc[r][t][4 * q + u] - be * gv[u] - al[t] * hv[u] + ab * qv[u];
-            const float y = fabsf(cr) + ev[u];
-            s = fmaf(dv[u] * y, y, s);
+          for (int u = 0; u < 4; u += 2) {
+            const v2f_ av = {acc[r][t][4 * q + u], acc[r][t][4 * q + u + 1]};
+            const v2f_ gv = {u ? g.z : g.x, u ? g.w : g.y}, hv = {u ? hh.z : hh.x, u ? hh.w : hh.y};
+            v2f_ cr = __builtin_elementwise_fma(nbe, gv, av);
+            cr = __builtin_elementwise_fma(nal, hv, cr);
+            s2 = __builtin_elementwise_fma(cr, cr, s2);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      lowrank[t] += (double)s;
+      lowrank[t] += (double)s2[0] + (double)s2[1];
     }
   };
   auto iter = [&](int b, bool first, int nch, int ncs) __attribute__((always_inline)) {
@@ -1047,11 +1043,77 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 }
 
 
+// ------------------------------------------------------------------ stage-2 side terms
+// E1 / Ed / E2 slice products (E1_t = L'q_t[i].b_j, Ed_t = Ldq_t[i].b_j^2, E2_t = a_i.R'q_t[j]) of the
+// stage-2 MX tiles' slots only, written into the launch's band arrays where cand_test reads them.
+// Nine int8 dot products over n_pad per (slot, column) on v_dot4_i32_i8 (the slots are a few per
+// cent of the flagged blocks; E3 and the code products are already there from the prefilter pass).
+struct SlotSideArgs {
+  const int8_t *Lq, *Ldq, *a, *b, *b2, *Rq;  // slices at stride ss
+  int64_t ss;
+};
+// Eight lanes per (slot, column) pair, each over an eighth of the individuals (a short dependent
+// load chain), reduced with shuffles; a workgroup covers 2 slots x 32 columns, 8 per tile.
+__global__ __launch_bounds__(512) void slot_side_kernel(ScreenArgs a, SlotSideArgs x) {
+  const int tile = blockIdx.x >> 3;
+  const int tl = a.tiles[MX_TE * tile];
+  if (tl < 0) return;
+  const int part = threadIdx.x & 7, pr = threadIdx.x >> 3;  // K part, pair of this workgroup
+  const int s = 2 * (blockIdx.x & 7) + (pr >> 5), c = pr & 31;
+  const int J = a.tiles[MX_TE * tile + 1 + s / (MX_BI / 2)];
+  const int r = a.tile_rows[(int64_t)tl * MX_BI + s];
+  const int64_t i = a.rows[r < 0 ? 0 : r], j = min((int64_t)(J < 0 ? 0 : J) * BJ + c, a.m - 1);
+  const int64_t n4 = a.n_pad / 16, q0 = part * (n4 / 8), q1 = part == 7 ? n4 : q0 + n4 / 8;
+  const v4i *li[SIDE_T], *ld[SIDE_T], *rq[SIDE_T];
+#pragma unroll
+  for (int t = 0; t < SIDE_T; ++t) {
+    li[t] = (const v4i *)(x.Lq + t * x.ss + i * a.n_pad);
+    ld[t] = (const v4i *)(x.Ldq + t * x.ss + i * a.n_pad);
+    rq[t] = (const v4i *)(x.Rq + t * x.ss + j * a.n_pad);
+  }
+  const v4i *pa = (const v4i *)(x.a + i * a.n_pad), *pb = (const v4i *)(x.b + j * a.n_pad),
+            *pb2 = (const v4i *)(x.b2 + j * a.n_pad);
+  int e1[SIDE_T] = {0, 0, 0}, ed[SIDE_T] = {0, 0, 0}, e2[SIDE_T] = {0, 0, 0};
+#pragma unroll 2
+  for (int64_t q = q0; q < q1; ++q) {
+    const v4i va = pa[q], vb = pb[q], vb2 = pb2[q];
+#pragma unroll
+    for (int t = 0; t < SIDE_T; ++t) {
+      const v4i l = li[t][q], d = ld[t][q], rr = rq[t][q];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        e1[t] = __builtin_amdgcn_sdot4(l[u], vb[u], e1[t], false);
+        ed[t] = __builtin_amdgcn_sdot4(d[u], vb2[u], ed[t], false);
+        e2[t] = __builtin_amdgcn_sdot4(va[u], rr[u], e2[t], false);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 8; off <<= 1)
+#pragma unroll
+    for (int t = 0; t < SIDE_T; ++t) {
+      e1[t] += __shfl_xor(e1[t], off);
+      ed[t] += __shfl_xor(ed[t], off);
+      e2[t] += __shfl_xor(e2[t], off);
+    }
+  const int64_t jj = (int64_t)J * BJ + c;
+  if (part != 0 || r < 0 || J < 0 || jj >= a.m || jj < a.j_lo) return;
+  const int64_t o1 = (int64_t)r * a.ld_e + (jj - a.j_lo), od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+  for (int t = 0; t < SIDE_T; ++t) {
+    ((int *)a.c13)[t * a.c13_stride + o1] = e1[t];
+    ((int *)a.c13)[t * a.c13_stride + od] = ed[t];
+    ((int *)a.c2)[t * a.c2_stride + o1] = e2[t];
+  }
+}
+
 // ------------------------------------------------------------------ exact fp64 refine
 // For pairs (pi[t], pj[t]): e = (a - alpha)(b - beta) in fp64 (storage order), var = e'Pe,
 // eff = e'Py.  64 pairs per workgroup; for every 64-row block of P the f64 MFMA tile
-// C = P[rows, :] E is formed over the full inner dimension and folded into var.
-constexpr int QT = 64, QK = 16;
+// C = P[rows, k >= rows] E (off-diagonal blocks x2, exact) is formed in 64-deep stages (the next
+// stage's P rows and code bytes fetched into registers while this one multiplies) and folded
+// into var.
+constexpr int QT = 64, QK = 64;
 
 __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double al, double be, int64_t q) {
   const double x = (double)l[q] - al;
@@ -1059,6 +1121,7 @@ __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double
   return x * y;
 }
 
+typedef double v2d_ __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
                                                      const double *__restrict__ py, const int8_t *left,
                                                      const int8_t *right, const double *alpha, const double *beta,
@@ -1069,16 +1132,28 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
   __shared__ double red[4][QT];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int64_t p0 = (int64_t)blockIdx.x * QT;
-  // the column this thread generates E for during staging: col = tid & 63
-  const int gcol = tid & 63;
+  // staging roles: A row ar = tid / 4, 16 doubles from column ak; E column gcol, 16 k from gk
+  const int ar = tid >> 2, ak = (tid & 3) * 16;
+  const int gcol = tid & 63, gk = (tid >> 6) * 16;
   const int64_t gp = p0 + gcol;
   const bool gval = gp < np;
   const int8_t *gl = gval ? left + pi[gp] * n_pad : left;
   const int8_t *gr = gval ? right + pj[gp] * n_pad : right;
   const double gal = gval ? alpha[pi[gp]] : 0.0, gbe = gval ? beta[pj[gp]] : 0.0;
-  double vpart[2][2] = {{0, 0}, {0, 0}};  // per (j-subtile, lane) partial of var
+  double vpart[2] = {0, 0};  // per j-subtile partial of var
   double effp = 0.0;
-  for (int64_t rb = 0; rb < n_pad; rb += QT) {
+  v2d_ ra[8];
+  v4i rl, rr;
+  auto fetch = [&](int64_t rb, int64_t k0) __attribute__((always_inline)) {
+    const v2d_ *src = (const v2d_ *)(P + (rb + ar) * n_pad + k0 + ak);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ra[q] = src[q];
+    rl = *(const v4i *)(gl + k0 + gk);
+    rr = *(const v4i *)(gr + k0 + gk);
+  };
+  int64_t rb = 0, k0 = 0;
+  fetch(0, 0);
+  while (rb < n_pad) {
     v4d acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1086,26 +1161,32 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
       for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
     // symmetric P: only column blocks k0 >= rb, the off-diagonal ones counted twice (x2 is
     // exact); the rb == 0 pass covers every k and also accumulates the eff partials
-    for (int64_t k0 = rb; k0 < n_pad; k0 += QK) {
-      // A: P[rb + r][k0 + k] (x2 beyond the diagonal block), contiguous along k
-      {
-        const int k = tid & 15, r = tid >> 4;
-        const double f = k0 >= rb + QT ? 2.0 : 1.0;
+    for (; k0 < n_pad; k0 += QK) {
+      const double f = k0 >= rb + QT ? 2.0 : 1.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) As[k][r + 16 * q] = f * P[(rb + r + 16 * q) * n_pad + k0 + k];
+      for (int q = 0; q < 8; ++q) {
+        As[ak + 2 * q][ar] = f * ra[q][0];
+        As[ak + 2 * q + 1][ar] = f * ra[q][1];
       }
-      // B: E[k0 + k][col]
       {
-        const int kq = tid >> 6;
+        const int8_t *lb = (const int8_t *)&rl, *rbb = (const int8_t *)&rr;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = kq + 4 * q;
-          const double e = gval ? ecode(gl, gr, gal, gbe, k0 + k) : 0.0;
-          Bs[k][gcol] = e;
-          if (rb == 0) effp += e * py[k0 + k];
+        for (int q = 0; q < 16; ++q) {
+          const double e = gval ? ((double)lb[q] - gal) * ((double)rbb[q] - gbe) : 0.0;
+          Bs[gk + q][gcol] = e;
+          if (rb == 0) effp += e * py[k0 + gk + q];
         }
       }
       __syncthreads();
+      // next stage (this row block's next columns, or the next row block's first)
+      {
+        int64_t nrb = rb, nk = k0 + QK;
+        if (nk >= n_pad) {
+          nrb = rb + QT;
+          nk = nrb;
+        }
+        if (nrb < n_pad) fetch(nrb, nk);
+      }
 #pragma unroll
       for (int ks = 0; ks < QK / 4; ++ks) {
         const int kk = ks * 4 + (lane >> 4);
@@ -1131,14 +1212,16 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t row = rb + wm * 32 + it * 16 + (lane >> 4) + 4 * e;
-          vpart[jt][0] += ecode(l, r, al, be, row) * acc[it][jt][e];
+          vpart[jt] += ecode(l, r, al, be, row) * acc[it][jt][e];
         }
     }
+    rb += QT;
+    k0 = rb;
   }
   // reduce var partials: lanes with equal (lane & 15) in a wave, then the two wm waves
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
-    double v = vpart[jt][0];
+    double v = vpart[jt];
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     if (lane < 16) red[wm * 2 + jt][wn * 16 + lane] = v;  // [wm][jt] x [wn*16 + lane]
@@ -1541,6 +1624,11 @@ __global__ void lr_shift_kernel(int64_t n, const double *P, const double *C, dou
   const int64_t r = idx / n, c = idx % n;
   A[idx] = P[idx] + C[idx] + (lam + tau) / (double)n - (r == c ? lam : 0.0);
 }
+// G'[j][r] = G[j][r] - soff[j] q1[r] (fp64, rounded once to fp32)
+__global__ void lr_adjust_kernel(int64_t m, int64_t R, const double *G, const double *soff, const double *q1, float *out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < m * R) out[idx] = (float)(G[idx] - soff[idx / R] * q1[idx % R]);
+}
 __global__ void f64_to_f32_kernel(int64_t count, const double *src, float *dst) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < count) dst[idx] = (float)src[idx];
@@ -1565,7 +1653,8 @@ struct Coding {
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
-  DBuf lrG;                       // low-rank screen: B' x screen codes, fp32 [m][lr_R]
+  DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
+                                  // soff x Q'1 (left side: folds the alpha beta q1 term)
 };
 
 struct gmat_epi {
@@ -1578,11 +1667,12 @@ struct gmat_epi {
   // spectral prefilter: e'Pe >= pf_mu * (|e|^2 - (1'e)^2 / n) - pf_eps * |e|^2 for every e,
   // certified by a Cholesky factorisation of P + pf_mu (11'/n - I); pf_mu = 0: disabled
   double pf_mu = 0, pf_tau = 0, pf_eps = 0;
-  // low-rank screen (lr_screen_kernel): e'Pe >= lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - sum_r d_r
-  // (B_r'e)^2 with B the fp6 bottom eigenvectors; lr_R = padded rank (0: disabled)
+  // low-rank screen (lr_screen_kernel): e'Pe >= lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - |Q'e|^2
+  // with Q = fp6(bottom eigenvectors x sqrt(d)); lr_R = padded rank (0: disabled)
   int lr_R = 0;
   double lr_lam = 0, lr_tau = 0, lr_eps = 0;
-  DBuf lr_tiles, lr_Bs, lr_q1, lr_d, lr_eta;  // B' tile images; B fp64 [n_pad][lr_R] storage order
+  double lr_E = 0;                  // sum_r eta_r^2 (the screen's fp32 error budget)
+  DBuf lr_tiles, lr_Bs, lr_q1;      // Q' tile images; Q fp64 [n_pad][lr_R] storage order; Q'1 (fp64)
   int nK = 0;                       // 128-individual stages
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
@@ -1590,6 +1680,7 @@ struct gmat_epi {
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
+  DBuf cand1_i, cand1_j, counter1;  // low-rank screen's candidates (stage 1; the MX screen re-tests them)
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
@@ -1598,6 +1689,7 @@ struct gmat_epi {
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
   struct ScanBufs {
     DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
+    DBuf mxt2[2], mxr2[2];  // stage-2 MX tiles of a launch
   } sb;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   ~gmat_epi() {
@@ -1704,6 +1796,9 @@ int build_coding(gmat_epi *e, int which) {
                        g64.as<double>(), Rp));
     hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)cdiv(m * Rp, 256)), dim3(256), 0, e->s, m * Rp,
                        g64.as<double>(), cd.lrG.as<float>());
+    GMAT_TRY(cd.lrGa.alloc((size_t)m * Rp * sizeof(float)));
+    hipLaunchKernelGGL(lr_adjust_kernel, dim3((unsigned)cdiv(m * Rp, 256)), dim3(256), 0, e->s, m, Rp, g64.as<double>(),
+                       cd.soff.as<double>(), e->lr_q1.as<double>(), cd.lrGa.as<float>());
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipStreamSynchronize(e->s));
   }
@@ -1778,52 +1873,47 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
   GMAT_HIP(hipMemcpy(lam_r.data(), W.p, ne * sizeof(double), hipMemcpyDeviceToHost));
   GMAT_HIP(hipMemcpy(Zh.data(), A.p, Zh.size() * sizeof(double), hipMemcpyDeviceToHost));
   const double t1 = now();
-  // fp6 B' (rows r, storage columns) -> tile images; dequantised B natural [k][r], storage [q][r]
+  // Q(lam) = fp6(sqrt(d_r(lam)) u_r), d_r = (lam - lam_r)_+ (1 + kappa): the rows of Q' are the
+  // A operand of the screen (tile images) and Q Q' = B D B' enters the certificate exactly.
   const int nK = e->nK, nC = Rp / MXK;
+  const double lam_top = lam_r[ne - 1];
+  const char *tenv = getenv("GMAT_LR_TAU");
+  const double tau = (tenv ? atof(tenv) : 0.5) * lam_top;
   std::vector<uint32_t> img((size_t)nC * nK * MX_TILE / 4, 0u);
-  std::vector<double> Bn((size_t)n * Rp, 0.0), Bs((size_t)n_pad * Rp, 0.0);
-  for (int r = 0; r < Rp; ++r)
-    for (int64_t bI = 0; bI < n_pad / 32; ++bI) {
-      double v[32], dq[32];
-      for (int j = 0; j < 32; ++j) {
-        const int64_t c = bI * 32 + perm_nat(j);
-        v[j] = (r < Re && c < n) ? Zh[(size_t)r * n + c] : 0.0;
-      }
-      uint32_t wds[8];
-      fp6_block(v, wds, dq);
-      fp6_store(img.data(), nK, r, bI, wds);
-      for (int j = 0; j < 32; ++j) {
-        const int64_t c = bI * 32 + perm_nat(j);
-        if (c < n) Bn[(size_t)c * Rp + r] = dq[j];
-        Bs[(size_t)(bI * 32 + j) * Rp + r] = dq[j];
-      }
-    }
-  std::vector<double> l1(Rp, 0.0), q1(Rp, 0.0);
-  for (int64_t k = 0; k < n; ++k)
+  std::vector<double> Bn((size_t)n * Rp, 0.0), Bs((size_t)n_pad * Rp, 0.0);  // natural [k][r], storage [q][r]
+  auto quantise = [&](double lam, bool images) {
+    std::fill(Bn.begin(), Bn.end(), 0.0);
+    std::fill(Bs.begin(), Bs.end(), 0.0);
     for (int r = 0; r < Rp; ++r) {
-      l1[r] += std::fabs(Bn[(size_t)k * Rp + r]);
-      q1[r] += Bn[(size_t)k * Rp + r];
+      const double sd = r < Re ? std::sqrt(std::max(lam - lam_r[r], 0.0) * (1.0 + kap)) : 0.0;
+      for (int64_t bI = 0; bI < n_pad / 32; ++bI) {
+        double v[32], dq[32];
+        for (int j = 0; j < 32; ++j) {
+          const int64_t c = bI * 32 + perm_nat(j);
+          v[j] = (sd > 0.0 && c < n) ? sd * Zh[(size_t)r * n + c] : 0.0;
+        }
+        uint32_t wds[8];
+        fp6_block(v, wds, dq);
+        if (images) fp6_store(img.data(), nK, r, bI, wds);
+        for (int j = 0; j < 32; ++j) {
+          const int64_t c = bI * 32 + perm_nat(j);
+          if (c < n) Bn[(size_t)c * Rp + r] = dq[j];
+          Bs[(size_t)(bI * 32 + j) * Rp + r] = dq[j];
+        }
+      }
     }
-  // certificate
-  DBuf dBn, dBD, C, dinv, ld, cinfo;
+  };
+  DBuf dBn, C, dinv, ld, cinfo;
   GMAT_TRY(dBn.alloc(Bn.size() * sizeof(double)));
-  GMAT_TRY(dBD.alloc(Bn.size() * sizeof(double)));
   GMAT_TRY(C.alloc(n * n * sizeof(double)));
   GMAT_TRY(dinv.alloc(n * 64 * sizeof(double)));
   GMAT_TRY(ld.alloc(sizeof(double)));
   GMAT_TRY(cinfo.alloc(sizeof(int)));
-  GMAT_HIP(hipMemcpy(dBn.p, Bn.data(), Bn.size() * sizeof(double), hipMemcpyHostToDevice));
-  const double lam_top = lam_r[ne - 1];
-  const double tau = 0.5 * lam_top;
-  std::vector<double> d(Rp, 0.0), BD(Bn.size());
-  auto dvec = [&](double lam) {
-    for (int r = 0; r < Rp; ++r) d[r] = r < Re ? std::max(lam - lam_r[r], 0.0) * (1.0 + kap) : 0.0;
-  };
-  auto eps_of = [&](double lam) {  // d must be dvec(lam)
+  auto eps_of = [&](double lam) {  // Bn must be quantise(lam)
     double trC = 0.0, cmax = 0.0;
     for (int64_t k = 0; k < n; ++k) {
       double ck = 0.0;
-      for (int r = 0; r < Rp; ++r) ck += d[r] * Bn[(size_t)k * Rp + r] * Bn[(size_t)k * Rp + r];
+      for (int r = 0; r < Rp; ++r) ck += Bn[(size_t)k * Rp + r] * Bn[(size_t)k * Rp + r];
       trC += ck;
       cmax = std::max(cmax, ck);
     }
@@ -1833,11 +1923,9 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
            (double)n * (Rp + 4) * u * (pmax + 2.0 * lam + 2.0 * (lam + tau) / (double)n + cmax);
   };
   auto ok = [&](double lam) -> int {
-    dvec(lam);
-    for (int64_t k = 0; k < n; ++k)
-      for (int r = 0; r < Rp; ++r) BD[(size_t)k * Rp + r] = Bn[(size_t)k * Rp + r] * d[r];
-    GMAT_HIP(hipMemcpy(dBD.p, BD.data(), BD.size() * sizeof(double), hipMemcpyHostToDevice));
-    GMAT_TRY(dgemm(0, n, n, Rp, 1.0, DView{dBD.as<double>(), Rp, 0}, DView{dBn.as<double>(), Rp, 1}, 0.0,
+    quantise(lam, false);
+    GMAT_HIP(hipMemcpy(dBn.p, Bn.data(), Bn.size() * sizeof(double), hipMemcpyHostToDevice));
+    GMAT_TRY(dgemm(0, n, n, Rp, 1.0, DView{dBn.as<double>(), Rp, 0}, DView{dBn.as<double>(), Rp, 1}, 0.0,
                    C.as<double>(), n));
     hipLaunchKernelGGL(lr_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dP, C.as<double>(), lam,
                        tau, A.as<double>());
@@ -1854,35 +1942,38 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
     if (r < 0) return r;
     (r ? lo : hi) = mid;
   }
-  dvec(lo);
+  quantise(lo, true);  // the certified Q (quantise is deterministic)
   const double eps = eps_of(lo);
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "lr_setup: R %d (padded %d) lam_0 %.4g lam_R %.4g -> lam %.4g tau %.3g eps %.3g (pf_mu %.4g); "
                     "eigen %.2f s, certificate %.2f s\n",
             Re, Rp, lam_r[0], lam_top, lo, tau, eps, e->pf_mu, t1 - t0, now() - t1);
   if (!(lo > 0.0) || lo <= e->pf_mu || lo < 1e3 * eps) return GMAT_OK;  // no better than the prefilter
-  // kernel constants: d rounded up, eta = u32 |B_r|_1 (8 n_pad + 400) (fp32 accumulation over
-  // n_pad products with the MFMA-order margin, fp32 G / H / q1 and the 6-term combination)
-  std::vector<float> fd(Rp), feta(Rp), fq1(Rp);
+  // |c~_r - c_r| <= eta_r = u32 |Q_r|_1 (8 n_pad + 400): fp32 accumulation over n_pad products
+  // (w <= 4, one rounding per product, x2 for the MFMA's internal order), the fp32 G' / H and the
+  // 2-term combination; the kernel bounds sum_r c_r^2 <= (|c~| + |eta|)^2 with E = |eta|^2
+  std::vector<double> q1(Rp, 0.0);
+  double Esum = 0.0;
   const double u32 = std::ldexp(1.0, -24);
   for (int r = 0; r < Rp; ++r) {
-    fd[r] = (float)(d[r] * (1.0 + 1e-6));
-    feta[r] = (float)(u32 * l1[r] * (8.0 * (double)n_pad + 400.0) * 1.01);
-    fq1[r] = (float)q1[r];
+    double l1 = 0.0;
+    for (int64_t k = 0; k < n; ++k) {
+      l1 += std::fabs(Bn[(size_t)k * Rp + r]);
+      q1[r] += Bn[(size_t)k * Rp + r];
+    }
+    const double eta = u32 * l1 * (8.0 * (double)n_pad + 400.0) * 1.01;
+    Esum += eta * eta;
   }
   GMAT_TRY(e->lr_tiles.alloc(img.size() * 4));
   GMAT_TRY(e->lr_Bs.alloc(Bs.size() * sizeof(double)));
-  GMAT_TRY(e->lr_q1.alloc(Rp * sizeof(float)));
-  GMAT_TRY(e->lr_d.alloc(Rp * sizeof(float)));
-  GMAT_TRY(e->lr_eta.alloc(Rp * sizeof(float)));
+  GMAT_TRY(e->lr_q1.alloc(Rp * sizeof(double)));
   GMAT_HIP(hipMemcpy(e->lr_tiles.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(e->lr_Bs.p, Bs.data(), Bs.size() * sizeof(double), hipMemcpyHostToDevice));
-  GMAT_HIP(hipMemcpy(e->lr_q1.p, fq1.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
-  GMAT_HIP(hipMemcpy(e->lr_d.p, fd.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
-  GMAT_HIP(hipMemcpy(e->lr_eta.p, feta.data(), Rp * sizeof(float), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_q1.p, q1.data(), Rp * sizeof(double), hipMemcpyHostToDevice));
   e->lr_lam = lo;
   e->lr_tau = tau;
   e->lr_eps = eps + 1e-15 * lo;
+  e->lr_E = Esum * 1.001;
   e->lr_R = Rp;
   return GMAT_OK;
 }
@@ -2208,6 +2299,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
   const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
   const bool use_lr = use_pf && e->lr_R > 0 && n_slice != -1;  // level 0 = low-rank screen
+  // GMAT_STAGE2=1: re-screen the low-rank candidates with the MX quadratic form before the refine
+  // (7x fewer refined pairs, but the sparse (row, block) slots fill MX tiles poorly: slower end to
+  // end at the bench configuration, kept for study)
+  const bool use_stage2 = use_lr && getenv("GMAT_STAGE2") != nullptr;
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
@@ -2231,6 +2326,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e->cchi.alloc(e->cand_cap * 8));
     GMAT_TRY(e->cp.alloc(e->cand_cap * 8));
     GMAT_TRY(e->counter.alloc(8));
+  }
+  if (e->cand1_i.bytes < (size_t)e->cand_cap * 8) {
+    GMAT_TRY(e->cand1_i.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cand1_j.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->counter1.alloc(8));
   }
   // scan-private streams (the null stream would serialise them): screen + refine on sm,
   // side terms on S2; ordered after the coding setup by a device synchronisation
@@ -2316,6 +2416,16 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
     return GMAT_OK;
   };
+
+  // stage-2 (low-rank level) events per buffer set, on S3
+  hipEvent_t s2beg[2], s2end[2];
+  for (int q = 0; q < 2; ++q) {
+    GMAT_HIP(hipEventCreate(&s2beg[q]));
+    GMAT_HIP(hipEventCreate(&s2end[q]));
+    GMAT_HIP(hipEventRecord(s2beg[q], S3));
+    GMAT_HIP(hipEventRecord(s2end[q], S3));
+  }
+  EvPair s2beg_guard{s2beg}, s2end_guard{s2end};
 
   // per-launch host plan (rows, tile list); empty launches dropped
   struct Launch {
@@ -2434,6 +2544,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const Launch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
       GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+      GMAT_HIP(hipStreamWaitEvent(S2, s2end[b], 0));       // ... and its stage-2 re-screen
       if (side_serial) GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b ^ 1], 0));  // A/B: no overlap with the screen
       GMAT_TRY(stage_rows(ln, b));
       GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
@@ -2478,6 +2589,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
+    GMAT_HIP(hipStreamWaitEvent(S2, s2end[b], 0));
     GMAT_TRY(stage_rows(ln, b));
     GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -2605,6 +2717,121 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
   if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0, S != 0));
+  // Stage 2 of the low-rank level: the low-rank screen's candidates (launch li, in cand1) are
+  // grouped into (band row, 32-column block) slots, packed into MX tiles (half-tiles per block,
+  // dealt to the XCDs like build_mx), their E1 / Ed / E2 computed (slot_side_kernel) and the MX
+  // quadratic form re-screens them into the main candidate buffer.  Returns the stage-2 tiles.
+  Pinned pin_count1, pin_c1, pin_t2[2], pin_r2[2];
+  GMAT_TRY(pin_count1.reserve(8));
+  GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
+  double t_stage2 = 0.0, n_stage1 = 0.0;
+  bool s2_timed[2] = {false, false};
+  int64_t pend_bound = 0;  // upper bound of the main candidate count while stage 2 runs on S3
+  auto s2_retire = [&](int b) -> int {  // stage 2 of buffer set b has completed: account its time
+    GMAT_HIP(hipEventSynchronize(s2end[b]));
+    if (s2_timed[b]) {
+      float ms2;
+      GMAT_HIP(hipEventElapsedTime(&ms2, s2beg[b], s2end[b]));
+      t_stage2 += ms2 * 1e-3;
+      s2_timed[b] = false;
+    }
+    return GMAT_OK;
+  };
+  auto main_count = [&](int64_t *out) -> int {  // drain stage 2 and read the main counter
+    GMAT_HIP(hipStreamSynchronize(sm));
+    GMAT_HIP(hipStreamSynchronize(S3));
+    GMAT_HIP(hipMemcpyAsync(pin_count.p, e->counter.p, 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipStreamSynchronize(S3));
+    *out = (int64_t)*pin_count.as<unsigned long long>();
+    return GMAT_OK;
+  };
+  const hipStream_t S2s = getenv("GMAT_STAGE2_SERIAL") ? sm : S3;  // A/B: stage 2 in line with the screens
+  auto stage2 = [&](size_t li, int b, const ScreenArgs &sa, const MxArgs &mx, int64_t n1) -> int {
+    const Launch &ln = plan[li];
+    GMAT_TRY(pin_c1.reserve((size_t)n1 * 16));
+    int64_t *ci = pin_c1.as<int64_t>(), *cj = ci + n1;
+    GMAT_HIP(hipMemcpyAsync(ci, e->cand1_i.p, n1 * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemcpyAsync(cj, e->cand1_j.p, n1 * 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
+    GMAT_HIP(hipStreamSynchronize(sm));  // cand1 is free for the next low-rank screen
+    std::vector<std::pair<int64_t, int>> rix(ln.rows.size());  // SNP -> band row
+    for (size_t r = 0; r < ln.rows.size(); ++r) rix[r] = {ln.rows[r], (int)r};
+    std::sort(rix.begin(), rix.end());
+    std::vector<std::pair<int, int>> sl(n1);  // (J, band row)
+    for (int64_t k = 0; k < n1; ++k) {
+      const auto it = std::lower_bound(rix.begin(), rix.end(), std::make_pair(ci[k], 0));
+      sl[k] = {(int)(cj[k] / BJ), it->second};
+    }
+    std::sort(sl.begin(), sl.end());
+    sl.erase(std::unique(sl.begin(), sl.end()), sl.end());
+    std::vector<int> lst, rl;
+    int halves = 0;
+    for (size_t q = 0; q < sl.size();) {
+      const int J = sl[q].first;
+      int cnt = 0;
+      for (; q < sl.size() && sl[q].first == J; ++q, ++cnt) {
+        if (cnt % (MX_BI / 2) == 0) {
+          if (halves % 2 == 0) {
+            lst.push_back((int)(rl.size() / MX_BI));
+            lst.push_back(J);
+            lst.push_back(-1);
+            rl.insert(rl.end(), MX_BI, -1);
+          } else {
+            lst.back() = J;
+          }
+          ++halves;
+        }
+        rl[rl.size() - MX_BI + ((halves - 1) % 2) * (MX_BI / 2) + cnt % (MX_BI / 2)] = sl[q].second;
+      }
+    }
+    const int64_t n2 = (int64_t)lst.size() / MX_TE, C = cdiv(n2, 8);
+    std::vector<int> t2((size_t)MX_TE * 8 * C, -1);
+    for (int64_t q = 0; q < n2; ++q) {
+      const int64_t bb = 8 * (q % C) + q / C;
+      for (int k = 0; k < MX_TE; ++k) t2[MX_TE * bb + k] = lst[MX_TE * q + k];
+    }
+    // at most 32 candidates per slot: keep the main buffer from overflowing by construction
+    const int64_t add = 32 * (int64_t)sl.size();
+    if (pend_bound + add > e->cand_cap) {
+      int64_t c = 0;
+      GMAT_TRY(main_count(&c));
+      GMAT_TRY(flush(c));
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, S3));
+      GMAT_HIP(hipStreamSynchronize(S3));
+      pend_bound = 0;
+    }
+    pend_bound += add;
+    GMAT_TRY(s2_retire(b));  // stage 2 two launches back no longer reads this buffer set
+    GMAT_TRY(e->sb.mxt2[b].alloc(t2.size() * sizeof(int)));
+    GMAT_TRY(e->sb.mxr2[b].alloc(rl.size() * sizeof(int)));
+    GMAT_TRY(pin_t2[b].reserve(t2.size() * sizeof(int)));
+    GMAT_TRY(pin_r2[b].reserve(rl.size() * sizeof(int)));
+    std::memcpy(pin_t2[b].p, t2.data(), t2.size() * sizeof(int));
+    std::memcpy(pin_r2[b].p, rl.data(), rl.size() * sizeof(int));
+    GMAT_HIP(hipEventRecord(s2beg[b], S2s));
+    GMAT_HIP(hipMemcpyAsync(e->sb.mxt2[b].p, pin_t2[b].p, t2.size() * sizeof(int), hipMemcpyHostToDevice, S2s));
+    GMAT_HIP(hipMemcpyAsync(e->sb.mxr2[b].p, pin_r2[b].p, rl.size() * sizeof(int), hipMemcpyHostToDevice, S2s));
+    ScreenArgs s2 = sa;
+    s2.tiles = e->sb.mxt2[b].as<int>();
+    s2.tile_rows = e->sb.mxr2[b].as<int>();
+    s2.n_slice = 0;
+    s2.delta = e->rho_mx;
+    SlotSideArgs sx;
+    sx.Lq = L.Lq.as<int8_t>();
+    sx.Ldq = L.Ldq.as<int8_t>();
+    sx.a = slp;
+    sx.b = srp;
+    sx.b2 = srq;
+    sx.Rq = R.Rq.as<int8_t>();
+    sx.ss = m * n_pad;
+    const unsigned g = (unsigned)(t2.size() / MX_TE);
+    hipLaunchKernelGGL(slot_side_kernel, dim3(8 * g), dim3(512), 0, S2s, s2, sx);
+    hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, S2s, s2, mx);
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipEventRecord(s2end[b], S2s));
+    s2_timed[b] = true;
+    return GMAT_OK;
+  };
   const bool stamps_on = getenv("GMAT_LR_STAMPS") != nullptr;
   DBuf dstamp;
   if (stamps_on) GMAT_TRY(dstamp.alloc((size_t)max_mx * 8 * 6 * 8));
@@ -2631,11 +2858,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     lx.nK = e->nK;
     lx.nC = e->lr_R / MXK;
     lx.R = e->lr_R;
-    lx.G = L.lrG.as<float>();
+    lx.G = L.lrGa.as<float>();
     lx.H = R.lrG.as<float>();
-    lx.q1 = e->lr_q1.as<float>();
-    lx.d = e->lr_d.as<float>();
-    lx.eta = e->lr_eta.as<float>();
+    lx.E = e->lr_E;
     lx.lam = e->lr_lam;
     lx.tau = e->lr_tau;
     lx.eps = e->lr_eps;
@@ -2656,9 +2881,16 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         GMAT_HIP(hipStreamSynchronize(S2));
       }
       ntiles = (int64_t)plan[li].tiles.size() / 2;
+      const bool two_stage = S == 0 && use_lr && use_stage2;
       if (S == 0 && use_lr && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
-        hipLaunchKernelGGL(lr_screen_kernel, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, lx);
+        ScreenArgs s1 = sa;  // with stage 2 the low-rank candidates go to cand1
+        if (two_stage) {
+          s1.counter = e->counter1.as<unsigned long long>();
+          s1.cand_i = e->cand1_i.as<int64_t>();
+          s1.cand_j = e->cand1_j.as<int64_t>();
+        }
+        hipLaunchKernelGGL(lr_screen_kernel, dim3(g), dim3(MxShape<1>::T), 0, sm, s1, lx);
       } else if (S == 0 && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
         hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, mx);
@@ -2672,6 +2904,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipEventRecord(ev[2], sm));
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
       GMAT_HIP(hipMemcpyAsync(pin_count.p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+      if (two_stage) GMAT_HIP(hipMemcpyAsync(pin_count1.p, e->counter1.p, 8, hipMemcpyDeviceToHost, sm));
       // next launch's side terms overlap this screen
       if (attempt == 0 && li + 1 < plan.size()) {
         GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
@@ -2680,6 +2913,23 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       GMAT_HIP(hipStreamSynchronize(sm));
       count = *pin_count.as<unsigned long long>();
+      if (two_stage) {
+        // stage 2 (MX re-screen of the low-rank candidates) runs on S3 beside the next launches;
+        // the main counter is read when the buffer is flushed
+        const int64_t n1 = (int64_t)*pin_count1.as<unsigned long long>();
+        if (n1 > e->cand_cap) {  // the low-rank band overflowed: escalate like an MX overflow
+          GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
+          GMAT_TRY(main_count(&pending));
+          pend_bound = 0;
+          count = (unsigned long long)n1;
+        } else {
+          if (n1 > 0) {
+            n_stage1 += (double)n1;
+            GMAT_TRY(stage2(li, b, sa, mx, n1));
+          }
+          count = 0;
+        }
+      }
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
       // overflowed on its own, redo it with one more slice (thinner candidate band)
@@ -2694,7 +2944,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       pending = 0;
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
-    pending = (int64_t)count;
+    const bool async_s2 = S == 0 && use_stage2;  // the main counter belongs to stage 2 on S3
+    if (!async_s2) pending = (int64_t)count;
     if (stamps_on && li == 5 && S == 0 && use_lr) {  // per-workgroup phase durations (diagnostics)
       const size_t g = mx_tiles.size() / MX_TE;
       std::vector<unsigned long long> hs(6 * g);
@@ -2735,13 +2986,17 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     else
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
-    if (pending > e->cand_cap / 2) {
+    if (!async_s2 && pending > e->cand_cap / 2) {
       GMAT_TRY(flush(pending));
       pending = 0;
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
   }
   GMAT_HIP(hipStreamSynchronize(S2));
+  if (use_stage2 && S == 0) {
+    GMAT_TRY(main_count(&pending));
+    for (int q = 0; q < 2; ++q) GMAT_TRY(s2_retire(q));
+  }
   GMAT_TRY(flush(pending));
   // sort hits by (i, j)
   std::vector<int64_t> ord(e->hit_i.size());
@@ -2765,7 +3020,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[2] = ops;
   e->stats[3] = t_screen;
   e->stats[4] = t_ref;
-  e->stats[5] = t_side;
+  e->stats[5] = t_side + t_stage2;  // side terms + the low-rank level's stage-2 MX re-screen
+  if (getenv("GMAT_DEBUG") && use_stage2)
+    fprintf(stderr, "gmat_epi_scan: low-rank screen candidates %.0f -> MX re-screen %.0f (%.3f s)\n", n_stage1,
+            ncand_total, t_stage2);
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
   const bool lr_only = use_lr && S_max_used == 0;

@@ -2,9 +2,9 @@
 
 The device screen bounds var = e'Pe from below by
     lam (|e|^2 - (1'e)^2/n) - tau (1'e)^2/n - eps |e|^2 - sum_r d_r (B_r'e)^2,
-B the fp6-quantised bottom eigenvectors of P, with lam certified by a Cholesky of
-P - lam I + (lam + tau) 11'/n + B D B'.  It never forms e: B_r'e is expanded as
-B_r'(a o b) - beta B_r'a - alpha B_r'b + alpha beta B_r'1.  These tests restate the fp6
+B the bottom eigenvectors of P, D = diag(d), with Q = fp6(B sqrt(D)) (what the MFMA multiplies)
+and lam certified by a Cholesky of P - lam I + (lam + tau) 11'/n + Q Q'.  It never forms e:
+Q_r'e is expanded as Q_r'(a o b) - beta (Q_r'a - alpha Q_r'1) - alpha Q_r'b.  These tests restate the fp6
 quantiser, the certificate and the expansion in numpy and check the bound on code vectors.
 """
 import numpy as np
@@ -38,22 +38,27 @@ def quantise(u):
 
 
 def certify_lowrank(p, rank, kappa=0.7, iters=30):
+    """lr_setup: Q(lam) = fp6(u_r sqrt(d_r(lam))) and a bisected Cholesky of
+    P - lam I + (lam + tau) 11'/n + Q Q'.  Returns lam, tau and the certified Q."""
     n = p.shape[0]
     w, v = np.linalg.eigh(p + 4.0 * np.trace(p) / n * np.ones((n, n)) / n)
-    b = quantise(v[:, :rank])
     lam_r, top = w[:rank], w[rank]
     tau = 0.5 * top
+
+    def q_of(lam):
+        return quantise(v[:, :rank] * np.sqrt(np.maximum(lam - lam_r, 0) * (1 + kappa)))
+
     lo, hi = 0.0, 1.3 * top
     for _ in range(iters):
         mid = 0.5 * (lo + hi)
-        d = np.maximum(mid - lam_r, 0) * (1 + kappa)
-        a = p - mid * np.eye(n) + (mid + tau) / n + (b * d) @ b.T
+        q = q_of(mid)
+        a = p - mid * np.eye(n) + (mid + tau) / n + q @ q.T
         try:
             np.linalg.cholesky(a)
             lo = mid
         except np.linalg.LinAlgError:
             hi = mid
-    return lo, tau, b, np.maximum(lo - lam_r, 0) * (1 + kappa)
+    return lo, tau, q_of(lo)
 
 
 def test_fp6_grid():
@@ -67,7 +72,7 @@ def test_lowrank_bound_holds_and_beats_the_prefilter():
     rng = np.random.default_rng(11)
     n, rank = 160, 64
     p = _projection(n, rng)
-    lam, tau, b, d = certify_lowrank(p, rank)
+    lam, tau, b = certify_lowrank(p, rank)
     w = np.linalg.eigvalsh(p)
     mu0 = w[1]  # the prefilter's ceiling: smallest eigenvalue on 1-perp
     assert lam > 1.2 * mu0 and lam > 0.95 * w[rank + 1]  # close to the first eigenvalue left out
@@ -79,11 +84,11 @@ def test_lowrank_bound_holds_and_beats_the_prefilter():
         bb = rng.integers(0, 3, n).astype(np.float64)
         al, be = a.mean(), bb.mean()
         e = (a - al) * (bb - be)
-        # the kernel's expansion of B'e
-        c = b.T @ (a * bb) - be * (b.T @ a) - al * (b.T @ bb) + al * be * q1
+        # the kernel's expansion of Q'e: G' = Q'a - alpha Q'1 (left), H = Q'b (right)
+        c = b.T @ (a * bb) - be * (b.T @ a - al * q1) - al * (b.T @ bb)
         np.testing.assert_allclose(c, b.T @ e, rtol=1e-9, atol=1e-9)
         ee, se = e @ e, e.sum()
-        lb = lam * (ee - se * se / n) - tau * se * se / n - d @ (c * c)
+        lb = lam * (ee - se * se / n) - tau * se * se / n - c @ c
         var = e @ p @ e
         assert lb <= var * (1 + 1e-9) + 1e-9
         worst = min(worst, var / max(lb, 1e-300))

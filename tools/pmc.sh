@@ -1,8 +1,11 @@
 #!/bin/bash
-# PMC passes (one counter group per rocprofv3 run, kernel-trace only) on a reduced scan.
+# PMC passes (one counter group per rocprofv3 run, kernel-trace only) on the bench scan; raw
+# output stays in /tmp on the box, only the rows of kernels matching $KEY come back.
 TAG=${1:-pmc}
+KEY=${KEY:-screen}
 OUT=gpurun_out/$TAG
-mkdir -p $OUT
+RAW=/tmp/pmc_raw_$TAG
+mkdir -p $OUT $RAW
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 ARGS="bench.py --n-snp ${NSNP:-10000} --steps 1 --warmup 0 --no-cpu --no-grm --no-eff"
 i=0
@@ -10,6 +13,12 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM" \
            "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $RAW/p$i -o run -- python3 $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  mkdir -p $OUT/p$i
+  for f in run_counter_collection.csv run_kernel_trace.csv; do
+    src=$(find $RAW/p$i -name $f | head -1)
+    [ -n "$src" ] && { head -1 $src; grep "$KEY" $src || true; } > $OUT/p$i/$f
+  done
+  rm -rf $RAW/p$i
 done
 echo done
