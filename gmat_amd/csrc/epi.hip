@@ -46,6 +46,7 @@ constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b1
 constexpr int BJ = 32;   // second-SNP columns per screen tile
 constexpr int ROWS_PER_LAUNCH = 512;
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
+constexpr int E3_PF = 2;         // L3 slices of the prefilter pass (eff to ~2^-14: enough to screen)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
 constexpr int SCREEN_SHAPE = 0;  // default tile shape of the screen kernel (Shape<SH> below)
 
@@ -80,6 +81,8 @@ struct ScreenArgs {
   int64_t c13_stride, c2_stride;
   const double *sL, *sL3, *sLd, *sR, *csum_l, *csum_r, *csq_l, *csq_r;
   double side_eps;
+  int e3_t;       // slices of E3 in c13 (E3_PF from the prefilter pass, SIDE_T from the full side path)
+  double e3_eps;  // their slicing bound (as side_eps)
   int64_t ld_e, j_lo;
   const double *alpha, *qa, *ra, *sa;
   const double *beta, *qb, *rb, *sb;
@@ -119,8 +122,9 @@ __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i
   double c1 = 0.0, c3 = 0.0, cd = 0.0, c2 = 0.0;
   const int so = slot * 32 + col;
 #pragma unroll
+  for (int t = a.e3_t - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+#pragma unroll
   for (int t = SIDE_T - 1; t >= 0; --t) {  // exact: |c| < 2^22, powers of two
-    c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
     if (ts) {
       c1 = c1 * (1.0 / 128.0) + (double)ts[(0 * SIDE_T + t) * MX_TS + so];
       cd = cd * (1.0 / 128.0) + (double)ts[(1 * SIDE_T + t) * MX_TS + so];
@@ -132,7 +136,7 @@ __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i
     }
   }
   const double E1 = a.sL[i] * c1, E3 = a.sL3[i] * c3, Ed = a.sLd[i] * cd, E2 = a.sR[j] * c2;
-  const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.side_eps * a.sL3[i] * a.csum_r[j],
+  const double dE1 = a.side_eps * a.sL[i] * a.csum_r[j], dE3 = a.e3_eps * a.sL3[i] * a.csum_r[j],
                dEd = a.side_eps * a.sLd[i] * a.csq_r[j], dE2 = a.side_eps * a.sR[j] * a.csum_l[i];
   const double al = a.alpha[i], be = a.beta[j];
   const double t1 = -2.0 * be * E1, t2 = -2.0 * al * E2, t3 = be * be * a.qa[i], t4 = -2.0 * al * be * be * a.ra[i],
@@ -173,10 +177,10 @@ __global__ __launch_bounds__(256) void prefilter_kernel(ScreenArgs a) {
       const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
       double c3 = 0.0;
 #pragma unroll
-      for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+      for (int t = a.e3_t - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
       const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
       const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-      const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
+      const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
       const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
                    sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
       const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
@@ -220,8 +224,8 @@ template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
   // PASS 1: row sets L3q_0..2, a, a^2 x column sets b, b^2 (7 products); PASS 2: E1 (L'q_t x b),
   // PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three products each
-  constexpr int NR = PASS == 1 ? 5 : PASS == 4 ? 1 : 3, NC = PASS == 1 ? 2 : PASS == 4 ? 3 : 1;
-  constexpr int NPR = PASS == 1 ? 7 : 3;
+  constexpr int NR = PASS == 1 ? E3_PF + 2 : PASS == 4 ? 1 : 3, NC = PASS == 1 ? 2 : PASS == 4 ? 3 : 1;
+  constexpr int NPR = PASS == 1 ? E3_PF + 4 : 3;
   const ScreenArgs &a = x.a;
   static_assert(NR <= 7 && NC <= 5, "operand sets");
   const int rt = blockIdx.x % x.n_rt, ct = blockIdx.x / x.n_rt;
@@ -253,8 +257,9 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
     for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
   };
   // product p: (row set, column set)
-  constexpr int PR[4][7] = {{0, 1, 2, 3, 4, 3, 4}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
-  constexpr int PC[4][7] = {{0, 0, 0, 0, 0, 1, 1}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
+  static_assert(E3_PF == 2, "product table");
+  constexpr int PR[4][6] = {{0, 1, 2, 3, 2, 3}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
+  constexpr int PC[4][6] = {{0, 0, 0, 0, 1, 1}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
   v16i acc[NPR];
 #pragma unroll
   for (int p = 0; p < NPR; ++p)
@@ -300,12 +305,12 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
           const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
           double c3 = 0.0;
 #pragma unroll
-          for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
+          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
           const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
           const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-          const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
-          const double sab = (double)acc[3][e], sa2b = (double)acc[4][e], sab2 = (double)acc[5][e],
-                       sa2b2 = (double)acc[6][e];
+          const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
+          const double sab = (double)acc[E3_PF][e], sa2b = (double)acc[E3_PF + 1][e],
+                       sab2 = (double)acc[E3_PF + 2][e], sa2b2 = (double)acc[E3_PF + 3][e];
           const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
                                   -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
           double ee = 0.0, mag = 0.0;
@@ -327,10 +332,10 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
       if (blk && rok && jok) {
         const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
-        for (int t = 0; t < SIDE_T; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
+        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
         if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = acc[3 + q][e];
+          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = acc[E3_PF + q][e];
       }
     } else {
       if (rok && jok && a.flags[(int64_t)r * a.nJ + J]) {
@@ -821,11 +826,11 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
   const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
   double c3 = 0.0;
 #pragma unroll
-  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
+  for (int t = a.e3_t - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
   const double al = a.alpha[i], be = a.beta[j], ca = a.csum_l[i], ca2 = a.csq_l[i], cb = a.csum_r[j],
                cb2 = a.csq_r[j], n = a.n_id;
   const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-  const double eff_hi = fabs(eff) + a.side_eps * a.sL3[i] * cb;
+  const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
   const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
                sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
   const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
@@ -2296,6 +2301,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   auto &drows = e->sb.drows, &dtiles = e->sb.dtiles, &bl = e->sb.bl, &ba = e->sb.ba, &e13 = e->sb.e13, &e2 = e->sb.e2,
        &pfc = e->sb.pfc, &flags = e->sb.flags, &mxt = e->sb.mxt, &mxr = e->sb.mxr;
   bool side_full[2] = {false, false};  // band arrays hold E1 / Ed / E2 too (int8 screens need them)
+  int e3_slices[2] = {SIDE_T, SIDE_T};  // E3 slices in the band arrays of each buffer set
   const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
   const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
   const bool use_lr = use_pf && e->lr_R > 0 && n_slice != -1;  // level 0 = low-rank screen
@@ -2503,6 +2509,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.nJ = (int)nJ;
     // per element |v - s sum_t 128^-t Q_t| <= s (0.5 * 128^-(T-1) + fp64 rounding)
     sa.side_eps = 0.5 * std::pow(128.0, -(SIDE_T - 1)) + 1e-12;
+    sa.e3_t = e3_slices[b];
+    sa.e3_eps = 0.5 * std::pow(128.0, -(sa.e3_t - 1)) + 1e-12;
     sa.ld_e = m;
     sa.j_lo = ln.j_lo;
     sa.alpha = L.soff.as<double>();
@@ -2540,6 +2548,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const bool side_serial = getenv("GMAT_SIDE_SERIAL") != nullptr;
   auto enqueue_side = [&](size_t li, int b, bool full) -> int {
     side_full[b] = full;
+    e3_slices[b] = (!full && use_pf) ? E3_PF : SIDE_T;
     if (!full && use_pf) {  // fused passes: prefilter flags + E3, then E1 / Ed / E2 for flagged blocks
       const Launch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
@@ -2557,9 +2566,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const int64_t ss = m * n_pad;
       const int64_t ncols = m - (ln.j_lo / 32) * 32;
       const unsigned grid = (unsigned)(x.n_rt * cdiv(ncols, SG_T));
-      for (int t = 0; t < SIDE_T; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
-      x.rs[3] = slp;
-      x.rs[4] = slq;
+      for (int t = 0; t < E3_PF; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
+      x.rs[E3_PF] = slp;
+      x.rs[E3_PF + 1] = slq;
       x.cs[0] = srp;
       x.cs[1] = srq;
       hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
@@ -2879,6 +2888,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         GMAT_HIP(hipStreamSynchronize(S2));
         GMAT_TRY(enqueue_side(li, b, true));
         GMAT_HIP(hipStreamSynchronize(S2));
+        sa.e3_t = e3_slices[b];
+        sa.e3_eps = 0.5 * std::pow(128.0, -(sa.e3_t - 1)) + 1e-12;
       }
       ntiles = (int64_t)plan[li].tiles.size() / 2;
       const bool two_stage = S == 0 && use_lr && use_stage2;
