@@ -897,17 +897,20 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   }
   if (trow[is] >= 0) voffI = (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16);
 
-  v4i ra[NA], rnj, rni;
-  auto load = [&](int ch, int cs) __attribute__((always_inline)) {
-    const int soffA = (ch * nK + cs) * MX_TILE;
+  // the A tile image is a straight copy: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
+  // instruction) into buffer nb, no registers or ds_write; the genotype records go through
+  // registers (the j side is swizzled per lane)
+  v4i rnj, rni;
+  auto load = [&](int nb, int ch, int cs) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) void *lds_t;
+    const uint8_t *src = x.tiles + (int64_t)(ch * nK + cs) * MX_TILE;
 #pragma unroll
-    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * MX_T) * 16, soffA, 0);
+    for (int u = 0; u < NA; ++u)
+      __builtin_amdgcn_global_load_lds(src + (tid + u * MX_T) * 16, (lds_t)&sA[nb][(w * 64 + u * MX_T) * 16], 16, 0, 0);
     rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
     rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
   };
   auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b][(tid + u * MX_T) * 16] = ra[u];
     *(v4i *)&sJ[b][(jh * BJ + js) * NB_REC + jq * 16] = rnj;
     *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
   };
@@ -1005,14 +1008,14 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
   };
   auto iter = [&](int b, bool first, int nch, int ncs) __attribute__((always_inline)) {
-    load(nch, ncs);
+    load(b ^ 1, nch, ncs);
     __builtin_amdgcn_sched_barrier(0);
     compute(b, first);
     store(b ^ 1);
     __syncthreads();
   };
 
-  load(0, 0);
+  load(0, 0, 0);
   store(0);
   __syncthreads();
   stamp(1);
@@ -1114,11 +1117,12 @@ __global__ __launch_bounds__(512) void slot_side_kernel(ScreenArgs a, SlotSideAr
 
 // ------------------------------------------------------------------ exact fp64 refine
 // For pairs (pi[t], pj[t]): e = (a - alpha)(b - beta) in fp64 (storage order), var = e'Pe,
-// eff = e'Py.  64 pairs per workgroup; for every 64-row block of P the f64 MFMA tile
-// C = P[rows, k >= rows] E (off-diagonal blocks x2, exact) is formed in 64-deep stages (the next
-// stage's P rows and code bytes fetched into registers while this one multiplies) and folded
-// into var.
-constexpr int QT = 64, QK = 64;
+// eff = e'Py.  RP pairs per workgroup (P, 32 MB in fp64, is streamed once per workgroup from
+// the MALL/HBM, so more pairs per workgroup = less traffic); for every RM-row block of P the f64
+// MFMA tile C = P[rows, k >= rows] E (off-diagonal blocks x2, exact) is formed in RK-deep stages
+// (the next stage's P rows and code bytes fetched into registers while this one multiplies) and
+// folded into var.  Waves: 2 (rows) x 2 (64-pair halves), each 32 x 64 of 16x16x4 f64 MFMA tiles.
+constexpr int RP = 128, RM = 64, RK = 32;
 
 __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double al, double be, int64_t q) {
   const double x = (double)l[q] - al;
@@ -1127,49 +1131,49 @@ __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double
 }
 
 typedef double v2d_ __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
+__global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
                                                      const double *__restrict__ py, const int8_t *left,
                                                      const int8_t *right, const double *alpha, const double *beta,
                                                      const int64_t *pi, const int64_t *pj, int64_t np, double *eff,
                                                      double *var) {
-  __shared__ double As[QK][QT + 1];
-  __shared__ double Bs[QK][QT + 1];
-  __shared__ double red[4][QT];
+  __shared__ double As[RK][RM + 1];
+  __shared__ double Bs[RK][RP + 1];
+  __shared__ double red[2][RP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
-  const int64_t p0 = (int64_t)blockIdx.x * QT;
-  // staging roles: A row ar = tid / 4, 16 doubles from column ak; E column gcol, 16 k from gk
-  const int ar = tid >> 2, ak = (tid & 3) * 16;
-  const int gcol = tid & 63, gk = (tid >> 6) * 16;
+  const int64_t p0 = (int64_t)blockIdx.x * RP;
+  // staging roles: A row ar = tid / 4, 8 doubles from column ak; E column gcol, 16 k from gk
+  const int ar = tid >> 2, ak = (tid & 3) * 8;
+  const int gcol = tid & (RP - 1), gk = (tid >> 7) * 16;
   const int64_t gp = p0 + gcol;
   const bool gval = gp < np;
   const int8_t *gl = gval ? left + pi[gp] * n_pad : left;
   const int8_t *gr = gval ? right + pj[gp] * n_pad : right;
   const double gal = gval ? alpha[pi[gp]] : 0.0, gbe = gval ? beta[pj[gp]] : 0.0;
-  double vpart[2] = {0, 0};  // per j-subtile partial of var
+  double vpart[4] = {0, 0, 0, 0};  // per 16-pair subtile partial of var
   double effp = 0.0;
-  v2d_ ra[8];
+  v2d_ ra[4];
   v4i rl, rr;
   auto fetch = [&](int64_t rb, int64_t k0) __attribute__((always_inline)) {
     const v2d_ *src = (const v2d_ *)(P + (rb + ar) * n_pad + k0 + ak);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) ra[q] = src[q];
+    for (int q = 0; q < 4; ++q) ra[q] = src[q];
     rl = *(const v4i *)(gl + k0 + gk);
     rr = *(const v4i *)(gr + k0 + gk);
   };
   int64_t rb = 0, k0 = 0;
   fetch(0, 0);
   while (rb < n_pad) {
-    v4d acc[2][2];
+    v4d acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4d{0, 0, 0, 0};
     // symmetric P: only column blocks k0 >= rb, the off-diagonal ones counted twice (x2 is
     // exact); the rb == 0 pass covers every k and also accumulates the eff partials
-    for (; k0 < n_pad; k0 += QK) {
-      const double f = k0 >= rb + QT ? 2.0 : 1.0;
+    for (; k0 < n_pad; k0 += RK) {
+      const double f = k0 >= rb + RM ? 2.0 : 1.0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 4; ++q) {
         As[ak + 2 * q][ar] = f * ra[q][0];
         As[ak + 2 * q + 1][ar] = f * ra[q][1];
       }
@@ -1183,31 +1187,31 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
         }
       }
       __syncthreads();
-      // next stage (this row block's next columns, or the next row block's first)
-      {
-        int64_t nrb = rb, nk = k0 + QK;
+      {  // next stage (this row block's next columns, or the next row block's first)
+        int64_t nrb = rb, nk = k0 + RK;
         if (nk >= n_pad) {
-          nrb = rb + QT;
+          nrb = rb + RM;
           nk = nrb;
         }
         if (nrb < n_pad) fetch(nrb, nk);
       }
 #pragma unroll
-      for (int ks = 0; ks < QK / 4; ++ks) {
+      for (int ks = 0; ks < RK / 4; ++ks) {
         const int kk = ks * 4 + (lane >> 4);
         const double a0 = As[kk][wm * 32 + (lane & 15)], a1 = As[kk][wm * 32 + 16 + (lane & 15)];
-        const double b0 = Bs[kk][wn * 32 + (lane & 15)], b1 = Bs[kk][wn * 32 + 16 + (lane & 15)];
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+          const double bj = Bs[kk][wn * 64 + jt * 16 + (lane & 15)];
+          acc[0][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bj, acc[0][jt], 0, 0, 0);
+          acc[1][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bj, acc[1][jt], 0, 0, 0);
+        }
       }
       __syncthreads();
     }
     // fold: var[col] += sum_rows E[row][col] * C[row][col]
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      const int col = wn * 32 + jt * 16 + (lane & 15);
+    for (int jt = 0; jt < 4; ++jt) {
+      const int col = wn * 64 + jt * 16 + (lane & 15);
       const int64_t p = p0 + col;
       if (p >= np) continue;
       const int8_t *l = left + pi[p] * n_pad, *r = right + pj[p] * n_pad;
@@ -1220,30 +1224,28 @@ __global__ __launch_bounds__(256) void refine_kernel(int64_t n_pad, const double
           vpart[jt] += ecode(l, r, al, be, row) * acc[it][jt][e];
         }
     }
-    rb += QT;
+    rb += RM;
     k0 = rb;
   }
   // reduce var partials: lanes with equal (lane & 15) in a wave, then the two wm waves
 #pragma unroll
-  for (int jt = 0; jt < 2; ++jt) {
+  for (int jt = 0; jt < 4; ++jt) {
     double v = vpart[jt];
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
-    if (lane < 16) red[wm * 2 + jt][wn * 16 + lane] = v;  // [wm][jt] x [wn*16 + lane]
+    if (lane < 16) red[wm][wn * 64 + jt * 16 + lane] = v;
   }
-  // eff partials: 4 threads per column (tid>>6), reduce via LDS after var
+  // eff partials: 2 threads per column (tid >> 7), reduce via LDS after var
   __syncthreads();
-  __shared__ double effr[4][QT];
-  effr[tid >> 6][gcol] = effp;
+  __shared__ double effr[2][RP];
+  effr[tid >> 7][gcol] = effp;
   __syncthreads();
-  if (tid < QT) {
+  if (tid < RP) {
     const int col = tid;
     const int64_t p = p0 + col;
     if (p < np) {
-      const int wn_ = col >> 5, jt = (col >> 4) & 1, ln = col & 15;
-      const double v = red[0 * 2 + jt][wn_ * 16 + ln] + red[1 * 2 + jt][wn_ * 16 + ln];
-      var[p] = v;
-      eff[p] = ((effr[0][col] + effr[1][col]) + effr[2][col]) + effr[3][col];
+      var[p] = red[0][col] + red[1][col];
+      eff[p] = effr[0][col] + effr[1][col];
     }
   }
 }
@@ -1817,7 +1819,7 @@ int build_coding(gmat_epi *e, int which) {
 int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp,
            const int64_t *pi, const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
   if (np <= 0) return GMAT_OK;
-  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, QT)), dim3(256), 0, st, e->n_pad, e->Ps.as<double>(),
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, RP)), dim3(256), 0, st, e->n_pad, e->Ps.as<double>(),
                      e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var);
   GMAT_HIP(hipGetLastError());
   hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
