@@ -41,6 +41,11 @@ using namespace gmat;
 
 namespace {
 
+typedef int v2i_ __attribute__((ext_vector_type(2)));
+typedef int v8i_ __attribute__((ext_vector_type(8)));
+typedef float v16f_ __attribute__((ext_vector_type(16)));
+typedef float v2f_ __attribute__((ext_vector_type(2)));
+
 constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
@@ -217,112 +222,231 @@ struct SideArgs {
   ScreenArgs a;  // rows, tri, j_lo, ld_e, scalars, prefilter constants, flags, c13 / c2 outputs
   const int8_t *rs[7];  // row-side sets [m][n_pad] (slices: stride slice_stride)
   const int8_t *cs[5];  // column-side sets
+  const uint8_t *rs4[2], *cs4[2];  // pass 1: fp4 code panels (a, a^2 | b, b^2) [m][n_pad / 2]
   int64_t n_pad;
   int n_rt;             // row tiles
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
-  // PASS 1: row sets L3q_0..2, a, a^2 x column sets b, b^2 (7 products); PASS 2: E1 (L'q_t x b),
-  // PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three products each
-  constexpr int NR = PASS == 1 ? E3_PF + 2 : PASS == 4 ? 1 : 3, NC = PASS == 1 ? 2 : PASS == 4 ? 3 : 1;
-  constexpr int NPR = PASS == 1 ? E3_PF + 4 : 3;
+  // PASS 1: E3 = L3q_t x b (t < E3_PF, int8) and the code products a.b, a^2.b, a.b^2, a^2.b^2 on
+  // the block-scaled MFMA in fp4 (codes 0..4 are exact e2m1 values; fp32 sums of integers < 2^24
+  // are exact): E3_PF int8 + 4 fp4 products, the fp4 ones at twice the int8 rate and half the bytes.
+  // PASS 2: E1 (L'q_t x b), PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three int8 products each.
+  constexpr int NR = PASS == 1 ? E3_PF : PASS == 4 ? 1 : 3, NC = PASS == 4 ? 3 : 1;
+  constexpr int NPR = PASS == 1 ? E3_PF : 3;
   const ScreenArgs &a = x.a;
   static_assert(NR <= 7 && NC <= 5, "operand sets");
-  const int rt = blockIdx.x % x.n_rt, ct = blockIdx.x / x.n_rt;
+  // XCD-aware tile order: workgroup b runs on XCD b mod 8; the bijective remap gives each XCD a
+  // contiguous range of tiles, so the n_rt row tiles of a column tile share one L2 (the column
+  // operands, streamed from HBM, are fetched once per XCD instead of once per row tile)
+  const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
+  const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
+  const int rt = tile % x.n_rt, ct = tile / x.n_rt;
   const int r0 = rt * SG_T;
   const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * SG_T;  // 32-aligned: a half-wave = one block
   if (r0 >= a.n_rows || c0 >= a.m) return;
   {  // tiles entirely on or left of the diagonal hold no pair (AA / DD)
     if (a.tri && c0 + SG_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
   }
-  __shared__ __attribute__((aligned(16))) int8_t sR[2][NR][SG_T * SG_P];
-  __shared__ __attribute__((aligned(16))) int8_t sC[2][NC][SG_T * SG_P];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
-  // staging: chunk q of a set = (tile row q >> 2, 16-byte piece q & 3); 256 chunks per set
-  const int srow = tid >> 2, spc = (tid & 3) * 16;
-  const int rr = min(r0 + srow, a.n_rows - 1);
-  const int64_t si = a.rows[rr];
-  const int64_t sj = min(c0 + srow, a.m - 1);
-  v4i rv[NR], cv[NC];
-  auto load = [&](int k0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NR; ++u) rv[u] = *(const v4i *)(x.rs[u] + si * x.n_pad + k0 + spc);
-#pragma unroll
-    for (int u = 0; u < NC; ++u) cv[u] = *(const v4i *)(x.cs[u] + sj * x.n_pad + k0 + spc);
-  };
-  auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < NR; ++u) *(v4i *)&sR[b][u][srow * SG_P + spc] = rv[u];
-#pragma unroll
-    for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
-  };
   // product p: (row set, column set)
-  static_assert(E3_PF == 2, "product table");
-  constexpr int PR[4][6] = {{0, 1, 2, 3, 2, 3}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
-  constexpr int PC[4][6] = {{0, 0, 0, 0, 1, 1}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
+  constexpr int PR[4][3] = {{0, 1, 0}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
+  constexpr int PC[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
   v16i acc[NPR];
+  v16f_ acc4[PASS == 1 ? 4 : 1];  // a.b, a^2.b, a.b^2, a^2.b^2
 #pragma unroll
   for (int p = 0; p < NPR; ++p)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[p][e] = 0;
-  load(0);
-  store(0);
-  __syncthreads();
-  int b = 0;
-  for (int k0 = 0; k0 < x.n_pad; k0 += SG_K) {
-    const bool more = k0 + SG_K < x.n_pad;
-    if (more) load(k0 + SG_K);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v4i fr[NR], fc[NC];
+  for (int p = 0; p < (PASS == 1 ? 4 : 1); ++p)
 #pragma unroll
-      for (int u = 0; u < NR; ++u) fr[u] = *(const v4i *)&sR[b][u][(32 * wr + c) * SG_P + 32 * kk + 16 * h];
+    for (int e = 0; e < 16; ++e) acc4[p][e] = 0.f;
+  if constexpr (PASS == 1) {
+    // Three-stage LDS ring filled by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction),
+    // two stages in flight: the pass has little arithmetic per byte, so it needs the loads
+    // further ahead than a register prefetch can hold.  Stage image (20 KB, 64 individuals):
+    // int8 L3 slices 0, 1 (64 rows x 64 B each), int8 b (64 columns x 64 B), fp4 a, a^2 (64 x 32 B
+    // each), fp4 b, b^2; 16-byte chunks XOR-swizzled through the DMA source address (int8: chunk ^
+    // (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1) so the fragment reads are conflict-free.
+    // Wave w issues instructions q = w + 4u (u < 5); the image holds instruction q at q KB.
+    constexpr int ST = 20 * 1024, O_C8 = 8192, O_R4 = 12288, O_C4 = 16384;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[3][ST];
+    const uint8_t *src[5];
+    int stp[5];
 #pragma unroll
-      for (int u = 0; u < NC; ++u) fc[u] = *(const v4i *)&sC[b][u][(32 * wc + c) * SG_P + 32 * kk + 16 * h];
-#pragma unroll
-      for (int p = 0; p < NPR; ++p)
-        acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[PR[PASS - 1][p]], fc[PC[PASS - 1][p]], acc[p], 0, 0, 0);
+    for (int u = 0; u < 5; ++u) {
+      const int q = w + 4 * u;
+      if (q < 12) {  // int8: 16 rows x 4 chunks per instruction
+        const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+        const int64_t idx = q < 8 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+        src[u] = (const uint8_t *)(q < 8 ? x.rs[q >> 2] : x.cs[0]) + idx * x.n_pad + 16 * lg;
+        stp[u] = SG_K;
+      } else {  // fp4: 32 rows x 2 chunks per instruction
+        const int qq = q - (q < 16 ? 12 : 16), row = (qq & 1) * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
+        const int64_t idx = q < 16 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+        src[u] = (q < 16 ? x.rs4[qq >> 1] : x.cs4[qq >> 1]) + idx * (x.n_pad / 2) + 16 * lg;
+        stp[u] = SG_K / 2;
+      }
     }
-    if (more) store(b ^ 1);
+    auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+      typedef __attribute__((address_space(3))) void *lds_t;
+#pragma unroll
+      for (int u = 0; u < 5; ++u)
+        __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[buf][(w + 4 * u) * 1024], 16, 0, 0);
+    };
+    const int S = (int)(x.n_pad / SG_K);
+    issue(0, 0);
+    if (S > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int st = 0; st < S; ++st) {
+      const uint8_t *bf = ring[st % 3];
+      if (st + 2 < S) issue(st + 2, (st + 2) % 3);
+      const int rrow = 32 * wr + c, crow = 32 * wc + c;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lr = (2 * kk + h) ^ ((rrow >> 2) & 3), lc = (2 * kk + h) ^ ((crow >> 2) & 3);
+        const v4i f0 = *(const v4i *)&bf[rrow * 64 + 16 * lr], f1 = *(const v4i *)&bf[4096 + rrow * 64 + 16 * lr];
+        const v4i fc = *(const v4i *)&bf[O_C8 + crow * 64 + 16 * lc];
+        acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[1], 0, 0, 0);
+      }
+      {  // one 64-deep fp4 MFMA per code product
+        const int lr = h ^ ((rrow >> 3) & 1), lc = h ^ ((crow >> 3) & 1);
+        v8i_ fa[2], fb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const v4i ra4 = *(const v4i *)&bf[O_R4 + u * 2048 + rrow * 32 + 16 * lr];
+          const v4i rb4 = *(const v4i *)&bf[O_C4 + u * 2048 + crow * 32 + 16 * lc];
+          fa[u] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+          fb[u] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          acc4[p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[p], 4, 4, 0, 127, 0, 127);
+      }
+      // this wave's reads of buffer st % 3 are done and stage st + 1 has landed (only stage
+      // st + 2's five instructions may still be in flight); then the workgroup barrier
+      if (st + 2 < S)
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    __shared__ __attribute__((aligned(16))) int8_t sR[2][NR][SG_T * SG_P];
+    __shared__ __attribute__((aligned(16))) int8_t sC[2][NC][SG_T * SG_P];
+    // staging: chunk q of an int8 set = (tile row q >> 2, 16-byte piece q & 3); 256 chunks per set
+    const int srow = tid >> 2, spc = (tid & 3) * 16;
+    const int rr = min(r0 + srow, a.n_rows - 1);
+    const int64_t si = a.rows[rr];
+    const int64_t sj = min(c0 + srow, a.m - 1);
+    v4i rv[NR], cv[NC];
+    auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < NR; ++u) rv[u] = *(const v4i *)(x.rs[u] + si * x.n_pad + k0 + spc);
+#pragma unroll
+      for (int u = 0; u < NC; ++u) cv[u] = *(const v4i *)(x.cs[u] + sj * x.n_pad + k0 + spc);
+    };
+    auto store = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < NR; ++u) *(v4i *)&sR[b][u][srow * SG_P + spc] = rv[u];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
+    };
+    load(0);
+    store(0);
     __syncthreads();
-    b ^= 1;
+    int b = 0;
+    for (int k0 = 0; k0 < x.n_pad; k0 += SG_K) {
+      const bool more = k0 + SG_K < x.n_pad;
+      if (more) load(k0 + SG_K);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        v4i fr[NR], fc[NC];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) fr[u] = *(const v4i *)&sR[b][u][(32 * wr + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+        for (int u = 0; u < NC; ++u) fc[u] = *(const v4i *)&sC[b][u][(32 * wc + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+        for (int p = 0; p < NPR; ++p)
+          acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[PR[PASS - 1][p]], fc[PC[PASS - 1][p]], acc[p], 0, 0, 0);
+      }
+      if (more) store(b ^ 1);
+      __syncthreads();
+      b ^= 1;
+    }
   }
   // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 32 wc + c; the 32
-  // columns of a block are the 32 lanes of one half-wave
+  // columns of a block are the 32 lanes of one half-wave.  Pass 1 reads its per-row scalars from
+  // LDS (staged once per tile; a global load per element would expose its latency 16 times) and
+  // its per-column ones from registers.
   const int64_t j = c0 + 32 * wc + c;
   const int J = (int)(j / 32);
   const bool jok = j < a.m && j >= a.j_lo;
+  // per-row: i (as double; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
+  __shared__ double rowv[PASS == 1 ? 7 : 1][SG_T];
+  // per-column (registers): beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum,
+  // beta spy - sb, sum_k (b + beta)^2
+  double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
+  bool cmono = true;
+  if constexpr (PASS == 1) {
+    const double n = a.n_id;
+    if (tid < SG_T) {
+      const int r = min(r0 + tid, a.n_rows - 1);
+      const int64_t i = a.rows[r];
+      const double al = a.alpha[i], ca = a.csum_l[i];
+      rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
+      rowv[1][tid] = al;
+      rowv[2][tid] = ca;
+      rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
+      rowv[4][tid] = a.sL3[i];
+      rowv[5][tid] = a.sa[i];
+      rowv[6][tid] = (2.0 + al) * (2.0 + al);
+    }
+    if (jok) {
+      cbe = a.beta[j];
+      ccb = a.csum_r[j];
+      const double cb2 = a.csq_r[j];
+      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
+      cnb = n * cbe - ccb;
+      cbsb = cbe * a.spy - a.sb[j];
+      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+      cmono = a.mono_r[j];
+    }
+    __syncthreads();
+  }
+  // vlo = (mu - eps)|e|^2 - (mu + tau)(1'e)^2/n - 1e-12 mu (|expansion terms| + (1'e)^2/n), the
+  // absolute terms bounded by sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2
+  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id, k2 = 1e-12 * a.pf_mu;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
     const bool rok = r < a.n_rows;
     const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
     if (PASS == 1) {
       bool live = false;
-      if (rok && jok) {
-        const int64_t i = a.rows[r];
-        if (!a.mono_l[i] && !(a.tri && j <= i) && !a.mono_r[j]) {
-          const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
+      const double iv = rowv[0][rl];
+      if (rok && jok && iv >= 0.0 && !cmono) {
+        const int64_t i = (int64_t)iv;
+        if (!(a.tri && j <= i)) {
+          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
           double c3 = 0.0;
 #pragma unroll
           for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
-          const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
-          const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-          const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
-          const double sab = (double)acc[E3_PF][e], sa2b = (double)acc[E3_PF + 1][e],
-                       sab2 = (double)acc[E3_PF + 2][e], sa2b2 = (double)acc[E3_PF + 3][e];
-          const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
-                                  -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
-          double ee = 0.0, mag = 0.0;
-#pragma unroll
-          for (int q = 0; q < 9; ++q) {
-            ee += t_ee[q];
-            mag += fabs(t_ee[q]);
-          }
-          const double se = sab - be * ca - al * cb + n * al * be;
-          const double pe = ee - se * se / n;
-          const double vlo =
-              a.pf_mu * pe - a.pf_tau * se * se / n - a.pf_eps * ee - 1e-12 * a.pf_mu * (mag + se * se / n);
+          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
+          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
+          const double sab = (double)acc4[0][e], sa2b = (double)acc4[1][e], sab2 = (double)acc4[2][e],
+                       sa2b2 = (double)acc4[3][e];
+          // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
+          const double ee = sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
+          const double se = sab - be * rowv[2][rl] + al * cnb;
+          const double vlo = mu_e * ee - k1 * se * se - k2 * rowv[6][rl] * cmag;
           live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
         }
       }
@@ -335,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
         for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
         if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
 #pragma unroll
-          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = acc[E3_PF + q][e];
+          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = (int)acc4[q][e];
       }
     } else {
       if (rok && jok && a.flags[(int64_t)r * a.nJ + J]) {
@@ -590,10 +714,6 @@ struct MxShape {
   static constexpr int NW = 8, PB = MX_BI / NW, T = 64 * NW, MINB = 1;
 };
 
-typedef int v2i_ __attribute__((ext_vector_type(2)));
-typedef int v8i_ __attribute__((ext_vector_type(8)));
-typedef float v16f_ __attribute__((ext_vector_type(16)));
-typedef float v2f_ __attribute__((ext_vector_type(2)));
 
 struct MxArgs {
   const uint8_t *tiles;    // [nK][nK] A tile images (upper ones used)
@@ -1624,6 +1744,18 @@ __global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double ta
   A[idx] = P[idx] + (mu + tau) / (double)n - (r == c ? mu : 0.0);
 }
 
+// fp4 e2m1 copies of a screen panel (codes 0, 1, 2 -> 0x0, 0x2, 0x4) and of its squares (0, 1, 4 ->
+// 0x0, 0x2, 0x6); individual 2q at the low nibble of byte q (the MFMA's packing)
+__global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4, uint8_t *p4sq) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= m * (n_pad / 2)) return;
+  const int v0 = panel[2 * idx], v1 = panel[2 * idx + 1];
+  auto code = [](int v) { return v == 0 ? 0 : v == 1 ? 2 : 4; };
+  auto csq = [](int v) { return v == 0 ? 0 : v == 1 ? 2 : 6; };
+  p4[idx] = (uint8_t)(code(v0) | (code(v1) << 4));
+  p4sq[idx] = (uint8_t)(csq(v0) | (csq(v1) << 4));
+}
+
 // A = P + C + (lam + tau) 11'/n - lam I (natural order) for the low-rank screen's certificate
 __global__ void lr_shift_kernel(int64_t n, const double *P, const double *C, double lam, double tau, double *A) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1660,6 +1792,7 @@ struct Coding {
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
+  DBuf p4, p4sq;                  // screen codes and their squares as fp4 e2m1 [m][n_pad / 2] (prefilter)
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
 };
@@ -1789,6 +1922,11 @@ int build_coding(gmat_epi *e, int which) {
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
                      cd.Rq.as<int8_t>(), cd.sR.as<double>());
   GMAT_HIP(hipGetLastError());
+  GMAT_TRY(cd.p4.alloc((size_t)m * n_pad / 2));
+  GMAT_TRY(cd.p4sq.alloc((size_t)m * n_pad / 2));
+  hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
+                     cd.p4.as<uint8_t>(), cd.p4sq.as<uint8_t>());
+  GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.nibI.alloc((size_t)m * n_pad));
   GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
   hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
@@ -1849,7 +1987,7 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
   const int Re = (int)std::min<int64_t>(R_req, n - 1);
   const int Rp = (int)cdiv(Re, MXK) * MXK;
   const int ne = (int)std::min<int64_t>(Re + 1, n);
-  const double kap = kenv ? atof(kenv) : 0.7;
+  const double kap = kenv ? atof(kenv) : 0.45;
   double trP = 0.0;
   for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
   const double t0 = now();
@@ -2569,10 +2707,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const int64_t ncols = m - (ln.j_lo / 32) * 32;
       const unsigned grid = (unsigned)(x.n_rt * cdiv(ncols, SG_T));
       for (int t = 0; t < E3_PF; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
-      x.rs[E3_PF] = slp;
-      x.rs[E3_PF + 1] = slq;
       x.cs[0] = srp;
-      x.cs[1] = srq;
+      x.rs4[0] = L.p4.as<uint8_t>();
+      x.rs4[1] = L.p4sq.as<uint8_t>();
+      x.cs4[0] = R.p4.as<uint8_t>();
+      x.cs4[1] = R.p4sq.as<uint8_t>();
       hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
       GMAT_HIP(hipGetLastError());
       if (x.a.pf_store) {  // the low-rank screen needs nothing else
