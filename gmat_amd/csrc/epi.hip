@@ -1797,6 +1797,28 @@ struct Coding {
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
 };
 
+// pinned host staging buffer (grown on demand, kept by the plan across scans)
+struct Pinned {
+  void *p = nullptr;
+  size_t cap = 0;
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+  int reserve(size_t n) {
+    if (n <= cap) return GMAT_OK;
+    if (p) GMAT_HIP(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
+    GMAT_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
+    cap = n;
+    return GMAT_OK;
+  }
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
 struct gmat_epi {
   gmat_geno *g = nullptr;
   int64_t n = 0, n_pad = 0, m = 0;
@@ -1831,6 +1853,10 @@ struct gmat_epi {
     DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
     DBuf mxt2[2], mxr2[2];  // stage-2 MX tiles of a launch
   } sb;
+  // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
+  struct ScanPins {
+    Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2];
+  } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
@@ -2355,26 +2381,7 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
 }
 
 namespace {
-struct Pinned {
-  void *p = nullptr;
-  size_t cap = 0;
-  ~Pinned() {
-    if (p) (void)hipHostFree(p);
-  }
-  int reserve(size_t n) {
-    if (n <= cap) return GMAT_OK;
-    if (p) GMAT_HIP(hipHostFree(p));
-    p = nullptr;
-    cap = 0;
-    GMAT_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
-    cap = n;
-    return GMAT_OK;
-  }
-  template <class T>
-  T *as() const {
-    return (T *)p;
-  }
-};
+
 }  // namespace
 
 extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
@@ -2530,7 +2537,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     issued = upto;
     return GMAT_OK;
   };
-  Pinned pin_res;
+  Pinned &pin_res = e->pins.res;
   // refine what is left of [0, count), collect the hits; the buffer is free afterwards
   auto flush = [&](int64_t count) -> int {
     if (count <= 0) return GMAT_OK;
@@ -2678,7 +2685,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // side terms of launch `li` into buffer set b (stream s2)
   // pinned host staging: asynchronous copies from / to pageable memory block the host until the
   // stream drains, which would serialise the side passes of launch li+1 behind screen li
-  Pinned pin_count, pin_rows[2], pin_flags[2], pin_mxt[2], pin_mxr[2];
+  Pinned &pin_count = e->pins.count;
+  auto &pin_rows = e->pins.rows, &pin_flags = e->pins.flags, &pin_mxt = e->pins.mxt, &pin_mxr = e->pins.mxr;
   GMAT_TRY(pin_count.reserve(8));
   auto stage_rows = [&](const Launch &ln, int b) -> int {
     GMAT_TRY(pin_rows[b].reserve(ln.rows.size() * 8));
@@ -2789,7 +2797,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   std::vector<int> mxT[2], mxR[2];
   int64_t nMX[2] = {0, 0};
   size_t built_for[2] = {SIZE_MAX, SIZE_MAX};
+  double t_build = 0.0;  // host seconds spent building MX / low-rank tile lists (diagnostics)
   auto build_mx = [&](size_t li, int b) -> int {
+    const double tb0 = now();
+    struct Acc {
+      double &t;
+      double t0;
+      ~Acc() { t += now() - t0; }
+    } acc_guard{t_build, tb0};
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     std::vector<int> &mx_tiles = mxT[b], &mx_rows = mxR[b];
@@ -2809,15 +2824,36 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       auto live = [&](int r, int64_t J) {
         return use_pf ? fl[(size_t)r * nJ + J] != 0 : (!tri || J * BJ + BJ - 1 > ln.rows[r]);
       };
-      for (int r = 0; r < Rn; ++r)
-        for (int64_t J = 0; J < nJ; ++J) jcnt[J + 1] += live(r, J);
+      // (r, J) with a set flag, in row-major order: the flags are sparse, scan 8 at a time
+      std::vector<std::pair<int, int>> set_rj;
+      if (use_pf) {
+        set_rj.reserve((size_t)Rn * nJ / 8);
+        for (int r = 0; r < Rn; ++r) {
+          const uint8_t *f = fl + (size_t)r * nJ;
+          int64_t J = 0;
+          for (; J + 8 <= nJ; J += 8) {
+            uint64_t wd;
+            std::memcpy(&wd, f + J, 8);
+            while (wd) {
+              const int bit = __builtin_ctzll(wd);
+              set_rj.push_back({r, (int)(J + bit / 8)});
+              wd &= ~(0xFFull << (bit & ~7));
+            }
+          }
+          for (; J < nJ; ++J)
+            if (f[J]) set_rj.push_back({r, (int)J});
+        }
+      } else {
+        for (int r = 0; r < Rn; ++r)
+          for (int64_t J = 0; J < nJ; ++J)
+            if (live(r, J)) set_rj.push_back({r, (int)J});
+      }
+      for (const auto &q : set_rj) ++jcnt[q.second + 1];
       for (int64_t J = 0; J < nJ; ++J) jcnt[J + 1] += jcnt[J];
       jrow.resize(jcnt[nJ]);
       {
         std::vector<int> fill(jcnt.begin(), jcnt.end() - 1);
-        for (int r = 0; r < Rn; ++r)
-          for (int64_t J = 0; J < nJ; ++J)
-            if (live(r, J)) jrow[fill[J]++] = r;
+        for (const auto &q : set_rj) jrow[fill[q.second]++] = q.first;
       }
       for (int64_t J = 0; J < nJ; ++J) {
         int cnt = 0;
@@ -2871,7 +2907,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // grouped into (band row, 32-column block) slots, packed into MX tiles (half-tiles per block,
   // dealt to the XCDs like build_mx), their E1 / Ed / E2 computed (slot_side_kernel) and the MX
   // quadratic form re-screens them into the main candidate buffer.  Returns the stage-2 tiles.
-  Pinned pin_count1, pin_c1, pin_t2[2], pin_r2[2];
+  Pinned &pin_count1 = e->pins.count1, &pin_c1 = e->pins.c1;
+  auto &pin_t2 = e->pins.t2, &pin_r2 = e->pins.r2;
   GMAT_TRY(pin_count1.reserve(8));
   GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
   double t_stage2 = 0.0, n_stage1 = 0.0;
@@ -2985,20 +3022,21 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const bool stamps_on = getenv("GMAT_LR_STAMPS") != nullptr;
   DBuf dstamp;
   if (stamps_on) GMAT_TRY(dstamp.alloc((size_t)max_mx * 8 * 6 * 8));
-  for (size_t li = 0; li < plan.size(); ++li) {
-    const Launch &ln = plan[li];
-    const int b = (int)(li & 1);
-    const int Rn = (int)ln.rows.size();
-    int64_t ntiles = 0;  // int8 screen workgroups (tile lists are built lazily)
-    ScreenArgs sa = make_args(li, b);
-    unsigned long long count = 0;
-    MxArgs mx;
-    mx.tiles = e->mx_tiles.as<uint8_t>();
-    mx.nib_i = L.nibI.as<uint8_t>();
-    mx.nib_j = R.nibJ.as<uint8_t>();
-    mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
-    mx.nib_bytes = m * n_pad;
-    mx.nK = e->nK;
+  // The next launch's low-rank screen is queued on sm right behind the current one (its side
+  // pass and tile list are ready by then), so the host's per-launch bookkeeping no longer leaves
+  // the GPU idle; a launch that overflows the candidate buffer discards the queued one.
+  const bool pipe_next = use_lr && !use_stage2 && !stamps_on;
+  std::vector<char> queued(plan.size(), 0);
+  hipEvent_t evs7[2], evs2[2];
+  for (int q = 0; q < 2; ++q) {
+    GMAT_HIP(hipEventCreate(&evs7[q]));
+    GMAT_HIP(hipEventCreate(&evs2[q]));
+  }
+  EvPair evs7_guard{evs7}, evs2_guard{evs2};
+  auto &pin_cnt = e->pins.cnt;
+  GMAT_TRY(pin_cnt[0].reserve(8));
+  GMAT_TRY(pin_cnt[1].reserve(8));
+  auto lr_args = [&](size_t li) {
     LrArgs lx;
     lx.tiles = e->lr_tiles.as<uint8_t>();
     lx.nib_i = L.nibI.as<uint8_t>();
@@ -3015,6 +3053,40 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     lx.tau = e->lr_tau;
     lx.eps = e->lr_eps;
     lx.stamp = (stamps_on && li == 5) ? dstamp.as<unsigned long long>() : nullptr;
+    return lx;
+  };
+  // queue the low-rank screen of launch li (level 0) on sm: waits for its side pass, counts after it
+  auto queue_lr = [&](size_t li, int b) -> int {
+    ScreenArgs sa = make_args(li, b);
+    sa.n_slice = 0;
+    sa.delta = e->rho_mx;
+    sa.tiles = mxt[b].as<int>();
+    const LrArgs lx = lr_args(li);
+    GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
+    GMAT_HIP(hipEventRecord(evs7[b], sm));
+    if (!mxT[b].empty())
+      hipLaunchKernelGGL(lr_screen_kernel, dim3((unsigned)(mxT[b].size() / MX_TE)), dim3(MxShape<1>::T), 0, sm, sa, lx);
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipEventRecord(evs2[b], sm));
+    GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipEventRecord(screen_end[b], sm));
+    return GMAT_OK;
+  };
+  for (size_t li = 0; li < plan.size(); ++li) {
+    const Launch &ln = plan[li];
+    const int b = (int)(li & 1);
+    const int Rn = (int)ln.rows.size();
+    int64_t ntiles = 0;  // int8 screen workgroups (tile lists are built lazily)
+    ScreenArgs sa = make_args(li, b);
+    unsigned long long count = 0;
+    MxArgs mx;
+    mx.tiles = e->mx_tiles.as<uint8_t>();
+    mx.nib_i = L.nibI.as<uint8_t>();
+    mx.nib_j = R.nibJ.as<uint8_t>();
+    mx.tiles_bytes = (int64_t)e->mx_tiles.bytes;
+    mx.nib_bytes = m * n_pad;
+    mx.nK = e->nK;
+    const LrArgs lx = lr_args(li);
     if (S == 0 && built_for[b] != li) GMAT_TRY(build_mx(li, b));
     const std::vector<int> &mx_tiles = mxT[b];
     const int64_t n_mx = nMX[b];
@@ -3022,8 +3094,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       sa.n_slice = S;
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
+      const bool two_stage = S == 0 && use_lr && use_stage2;
+      if (queued[li] && S == 0) {  // queued behind the previous launch
+        queued[li] = 0;
+      } else {
+      queued[li] = 0;
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
-      GMAT_HIP(hipEventRecord(ev[7], sm));
+      GMAT_HIP(hipEventRecord(evs7[b], sm));
       sa.tiles = S == 0 ? mxt[b].as<int>() : dtiles[b].as<int>();
       if (S != 0 && !side_full[b]) {  // escalated from the MX screen: the int8 screen needs E1 / Ed / E2
         GMAT_HIP(hipStreamSynchronize(S2));
@@ -3033,7 +3110,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         sa.e3_eps = 0.5 * std::pow(128.0, -(sa.e3_t - 1)) + 1e-12;
       }
       ntiles = (int64_t)plan[li].tiles.size() / 2;
-      const bool two_stage = S == 0 && use_lr && use_stage2;
       if (S == 0 && use_lr && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
         ScreenArgs s1 = sa;  // with stage 2 the low-rank candidates go to cand1
@@ -3053,18 +3129,23 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       else
         hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       GMAT_HIP(hipGetLastError());
-      GMAT_HIP(hipEventRecord(ev[2], sm));
-      GMAT_HIP(hipEventRecord(screen_end[b], sm));
-      GMAT_HIP(hipMemcpyAsync(pin_count.p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+      GMAT_HIP(hipEventRecord(evs2[b], sm));
+      GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
       if (two_stage) GMAT_HIP(hipMemcpyAsync(pin_count1.p, e->counter1.p, 8, hipMemcpyDeviceToHost, sm));
-      // next launch's side terms overlap this screen
-      if (attempt == 0 && li + 1 < plan.size()) {
-        GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
-        // the next launch's tile list is built on the host while this screen runs
-        if (S == 0) GMAT_TRY(build_mx(li + 1, b ^ 1));
+      GMAT_HIP(hipEventRecord(screen_end[b], sm));
       }
-      GMAT_HIP(hipStreamSynchronize(sm));
-      count = *pin_count.as<unsigned long long>();
+      // next launch's side terms overlap this screen; its tile list is built on the host
+      // meanwhile, and its low-rank screen queued behind this one
+      if (attempt == 0 && li + 1 < plan.size() && !queued[li + 1]) {
+        GMAT_TRY(enqueue_side(li + 1, b ^ 1, S != 0));
+        if (S == 0) GMAT_TRY(build_mx(li + 1, b ^ 1));
+        if (S == 0 && pipe_next) {
+          GMAT_TRY(queue_lr(li + 1, b ^ 1));
+          queued[li + 1] = 1;
+        }
+      }
+      GMAT_HIP(hipEventSynchronize(screen_end[b]));
+      count = *pin_cnt[b].as<unsigned long long>();
       if (two_stage) {
         // stage 2 (MX re-screen of the low-rank candidates) runs on S3 beside the next launches;
         // the main counter is read when the buffer is flushed
@@ -3084,7 +3165,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
-      // overflowed on its own, redo it with one more slice (thinner candidate band)
+      // overflowed on its own, redo it with one more slice (thinner candidate band).  A queued
+      // next launch appended behind the overflow: drain it and run it again later.
+      GMAT_HIP(hipStreamSynchronize(sm));
+      if (li + 1 < plan.size()) queued[li + 1] = 0;
       if (pending == 0) {
         GMAT_CHECK(S < e->n_slice, GMAT_E_OVERFLOW,
                    "one screen launch produced %llu candidates (capacity %lld) with %d slices: p_cut too large "
@@ -3126,7 +3210,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     float ms_side, ms_screen;
     GMAT_HIP(hipEventSynchronize(side_end[b]));
     GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
-    GMAT_HIP(hipEventElapsedTime(&ms_screen, ev[7], ev[2]));
+    GMAT_HIP(hipEventElapsedTime(&ms_screen, evs7[b], evs2[b]));
     t_side += ms_side * 1e-3;
     t_screen += ms_screen * 1e-3;
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
@@ -3139,6 +3223,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
     if (!async_s2 && pending > e->cand_cap / 2) {
+      GMAT_HIP(hipStreamSynchronize(sm));  // a queued next launch is discarded: the counter restarts
+      if (li + 1 < plan.size()) queued[li + 1] = 0;
       GMAT_TRY(flush(pending));
       pending = 0;
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
@@ -3173,6 +3259,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[3] = t_screen;
   e->stats[4] = t_ref;
   e->stats[5] = t_side + t_stage2;  // side terms + the low-rank level's stage-2 MX re-screen
+  if (getenv("GMAT_DEBUG"))
+    fprintf(stderr, "gmat_epi_scan: %lld launches, tile-list building %.3f s on the host, total %.3f s\n",
+            (long long)launches_done, t_build, e->stats[6]);
   if (getenv("GMAT_DEBUG") && use_stage2)
     fprintf(stderr, "gmat_epi_scan: low-rank screen candidates %.0f -> MX re-screen %.0f (%.3f s)\n", n_stage1,
             ncand_total, t_stage2);
