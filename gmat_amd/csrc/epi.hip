@@ -476,6 +476,201 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
   }
 }
 
+// ------------------------------------------------------------------ prefilter pass
+// The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 128 x 128
+// (band row, column) tiles, 8 waves of 32 x 64: the pass streams its operands at ~20 bytes per
+// 64 x 64 x 64 MFMA block, so it is bound by each CU's load rate; a 128-wide tile halves the bytes
+// per pair.  Stage image (40 KB, 64 individuals), three-stage LDS-DMA ring (120 KB), two stages in
+// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), int8 b (128 columns x 64 B), fp4 a, a^2
+// (128 x 32 B each), fp4 b, b^2.  16-byte chunks XOR-swizzled through the DMA source address (int8:
+// chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA instruction q (1 KB) at
+// q KB, wave w issuing q = w + 8u (u < 5).
+constexpr int PF_T = 128, PF_ST = 40 * 1024;
+__global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
+  const ScreenArgs &a = x.a;
+  const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
+  const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
+  const int rt = tile % x.n_rt, ct = tile / x.n_rt;
+  const int r0 = rt * PF_T;
+  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PF_T;
+  if (r0 >= a.n_rows || c0 >= a.m) return;
+  if (a.tri && c0 + PF_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
+  // 8 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
+  constexpr int O_R8 = 0, O_C8 = 16384, O_R4 = 24576, O_C4 = 32768;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[3][PF_ST];
+  const uint8_t *src[5];
+  int stp[5];
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int q = w + 8 * u;
+    if (q < 24) {  // int8: 16 rows x 4 chunks per instruction
+      const int row = (q & 7) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+      const int64_t idx = q < 16 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+      src[u] = (const uint8_t *)(q < 16 ? x.rs[q >> 3] : x.cs[0]) + idx * x.n_pad + 16 * lg;
+      stp[u] = SG_K;
+    } else {  // fp4: 32 rows x 2 chunks per instruction
+      const int qq = q - (q < 32 ? 24 : 32), row = (qq & 3) * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
+      const int64_t idx = q < 32 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+      src[u] = (q < 32 ? x.rs4[qq >> 2] : x.cs4[qq >> 2]) + idx * (x.n_pad / 2) + 16 * lg;
+      stp[u] = SG_K / 2;
+    }
+  }
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) void *lds_t;
+#pragma unroll
+    for (int u = 0; u < 5; ++u)
+      __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[buf][(w + 8 * u) * 1024], 16, 0, 0);
+  };
+  v16i acc[2][E3_PF];
+  v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+#pragma unroll
+    for (int p = 0; p < E3_PF; ++p)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q][p][e] = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc4[q][p][e] = 0.f;
+  }
+  const int S = (int)(x.n_pad / SG_K);
+  issue(0, 0);
+  if (S > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  const int rrow = 32 * wr + c;
+  for (int st = 0; st < S; ++st) {
+    const uint8_t *bf = ring[st % 3];
+    if (st + 2 < S) issue(st + 2, (st + 2) % 3);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lr = (2 * kk + h) ^ ((rrow >> 2) & 3);
+      const v4i f0 = *(const v4i *)&bf[O_R8 + rrow * 64 + 16 * lr];
+      const v4i f1 = *(const v4i *)&bf[O_R8 + 8192 + rrow * 64 + 16 * lr];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int crow = 64 * wc + 32 * q + c, lc = (2 * kk + h) ^ ((crow >> 2) & 3);
+        const v4i fc = *(const v4i *)&bf[O_C8 + crow * 64 + 16 * lc];
+        acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
+        acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
+      }
+    }
+    {
+      const int lr = h ^ ((rrow >> 3) & 1);
+      v8i_ fa[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const v4i ra4 = *(const v4i *)&bf[O_R4 + u * 4096 + rrow * 32 + 16 * lr];
+        fa[u] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
+        v8i_ fb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const v4i rb4 = *(const v4i *)&bf[O_C4 + u * 4096 + crow * 32 + 16 * lc];
+          fb[u] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
+      }
+    }
+    if (st + 2 < S)
+      asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
+  // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
+  // per-row: i (as double; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
+  __shared__ double rowv[7][PF_T];
+  const double n = a.n_id;
+  if (tid < PF_T) {
+    const int r = min(r0 + tid, a.n_rows - 1);
+    const int64_t i = a.rows[r];
+    const double al = a.alpha[i], ca = a.csum_l[i];
+    rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
+    rowv[1][tid] = al;
+    rowv[2][tid] = ca;
+    rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
+    rowv[4][tid] = a.sL3[i];
+    rowv[5][tid] = a.sa[i];
+    rowv[6][tid] = (2.0 + al) * (2.0 + al);
+  }
+  __syncthreads();
+  // vlo = (mu - eps)|e|^2 - (mu + tau)(1'e)^2/n - 1e-12 mu (|expansion terms| + (1'e)^2/n), the
+  // absolute terms bounded by sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2
+  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int64_t j = c0 + 64 * wc + 32 * q + c;
+    const int J = (int)(j / 32);
+    const bool jok = j < a.m && j >= a.j_lo;
+    // per-column: beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum, beta spy - sb,
+    // sum_k (b + beta)^2
+    double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
+    bool cmono = true;
+    if (jok) {
+      cbe = a.beta[j];
+      ccb = a.csum_r[j];
+      const double cb2 = a.csq_r[j];
+      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
+      cnb = n * cbe - ccb;
+      cbsb = cbe * a.spy - a.sb[j];
+      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+      cmono = a.mono_r[j];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+      const bool rok = r < a.n_rows;
+      const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
+      bool live = false;
+      const double iv = rowv[0][rl];
+      if (rok && jok && iv >= 0.0 && !cmono) {
+        const int64_t i = (int64_t)iv;
+        if (!(a.tri && j <= i)) {
+          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
+          double c3 = 0.0;
+#pragma unroll
+          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[q][t][e];
+          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
+          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
+          const double sab = (double)acc4[q][0][e], sa2b = (double)acc4[q][1][e], sab2 = (double)acc4[q][2][e],
+                       sa2b2 = (double)acc4[q][3][e];
+          // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
+          const double ee =
+              sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
+          const double se = sab - be * rowv[2][rl] + al * cnb;
+          const double vlo = mu_e * ee - k1 * se * se - k2 * rowv[6][rl] * cmag;
+          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
+        }
+      }
+      const unsigned long long bal = __ballot(live);
+      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
+      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+      if (blk && rok && jok) {
+        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
+        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+#pragma unroll
+          for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one element's prefilter at a time
+    }
+  }
+}
+
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
 // PB per wave.  SH 0: MT 128, PB 2 -> 8 first SNPs x 32 second SNPs per workgroup; each
 //   generated B fragment feeds 4 MFMAs.
@@ -2720,7 +2915,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.rs4[1] = L.p4sq.as<uint8_t>();
       x.cs4[0] = R.p4.as<uint8_t>();
       x.cs4[1] = R.p4sq.as<uint8_t>();
-      hipLaunchKernelGGL(side_gemm_kernel<1>, dim3(grid), dim3(256), 0, S2, x);
+      {  // prefilter pass: 128 x 128 tiles
+        SideArgs xp = x;
+        xp.n_rt = (int)cdiv(Rn, PF_T);
+        const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_T));
+        hipLaunchKernelGGL(prefilter_pass_kernel, dim3(gp), dim3(512), 0, S2, xp);
+      }
       GMAT_HIP(hipGetLastError());
       if (x.a.pf_store) {  // the low-rank screen needs nothing else
         GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
