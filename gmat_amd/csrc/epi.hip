@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(512) void slot_side_kernel(ScreenArgs a, SlotSideAr
 // MFMA tile C = P[rows, k >= rows] E (off-diagonal blocks x2, exact) is formed in RK-deep stages
 // (the next stage's P rows and code bytes fetched into registers while this one multiplies) and
 // folded into var.  Waves: 2 (rows) x 2 (64-pair halves), each 32 x 64 of 16x16x4 f64 MFMA tiles.
-constexpr int RP = 128, RM = 64, RK = 32;
+constexpr int RP = 128, RM = 128, RK = 32, RT = 512;
 
 __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double al, double be, int64_t q) {
   const double x = (double)l[q] - al;
@@ -1446,19 +1446,21 @@ __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double
 }
 
 typedef double v2d_ __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
-                                                     const double *__restrict__ py, const int8_t *left,
-                                                     const int8_t *right, const double *alpha, const double *beta,
-                                                     const int64_t *pi, const int64_t *pj, int64_t np, double *eff,
-                                                     double *var) {
+typedef int v2i__ __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const double *__restrict__ P,
+                                                       const double *__restrict__ py, const int8_t *left,
+                                                       const int8_t *right, const double *alpha, const double *beta,
+                                                       const int64_t *pi, const int64_t *pj, int64_t np, double *eff,
+                                                       double *var) {
   __shared__ double As[RK][RM + 1];
   __shared__ double Bs[RK][RP + 1];
-  __shared__ double red[2][RP];
+  __shared__ double red[4][RP];
+  // 8 waves: rows 32 (w >> 1) .. +32 of the row block x pairs 64 (w & 1) .. +64
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int64_t p0 = (int64_t)blockIdx.x * RP;
-  // staging roles: A row ar = tid / 4, 8 doubles from column ak; E column gcol, 16 k from gk
+  // staging roles: A row ar = tid / 4, 8 doubles from column ak; E column gcol, 8 k from gk
   const int ar = tid >> 2, ak = (tid & 3) * 8;
-  const int gcol = tid & (RP - 1), gk = (tid >> 7) * 16;
+  const int gcol = tid & (RP - 1), gk = (tid >> 7) * 8;
   const int64_t gp = p0 + gcol;
   const bool gval = gp < np;
   const int8_t *gl = gval ? left + pi[gp] * n_pad : left;
@@ -1467,13 +1469,13 @@ __global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const dou
   double vpart[4] = {0, 0, 0, 0};  // per 16-pair subtile partial of var
   double effp = 0.0;
   v2d_ ra[4];
-  v4i rl, rr;
+  v2i__ rl, rr;
   auto fetch = [&](int64_t rb, int64_t k0) __attribute__((always_inline)) {
     const v2d_ *src = (const v2d_ *)(P + (rb + ar) * n_pad + k0 + ak);
 #pragma unroll
     for (int q = 0; q < 4; ++q) ra[q] = src[q];
-    rl = *(const v4i *)(gl + k0 + gk);
-    rr = *(const v4i *)(gr + k0 + gk);
+    rl = *(const v2i__ *)(gl + k0 + gk);
+    rr = *(const v2i__ *)(gr + k0 + gk);
   };
   int64_t rb = 0, k0 = 0;
   fetch(0, 0);
@@ -1495,7 +1497,7 @@ __global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const dou
       {
         const int8_t *lb = (const int8_t *)&rl, *rbb = (const int8_t *)&rr;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        for (int q = 0; q < 8; ++q) {
           const double e = gval ? ((double)lb[q] - gal) * ((double)rbb[q] - gbe) : 0.0;
           Bs[gk + q][gcol] = e;
           if (rb == 0) effp += e * py[k0 + gk + q];
@@ -1542,7 +1544,7 @@ __global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const dou
     rb += RM;
     k0 = rb;
   }
-  // reduce var partials: lanes with equal (lane & 15) in a wave, then the two wm waves
+  // reduce var partials: lanes with equal (lane & 15) in a wave, then the four wm waves
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt) {
     double v = vpart[jt];
@@ -1550,17 +1552,17 @@ __global__ __launch_bounds__(256, 2) void refine_kernel(int64_t n_pad, const dou
     v += __shfl_xor(v, 32);
     if (lane < 16) red[wm][wn * 64 + jt * 16 + lane] = v;
   }
-  // eff partials: 2 threads per column (tid >> 7), reduce via LDS after var
+  // eff partials: 4 threads per column (tid >> 7), reduce via LDS after var
   __syncthreads();
-  __shared__ double effr[2][RP];
+  __shared__ double effr[4][RP];
   effr[tid >> 7][gcol] = effp;
   __syncthreads();
   if (tid < RP) {
     const int col = tid;
     const int64_t p = p0 + col;
     if (p < np) {
-      var[p] = red[0][col] + red[1][col];
-      eff[p] = effr[0][col] + effr[1][col];
+      var[p] = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+      eff[p] = (effr[0][col] + effr[1][col]) + (effr[2][col] + effr[3][col]);
     }
   }
 }
@@ -2178,7 +2180,7 @@ int build_coding(gmat_epi *e, int which) {
 int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp,
            const int64_t *pi, const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
   if (np <= 0) return GMAT_OK;
-  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, RP)), dim3(256), 0, st, e->n_pad, e->Ps.as<double>(),
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, RP)), dim3(RT), 0, st, e->n_pad, e->Ps.as<double>(),
                      e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var);
   GMAT_HIP(hipGetLastError());
   hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
