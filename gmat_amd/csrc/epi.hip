@@ -163,60 +163,15 @@ __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i
   }
 }
 
-// Spectral prefilter (one thread per band row r and 32-column block J): flags[r][J] = 1 unless
-// every pair (i = rows[r], j in block J) provably has p >= p_cut by
-//   var = e'Pe >= pf_mu (|e|^2 - (1'e)^2 / n) - pf_eps |e|^2,
-// with |e|^2 and 1'e exact from the int8 code products (e = (a - alpha) o (b - beta) expanded)
-// and eff from the sliced side term (bound dE3), as in cand_test.
-__global__ __launch_bounds__(256) void prefilter_kernel(ScreenArgs a) {
-  // one thread per (band row r, column j), j fastest; a 32-lane half-wave covers one block
-  const int64_t nb = (int64_t)a.nJ * 32;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int r = (int)(idx / nb);
-  const int64_t j = idx % nb;
-  bool live = false;
-  if (r < a.n_rows) {
-    const int64_t i = a.rows[r];
-    if (!a.mono_l[i] && j < a.m && j >= a.j_lo && !(a.tri && j <= i) && !a.mono_r[j]) {
-      const double al = a.alpha[i], ca = a.csum_l[i], ca2 = a.csq_l[i], n = a.n_id;
-      const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-      double c3 = 0.0;
-#pragma unroll
-      for (int t = a.e3_t - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
-      const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
-      const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-      const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
-      const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
-                   sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
-      const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
-                              -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
-      double ee = 0.0, mag = 0.0;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        ee += t_ee[k];
-        mag += fabs(t_ee[k]);
-      }
-      const double se = sab - be * ca - al * cb + n * al * be;
-      const double pe = ee - se * se / n;
-      const double vlo = a.pf_mu * pe - a.pf_tau * se * se / n - a.pf_eps * ee - 1e-12 * a.pf_mu * (mag + se * se / n);
-      live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
-    }
-  }
-  const unsigned long long bal = __ballot(live);
-  const int lane = threadIdx.x & 63;
-  if ((lane & 31) == 0 && r < a.n_rows) a.flags[idx >> 5] = ((bal >> lane) & 0xFFFFFFFFull) != 0;
-}
-
 // ------------------------------------------------------------------ fused side pass
 // Multi-product int8 GEMMs over a launch's band rows x all columns, 64 x 64 (band row, column)
 // tiles, exact int32 on v_mfma_i32_32x32x32_i8 from double-buffered LDS stages of 64 individuals.
 // Row-side operand sets are read straight from the per-SNP arrays through rows[] (no band
 // gather), column-side sets by column.
-//   PASS 1: products E3_t = L3q_t[i].b_j (t < SIDE_T) and the code products a.b, a^2.b, a.b^2,
-//           a^2.b^2; the epilogue evaluates the spectral prefilter per pair (in registers), sets
-//           flags[r][J] for 32-column blocks that may hold a hit, and writes E3 for those blocks.
-//   PASS 2: products E1_t = L'q_t[i].b_j, Ed_t = Ldq_t[i].b_j^2, E2_t = a_i.R'q_t[j], written only
-//           for flagged blocks (the screen reads nothing else).
+//   PASS 1 (prefilter_pass_kernel below): E3 and the code products, the spectral prefilter in the
+//           epilogue, flags per (band row, 32-column block), E3 (and the code products) of flagged blocks.
+//   PASS 2..4: E1_t = L'q_t[i].b_j, Ed_t = Ldq_t[i].b_j^2, E2_t = a_i.R'q_t[j], written only for
+//           flagged blocks (the MX screen's side terms; the low-rank screen needs none).
 constexpr int SG_T = 64, SG_K = 64, SG_P = 80;  // tile edge, individuals per stage, LDS pitch
 struct SideArgs {
   ScreenArgs a;  // rows, tri, j_lo, ld_e, scalars, prefilter constants, flags, c13 / c2 outputs
@@ -228,251 +183,85 @@ struct SideArgs {
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
-  // PASS 1: E3 = L3q_t x b (t < E3_PF, int8) and the code products a.b, a^2.b, a.b^2, a^2.b^2 on
-  // the block-scaled MFMA in fp4 (codes 0..4 are exact e2m1 values; fp32 sums of integers < 2^24
-  // are exact): E3_PF int8 + 4 fp4 products, the fp4 ones at twice the int8 rate and half the bytes.
-  // PASS 2: E1 (L'q_t x b), PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three int8 products each.
-  constexpr int NR = PASS == 1 ? E3_PF : PASS == 4 ? 1 : 3, NC = PASS == 4 ? 3 : 1;
-  constexpr int NPR = PASS == 1 ? E3_PF : 3;
+  // PASS 2: E1 (L'q_t x b), PASS 3: Ed (Ldq_t x b^2), PASS 4: E2 (a x R'q_t) -- three int8 products
+  // each, written for the blocks the prefilter flagged (the MX quadratic-form screen's side terms)
+  static_assert(PASS >= 2 && PASS <= 4, "PASS 1 is prefilter_pass_kernel");
+  constexpr int NR = PASS == 4 ? 1 : 3, NC = PASS == 4 ? 3 : 1, NPR = 3;
   const ScreenArgs &a = x.a;
-  static_assert(NR <= 7 && NC <= 5, "operand sets");
   // XCD-aware tile order: workgroup b runs on XCD b mod 8; the bijective remap gives each XCD a
-  // contiguous range of tiles, so the n_rt row tiles of a column tile share one L2 (the column
-  // operands, streamed from HBM, are fetched once per XCD instead of once per row tile)
+  // contiguous range of tiles, so the n_rt row tiles of a column tile share one L2
   const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
   const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
   const int rt = tile % x.n_rt, ct = tile / x.n_rt;
   const int r0 = rt * SG_T;
   const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * SG_T;  // 32-aligned: a half-wave = one block
   if (r0 >= a.n_rows || c0 >= a.m) return;
-  {  // tiles entirely on or left of the diagonal hold no pair (AA / DD)
-    if (a.tri && c0 + SG_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
-  }
+  if (a.tri && c0 + SG_T - 1 <= a.rows[r0]) return;  // tiles left of the diagonal hold no pair
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
   // product p: (row set, column set)
-  constexpr int PR[4][3] = {{0, 1, 0}, {0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
-  constexpr int PC[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
+  constexpr int PR[3][3] = {{0, 1, 2}, {0, 1, 2}, {0, 0, 0}};
+  constexpr int PC[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 1, 2}};
   v16i acc[NPR];
-  v16f_ acc4[PASS == 1 ? 4 : 1];  // a.b, a^2.b, a.b^2, a^2.b^2
 #pragma unroll
   for (int p = 0; p < NPR; ++p)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[p][e] = 0;
+  __shared__ __attribute__((aligned(16))) int8_t sR[2][NR][SG_T * SG_P];
+  __shared__ __attribute__((aligned(16))) int8_t sC[2][NC][SG_T * SG_P];
+  // staging: chunk q of an int8 set = (tile row q >> 2, 16-byte piece q & 3); 256 chunks per set
+  const int srow = tid >> 2, spc = (tid & 3) * 16;
+  const int64_t si = a.rows[min(r0 + srow, a.n_rows - 1)];
+  const int64_t sj = min(c0 + srow, a.m - 1);
+  v4i rv[NR], cv[NC];
+  auto load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int p = 0; p < (PASS == 1 ? 4 : 1); ++p)
+    for (int u = 0; u < NR; ++u) rv[u] = *(const v4i *)(x.rs[u] + si * x.n_pad + k0 + spc);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc4[p][e] = 0.f;
-  if constexpr (PASS == 1) {
-    // Three-stage LDS ring filled by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction),
-    // two stages in flight: the pass has little arithmetic per byte, so it needs the loads
-    // further ahead than a register prefetch can hold.  Stage image (20 KB, 64 individuals):
-    // int8 L3 slices 0, 1 (64 rows x 64 B each), int8 b (64 columns x 64 B), fp4 a, a^2 (64 x 32 B
-    // each), fp4 b, b^2; 16-byte chunks XOR-swizzled through the DMA source address (int8: chunk ^
-    // (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1) so the fragment reads are conflict-free.
-    // Wave w issues instructions q = w + 4u (u < 5); the image holds instruction q at q KB.
-    constexpr int ST = 20 * 1024, O_C8 = 8192, O_R4 = 12288, O_C4 = 16384;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[3][ST];
-    const uint8_t *src[5];
-    int stp[5];
+    for (int u = 0; u < NC; ++u) cv[u] = *(const v4i *)(x.cs[u] + sj * x.n_pad + k0 + spc);
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int q = w + 4 * u;
-      if (q < 12) {  // int8: 16 rows x 4 chunks per instruction
-        const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-        const int64_t idx = q < 8 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-        src[u] = (const uint8_t *)(q < 8 ? x.rs[q >> 2] : x.cs[0]) + idx * x.n_pad + 16 * lg;
-        stp[u] = SG_K;
-      } else {  // fp4: 32 rows x 2 chunks per instruction
-        const int qq = q - (q < 16 ? 12 : 16), row = (qq & 1) * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-        const int64_t idx = q < 16 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-        src[u] = (q < 16 ? x.rs4[qq >> 1] : x.cs4[qq >> 1]) + idx * (x.n_pad / 2) + 16 * lg;
-        stp[u] = SG_K / 2;
-      }
+    for (int u = 0; u < NR; ++u) *(v4i *)&sR[b][u][srow * SG_P + spc] = rv[u];
+#pragma unroll
+    for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  int b = 0;
+  for (int k0 = 0; k0 < x.n_pad; k0 += SG_K) {
+    const bool more = k0 + SG_K < x.n_pad;
+    if (more) load(k0 + SG_K);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v4i fr[NR], fc[NC];
+#pragma unroll
+      for (int u = 0; u < NR; ++u) fr[u] = *(const v4i *)&sR[b][u][(32 * wr + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+      for (int u = 0; u < NC; ++u) fc[u] = *(const v4i *)&sC[b][u][(32 * wc + c) * SG_P + 32 * kk + 16 * h];
+#pragma unroll
+      for (int p = 0; p < NPR; ++p)
+        acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[PR[PASS - 2][p]], fc[PC[PASS - 2][p]], acc[p], 0, 0, 0);
     }
-    auto issue = [&](int st, int buf) __attribute__((always_inline)) {
-      typedef __attribute__((address_space(3))) void *lds_t;
-#pragma unroll
-      for (int u = 0; u < 5; ++u)
-        __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[buf][(w + 4 * u) * 1024], 16, 0, 0);
-    };
-    const int S = (int)(x.n_pad / SG_K);
-    issue(0, 0);
-    if (S > 1) {
-      issue(1, 1);
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    for (int st = 0; st < S; ++st) {
-      const uint8_t *bf = ring[st % 3];
-      if (st + 2 < S) issue(st + 2, (st + 2) % 3);
-      const int rrow = 32 * wr + c, crow = 32 * wc + c;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int lr = (2 * kk + h) ^ ((rrow >> 2) & 3), lc = (2 * kk + h) ^ ((crow >> 2) & 3);
-        const v4i f0 = *(const v4i *)&bf[rrow * 64 + 16 * lr], f1 = *(const v4i *)&bf[4096 + rrow * 64 + 16 * lr];
-        const v4i fc = *(const v4i *)&bf[O_C8 + crow * 64 + 16 * lc];
-        acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[1], 0, 0, 0);
-      }
-      {  // one 64-deep fp4 MFMA per code product
-        const int lr = h ^ ((rrow >> 3) & 1), lc = h ^ ((crow >> 3) & 1);
-        v8i_ fa[2], fb[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const v4i ra4 = *(const v4i *)&bf[O_R4 + u * 2048 + rrow * 32 + 16 * lr];
-          const v4i rb4 = *(const v4i *)&bf[O_C4 + u * 2048 + crow * 32 + 16 * lc];
-          fa[u] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
-          fb[u] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-          acc4[p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[p], 4, 4, 0, 127, 0, 127);
-      }
-      // this wave's reads of buffer st % 3 are done and stage st + 1 has landed (only stage
-      // st + 2's five instructions may still be in flight); then the workgroup barrier
-      if (st + 2 < S)
-        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-    __shared__ __attribute__((aligned(16))) int8_t sR[2][NR][SG_T * SG_P];
-    __shared__ __attribute__((aligned(16))) int8_t sC[2][NC][SG_T * SG_P];
-    // staging: chunk q of an int8 set = (tile row q >> 2, 16-byte piece q & 3); 256 chunks per set
-    const int srow = tid >> 2, spc = (tid & 3) * 16;
-    const int rr = min(r0 + srow, a.n_rows - 1);
-    const int64_t si = a.rows[rr];
-    const int64_t sj = min(c0 + srow, a.m - 1);
-    v4i rv[NR], cv[NC];
-    auto load = [&](int k0) __attribute__((always_inline)) {
-#pragma unroll
-      for (int u = 0; u < NR; ++u) rv[u] = *(const v4i *)(x.rs[u] + si * x.n_pad + k0 + spc);
-#pragma unroll
-      for (int u = 0; u < NC; ++u) cv[u] = *(const v4i *)(x.cs[u] + sj * x.n_pad + k0 + spc);
-    };
-    auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-      for (int u = 0; u < NR; ++u) *(v4i *)&sR[b][u][srow * SG_P + spc] = rv[u];
-#pragma unroll
-      for (int u = 0; u < NC; ++u) *(v4i *)&sC[b][u][srow * SG_P + spc] = cv[u];
-    };
-    load(0);
-    store(0);
+    if (more) store(b ^ 1);
     __syncthreads();
-    int b = 0;
-    for (int k0 = 0; k0 < x.n_pad; k0 += SG_K) {
-      const bool more = k0 + SG_K < x.n_pad;
-      if (more) load(k0 + SG_K);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        v4i fr[NR], fc[NC];
-#pragma unroll
-        for (int u = 0; u < NR; ++u) fr[u] = *(const v4i *)&sR[b][u][(32 * wr + c) * SG_P + 32 * kk + 16 * h];
-#pragma unroll
-        for (int u = 0; u < NC; ++u) fc[u] = *(const v4i *)&sC[b][u][(32 * wc + c) * SG_P + 32 * kk + 16 * h];
-#pragma unroll
-        for (int p = 0; p < NPR; ++p)
-          acc[p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fr[PR[PASS - 1][p]], fc[PC[PASS - 1][p]], acc[p], 0, 0, 0);
-      }
-      if (more) store(b ^ 1);
-      __syncthreads();
-      b ^= 1;
-    }
+    b ^= 1;
   }
-  // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 32 wc + c; the 32
-  // columns of a block are the 32 lanes of one half-wave.  Pass 1 reads its per-row scalars from
-  // LDS (staged once per tile; a global load per element would expose its latency 16 times) and
-  // its per-column ones from registers.
+  // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 32 wc + c
   const int64_t j = c0 + 32 * wc + c;
   const int J = (int)(j / 32);
   const bool jok = j < a.m && j >= a.j_lo;
-  // per-row: i (as double; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
-  __shared__ double rowv[PASS == 1 ? 7 : 1][SG_T];
-  // per-column (registers): beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum,
-  // beta spy - sb, sum_k (b + beta)^2
-  double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
-  bool cmono = true;
-  if constexpr (PASS == 1) {
-    const double n = a.n_id;
-    if (tid < SG_T) {
-      const int r = min(r0 + tid, a.n_rows - 1);
-      const int64_t i = a.rows[r];
-      const double al = a.alpha[i], ca = a.csum_l[i];
-      rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
-      rowv[1][tid] = al;
-      rowv[2][tid] = ca;
-      rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
-      rowv[4][tid] = a.sL3[i];
-      rowv[5][tid] = a.sa[i];
-      rowv[6][tid] = (2.0 + al) * (2.0 + al);
-    }
-    if (jok) {
-      cbe = a.beta[j];
-      ccb = a.csum_r[j];
-      const double cb2 = a.csq_r[j];
-      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
-      cnb = n * cbe - ccb;
-      cbsb = cbe * a.spy - a.sb[j];
-      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
-      cmono = a.mono_r[j];
-    }
-    __syncthreads();
-  }
-  // vlo = (mu - eps)|e|^2 - (mu + tau)(1'e)^2/n - 1e-12 mu (|expansion terms| + (1'e)^2/n), the
-  // absolute terms bounded by sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2
-  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id, k2 = 1e-12 * a.pf_mu;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
-    const bool rok = r < a.n_rows;
-    const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
-    if (PASS == 1) {
-      bool live = false;
-      const double iv = rowv[0][rl];
-      if (rok && jok && iv >= 0.0 && !cmono) {
-        const int64_t i = (int64_t)iv;
-        if (!(a.tri && j <= i)) {
-          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
-          double c3 = 0.0;
+    const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (r >= a.n_rows || !jok || !a.flags[(int64_t)r * a.nJ + J]) continue;
+    const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
-          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
-          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
-          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
-          const double sab = (double)acc4[0][e], sa2b = (double)acc4[1][e], sab2 = (double)acc4[2][e],
-                       sa2b2 = (double)acc4[3][e];
-          // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
-          const double ee = sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
-          const double se = sab - be * rowv[2][rl] + al * cnb;
-          const double vlo = mu_e * ee - k1 * se * se - k2 * rowv[6][rl] * cmag;
-          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
-        }
-      }
-      const unsigned long long bal = __ballot(live);
-      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
-      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
-      if (blk && rok && jok) {
-        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-#pragma unroll
-        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
-        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ((int *)a.pfc)[q * a.pfc_stride + o1] = (int)acc4[q][e];
-      }
-    } else {
-      if (rok && jok && a.flags[(int64_t)r * a.nJ + J]) {
-        const int64_t od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
-#pragma unroll
-        for (int t = 0; t < SIDE_T; ++t) {
-          if (PASS == 2) ((int *)a.c13)[t * a.c13_stride + o1] = acc[t][e];
-          if (PASS == 3) ((int *)a.c13)[t * a.c13_stride + od] = acc[t][e];
-          if (PASS == 4) ((int *)a.c2)[t * a.c2_stride + o1] = acc[t][e];
-        }
-      }
+    for (int t = 0; t < SIDE_T; ++t) {
+      if (PASS == 2) ((int *)a.c13)[t * a.c13_stride + o1] = acc[t][e];
+      if (PASS == 3) ((int *)a.c13)[t * a.c13_stride + od] = acc[t][e];
+      if (PASS == 4) ((int *)a.c2)[t * a.c2_stride + o1] = acc[t][e];
     }
-    if (PASS == 1) __builtin_amdgcn_sched_barrier(0);  // one element's prefilter at a time
   }
 }
 
@@ -2977,17 +2766,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       if (full)
         GMAT_TRY(i8gemm_nt(S2, SIDE_T, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad, 0,
                            R.Rq.as<int8_t>() + jg * n_pad, n_pad, ss, e2[b].as<int>() + (int64_t)g0 * m + coff, m, z2));
-      if (use_pf) {  // exact code products [Sab; Sa2b] (x b) and [Sab2; Sa2b2] (x b^2)
-        for (int bq = 0; bq < 2; ++bq)
-          GMAT_TRY(i8gemm_nt(S2, 2, gn, (int)nc, (int)n_pad, ba[b].as<int8_t>() + (int64_t)g0 * n_pad, n_pad,
-                             (int64_t)Rn * n_pad, (bq ? srq : srp) + jg * n_pad, n_pad, 0,
-                             pfc[b].as<int>() + (int64_t)(2 * bq) * Rn * m + (int64_t)g0 * m + coff, m, (int64_t)Rn * m));
-      }
-    }
-    if (use_pf) {
-      const ScreenArgs pa = make_args(li, b);
-      hipLaunchKernelGGL(prefilter_kernel, dim3((unsigned)cdiv((int64_t)Rn * nJ * 32, 256)), dim3(256), 0, S2, pa);
-      GMAT_HIP(hipGetLastError());
     }
     GMAT_HIP(hipEventRecord(side_end[b], S2));
     return GMAT_OK;
