@@ -1,18 +1,21 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, kernel-trace only) on the bench scan; raw
-# output stays in /tmp on the box, only the rows of kernels matching $KEY come back.
+# output goes to gpurun_out/TAG/raw while a pass runs (visible progress) and is deleted after the rows
+# of kernels matching $KEY are kept.  PASSES="3 4 5" runs only those passes.
 TAG=${1:-pmc}
 KEY=${KEY:-screen}
 OUT=gpurun_out/$TAG
-RAW=/tmp/pmc_raw_$TAG
+RAW=gpurun_out/$TAG/raw  # inside gpurun_out so a long pass shows progress; deleted after filtering
 mkdir -p $OUT $RAW
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 ARGS="bench.py --n-snp ${NSNP:-10000} --steps 1 --warmup 0 --no-cpu --no-grm --no-eff"
 i=0
+PASSES=${PASSES:-all}
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM" \
            "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
+  if [ "$PASSES" != "all" ] && ! echo " $PASSES " | grep -q " $i "; then continue; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $RAW/p$i -o run -- python3 $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   mkdir -p $OUT/p$i
   for f in run_counter_collection.csv run_kernel_trace.csv; do
@@ -21,4 +24,5 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   done
   rm -rf $RAW/p$i
 done
+rm -rf $RAW
 echo done
