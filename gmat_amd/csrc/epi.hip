@@ -962,12 +962,15 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
 // Workgroup / wave layout, tile list, staging and LDS images as mx_screen_kernel (MxShape<1>);
 // the loop is chunk ch (128 eigen-directions) -> stage cs (128 individuals), every stage a full
 // K-sweep step (no symmetry), with the chunk's epilogue after its last stage.
+// SK tile images (128 individuals each) per LDS stage and barrier (SK = 2: 256-deep stages, half
+// the barriers, 144 KB of LDS)
+template <int SK>
 __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
   constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
-  constexpr int NJC = 2 * 8 * BJ;
-  __shared__ __attribute__((aligned(16))) uint8_t sA[2][MX_TILE];
-  __shared__ __attribute__((aligned(16))) uint8_t sI[2][MX_BI * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][2 * BJ * NB_REC];
+  constexpr int NJC = 2 * 8 * BJ, SI = MX_BI * NB_REC, SJ = 2 * BJ * NB_REC;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[2][SK * MX_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[2][SK * SI];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][SK * SJ];
   __shared__ __attribute__((aligned(16))) uint8_t sE[40 * 1024];  // chunk epilogue operands (LDS-DMA)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int tl = a.tiles[MX_TE * blockIdx.x];
@@ -1004,19 +1007,27 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   // the A tile image is a straight copy: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
   // instruction) into buffer nb, no registers or ds_write; the genotype records go through
   // registers (the j side is swizzled per lane)
-  v4i rnj, rni;
-  auto load = [&](int nb, int ch, int cs) __attribute__((always_inline)) {
+  v4i rnj[SK], rni[SK];
+  auto load = [&](int nb, int ch, int cs2) __attribute__((always_inline)) {
     typedef __attribute__((address_space(3))) void *lds_t;
-    const uint8_t *src = x.tiles + (int64_t)(ch * nK + cs) * MX_TILE;
 #pragma unroll
-    for (int u = 0; u < NA; ++u)
-      __builtin_amdgcn_global_load_lds(src + (tid + u * MX_T) * 16, (lds_t)&sA[nb][(w * 64 + u * MX_T) * 16], 16, 0, 0);
-    rnj = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
-    rni = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
+    for (int s = 0; s < SK; ++s) {
+      const int cs = cs2 * SK + s;
+      const uint8_t *src = x.tiles + (int64_t)(ch * nK + cs) * MX_TILE;
+#pragma unroll
+      for (int u = 0; u < NA; ++u)
+        __builtin_amdgcn_global_load_lds(src + (tid + u * MX_T) * 16, (lds_t)&sA[nb][s * MX_TILE + (w * 64 + u * MX_T) * 16],
+                                         16, 0, 0);
+      rnj[s] = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
+      rni[s] = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
+    }
   };
   auto store = [&](int b) __attribute__((always_inline)) {
-    *(v4i *)&sJ[b][(jh * BJ + js) * NB_REC + jq * 16] = rnj;
-    *(v4i *)&sI[b][is * NB_REC + jq * 16] = rni;
+#pragma unroll
+    for (int s = 0; s < SK; ++s) {
+      *(v4i *)&sJ[b][s * SJ + (jh * BJ + js) * NB_REC + jq * 16] = rnj[s];
+      *(v4i *)&sI[b][s * SI + is * NB_REC + jq * 16] = rni[s];
+    }
   };
 
   v16f_ acc[RB][PB];
@@ -1026,29 +1037,31 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   auto compute = [&](int b, bool first) __attribute__((always_inline)) {
     const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const v4i j1 = *(const v4i *)&sJ[b][jrow + 16 * ((2 * kk + h) ^ jf)];
-      const v4i j2 = j1 << 1;
-      v8i_ fb[PB];
+    for (int s = 0; s < SK; ++s)
 #pragma unroll
-      for (int t = 0; t < PB; ++t) {
-        const v4i i1 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
-        const v4i i2 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+      for (int kk = 0; kk < 2; ++kk) {
+        const v4i j1 = *(const v4i *)&sJ[b][s * SJ + jrow + 16 * ((2 * kk + h) ^ jf)];
+        const v4i j2 = j1 << 1;
+        v8i_ fb[PB];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
+        for (int t = 0; t < PB; ++t) {
+          const v4i i1 = *(const v4i *)&sI[b][s * SI + (PB * w + t) * NB_REC + 32 * kk + 16 * h];
+          const v4i i2 = *(const v4i *)&sI[b][s * SI + (PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
 #pragma unroll
-        for (int q = 4; q < 8; ++q) fb[t][q] = 0;
+          for (int q = 0; q < 4; ++q) fb[t][q] = (i1[q] & j1[q]) | (i2[q] & j2[q]);
+#pragma unroll
+          for (int q = 4; q < 8; ++q) fb[t][q] = 0;
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const uint8_t *ar = &sA[b][s * MX_TILE + (2 * kk + h) * 4096 + (32 * r + c) * 32];
+          const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+          const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int t = 0; t < PB; ++t)  // x2 (scale 128): the fp4 codes hold w/2
+            acc[r][t] = mfma_mx(fa, fb[t], (first && s == 0 && kk == 0) ? z : acc[r][t], hi[2], 128);
+        }
       }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
-        const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
-        const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int t = 0; t < PB; ++t)
-          acc[r][t] = mfma_mx(fa, fb[t], (first && kk == 0) ? z : acc[r][t], hi[2], 128);  // x2: codes hold w/2
-      }
-    }
   };
   // Chunk epilogue operands staged in LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
   // instruction q, written linearly at sE + q KB): q 0..7 = G' rows of the 16 slots (512 B each),
@@ -1124,16 +1137,17 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   __syncthreads();
   stamp(1);
   int b = 0;
+  const int nS = nK / SK;  // stages per chunk
   for (int ch = 0; ch < nC; ++ch) {
     const bool lastch = ch + 1 == nC;
     if (ch > 0) __syncthreads();  // every wave is past the previous chunk's epilogue reads of sE
     fetch_epi(ch);                // lands during this chunk's stages
-    if (nK > 1) iter(b, true, ch, 1);
+    if (nS > 1) iter(b, true, ch, 1);
     else iter(b, true, lastch ? ch : ch + 1, 0);
     b ^= 1;
 #pragma unroll 1
-    for (int cs = 1; cs < nK; ++cs) {
-      const bool lastc = cs + 1 == nK;
+    for (int cs = 1; cs < nS; ++cs) {
+      const bool lastc = cs + 1 == nS;
       iter(b, false, lastc ? (lastch ? ch : ch + 1) : ch, lastc ? 0 : cs + 1);
       b ^= 1;
     }
@@ -3016,6 +3030,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   auto &pin_cnt = e->pins.cnt;
   GMAT_TRY(pin_cnt[0].reserve(8));
   GMAT_TRY(pin_cnt[1].reserve(8));
+  // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
+  const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
+  auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, const LrArgs &lx_) {
+    if (lr_sk == 2)
+      hipLaunchKernelGGL(lr_screen_kernel<2>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    else
+      hipLaunchKernelGGL(lr_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+  };
   auto lr_args = [&](size_t li) {
     LrArgs lx;
     lx.tiles = e->lr_tiles.as<uint8_t>();
@@ -3045,7 +3067,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
     GMAT_HIP(hipEventRecord(evs7[b], sm));
     if (!mxT[b].empty())
-      hipLaunchKernelGGL(lr_screen_kernel, dim3((unsigned)(mxT[b].size() / MX_TE)), dim3(MxShape<1>::T), 0, sm, sa, lx);
+      launch_lr_kernel((unsigned)(mxT[b].size() / MX_TE), sa, lx);
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipEventRecord(evs2[b], sm));
     GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
@@ -3098,7 +3120,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
           s1.cand_i = e->cand1_i.as<int64_t>();
           s1.cand_j = e->cand1_j.as<int64_t>();
         }
-        hipLaunchKernelGGL(lr_screen_kernel, dim3(g), dim3(MxShape<1>::T), 0, sm, s1, lx);
+        launch_lr_kernel(g, s1, lx);
       } else if (S == 0 && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
         hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, mx);
