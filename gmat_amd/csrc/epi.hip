@@ -177,7 +177,7 @@ struct SideArgs {
   ScreenArgs a;  // rows, tri, j_lo, ld_e, scalars, prefilter constants, flags, c13 / c2 outputs
   const int8_t *rs[7];  // row-side sets [m][n_pad] (slices: stride slice_stride)
   const int8_t *cs[5];  // column-side sets
-  const uint8_t *rs4[2], *cs4[2];  // pass 1: fp4 code panels (a, a^2 | b, b^2) [m][n_pad / 2]
+  const uint8_t *rs4, *cs4;  // prefilter: fp4 code panels (a | b) [m][n_pad / 2]
   int64_t n_pad;
   int n_rt;             // row tiles
 };
@@ -269,12 +269,19 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
 // The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 128 x 128
 // (band row, column) tiles, 8 waves of 32 x 64: the pass streams its operands at ~20 bytes per
 // 64 x 64 x 64 MFMA block, so it is bound by each CU's load rate; a 128-wide tile halves the bytes
-// per pair.  Stage image (40 KB, 64 individuals), three-stage LDS-DMA ring (120 KB), two stages in
-// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), int8 b (128 columns x 64 B), fp4 a, a^2
-// (128 x 32 B each), fp4 b, b^2.  16-byte chunks XOR-swizzled through the DMA source address (int8:
-// chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA instruction q (1 KB) at
-// q KB, wave w issuing q = w + 8u (u < 5).
-constexpr int PF_T = 128, PF_ST = 40 * 1024;
+// per pair.  Stage image (32 KB, 64 individuals), four-slot LDS-DMA ring (128 KB), three stages in
+// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), int8 b (128 columns x 64 B), fp4 a (128 x
+// 32 B), fp4 b.  The squares' fp4 codes come from the codes in registers (sq4).  16-byte chunks
+// XOR-swizzled through the DMA source address (int8: chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3)
+// & 1); the image holds DMA instruction q (1 KB) at q KB, wave w issuing q = w + 8u (u < 4).
+constexpr int PF_T = 128, PF_ST = 32 * 1024, PF_NS = 4, PF_Q = 4;
+// fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
+__device__ __forceinline__ v8i_ sq4(v4i x) {
+  v8i_ r = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = x[q] | ((x[q] >> 1) & 0x22222222);
+  return r;
+}
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const ScreenArgs &a = x.a;
   const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
@@ -286,30 +293,41 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   if (a.tri && c0 + PF_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
   // 8 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
-  constexpr int O_R8 = 0, O_C8 = 16384, O_R4 = 24576, O_C4 = 32768;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[3][PF_ST];
-  const uint8_t *src[5];
-  int stp[5];
+  constexpr int O_R8 = 0, O_C8 = 16384, O_R4 = 24576, O_C4 = 28672;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
+  const uint8_t *src[PF_Q];
+  int stp[PF_Q];
 #pragma unroll
-  for (int u = 0; u < 5; ++u) {
+  for (int u = 0; u < PF_Q; ++u) {
     const int q = w + 8 * u;
     if (q < 24) {  // int8: 16 rows x 4 chunks per instruction
       const int row = (q & 7) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
       const int64_t idx = q < 16 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
       src[u] = (const uint8_t *)(q < 16 ? x.rs[q >> 3] : x.cs[0]) + idx * x.n_pad + 16 * lg;
       stp[u] = SG_K;
-    } else {  // fp4: 32 rows x 2 chunks per instruction
-      const int qq = q - (q < 32 ? 24 : 32), row = (qq & 3) * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-      const int64_t idx = q < 32 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (q < 32 ? x.rs4[qq >> 2] : x.cs4[qq >> 2]) + idx * (x.n_pad / 2) + 16 * lg;
+    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 24..27 rows, 28..31 columns)
+      const int qq = q & 3, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
+      const int64_t idx = q < 28 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+      src[u] = (q < 28 ? x.rs4 : x.cs4) + idx * (x.n_pad / 2) + 16 * lg;
       stp[u] = SG_K / 2;
     }
   }
-  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+  auto issue = [&](int st) __attribute__((always_inline)) {
     typedef __attribute__((address_space(3))) void *lds_t;
 #pragma unroll
-    for (int u = 0; u < 5; ++u)
-      __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[buf][(w + 8 * u) * 1024], 16, 0, 0);
+    for (int u = 0; u < PF_Q; ++u)
+      __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[st % PF_NS][(w + 8 * u) * 1024],
+                                       16, 0, 0);
+  };
+  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q DMAs per stage)
+  auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
+    const int ahead = last - st;
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
   v16i acc[2][E3_PF];
   v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
@@ -325,18 +343,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       for (int e = 0; e < 16; ++e) acc4[q][p][e] = 0.f;
   }
   const int S = (int)(x.n_pad / SG_K);
-  issue(0, 0);
-  if (S > 1) {
-    issue(1, 1);
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  const int pre = min(S, PF_NS - 1);
+  for (int st = 0; st < pre; ++st) issue(st);
+  wait_for(0, pre - 1);
   __builtin_amdgcn_s_barrier();
   const int rrow = 32 * wr + c;
   for (int st = 0; st < S; ++st) {
-    const uint8_t *bf = ring[st % 3];
-    if (st + 2 < S) issue(st + 2, (st + 2) % 3);
+    const uint8_t *bf = ring[st % PF_NS];
+    // slot (st + 3) % 4 was read in stage st - 1, which every wave has left (barrier)
+    if (st + PF_NS - 1 < S) issue(st + PF_NS - 1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int lr = (2 * kk + h) ^ ((rrow >> 2) & 3);
@@ -353,29 +368,24 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     {
       const int lr = h ^ ((rrow >> 3) & 1);
       v8i_ fa[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const v4i ra4 = *(const v4i *)&bf[O_R4 + u * 4096 + rrow * 32 + 16 * lr];
-        fa[u] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+      {
+        const v4i ra4 = *(const v4i *)&bf[O_R4 + rrow * 32 + 16 * lr];
+        fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+        fa[1] = sq4(ra4);
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
         v8i_ fb[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const v4i rb4 = *(const v4i *)&bf[O_C4 + u * 4096 + crow * 32 + 16 * lc];
-          fb[u] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
-        }
+        const v4i rb4 = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
+        fb[0] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
+        fb[1] = sq4(rb4);
 #pragma unroll
         for (int p = 0; p < 4; ++p)
           acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
       }
     }
-    if (st + 2 < S)
-      asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    wait_for(st + 1, min(st + PF_NS - 1, S - 1));
     __builtin_amdgcn_s_barrier();
   }
   // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
@@ -1239,8 +1249,11 @@ __global__ __launch_bounds__(512) void slot_side_kernel(ScreenArgs a, SlotSideAr
 // the MALL/HBM, so more pairs per workgroup = less traffic); for every RM-row block of P the f64
 // MFMA tile C = P[rows, k >= rows] E (off-diagonal blocks x2, exact) is formed in RK-deep stages
 // (the next stage's P rows and code bytes fetched into registers while this one multiplies) and
-// folded into var.  Waves: 2 (rows) x 2 (64-pair halves), each 32 x 64 of 16x16x4 f64 MFMA tiles.
-constexpr int RP = 128, RM = 128, RK = 32, RT = 512;
+// folded into var.  Waves: 4 (rows) x 2 (64-pair halves), each 32 x 64 of 16x16x4 f64 MFMA tiles.
+// The (row block, column stage) sequence of a pair tile splits into gridDim.y segments of equal
+// work (blockIdx.y = segment) so that a short candidate list still fills whole rounds of the
+// chip; segment partials of var / eff go to var_part / eff_part and refine_sum adds them in order.
+constexpr int RP = 128, RM = 128, RK = 32, RT = 512, RF_SEG = 4;
 
 __device__ __forceinline__ double ecode(const int8_t *l, const int8_t *r, double al, double be, int64_t q) {
   const double x = (double)l[q] - al;
@@ -1254,7 +1267,7 @@ __global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const doub
                                                        const double *__restrict__ py, const int8_t *left,
                                                        const int8_t *right, const double *alpha, const double *beta,
                                                        const int64_t *pi, const int64_t *pj, int64_t np, double *eff,
-                                                       double *var) {
+                                                       double *var, double *eff_part, double *var_part) {
   __shared__ double As[RK][RM + 1];
   __shared__ double Bs[RK][RP + 1];
   __shared__ double red[4][RP];
@@ -1280,17 +1293,27 @@ __global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const doub
     rl = *(const v2i__ *)(gl + k0 + gk);
     rr = *(const v2i__ *)(gr + k0 + gk);
   };
-  int64_t rb = 0, k0 = 0;
-  fetch(0, 0);
-  while (rb < n_pad) {
+  // this segment's stages [tb, te) of the sequence (rb = 0, RM, ..; k0 = rb, rb + RK, .. < n_pad)
+  int64_t T = 0;
+  for (int64_t b = 0; b < n_pad; b += RM) T += (n_pad - b) / RK;
+  const int seg = blockIdx.y, nseg = gridDim.y;
+  const int64_t tb = T * seg / nseg, te = T * (seg + 1) / nseg;
+  int64_t rb = 0, t = 0;
+  while (t + (n_pad - rb) / RK <= tb) {
+    t += (n_pad - rb) / RK;
+    rb += RM;
+  }
+  int64_t k0 = rb + (tb - t) * RK, nleft = te - tb;
+  if (nleft > 0) fetch(rb, k0);
+  while (nleft > 0) {
     v4d acc[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = v4d{0, 0, 0, 0};
     // symmetric P: only column blocks k0 >= rb, the off-diagonal ones counted twice (x2 is
-    // exact); the rb == 0 pass covers every k and also accumulates the eff partials
-    for (; k0 < n_pad; k0 += RK) {
+    // exact); the rb == 0 stages cover every k and also accumulate the eff partials
+    for (; k0 < n_pad && nleft > 0; k0 += RK, --nleft) {
       const double f = k0 >= rb + RM ? 2.0 : 1.0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1313,7 +1336,7 @@ __global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const doub
           nrb = rb + RM;
           nk = nrb;
         }
-        if (nrb < n_pad) fetch(nrb, nk);
+        if (nleft > 1 && nrb < n_pad) fetch(nrb, nk);
       }
 #pragma unroll
       for (int ks = 0; ks < RK / 4; ++ks) {
@@ -1344,8 +1367,10 @@ __global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const doub
           vpart[jt] += ecode(l, r, al, be, row) * acc[it][jt][e];
         }
     }
-    rb += RM;
-    k0 = rb;
+    if (k0 >= n_pad) {
+      rb += RM;
+      k0 = rb;
+    }
   }
   // reduce var partials: lanes with equal (lane & 15) in a wave, then the four wm waves
 #pragma unroll
@@ -1364,10 +1389,31 @@ __global__ __launch_bounds__(RT, 2) void refine_kernel(int64_t n_pad, const doub
     const int col = tid;
     const int64_t p = p0 + col;
     if (p < np) {
-      var[p] = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
-      eff[p] = (effr[0][col] + effr[1][col]) + (effr[2][col] + effr[3][col]);
+      const double v = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+      const double f = (effr[0][col] + effr[1][col]) + (effr[2][col] + effr[3][col]);
+      if (nseg == 1) {
+        var[p] = v;
+        eff[p] = f;
+      } else {
+        var_part[seg * np + p] = v;
+        eff_part[seg * np + p] = f;
+      }
     }
   }
+}
+
+// var / eff = the segments' partials added in segment order (deterministic)
+__global__ void refine_sum_kernel(int64_t np, int nseg, const double *eff_part, const double *var_part, double *eff,
+                                  double *var) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  double v = 0.0, f = 0.0;
+  for (int s = 0; s < nseg; ++s) {
+    v += var_part[s * np + t];
+    f += eff_part[s * np + t];
+  }
+  var[t] = v;
+  eff[t] = f;
 }
 
 // p-values and hit compaction: chi = eff^2/var, p = chi2.sf(chi, 1) = erfc(sqrt(chi/2))
@@ -1744,16 +1790,14 @@ __global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double ta
   A[idx] = P[idx] + (mu + tau) / (double)n - (r == c ? mu : 0.0);
 }
 
-// fp4 e2m1 copies of a screen panel (codes 0, 1, 2 -> 0x0, 0x2, 0x4) and of its squares (0, 1, 4 ->
-// 0x0, 0x2, 0x6); individual 2q at the low nibble of byte q (the MFMA's packing)
-__global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4, uint8_t *p4sq) {
+// fp4 e2m1 copy of a screen panel (codes 0, 1, 2 -> 0x0, 0x2, 0x4; the prefilter derives the
+// squares' codes in registers, sq4); individual 2q at the low nibble of byte q (the MFMA's packing)
+__global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= m * (n_pad / 2)) return;
   const int v0 = panel[2 * idx], v1 = panel[2 * idx + 1];
   auto code = [](int v) { return v == 0 ? 0 : v == 1 ? 2 : 4; };
-  auto csq = [](int v) { return v == 0 ? 0 : v == 1 ? 2 : 6; };
   p4[idx] = (uint8_t)(code(v0) | (code(v1) << 4));
-  p4sq[idx] = (uint8_t)(csq(v0) | (csq(v1) << 4));
 }
 
 // A = P + C + (lam + tau) 11'/n - lam I (natural order) for the low-rank screen's certificate
@@ -1792,7 +1836,7 @@ struct Coding {
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
-  DBuf p4, p4sq;                  // screen codes and their squares as fp4 e2m1 [m][n_pad / 2] (prefilter)
+  DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
 };
@@ -1836,6 +1880,7 @@ struct gmat_epi {
   double lr_E = 0;                  // sum_r eta_r^2 (the screen's fp32 error budget)
   DBuf lr_tiles, lr_Bs, lr_q1;      // Q' tile images; Q fp64 [n_pad][lr_R] storage order; Q'1 (fp64)
   int nK = 0;                       // 128-individual stages
+  DBuf rf_part;                     // refine segment partials [2][nseg][np]
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
   DBuf spanels;  // screen codes, one allocation: [0] minor-allele dosage, [1] heterozygote [m][n_pad]
@@ -1949,9 +1994,8 @@ int build_coding(gmat_epi *e, int which) {
                      cd.Rq.as<int8_t>(), cd.sR.as<double>());
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.p4.alloc((size_t)m * n_pad / 2));
-  GMAT_TRY(cd.p4sq.alloc((size_t)m * n_pad / 2));
   hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
-                     cd.p4.as<uint8_t>(), cd.p4sq.as<uint8_t>());
+                     cd.p4.as<uint8_t>());
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.nibI.alloc((size_t)m * n_pad));
   GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
@@ -1983,9 +2027,22 @@ int build_coding(gmat_epi *e, int which) {
 int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp,
            const int64_t *pi, const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
   if (np <= 0) return GMAT_OK;
-  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)cdiv(np, RP)), dim3(RT), 0, st, e->n_pad, e->Ps.as<double>(),
-                     e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var);
+  // a fixed number of segments per pair tile (not one chosen from np: a pair's numbers must not
+  // depend on the length of the list it came in, scan vs pairs); 4 segments fill >= 90 % of the
+  // last round of resident workgroups (two per CU) from about 1,000 tiles up
+  const int64_t tiles = cdiv(np, RP);
+  const int nseg = RF_SEG;
+  if (nseg > 1) GMAT_TRY(e->rf_part.alloc((size_t)2 * nseg * np * sizeof(double)));
+  double *epart = nseg > 1 ? e->rf_part.as<double>() : nullptr, *vpart = nseg > 1 ? epart + nseg * np : nullptr;
+  hipLaunchKernelGGL(refine_kernel, dim3((unsigned)tiles, (unsigned)nseg), dim3(RT), 0, st, e->n_pad, e->Ps.as<double>(),
+                     e->py.as<double>(), lp, rp, L.off.as<double>(), R.off.as<double>(), pi, pj, np, eff, var, epart,
+                     vpart);
   GMAT_HIP(hipGetLastError());
+  if (nseg > 1) {
+    hipLaunchKernelGGL(refine_sum_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, nseg, epart, vpart, eff,
+                       var);
+    GMAT_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
   GMAT_HIP(hipGetLastError());
   return GMAT_OK;
@@ -2716,10 +2773,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const unsigned grid = (unsigned)(x.n_rt * cdiv(ncols, SG_T));
       for (int t = 0; t < E3_PF; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
       x.cs[0] = srp;
-      x.rs4[0] = L.p4.as<uint8_t>();
-      x.rs4[1] = L.p4sq.as<uint8_t>();
-      x.cs4[0] = R.p4.as<uint8_t>();
-      x.cs4[1] = R.p4sq.as<uint8_t>();
+      x.rs4 = L.p4.as<uint8_t>();
+      x.cs4 = R.p4.as<uint8_t>();
       {  // prefilter pass: 128 x 128 tiles
         SideArgs xp = x;
         xp.n_rt = (int)cdiv(Rn, PF_T);
