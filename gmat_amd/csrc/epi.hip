@@ -269,17 +269,29 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
 // The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 128 x 128
 // (band row, column) tiles, 8 waves of 32 x 64: the pass streams its operands at ~20 bytes per
 // 64 x 64 x 64 MFMA block, so it is bound by each CU's load rate; a 128-wide tile halves the bytes
-// per pair.  Stage image (32 KB, 64 individuals), four-slot LDS-DMA ring (128 KB), three stages in
-// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), int8 b (128 columns x 64 B), fp4 a (128 x
-// 32 B), fp4 b.  The squares' fp4 codes come from the codes in registers (sq4).  16-byte chunks
-// XOR-swizzled through the DMA source address (int8: chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3)
-// & 1); the image holds DMA instruction q (1 KB) at q KB, wave w issuing q = w + 8u (u < 4).
-constexpr int PF_T = 128, PF_ST = 32 * 1024, PF_NS = 4, PF_Q = 4;
+// per pair.  Stage image (24 KB, 64 individuals), five-slot LDS-DMA ring (120 KB), four stages in
+// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), fp4 codes a (128 rows x 32 B) and b (128
+// columns x 32 B).  The squares' fp4 codes (sq4) and the int8 b of the E3 products (i8_of_fp4) come
+// from the codes in registers.  16-byte chunks XOR-swizzled through the DMA source address (int8:
+// chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA instruction q (1 KB) at
+// q KB, wave w issuing q = w + 8u (u < 3).
+constexpr int PF_T = 128, PF_ST = 24 * 1024, PF_NS = 5, PF_Q = 3;
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
   v8i_ r = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int q = 0; q < 4; ++q) r[q] = x[q] | ((x[q] >> 1) & 0x22222222);
+  return r;
+}
+// int8 values of 16 fp4 codes (two dwords, individual i at nibble i): code >> 1, in order
+__device__ __forceinline__ v4i i8_of_fp4(unsigned x0, unsigned x1) {
+  const unsigned l0 = (x0 >> 1) & 0x07070707u, h0 = (x0 >> 5) & 0x07070707u;
+  const unsigned l1 = (x1 >> 1) & 0x07070707u, h1 = (x1 >> 5) & 0x07070707u;
+  v4i r;
+  r[0] = (int)__builtin_amdgcn_perm(h0, l0, 0x05010400u);
+  r[1] = (int)__builtin_amdgcn_perm(h0, l0, 0x07030602u);
+  r[2] = (int)__builtin_amdgcn_perm(h1, l1, 0x05010400u);
+  r[3] = (int)__builtin_amdgcn_perm(h1, l1, 0x07030602u);
   return r;
 }
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
@@ -293,22 +305,21 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   if (a.tri && c0 + PF_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
   // 8 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
-  constexpr int O_R8 = 0, O_C8 = 16384, O_R4 = 24576, O_C4 = 28672;
+  constexpr int O_R8 = 0, O_R4 = 16384, O_C4 = 20480;
   __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
   const uint8_t *src[PF_Q];
   int stp[PF_Q];
 #pragma unroll
   for (int u = 0; u < PF_Q; ++u) {
     const int q = w + 8 * u;
-    if (q < 24) {  // int8: 16 rows x 4 chunks per instruction
+    if (q < 16) {  // int8 L3 slices: 16 rows x 4 chunks per instruction
       const int row = (q & 7) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-      const int64_t idx = q < 16 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (const uint8_t *)(q < 16 ? x.rs[q >> 3] : x.cs[0]) + idx * x.n_pad + 16 * lg;
+      src[u] = (const uint8_t *)x.rs[q >> 3] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
       stp[u] = SG_K;
-    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 24..27 rows, 28..31 columns)
+    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 16..19 rows, 20..23 columns)
       const int qq = q & 3, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-      const int64_t idx = q < 28 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (q < 28 ? x.rs4 : x.cs4) + idx * (x.n_pad / 2) + 16 * lg;
+      const int64_t idx = q < 20 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+      src[u] = (q < 20 ? x.rs4 : x.cs4) + idx * (x.n_pad / 2) + 16 * lg;
       stp[u] = SG_K / 2;
     }
   }
@@ -319,13 +330,16 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[st % PF_NS][(w + 8 * u) * 1024],
                                        16, 0, 0);
   };
-  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q DMAs per stage)
+  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage)
+  static_assert(PF_Q == 3 && PF_NS == 5, "wait_for's vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
     const int ahead = last - st;
-    if (ahead >= 2)
-      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    if (ahead >= 3)
+      asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+    else if (ahead == 2)
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
     else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
@@ -350,17 +364,24 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int rrow = 32 * wr + c;
   for (int st = 0; st < S; ++st) {
     const uint8_t *bf = ring[st % PF_NS];
-    // slot (st + 3) % 4 was read in stage st - 1, which every wave has left (barrier)
+    // slot (st + 4) % 5 was read in stage st - 1, which every wave has left (barrier)
     if (st + PF_NS - 1 < S) issue(st + PF_NS - 1);
+    // lane (c, h) holds the fp4 codes of individuals 32h .. 32h + 31 of the stage; the int8 E3
+    // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
+    v4i rb4[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
+      rb4[q] = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int lr = (2 * kk + h) ^ ((rrow >> 2) & 3);
+      const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
       const v4i f0 = *(const v4i *)&bf[O_R8 + rrow * 64 + 16 * lr];
       const v4i f1 = *(const v4i *)&bf[O_R8 + 8192 + rrow * 64 + 16 * lr];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int crow = 64 * wc + 32 * q + c, lc = (2 * kk + h) ^ ((crow >> 2) & 3);
-        const v4i fc = *(const v4i *)&bf[O_C8 + crow * 64 + 16 * lc];
+        const v4i fc = i8_of_fp4((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
         acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
         acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
       }
@@ -375,11 +396,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
         v8i_ fb[2];
-        const v4i rb4 = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
-        fb[0] = v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0};
-        fb[1] = sq4(rb4);
+        fb[0] = v8i_{rb4[q][0], rb4[q][1], rb4[q][2], rb4[q][3], 0, 0, 0, 0};
+        fb[1] = sq4(rb4[q]);
 #pragma unroll
         for (int p = 0; p < 4; ++p)
           acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
