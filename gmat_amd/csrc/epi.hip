@@ -265,6 +265,18 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
   }
 }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4: lane i's bytes land at lds + 16 i) issued
+// through inline asm.  With the builtin the compiler tracks the DMA as an LDS write and, unable to
+// tell the ring slot being filled from the one being read, puts an s_waitcnt vmcnt(0) before the
+// next ds_read: every stage then waits for its own prefetch.  Here the kernels count vmcnt
+// themselves (the compiler's own loads stay safe: vmcnt retires in order, so its waits can only
+// over-wait on these).
+__device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)lds);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(m) : "memory");
+}
+
 // ------------------------------------------------------------------ prefilter pass
 // The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 128 x 128
 // (band row, column) tiles, 8 waves of 32 x 64: the pass streams its operands at ~20 bytes per
@@ -324,11 +336,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
   }
   auto issue = [&](int st) __attribute__((always_inline)) {
-    typedef __attribute__((address_space(3))) void *lds_t;
 #pragma unroll
     for (int u = 0; u < PF_Q; ++u)
-      __builtin_amdgcn_global_load_lds(src[u] + (int64_t)st * stp[u], (lds_t)&ring[st % PF_NS][(w + 8 * u) * 1024],
-                                       16, 0, 0);
+      lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PF_NS][(w + 8 * u) * 1024]);
   };
   // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage)
   static_assert(PF_Q == 3 && PF_NS == 5, "wait_for's vmcnt values");
@@ -1038,15 +1048,13 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   // registers (the j side is swizzled per lane)
   v4i rnj[SK], rni[SK];
   auto load = [&](int nb, int ch, int cs2) __attribute__((always_inline)) {
-    typedef __attribute__((address_space(3))) void *lds_t;
 #pragma unroll
     for (int s = 0; s < SK; ++s) {
       const int cs = cs2 * SK + s;
       const uint8_t *src = x.tiles + (int64_t)(ch * nK + cs) * MX_TILE;
 #pragma unroll
       for (int u = 0; u < NA; ++u)
-        __builtin_amdgcn_global_load_lds(src + (tid + u * MX_T) * 16, (lds_t)&sA[nb][s * MX_TILE + (w * 64 + u * MX_T) * 16],
-                                         16, 0, 0);
+        lds_dma16(src + (tid + u * MX_T) * 16, &sA[nb][s * MX_TILE + (w * 64 + u * MX_T) * 16]);
       rnj[s] = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
       rni[s] = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
     }
@@ -1115,11 +1123,10 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
   }
   auto fetch_epi = [&](int ch) __attribute__((always_inline)) {
-    typedef __attribute__((address_space(3))) void *lds_t;
-    __builtin_amdgcn_global_load_lds(x.G + offG + ch * MXK, (lds_t)&sE[w * 1024], 16, 0, 0);
+    lds_dma16(x.G + offG + ch * MXK, &sE[w * 1024]);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      __builtin_amdgcn_global_load_lds(x.H + offH[u] + ch * MXK, (lds_t)&sE[(8 + w + 8 * u) * 1024], 16, 0, 0);
+      lds_dma16(x.H + offH[u] + ch * MXK, &sE[(8 + w + 8 * u) * 1024]);
   };
   // sum of c~_r^2 over the chunk's rows: c~ = acc - beta G' - alpha H, two rows per v_pk_fma_f32
   double lowrank[PB];
@@ -1158,11 +1165,13 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     __builtin_amdgcn_sched_barrier(0);
     compute(b, first);
     store(b ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of the next stage
     __syncthreads();
   };
 
   load(0, 0, 0);
   store(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   stamp(1);
   int b = 0;
