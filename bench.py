@@ -28,6 +28,7 @@ sys.path.insert(0, REPO)
 METRIC = "SNP-pairs tested/sec (whole node) + GRM GFLOP/s, mouse-sized cohort"
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x the 2.5 PF dense bf16), MI355X_MICROARCH.md
 MX_PEAK_TFLOPS = 10000.0  # dense block-scaled fp6/fp4 MFMA (4x bf16 per clock), MI355X_MICROARCH.md
+FP64_PEAK_TFLOPS = 78.6  # dense fp64 MFMA, MI355X_MICROARCH.md
 
 
 def log(*a):
@@ -50,7 +51,7 @@ def build_inputs(n, m, seed, var, rank, ws):
     import ctypes
     from gmat_amd.plink import Geno
     g = Geno(body=body, n_id=n, n_snp=m)
-    pvp = py = None
+    pvp = py = ka = y = None
     if rank == 0:
         lib = N.ensure_device()
         ka = np.empty((n, n))
@@ -66,30 +67,56 @@ def build_inputs(n, m, seed, var, rank, ws):
         pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), [ka, ka * ka], var)
     pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
     py = dist.broadcast_array(py, 0, shape=(n,))
-    return geno, g, pvp, py
+    return geno, g, pvp, py, ka, y
 
 
 def cpu_baseline(geno, pvp, py, budget_s):
     """The oracle's restatement of _remma_epiAA's per-row loop (remma_epiAA.py:71-82, numpy
-    fp64 + the host BLAS), timed on stratified rows until `budget_s` elapses."""
+    fp64 + the host BLAS), timed on stratified rows until `budget_s` elapses.  Returns the
+    baseline record plus the rows used and the oracle's hits on them (the parity check)."""
     from oracle import gmat_oracle as O  # checker / CPU baseline only
     snp = np.ascontiguousarray(geno.T, dtype=np.float64)
     m = snp.shape[1]
     order = np.linspace(0, m - 2, 64).astype(np.int64)
     rng = np.random.default_rng(0)
     rng.shuffle(order)
-    pairs, t0, used = 0, time.perf_counter(), []
+    pairs, t0, used, hits = 0, time.perf_counter(), [], []
     for i in order:
-        O.epi_scan("AA", snp, pvp, py.reshape(-1, 1), snp_lst_0=[int(i)], p_cut=1e-5)
+        hits.append(O.epi_scan("AA", snp, pvp, py.reshape(-1, 1), snp_lst_0=[int(i)], p_cut=1e-5))
         pairs += m - 1 - int(i)
         used.append(int(i))
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": pairs / dt, "unit": "SNP-pairs/s", "cores": cores, "kind": "port",
-            "sample": "%d stratified rows of the same 2000x50000 cohort (%d pairs, %.1f s), numpy/BLAS fp64 "
-                      "restatement of remma_epiAA.py:71-82" % (len(used), pairs, dt)}
+    rec = {"value": pairs / dt, "unit": "SNP-pairs/s", "cores": cores, "kind": "port",
+           "sample": "%d stratified rows of the same 2000x50000 cohort (%d pairs, %.1f s), numpy/BLAS fp64 "
+                     "restatement of remma_epiAA.py:71-82" % (len(used), pairs, dt)}
+    exp = np.concatenate(hits) if hits else np.zeros((0, 5))
+    return rec, np.array(used, dtype=np.int64), exp
+
+
+def parity_check(plan, rows, exp, p_cut):
+    """GPU hits on the oracle's rows (every screen level the plan has) against the oracle's
+    exact fp64 hits: identical (i, j) sets, eff / chi / p within 1e-8 relative."""
+    order = np.argsort(rows)
+    rows = rows[order]
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))] if exp.size else exp
+    out = {"rows": int(rows.size), "oracle_hits": int(exp.shape[0]), "levels": {}}
+    ok = True
+    for ns, name in ((0, "auto"), (-1, "mx"), (1, "int8x1")):
+        hi, hj, eff, var, chi, p = plan.scan("AA", rows, p_cut, n_slice=ns)
+        same = hi.size == exp.shape[0] and np.array_equal(np.column_stack([hi, hj]), exp[:, :2].astype(np.int64))
+        err = 0.0
+        if same and hi.size:
+            got = np.column_stack([eff, chi, p])
+            err = float(np.max(np.abs(got - exp[:, 2:]) / np.maximum(np.abs(exp[:, 2:]), 1e-300)))
+        lev_ok = bool(same and err <= 1e-8)
+        out["levels"][name] = {"hits": int(hi.size), "identical_pairs": bool(same), "max_rel_err": err,
+                               "screen_level": int(plan.stats()["n_slice"])}
+        ok = ok and lev_ok
+    out["identical"] = ok
+    return out
 
 
 def grm_bench(n, m_grm, seed, reps=5):
@@ -113,6 +140,7 @@ def grm_bench(n, m_grm, seed, reps=5):
         if r:
             times.append((st[0], wall))
     g.close()
+    grm_bench.last_k = k
     kern = float(np.median([t[0] for t in times]))
     wall = float(np.median([t[1] for t in times]))
     flop = 2.0 * n * n * m_grm
@@ -120,6 +148,55 @@ def grm_bench(n, m_grm, seed, reps=5):
             "gflops_end_to_end": flop / wall / 1e9, "kernel_ms": kern * 1e3, "end_to_end_ms": wall * 1e3,
             "flop_convention": "dense-equivalent 2 n^2 m", "int8_ops_issued": float(st[1]),
             "int8_tops": st[1] / kern / 1e12}
+
+
+def reml_bench(k, seed):
+    """configs[1] REML: 2-GRM ([A, AxA] + residual) weighted EM-AI REML at n = 2,000 on the
+    device (gmat_reml), synthetic phenotype with (0.4, 0.2, 0.4); seconds per iteration from the
+    library's own clock (every iteration ends in a host sync)."""
+    from gmat_amd import _native as N
+    from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat
+    from scipy.sparse import identity
+    lib = N.ensure_device()
+    n = k.shape[0]
+    rng = np.random.Generator(np.random.PCG64(seed + 3))
+    kk = k * k
+    y = np.ones(n)
+    for g, s_ in ((k, 0.4), (kk, 0.2)):
+        y += np.sqrt(s_) * (np.linalg.cholesky(g + 1e-4 * np.eye(n)) @ rng.standard_normal(n))
+    y += np.sqrt(0.4) * rng.standard_normal(n)
+    t0 = time.perf_counter()
+    var = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), [k, kk])
+    wall = time.perf_counter() - t0
+    st = np.zeros(4)
+    N.check(lib.gmat_reml_stats(N.ptr(st)), "gmat_reml_stats")
+    flop = st[3]
+    return {"config": "configs[1]: 2-GRM REML [A, AxA] n=%d" % n, "iters": int(st[1]),
+            "ms_per_iter": st[2] * 1e3, "wall_s": wall, "var": [float(v) for v in var],
+            "fp64_tflops": flop / st[2] / 1e12 if st[2] > 0 else None,
+            "frac": flop / st[2] / 1e12 / FP64_PEAK_TFLOPS if st[2] > 0 else None,
+            "flop_convention": "n^3/3 potrf + 2n^3/3 inverse + 2n^2(2c+1) per iteration"}
+
+
+def e2e_bench(geno, ka, y, var, p_cut, hits_step):
+    """User-facing remma_epiAA end to end (SURVEY.md 8(b) signature): .bed/.bim/.fam/pheno on
+    disk -> design matrix -> P, Py on the device -> genotype decode -> plan (certificates)
+    -> exhaustive scan -> hits file.  Same cohort and hits as the timed step."""
+    import tempfile
+    from gmat_amd import synth
+    from gmat_amd.remma import remma_epiAA
+    n = geno.shape[1]
+    with tempfile.TemporaryDirectory() as d:
+        prefix = os.path.join(d, "c")
+        synth.write_plink(prefix, geno)
+        synth.write_pheno(prefix + ".pheno", [("F%d" % (i // 10), "I%d" % i) for i in range(n)], y)
+        t0 = time.perf_counter()
+        remma_epiAA(prefix + ".pheno", prefix, [ka, ka * ka], var, p_cut=p_cut, out_file=prefix + ".epiAA")
+        wall = time.perf_counter() - t0
+        with open(prefix + ".epiAA") as f:
+            n_hits = sum(1 for _ in f) - 1
+    return {"wall_s": wall, "hits": n_hits, "hits_match_step": bool(n_hits == hits_step),
+            "what": "remma_epiAA(pheno, bed, [A, AxA], var, p_cut) from files to the hits file"}
 
 
 def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
@@ -170,6 +247,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-grm", action="store_true")
     ap.add_argument("--no-eff", action="store_true")
+    ap.add_argument("--no-reml", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
 
@@ -180,23 +259,31 @@ def main():
     N.ensure_device()
     n, m = args.n_id, args.n_snp
     var = np.array([0.4, 0.2, 0.4])
-    geno, g, pvp, py = build_inputs(n, m, args.seed, var, rank, ws)
+    geno, g, pvp, py, ka, y = build_inputs(n, m, args.seed, var, rank, ws)
 
     from gmat_amd.remma._scan import EpiPlan
+    lib = N.ensure_device()
+    lib.gmat_device_synchronize()
+    t_plan = time.perf_counter()
     plan = EpiPlan(g, pvp, py)
+    t_plan = time.perf_counter() - t_plan
     rows = dist.rank_rows("AA", m, rank, ws)
     total_pairs = m * (m - 1) // 2
 
     def step():
         return plan.scan("AA", rows, args.p_cut)
 
+    t_first = time.perf_counter()
     for _ in range(args.warmup):
         step()
-    try:
-        import torch
-        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
-    except Exception:
-        sync = lambda: None  # noqa: E731
+    t_first = time.perf_counter() - t_first
+    setup = plan.setup_stats()
+    setup["plan_create_wall_s"] = t_plan
+    setup["warmup_wall_s"] = t_first
+
+    def sync():
+        N.check(lib.gmat_device_synchronize(), "gmat_device_synchronize")
+
     dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -258,12 +345,18 @@ def main():
                 "issued_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
                 "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and ws == 1 and not args.no_cpu:
-        cpu = cpu_baseline(geno, pvp, py, args.cpu_budget)
-    grm = None
+        cpu, used_rows, exp_hits = cpu_baseline(geno, pvp, py, args.cpu_budget)
+        parity = parity_check(plan, used_rows, exp_hits, args.p_cut)
+    grm = reml = None
     if rank == 0 and not args.no_grm:
         grm = grm_bench(n, 20000, args.seed)
+        if not args.no_reml:
+            reml = reml_bench(grm_bench.last_k, args.seed)
+    e2e = None
+    if rank == 0 and ws == 1 and not args.no_e2e:
+        e2e = e2e_bench(geno, ka, y, var, args.p_cut, int(round(hits_all)))
     eff = None
     if rank == 0 and ws == 1 and not args.no_eff:
         eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed)
@@ -277,13 +370,17 @@ def main():
                           "n_id": n, "n_snp": m, "p_cut": args.p_cut, "kind": "AA",
                           "parallelism": "rows folded over %d rank(s) (parallel=[N,k] split), backend %s"
                                          % (ws, backend or "single")},
-               "roofline": roofline, "cpu_baseline": cpu, "grm": grm, "eff_screen": eff,
+               "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "setup": setup, "grm": grm,
+               "reml": reml, "end_to_end": e2e, "eff_screen": eff,
                "scan": {"hits_per_step": hits_all, "candidates_per_step": cands_all,
                         "screen_s_per_step_rank0": screen_s / args.steps, "side_s_per_step_rank0": side_s / args.steps,
                         "refine_s_per_step_rank0": ref_s / args.steps}}
         print(json.dumps(out), flush=True)
     plan.close()
     g.close()
+    if parity is not None and not parity["identical"]:
+        log("PARITY FAILURE: GPU hits differ from the oracle on the sampled rows")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

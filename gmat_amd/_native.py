@@ -26,6 +26,9 @@ _PROTOS = {
     "gmat_version": (_INT, []),
     "gmat_device_count": (_INT, [_P]),
     "gmat_set_device": (_INT, [_INT]),
+    "gmat_device_synchronize": (_INT, []),
+    "gmat_reml_stats": (_INT, [_P]),
+    "gmat_epi_setup_stats": (_INT, [_P, _P]),
     "gmat_geno_create": (_INT, [_P, _P, _I64, _I64, _I64]),
     "gmat_geno_counts": (_INT, [_P, _P, _P, _P]),
     "gmat_geno_destroy": (_INT, [_P]),
@@ -48,6 +51,7 @@ _PROTOS = {
     "gmat_write_grm_text": (_INT, [ctypes.c_char_p, _P, _I64, _INT, ctypes.c_char_p, _INT]),
     "gmat_float_repr": (_INT, [_D, ctypes.c_char_p, _INT]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
+    "gmat_probe_mx_accum": (_INT, [_INT, _P, _P, _P]),
     # include/gmat_remma_eff.h: the reference's cffi prototypes (char*, long long, ...)
     "read_plink_bed": (_INT, [ctypes.c_char_p, _I64, _I64, _P]),
     "remma_epiAA_eff_cpu": (_INT, [ctypes.c_char_p, _I64, _I64, _P, _I64, _P, _D, ctypes.c_char_p]),

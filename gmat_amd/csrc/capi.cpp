@@ -33,3 +33,8 @@ extern "C" int gmat_set_device(int device) {
   GMAT_HIP(hipSetDevice(device));
   return GMAT_OK;
 }
+
+extern "C" int gmat_device_synchronize(void) {
+  GMAT_HIP(hipDeviceSynchronize());
+  return GMAT_OK;
+}

@@ -340,18 +340,22 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     for (int u = 0; u < PF_Q; ++u)
       lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PF_NS][(w + 8 * u) * 1024]);
   };
-  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage)
+  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage),
+  // then the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm
+  // writes LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist
+  // the next stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations
+  // retire in order (they do on gfx9 for loads).
   static_assert(PF_Q == 3 && PF_NS == 5, "wait_for's vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
     const int ahead = last - st;
     if (ahead >= 3)
-      asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if (ahead == 2)
-      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   v16i acc[2][E3_PF];
   v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
@@ -370,7 +374,6 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int pre = min(S, PF_NS - 1);
   for (int st = 0; st < pre; ++st) issue(st);
   wait_for(0, pre - 1);
-  __builtin_amdgcn_s_barrier();
   const int rrow = 32 * wr + c;
   for (int st = 0; st < S; ++st) {
     const uint8_t *bf = ring[st % PF_NS];
@@ -415,7 +418,6 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       }
     }
     wait_for(st + 1, min(st + PF_NS - 1, S - 1));
-    __builtin_amdgcn_s_barrier();
   }
   // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
   // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
@@ -1920,6 +1922,10 @@ struct gmat_epi {
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
   double stats[10] = {0};
+  // plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition,
+  // [3] low-rank certificate, [4] slices + residual bounds, [5] coding builds (side vectors, lazily
+  // in the first scan of a kind), [6] Cholesky factorisations run by the certificates, [7] reserved
+  double setup[8] = {0};
   hipStream_t s = 0;
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
   struct ScanBufs {
@@ -1946,9 +1952,16 @@ const int8_t *screen_sq(const gmat_epi *e, int which) {
   return which == 0 ? e->code[0].sq.as<int8_t>() : screen_panel(e, 1);  // 0/1 codes: a^2 = a
 }
 
+int build_coding_impl(gmat_epi *e, int which);
 int build_coding(gmat_epi *e, int which) {
+  if (e->code[which].ready) return GMAT_OK;
+  const double t0 = now();
+  const int rc = build_coding_impl(e, which);
+  e->setup[5] += now() - t0;
+  return rc;
+}
+int build_coding_impl(gmat_epi *e, int which) {
   Coding &cd = e->code[which];
-  if (cd.ready) return GMAT_OK;
   const int64_t m = e->m, n_pad = e->n_pad, n = e->n;
   // centring offsets exactly as the reference (for the refine): freq = sum/(2n); A: 2*freq,
   // D: 2*freq*(1-freq).  Screen codes: the additive coding counts the minor allele
@@ -2187,6 +2200,7 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
                        tau, A.as<double>());
     GMAT_HIP(hipGetLastError());
     GMAT_TRY(cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), cinfo.as<int>()));
+    e->setup[6] += 1;
     int hi = 1;
     GMAT_HIP(hipMemcpy(&hi, cinfo.p, sizeof(int), hipMemcpyDeviceToHost));
     return hi == 0 ? 1 : 0;
@@ -2199,6 +2213,8 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
     (r ? lo : hi) = mid;
   }
   quantise(lo, true);  // the certified Q (quantise is deterministic)
+  e->setup[2] = t1 - t0;
+  e->setup[3] = now() - t1;
   const double eps = eps_of(lo);
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "lr_setup: R %d (padded %d) lam_0 %.4g lam_R %.4g -> lam %.4g tau %.3g eps %.3g (pf_mu %.4g); "
@@ -2241,6 +2257,7 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
   GMAT_CHECK(g->n_pad <= 8192 && 2 * g->m * g->n_pad < (1LL << 32), GMAT_E_ARG,
              "gmat_epi_create: supports n_id <= 8192 and 2 * n_snp * n_pad < 2^32 (32-bit buffer offsets)");
+  const double t_create = now();
   auto *e = new gmat_epi();
   e->g = g;
   e->n = g->n;
@@ -2352,6 +2369,9 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
     const double u = std::ldexp(1.0, -24);
     e->rho_mx = 1.05 * fr / os + 1e-15 * pmax * (double)n + 1.01 * (2.0 * (double)n_pad + 64.0) * u * amax;
   }
+  (void)hipDeviceSynchronize();
+  e->setup[4] = now() - t_create;
+  const double t_pf = now();
   // Spectral prefilter certificate.  If the fp64 Cholesky of A = P + (mu + tau) 11'/n - mu I
   // completes with positive pivots, A + E = LL' with |E| <= gamma_{n+1} |L||L'|, so lambda_min(A)
   // >= -||E||_2 >= -gamma_{n+1} trace(A) (||L||_F^2 = trace(LL')), i.e. for every e
@@ -2371,6 +2391,7 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
                          tau0 + 1e-6 * mu, A.as<double>());
       if (hipGetLastError() != hipSuccess) return -1;
       if (cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), info.as<int>()) != GMAT_OK) return -1;
+      e->setup[6] += 1;
       int hinfo = 1;
       if (hipMemcpy(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
       return hinfo == 0 ? 1 : 0;
@@ -2393,6 +2414,7 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
     }
     if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: prefilter mu %.6g eps %.3g (trace/n %.4g)\n", lo, eps, trP / n);
   }
+  e->setup[1] = now() - t_pf;
   if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax)) != GMAT_OK) {
     // the low-rank screen is an accelerator: without it the MX screen runs
     if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: low-rank screen unavailable: %s\n", gmat_last_error());
@@ -2407,7 +2429,14 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   double zz = 0.0;
   for (double v : hz) zz += v;
   e->zz = zz;
+  e->setup[0] = now() - t_create;
   *out = e;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_setup_stats(const gmat_epi *e, double *out8) {
+  GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_setup_stats: bad arguments");
+  for (int k = 0; k < 8; ++k) out8[k] = e->setup[k];
   return GMAT_OK;
 }
 

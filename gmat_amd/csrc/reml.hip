@@ -8,6 +8,7 @@
 // the reference's O(n^3) np.trace(np.dot(P, ZGZ)) at :66), W = [ZG_kZ'Py..., Py] and
 // AI = W'PW/2.  The (c+1)-sized EM/AI weight search and the convergence test run on the
 // host exactly as :78-99.
+#include <chrono>
 #include <cmath>
 
 #include "dla.h"
@@ -246,15 +247,29 @@ struct Model {
   }
 };
 
+double wall_now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double g_reml_stats[4] = {0, 0, 0, 0};
+
 }  // namespace
+
+extern "C" int gmat_reml_stats(double *out4) {
+  GMAT_CHECK(out4, GMAT_E_ARG, "gmat_reml_stats: null");
+  for (int k = 0; k < 4; ++k) out4[k] = g_reml_stats[k];
+  return GMAT_OK;
+}
 
 extern "C" int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y, const double *xmat,
                          const int64_t *z_col, const double *const *gmat, const double *init, int maxiter,
                          double cc_par, double cc_gra, double *var_out, int *n_iter, double *history) {
   GMAT_CHECK(y && xmat && z_col && var_out && (n_gmat == 0 || gmat), GMAT_E_ARG, "gmat_reml: bad arguments");
+  const double t_start = wall_now();
   Model md;
   GMAT_TRY(md.setup(n_rec, n_fix, n_id, n_gmat, y, xmat, z_col, gmat));
   const int c1 = n_gmat + 1;
+  GMAT_HIP(hipDeviceSynchronize());
+  const double t_loop = wall_now();
   {  // ones vector used to copy Py into W
     double one = 1.0;
     GMAT_HIP(hipMemcpy(md.small.as<double>() + 3000, &one, sizeof(double), hipMemcpyHostToDevice));
@@ -301,6 +316,13 @@ extern "C" int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat,
   }
   for (int a = 0; a < c1; ++a) var_out[a] = var[a];
   if (n_iter) *n_iter = it;
+  GMAT_HIP(hipDeviceSynchronize());
+  const double t_end = wall_now(), nn = (double)n_rec;
+  g_reml_stats[0] = t_end - t_start;
+  g_reml_stats[1] = it;
+  g_reml_stats[2] = it ? (t_end - t_loop) / it : 0.0;
+  // algorithmic flop per iteration: potrf n^3/3, inverse 2n^3/3, traces/AI
+  g_reml_stats[3] = nn * nn * nn + 2.0 * nn * nn * (2 * n_gmat + 1);
   return GMAT_OK;
 }
 

@@ -143,11 +143,15 @@ def merge_hits(parts):
 def distributed_scan(scan_fn, kind, num_snp, p_cut, rows=None):
     """Run ``scan_fn(kind, my_rows, p_cut) -> (i, j, eff, var, chi, p)`` on this rank's
     share and gather the merged hits on rank 0 (other ranks get None)."""
-    import torch.distributed as dist
     rank, ws, _ = world()
+    if ws > 1:
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("WORLD_SIZE=%d but no process group is initialised: a single rank would "
+                               "return only its own share of the hits (call dist.init() first)" % ws)
     mine = rank_rows(kind, num_snp, rank, ws, rows)
     local = scan_fn(kind, mine, p_cut) if mine.size else None
-    if not (dist.is_available() and dist.is_initialized()) or ws == 1:
+    if ws == 1:
         return merge_hits([local])
     gathered = [None] * ws if rank == 0 else None
     dist.gather_object(None if local is None else tuple(np.asarray(a) for a in local), gathered, dst=0)

@@ -10,8 +10,8 @@ import time
 
 import numpy as np
 
-from . import _native as N
-from .plink import Geno, read_fam_ids
+from .. import _native as N
+from ..plink import Geno, read_fam_ids
 
 
 def _fam_ids_as_pandas(bed_file):

@@ -61,24 +61,34 @@ def _pack(codes):
     return (pad[:, :, 0] | (pad[:, :, 1] << 2) | (pad[:, :, 2] << 4) | (pad[:, :, 3] << 6)).astype(np.uint8).ravel()
 
 
+def missing_column_order(miss_nm):
+    """SNP columns holding missing calls, in the order impute_geno visits them: the
+    iteration order of ``set(np.where(np.isnan(snp_mat))[1])`` on the n x m matrix
+    (process_plink.py:13-15).  With the same np.random state the draws are then the
+    reference's own."""
+    return list(set(np.where(miss_nm)[1]))
+
+
 def impute_missing(body, n, m, rng=None):
     """Replace missing calls (code 01) per SNP by random draws from that SNP's observed
-    0/1/2 frequencies, as impute_geno (process_plink.py:12-25).  The reference's draws are
-    unseeded, so imputed genotypes are not reproducible there either."""
+    0/1/2 frequencies, as impute_geno (process_plink.py:12-25): same column order, same
+    probabilities (count / total as float64) and the same np.random.choice call, so a
+    caller that seeds np.random gets the reference's imputed genotypes.  The reference's
+    draws are unseeded, so imputed genotypes are not reproducible there by default."""
     rng = np.random if rng is None else rng
     codes = _codes(body, n, m)
     miss = codes == 1
-    cols = np.where(miss.any(axis=1))[0]
-    if cols.size == 0:
+    if not miss.any():
         return body
     codes = codes.copy()
     dose_code = np.array([0b00, 0b10, 0b11], dtype=np.uint8)
-    for j in cols:
+    for j in missing_column_order(miss.T):
         c = codes[j]
-        cnt = np.array([(c == 0).sum(), (c == 2).sum(), (c == 3).sum()], dtype=float)
+        cnt = [np.sum(c == 0), np.sum(c == 2), np.sum(c == 3)]
+        tot = cnt[0] + cnt[1] + cnt[2]
         k = miss[j]
-        draw = rng.choice([0, 1, 2], int(k.sum()), p=cnt / cnt.sum())
-        c[k] = dose_code[draw]
+        draw = rng.choice([0.0, 1.0, 2.0], int(k.sum()), p=[cnt[0] / tot, cnt[1] / tot, cnt[2] / tot])
+        c[k] = dose_code[draw.astype(np.int64)]
     return _pack(codes)
 
 

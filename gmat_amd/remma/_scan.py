@@ -66,6 +66,16 @@ class EpiPlan:
                 "n_slice", "bound_coef")
         return dict(zip(keys, s.tolist()))
 
+    def setup_stats(self):
+        """Plan setup seconds (gmat_epi_setup_stats): create total, prefilter certificate,
+        eigendecomposition, low-rank certificate, slices/residual bounds, coding builds, and
+        the number of Cholesky factorisations the certificates ran."""
+        s = np.zeros(8)
+        N.check(self._lib.gmat_epi_setup_stats(self._h, N.ptr(s)), "gmat_epi_setup_stats")
+        keys = ("create_s", "prefilter_cert_s", "eigen_s", "lowrank_cert_s", "slices_bounds_s", "coding_s",
+                "cholesky_count")
+        return dict(zip(keys, s.tolist()))
+
     def lowrank_rank(self):
         """Rank of the plan's low-rank spectral screen (0: scans use the fp6 quadratic form)."""
         s = np.zeros(4)

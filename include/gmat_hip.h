@@ -39,6 +39,8 @@ const char *gmat_last_error(void);
 int gmat_version(void);
 int gmat_device_count(int *n);
 int gmat_set_device(int device);
+/* wait for all work queued by this process on the current device (hipDeviceSynchronize) */
+int gmat_device_synchronize(void);
 
 /* ---------------------------------------------------------------- genotype panel
  * Uploads the packed .bed body once and decodes it on the device into SNP-major int8
@@ -76,6 +78,11 @@ int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const doub
               const double *xmat, const int64_t *z_col, const double *const *gmat, const double *init,
               int maxiter, double cc_par, double cc_gra, double *var_out, int *n_iter, double *history);
 
+/* last gmat_reml call on this process: [0] seconds (setup + iterations), [1] iterations,
+ * [2] seconds per iteration, [3] algorithmic flop per iteration (n^3/3 potrf + 2n^3/3 inverse
+ * + 2n^2(2c+1) traces / AI) */
+int gmat_reml_stats(double *out4);
+
 /* pvp = Z'PZ (n_id x n_id) and py = Z'Py (n_id) of the scans' setup (remma_epiAA.py:33-49). */
 int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y,
                     const double *xmat, const int64_t *z_col, const double *const *gmat,
@@ -109,6 +116,11 @@ int gmat_epi_stats(const gmat_epi *e, double *out10);
  * none, scans use the fp6 quadratic form), [1] its lam, [2] the prefilter's mu, [3] n_pad.  In
  * gmat_epi_stats, [8] = -1 marks a scan screened by the low-rank bound. */
 int gmat_epi_info(const gmat_epi *e, double *out4);
+/* plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition
+ * of P, [3] low-rank certificate, [4] slices and residual bounds, [5] coding builds (side vectors;
+ * done lazily by the first scan of each coding), [6] Cholesky factorisations the certificates ran,
+ * [7] reserved */
+int gmat_epi_setup_stats(const gmat_epi *e, double *out8);
 int gmat_epi_destroy(gmat_epi *e);
 
 /* Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-166) at var_com, as
@@ -151,6 +163,14 @@ int gmat_snp_test(gmat_geno *g, int kind, const double *pvp, const double *py, d
 /* Decoded fp64 dosage (m x n, SNP-major, .fam order; (c^2+c)/6: missing = 1/3) -- the
  * reference's read_plink_bed (_read_plink_bed.c:5-51). */
 int gmat_geno_decode(const gmat_geno *g, double *marker_mat);
+
+/* ---- diagnostics ----
+ * The low-rank screen's accumulation (lr_screen_kernel) on one wave: a chain of n_steps
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (A fp6 e2m3 codes[n_steps][32 rows][2 halves][32] with e8m0
+ * scales[n_steps][32][2], one per (row, half); B = the screen's worst case w = 4 everywhere)
+ * accumulated in fp32; out[32 x 32] (every column = 4 sum_k A[r][k]).  Lets tests check the
+ * screen's fp32 accumulation bound (eta_r) on the hardware. */
+int gmat_probe_mx_accum(int n_steps, const uint8_t *codes, const uint8_t *scales, float *out);
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,22 @@ def read_plink(prefix):
     return np.ascontiguousarray(mat.T)
 
 
+def impute_geno(snp_mat):
+    """impute_geno (process_plink.py:12-25): each NaN becomes a draw from the SNP's observed
+    0/1/2 frequencies, columns visited in the order of set(np.where(isnan)[1]), one
+    np.random.choice per column on the global RNG.  In place; returns snp_mat."""
+    for i in set(np.where(np.isnan(snp_mat))[1]):
+        col = snp_mat[:, i]
+        c0 = np.sum(np.absolute(col - 0.0) < 1e-10)
+        c1 = np.sum(np.absolute(col - 1.0) < 1e-10)
+        c2 = np.sum(np.absolute(col - 2.0) < 1e-10)
+        tot = c0 + c1 + c2
+        na = np.where(np.isnan(col))
+        col[na] = np.random.choice([0.0, 1.0, 2.0], len(na[0]), p=[c0 / tot, c1 / tot, c2 / tot])
+        snp_mat[:, i] = col
+    return snp_mat
+
+
 # ----------------------------------------------------------------------------- GRM
 
 
@@ -317,6 +333,24 @@ def annotation_snp_pos(res_lines, bim_lines, p_cut=1, dis=0):
         s1 = info[int(a[1])].split()
         if float(a[-1]) <= p_cut and (s0[0] != s1[0] or abs(float(s0[3]) - float(s1[3])) > dis):
             out.append(" ".join([a[0], info[int(a[0])], a[1], info[int(a[1])]]) + " " + " ".join(a[2:]))
+    return out
+
+
+def ld_filter(anno_lines, ld_lines, r2=0.2):
+    """LD filter of annotation_snp_pos (annotation.py:57-73): drop annotated rows whose SNP id
+    pair (columns 2 and 9) is listed in the LD file (ids in columns 2 and 5, r2 last, header
+    skipped) with r2 above the cut, in either order."""
+    ld = set()
+    for line in ld_lines[1:]:
+        a = line.split()
+        if float(a[-1]) > r2:
+            ld.add((a[2], a[5]))
+            ld.add((a[5], a[2]))
+    out = [anno_lines[0]]
+    for line in anno_lines[1:]:
+        a = line.split()
+        if (a[2], a[9]) not in ld:
+            out.append(line)
     return out
 
 

@@ -12,6 +12,8 @@ Fixtures ("reference code + its own C decoder in fp64"):
   tiny/    a 150 x 200 related synthetic cohort (n % 4 == 2, two monomorphic SNPs and one
            all-heterozygous SNP) with full K/D and every testable pair for AA/AD/DD.
            rep*: repeated records (Z != I) REML + epiAA, and wemai_multi_gmat_pred.
+  readme/  the README exact-test workflow on a cohort with missing calls and covariates
+           (seeded imputation), including the annotation LD filter.
   both:    remma_add / remma_dom result files (``python tests/golden/make_golden.py singles``
            regenerates only these).
 """
@@ -283,10 +285,63 @@ def maf_eff(gmat, work, out_mouse):
         os.chdir(cwd)
 
 
+def readme(gmat, work, out):
+    """The README's exact-test workflow (README.md:94-120): agmat -> np.loadtxt('.agrm0') ->
+    wemai_multi_gmat -> remma_epiAA -> annotation_snp_pos (with an LD file), run unchanged on a
+    cohort with missing calls (imputation, process_plink.py:12-25) and two covariates besides
+    the intercept.  np.random is seeded before each call that imputes (the reference's draws use
+    the global state), so the imputed genotypes are reproducible."""
+    from gmat.gmatrix import agmat
+    from gmat.uvlmm.uvlmm_varcom import wemai_multi_gmat
+    from gmat.remma.remma_epiAA import remma_epiAA
+    from gmat.remma import annotation_snp_pos
+    os.makedirs(out, exist_ok=True)
+    n, m = 160, 240
+    geno = synth.simulate_genotypes(n, m, seed=21, n_founder=20, n_gen=4, block=40)
+    rng = np.random.Generator(np.random.PCG64(22))
+    missing = rng.random((m, n)) < 0.03
+    prefix = os.path.join(out, "plink")
+    synth.write_plink(prefix, geno, missing=missing, seed=21)
+    y = synth.simulate_phenotype(geno, seed=23)
+    cov = np.column_stack([rng.integers(0, 2, n), rng.uniform(20, 60, n)])
+    y = y + 0.5 * cov[:, 0] + 0.02 * cov[:, 1]
+    synth.write_pheno(os.path.join(out, "pheno"), [("F%d" % (i // 10), "I%d" % i) for i in range(n)], y, covar=cov)
+    # PLINK --r2 layout: CHR_A BP_A SNP_A CHR_B BP_B SNP_B R2 (annotation.py:57-64 reads 2, 5, -1)
+    bim = [l.split() for l in open(prefix + ".bim")]
+    with open(os.path.join(out, "plink.ld"), "w") as f:
+        f.write(" CHR_A BP_A SNP_A CHR_B BP_B SNP_B R2\n")
+        for a in range(0, m - 1, 2):
+            for b in (a + 1, a + 7):
+                if b < m:
+                    f.write(" %s %s %s %s %s %s %.6f\n" % (bim[a][0], bim[a][3], bim[a][1], bim[b][0], bim[b][3],
+                                                           bim[b][1], rng.uniform(0, 0.5)))
+    for name in ("plink.bed", "plink.bim", "plink.fam", "pheno", "plink.ld"):
+        shutil.copy(os.path.join(out, name), work)
+    cwd = os.getcwd()
+    os.chdir(work)
+    try:
+        bed_file = "plink"
+        np.random.seed(1234)
+        agmat(bed_file)
+        pheno_file = "pheno"
+        ag = np.loadtxt(bed_file + ".agrm0")
+        gmat_lst = [ag, ag * ag]
+        wemai_multi_gmat(pheno_file, bed_file, gmat_lst, out_file="var_a_axa.txt")
+        var_com = np.loadtxt("var_a_axa.txt")
+        np.random.seed(4321)
+        remma_epiAA(pheno_file, bed_file, gmat_lst, var_com, p_cut=1.0e-2, out_file="epiAA_a_axa")
+        annotation_snp_pos("epiAA_a_axa", bed_file, p_cut=1.0e-2, dis=0, ld_file="plink.ld", r2=0.2)
+        np.savez(os.path.join(out, "agrm.npz"), agrm=ag)
+        for name in ("var_a_axa.txt", "epiAA_a_axa", "epiAA_a_axa.anno", "epiAA_a_axa.anno.ld"):
+            shutil.copy(name, os.path.join(out, name))
+    finally:
+        os.chdir(cwd)
+
+
 def main():
     gmat = import_reference()
     logging.getLogger().setLevel(logging.WARNING)
-    what = sys.argv[1:] or ["tiny", "mouse", "singles", "repeated", "maf"]
+    what = sys.argv[1:] or ["tiny", "mouse", "singles", "repeated", "maf", "readme"]
     if "tiny" in what:
         with tempfile.TemporaryDirectory() as work:
             tiny(gmat, work, os.path.join(HERE, "tiny"))
@@ -302,6 +357,9 @@ def main():
     if "repeated" in what:
         with tempfile.TemporaryDirectory() as work:
             repeated(gmat, work, os.path.join(HERE, "tiny"))
+    if "readme" in what:
+        with tempfile.TemporaryDirectory() as work:
+            readme(gmat, work, os.path.join(HERE, "readme"))
     print("golden fixtures written to", HERE)
 
 

@@ -262,3 +262,37 @@ def test_mouse_maf_eff_screen_golden(mouse_eff_inputs, kind, base):
         assert abs(float(cols[0]) - got_d[(i, j)]) <= 5e-6 * abs(got_d[(i, j)])
         chi_app = float(float(cols[0]) * float(cols[0]) / deno[fi[i] * 10 + fj[j]])
         assert cols[1] == repr(chi_app) and cols[2] == repr(float(chi2.sf(chi_app, 1)))
+
+
+README = os.path.join(os.path.dirname(__file__), "golden", "readme")
+
+
+def test_readme_workflow_golden():
+    """The README workflow fixture (missing calls, two covariates, seeded imputation, LD
+    filter): the oracle's impute_geno with the same seed reproduces the reference's imputed
+    GRM, its REML the variances, its scan the hit set, its annotation + LD filter the files."""
+    prefix = os.path.join(README, "plink")
+    snp = O.read_plink(prefix)
+    assert np.isnan(snp).sum() > 0
+    np.random.seed(1234)
+    k = O.agmat(O.impute_geno(snp.copy()))
+    ref_k = np.load(os.path.join(README, "agrm.npz"))["agrm"]
+    np.testing.assert_allclose(k, ref_k, rtol=1e-12, atol=1e-14)
+    y, x, col, nid = O.design_matrix(os.path.join(README, "pheno"), prefix)
+    assert x.shape[1] == 3
+    var = O.wemai_multi_gmat(y, x, col, nid, [ref_k, ref_k * ref_k])
+    np.testing.assert_allclose(var, np.loadtxt(os.path.join(README, "var_a_axa.txt")), rtol=1e-8)
+    np.random.seed(4321)
+    snp2 = O.impute_geno(O.read_plink(prefix))
+    var_ref = np.loadtxt(os.path.join(README, "var_a_axa.txt"))
+    pvp, py = O.projection(y, x, col, nid, [ref_k, ref_k * ref_k], var_ref)
+    exp = O.epi_scan("AA", snp2, pvp, py, p_cut=1e-2)
+    got = np.loadtxt(os.path.join(README, "epiAA_a_axa"), skiprows=1, ndmin=2)
+    np.testing.assert_array_equal(exp[:, :2], got[:, :2])
+    np.testing.assert_allclose(exp[:, 2:], got[:, 2:], rtol=1e-9)
+    res = open(os.path.join(README, "epiAA_a_axa")).read().splitlines()
+    anno = O.annotation_snp_pos(res, open(prefix + ".bim").read().splitlines(), p_cut=1e-2, dis=0)
+    assert [l.rstrip() for l in open(os.path.join(README, "epiAA_a_axa.anno")).read().splitlines()] == anno
+    ld = O.ld_filter(anno, open(os.path.join(README, "plink.ld")).read().splitlines(), r2=0.2)
+    exp_ld = open(os.path.join(README, "epiAA_a_axa.anno.ld")).read().splitlines()
+    assert [l.rstrip() for l in exp_ld] == ld and len(ld) < len(anno)
