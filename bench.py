@@ -199,6 +199,40 @@ def e2e_bench(geno, ka, y, var, p_cut, hits_step):
             "what": "remma_epiAA(pheno, bed, [A, AxA], var, p_cut) from files to the hits file"}
 
 
+def covariate_bench(g, ka, n, m, p_cut, seed, steps, ms_intercept):
+    """configs[2] with intercept + 3 covariates (binary, integer-valued, binary: the layout of the
+    reference's example pheno): P gains three null directions besides 1; the plan certifies the
+    prefilter with them (prefilter_cov_kernel) and keeps the low-rank screen.  Whole-scan time."""
+    from gmat_amd import _native as N
+    from gmat_amd.remma._scan import EpiPlan
+    from gmat_amd.uvlmm.uvlmm_varcom import projection
+    from scipy.sparse import identity
+    lib = N.ensure_device()
+    rng = np.random.Generator(np.random.PCG64(seed + 9))
+    x = np.column_stack([np.ones(n), rng.integers(0, 2, n), rng.integers(90, 130, n), rng.integers(0, 2, n)])
+    y = 1.0 + 0.3 * x[:, 1] + 0.01 * x[:, 2] + rng.standard_normal(n)
+    pvp, py = projection(y, x.astype(float), identity(n, format="csr"), [ka, ka * ka], [0.4, 0.2, 0.4])
+    rows = np.arange(m - 1, dtype=np.int64)
+    t0 = time.perf_counter()
+    plan = EpiPlan(g, pvp, py)
+    t_plan = time.perf_counter() - t0
+    plan.scan("AA", rows, p_cut)
+    lib.gmat_device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = plan.scan("AA", rows, p_cut)
+    lib.gmat_device_synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    st = plan.stats()
+    out = {"config": "configs[2] cohort, X = [1, binary, integer 90-129, binary]", "ms_per_step": ms,
+           "pairs_per_s": m * (m - 1) / 2 / ms * 1e3, "ratio_to_intercept_only": ms / ms_intercept,
+           "hits": int(res[0].size), "candidates": st["candidates"], "screen_level": int(st["n_slice"]),
+           "covariate_directions": int(plan.setup_stats()["covariate_directions"]), "plan_create_s": t_plan,
+           "lowrank_rank": plan.lowrank_rank()}
+    plan.close()
+    return out
+
+
 def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
     """Effect-only screen (the remma_epiAA_eff_cpu replacement) over the
     same cohort, threshold from the exact variance median of 20,000 random pairs as
@@ -249,6 +283,7 @@ def main():
     ap.add_argument("--no-eff", action="store_true")
     ap.add_argument("--no-reml", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-cov", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
 
@@ -354,6 +389,9 @@ def main():
         grm = grm_bench(n, 20000, args.seed)
         if not args.no_reml:
             reml = reml_bench(grm_bench.last_k, args.seed)
+    cov = None
+    if rank == 0 and ws == 1 and not args.no_cov:
+        cov = covariate_bench(g, ka, n, m, args.p_cut, args.seed, 2, t_max / args.steps * 1e3)
     e2e = None
     if rank == 0 and ws == 1 and not args.no_e2e:
         e2e = e2e_bench(geno, ka, y, var, args.p_cut, int(round(hits_all)))
@@ -371,7 +409,7 @@ def main():
                           "parallelism": "rows folded over %d rank(s) (parallel=[N,k] split), backend %s"
                                          % (ws, backend or "single")},
                "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "setup": setup, "grm": grm,
-               "reml": reml, "end_to_end": e2e, "eff_screen": eff,
+               "reml": reml, "end_to_end": e2e, "covariates": cov, "eff_screen": eff,
                "scan": {"hits_per_step": hits_all, "candidates_per_step": cands_all,
                         "screen_s_per_step_rank0": screen_s / args.steps, "side_s_per_step_rank0": side_s / args.steps,
                         "refine_s_per_step_rank0": ref_s / args.steps}}

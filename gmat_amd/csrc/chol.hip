@@ -3,8 +3,9 @@
 // scipy.linalg.inv at remma_epiAA.py:39 / gmatrix.py:84: V is symmetric positive
 // definite, so L L' factorisation gives the same inverse and log-determinant).
 //
-// Right-looking, 64-wide panels: a one-workgroup LDS kernel factors the diagonal block
-// and inverts its factor; the panel solve and the trailing update are MFMA dgemm calls.
+// Right-looking, 64-wide panels: a one-workgroup kernel factors the diagonal block (16-wide
+// sub-panels in registers) and inverts its factor; the panel solve and the trailing update are
+// MFMA dgemm calls.
 #include "dla.h"
 
 namespace gmat {
@@ -12,64 +13,122 @@ namespace gmat {
 namespace {
 constexpr int NB = 64;
 
-// Factor the kb x kb diagonal block at a (lda) in LDS; write L back, write inv(L) to dinv
-// (kb rows of NB doubles), add 2*sum(log diag) to *logdet, flag a bad pivot in *info.
-__global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv,
-                                                    double *logdet, int *info, int64_t k0) {
-  __shared__ double s[NB][NB + 1];
-  __shared__ double x[NB][NB + 1];
-  __shared__ int bad;
-  const int tid = threadIdx.x;
-  if (tid == 0) bad = 0;
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  union {
+    double d;
+    int w[2];
+  } u;
+  u.d = v;
+  u.w[0] = __builtin_amdgcn_readlane(u.w[0], l);
+  u.w[1] = __builtin_amdgcn_readlane(u.w[1], l);
+  return u.d;
+}
+
+// Factor the kb x kb (kb <= 64) diagonal block at a (lda) in LDS with 4 barrier-separated
+// 16-column panels (instead of one barrier group per column): wave 0 factors a panel with its rows
+// in registers (pivot and the panel's column entries broadcast by readlane, no LDS round trips),
+// then all 256 threads apply the panel to the trailing lower triangle.  inv(L) is blocked the same
+// way: the four 16 x 16 diagonal inverses by forward substitution (one thread per column, the
+// column in registers), then the off-diagonal blocks by distance d = i - j as two small products,
+// X_ij = -X_ii (sum_{j<=k<i} L_ik X_kj).  Rows / columns >= kb are an uncoupled identity.  Writes
+// L back, inv(L) to dinv (kb rows of NB doubles), adds 2 sum(log diag) to *logdet, flags a bad
+// pivot's block in *info.
+__global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv, double *logdet,
+                                                    int *info, int64_t k0) {
+  constexpr int PW = 16, NP = NB / PW;
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double Xs[NB][NB + 1];
+  __shared__ double Ts[NP - 1][PW][PW + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int e = tid; e < NB * NB; e += 256) {
-    int r = e / NB, c = e % NB;
-    s[r][c] = (r < kb && c < kb && c <= r) ? a[r * lda + c] : 0.0;
-    x[r][c] = 0.0;
+    const int rr = e / NB, cc = e % NB;
+    Ls[rr][cc] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
+    Xs[rr][cc] = 0.0;
   }
   __syncthreads();
-  for (int j = 0; j < kb; ++j) {
-    if (tid == 0) {
-      double d = s[j][j];
-      if (!(d > 0.0)) {
-        bad = 1;
-        d = 1.0;
+  bool bad = false;
+  double ld = 0.0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int c0 = PW * p;
+    if (w == 0) {
+      const int i = lane;
+      double r[PW];
+#pragma unroll
+      for (int q = 0; q < PW; ++q) r[q] = Ls[i][c0 + q];
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        double d = readlane_d(r[j], c0 + j);
+        if (!(d > 0.0)) {
+          if (c0 + j < kb) bad = true;
+          d = 1.0;
+        }
+        const double ljj = sqrt(d), inv = 1.0 / ljj;
+        if (c0 + j < kb) ld += log(ljj);
+        r[j] = (i > c0 + j) ? r[j] * inv : (i == c0 + j ? ljj : r[j]);
+#pragma unroll
+        for (int k = j + 1; k < PW; ++k) r[k] = fma(-r[j], readlane_d(r[j], c0 + k), r[k]);
       }
-      s[j][j] = sqrt(d);
+      if (i >= c0)
+#pragma unroll
+        for (int q = 0; q < PW; ++q) Ls[i][c0 + q] = (c0 + q <= i) ? r[q] : 0.0;
     }
     __syncthreads();
-    const double ljj = s[j][j];
-    for (int i = j + 1 + tid; i < kb; i += 256) s[i][j] /= ljj;
-    __syncthreads();
-    const int m = kb - j - 1;  // trailing (m x m) lower update
-    for (int e = tid; e < m * m; e += 256) {
-      int i = j + 1 + e / m, k = j + 1 + e % m;
-      if (k <= i) s[i][k] -= s[i][j] * s[k][j];
+    const int t0 = c0 + PW, mt = NB - t0;
+    for (int e = tid; e < mt * mt; e += 256) {
+      const int i = t0 + e / mt, k = t0 + e % mt;
+      if (k <= i) {
+        double sacc = Ls[i][k];
+#pragma unroll
+        for (int q = 0; q < PW; ++q) sacc = fma(-Ls[i][c0 + q], Ls[k][c0 + q], sacc);
+        Ls[i][k] = sacc;
+      }
     }
     __syncthreads();
   }
-  // inverse of the lower-triangular factor, one column per thread
-  if (tid < kb) {
-    const int c = tid;
-    x[c][c] = 1.0 / s[c][c];
-    for (int i = c + 1; i < kb; ++i) {
-      double acc = 0.0;
-      for (int k = c; k < i; ++k) acc += s[i][k] * x[k][c];
-      x[i][c] = -acc / s[i][i];
+  // inv(L): diagonal blocks (thread t < 64: block t / 16, column t % 16)
+  if (tid < NB) {
+    const int o = PW * (tid / PW), c = tid % PW;
+    double x[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int k = 0; k < q; ++k) sacc = fma(Ls[o + q][o + k], x[k], sacc);
+      const double v = (q == c) ? 1.0 : -sacc;
+      x[q] = (q >= c) ? v / Ls[o + q][o + q] : 0.0;
     }
+#pragma unroll
+    for (int q = 0; q < PW; ++q) Xs[o + q][o + c] = x[q];
   }
   __syncthreads();
-  for (int e = tid; e < kb * NB; e += 256) {
-    int r = e / NB, c = e % NB;
-    if (c < kb) {
-      a[r * lda + c] = (c <= r) ? s[r][c] : 0.0;
-      dinv[r * NB + c] = x[r][c];
-    } else {
-      dinv[r * NB + c] = 0.0;
+  const int rr = tid / PW, cc = tid % PW;
+#pragma unroll
+  for (int d = 1; d < NP; ++d) {
+    for (int j = 0; j + d < NP; ++j) {  // T_j = sum_{k=j}^{i-1} L_ik X_kj, i = j + d
+      const int i = j + d;
+      double sacc = 0.0;
+      for (int k = j; k < i; ++k)
+#pragma unroll
+        for (int q = 0; q < PW; ++q) sacc = fma(Ls[PW * i + rr][PW * k + q], Xs[PW * k + q][PW * j + cc], sacc);
+      Ts[j][rr][cc] = sacc;
     }
+    __syncthreads();
+    for (int j = 0; j + d < NP; ++j) {  // X_ij = -X_ii T_j
+      const int i = j + d;
+      double sacc = 0.0;
+#pragma unroll
+      for (int q = 0; q < PW; ++q) sacc = fma(Xs[PW * i + rr][PW * i + q], Ts[j][q][cc], sacc);
+      Xs[PW * i + rr][PW * j + cc] = -sacc;
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < kb * NB; e += 256) {
+    const int r2 = e / NB, c2 = e % NB;
+    if (c2 < kb) a[(int64_t)r2 * lda + c2] = Ls[r2][c2];
+    dinv[r2 * NB + c2] = (c2 < kb) ? Xs[r2][c2] : 0.0;
   }
   if (tid == 0) {
-    double ld = 0.0;
-    for (int j = 0; j < kb; ++j) ld += log(s[j][j]);
     *logdet += 2.0 * ld;
     if (bad && *info == 0) *info = (int)(k0 + 1);
   }

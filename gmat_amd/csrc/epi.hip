@@ -104,6 +104,14 @@ struct ScreenArgs {
   uint8_t *flags;
   int nJ;
   int pf_store;  // side pass 1 also writes the code products of flagged blocks to pfc
+  // covariate directions of the prefilter certificate (P's null space besides 1, pf_ncov of them):
+  // per direction k, the left coding's int8 row images are in SideArgs rs[E3_PF + k] with scales
+  // pf_sU[k][i]; pf_ua[k][i] = u_k . a_i (left screen codes), pf_ub[k][j] = u_k . b_j (right);
+  // pf_su[k] = 1'u_k; the certificate's coefficient of |U'e|^2 is pf_ku
+  const double *pf_sU, *pf_ua, *pf_ub;
+  double pf_su[4];
+  double pf_ku;
+  int pf_ncov;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -497,6 +505,240 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
           for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
       }
       __builtin_amdgcn_sched_barrier(0);  // one element's prefilter at a time
+    }
+  }
+}
+
+// ------------------------------------------------------------------ prefilter pass, covariate designs
+// The same prefilter when P has null directions besides 1 (covariate columns of X): the certificate
+// (gmat_epi_create) is  e'Pe >= mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2  with U the
+// orthonormal null directions, so every pair also needs u_k'e = (a o u_k).b - beta u_k.a - alpha
+// u_k.b + alpha beta 1'u_k for k < NC.  (a o u_k) is a one-slice int8 row image (per-row scale sU):
+// |u_k'e - c~_k| <= sU/2 sum_t b_t = sU csum_r / 2, so |U'e|^2 <= sum_k (|c~_k| + err_k)^2.
+// 64 x 128 (row, column) tiles, 4 waves of 32 x 64 at one wave per SIMD (the NC extra int32
+// accumulator sets per wave need the registers of two); stage image (14 + 4 NC KB, 64 individuals):
+// L3 slices 0, 1 and the NC direction images (64 rows x 64 B each), fp4 codes of a (64 rows x 32 B)
+// and b (128 columns x 32 B); DMA instruction q (1 KB) lands at q KB, wave w issuing q = w + 4u.
+// Five-slot LDS-DMA ring, four stages in flight.
+constexpr int PC_TR = 64, PC_TC = 128, PC_NS = 5, PF_NCOV_MAX = 4;
+template <int NC>
+struct PcShape {
+  static constexpr int NREG = 2 + NC;                  // int8 row regions: L3 slices + directions
+  static constexpr int O_A4 = 4096 * NREG, O_B4 = O_A4 + 2048, ST = O_B4 + 4096;
+  static constexpr int QT = ST / 1024;                 // DMA instructions per stage
+  static constexpr int QW = (QT + 3) / 4;              // per wave (the last ones partly idle)
+};
+// s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier as ONE asm statement (see prefilter_pass_kernel)
+__device__ __forceinline__ void vm_wait_barrier(int n) {
+#define VMW(k) \
+  case k:      \
+    asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+    break;
+  switch (n) {
+    VMW(1) VMW(2) VMW(3) VMW(4) VMW(5) VMW(6) VMW(7) VMW(8) VMW(9) VMW(10) VMW(11) VMW(12) VMW(13) VMW(14)
+    VMW(15) VMW(16) VMW(17) VMW(18) VMW(19) VMW(20) VMW(21) VMW(22) VMW(23) VMW(24) VMW(25) VMW(26) VMW(27)
+    VMW(28) VMW(29) VMW(30) VMW(31) VMW(32)
+    default:
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+#undef VMW
+}
+template <int NC>
+__global__ __launch_bounds__(256, 1) void prefilter_cov_kernel(SideArgs x) {
+  using SH = PcShape<NC>;
+  const ScreenArgs &a = x.a;
+  const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
+  const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
+  const int rt = tile % x.n_rt, ct = tile / x.n_rt;
+  const int r0 = rt * PC_TR;
+  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PC_TC;
+  if (r0 >= a.n_rows || c0 >= a.m) return;
+  if (a.tri && c0 + PC_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
+  // 4 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[PC_NS][SH::ST];
+  const uint8_t *src[SH::QW];
+  int stp[SH::QW];
+  int nq = 0;  // DMA instructions this wave issues per stage
+#pragma unroll
+  for (int u = 0; u < SH::QW; ++u) {
+    const int q = w + 4 * u;
+    src[u] = nullptr;
+    stp[u] = 0;
+    if (q < 4 * SH::NREG) {  // int8 rows: region q / 4, 16 rows x 4 chunks per instruction
+      const int g = q >> 2, row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+      src[u] = (const uint8_t *)x.rs[g] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
+      stp[u] = SG_K;
+      ++nq;
+    } else if (q < SH::QT) {  // fp4 codes: 32 rows x 2 chunks per instruction (2 for a, 4 for b)
+      const int qq = q - 4 * SH::NREG, isb = qq >= 2, row = (isb ? qq - 2 : qq) * 32 + (lane >> 1);
+      const int lg = (lane & 1) ^ ((row >> 3) & 1);
+      const int64_t idx = isb ? min(c0 + row, a.m - 1) : a.rows[min(r0 + row, a.n_rows - 1)];
+      src[u] = (isb ? x.cs4 : x.rs4) + idx * (x.n_pad / 2) + 16 * lg;
+      stp[u] = SG_K / 2;
+      ++nq;
+    }
+  }
+  auto issue = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < SH::QW; ++u)
+      if (w + 4 * u < SH::QT) lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PC_NS][(w + 4 * u) * 1024]);
+  };
+  v16i acc[2][E3_PF], accu[2][NC];
+  v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+#pragma unroll
+      for (int p = 0; p < E3_PF; ++p) acc[q][p][e] = 0;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) accu[q][k][e] = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc4[q][p][e] = 0.f;
+    }
+  }
+  const int S = (int)(x.n_pad / SG_K);
+  const int pre = min(S, PC_NS - 1);
+  for (int st = 0; st < pre; ++st) issue(st);
+  vm_wait_barrier(nq * (pre - 1));
+  const int rrow = 32 * wr + c;
+  for (int st = 0; st < S; ++st) {
+    const uint8_t *bf = ring[st % PC_NS];
+    if (st + PC_NS - 1 < S) issue(st + PC_NS - 1);
+    v4i rb4[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
+      rb4[q] = *(const v4i *)&bf[SH::O_B4 + crow * 32 + 16 * lc];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
+      v4i f[SH::NREG];
+#pragma unroll
+      for (int g = 0; g < SH::NREG; ++g) f[g] = *(const v4i *)&bf[4096 * g + rrow * 64 + 16 * lr];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const v4i fc = i8_of_fp4((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
+#pragma unroll
+        for (int p = 0; p < E3_PF; ++p) acc[q][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[p], fc, acc[q][p], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < NC; ++k)
+          accu[q][k] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[E3_PF + k], fc, accu[q][k], 0, 0, 0);
+      }
+    }
+    {
+      const int lr = h ^ ((rrow >> 3) & 1);
+      v8i_ fa[2];
+      {
+        const v4i ra4 = *(const v4i *)&bf[SH::O_A4 + rrow * 32 + 16 * lr];
+        fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+        fa[1] = sq4(ra4);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        v8i_ fb[2];
+        fb[0] = v8i_{rb4[q][0], rb4[q][1], rb4[q][2], rb4[q][3], 0, 0, 0, 0};
+        fb[1] = sq4(rb4[q]);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
+      }
+    }
+    vm_wait_barrier(nq * (min(st + PC_NS - 1, S - 1) - (st + 1)));
+  }
+  // epilogue as prefilter_pass_kernel, plus the direction terms
+  __shared__ double rowv[7][PC_TR];
+  __shared__ double rowu[2][NC][PC_TR];  // sU, u.a per direction
+  const double n = a.n_id;
+  if (tid < PC_TR) {
+    const int r = min(r0 + tid, a.n_rows - 1);
+    const int64_t i = a.rows[r];
+    const double al = a.alpha[i], ca = a.csum_l[i];
+    rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
+    rowv[1][tid] = al;
+    rowv[2][tid] = ca;
+    rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
+    rowv[4][tid] = a.sL3[i];
+    rowv[5][tid] = a.sa[i];
+    rowv[6][tid] = (2.0 + al) * (2.0 + al);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      rowu[0][k][tid] = a.pf_sU[k * a.m + i];
+      rowu[1][k][tid] = a.pf_ua[k * a.m + i];
+    }
+  }
+  __syncthreads();
+  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
+  const double ku = a.pf_ku * (1.0 + 1e-12);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int64_t j = c0 + 64 * wc + 32 * q + c;
+    const int J = (int)(j / 32);
+    const bool jok = j < a.m && j >= a.j_lo;
+    double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) cub[k] = 0.0;
+    bool cmono = true;
+    if (jok) {
+      cbe = a.beta[j];
+      ccb = a.csum_r[j];
+      const double cb2 = a.csq_r[j];
+      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
+      cnb = n * cbe - ccb;
+      cbsb = cbe * a.spy - a.sb[j];
+      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+      cmono = a.mono_r[j];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) cub[k] = a.pf_ub[k * a.m + j];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+      const bool rok = r < a.n_rows;
+      const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
+      bool live = false;
+      const double iv = rowv[0][rl];
+      if (rok && jok && iv >= 0.0 && !cmono) {
+        const int64_t i = (int64_t)iv;
+        if (!(a.tri && j <= i)) {
+          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
+          double c3 = 0.0;
+#pragma unroll
+          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[q][t][e];
+          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
+          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
+          const double sab = (double)acc4[q][0][e], sa2b = (double)acc4[q][1][e], sab2 = (double)acc4[q][2][e],
+                       sa2b2 = (double)acc4[q][3][e];
+          const double ee =
+              sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
+          const double se = sab - be * rowv[2][rl] + al * cnb;
+          double u2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) {
+            const double sU = rowu[0][k][rl], t1 = sU * (double)accu[q][k][e], t2 = be * rowu[1][k][rl],
+                         t3 = al * cub[k], t4 = al * be * a.pf_su[k];
+            const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sU * ccb * (1.0 + 1e-9) +
+                              1e-12 * (fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4));
+            u2 += ck * ck;
+          }
+          const double vlo = mu_e * ee - k1 * se * se - ku * u2 - k2 * rowv[6][rl] * cmag;
+          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
+        }
+      }
+      const unsigned long long bal = __ballot(live);
+      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
+      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+      if (blk && rok && jok) {
+        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
+        if (a.pf_store)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -1822,6 +2064,49 @@ __global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double ta
 
 // fp4 e2m1 copy of a screen panel (codes 0, 1, 2 -> 0x0, 0x2, 0x4; the prefilter derives the
 // squares' codes in registers, sq4); individual 2q at the low nibble of byte q (the MFMA's packing)
+// A = P + (mu + tau) 11'/n + ku C - mu I  (C = U U', or none)
+__global__ void pf_shift_u_kernel(int64_t n, const double *P, const double *C, double mu, double tau, double ku,
+                                  double *A) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * n) return;
+  double v = P[idx] + (mu + tau) / (double)n;
+  if (C) v += ku * C[idx];
+  if (idx / n == idx % n) v -= mu;
+  A[idx] = v;
+}
+// covariate direction images of a coding: img[j][t] = rint(code[j][t] u[t] / sU[j]) (int8, |.| <= 127),
+// sU[j] = max_t |code u| / 127, dot[j] = sum_t code[j][t] u[t] (fixed-order reduction)
+__global__ __launch_bounds__(256) void cov_image_kernel(int64_t n_pad, const int8_t *panel, const double *u,
+                                                        int8_t *img, double *sU, double *dot) {
+  const int64_t j = blockIdx.x;
+  const int8_t *pj = panel + j * n_pad;
+  __shared__ double rmax[256], rsum[256];
+  double mx = 0.0, sm = 0.0;
+  for (int64_t t = threadIdx.x; t < n_pad; t += 256) {
+    const double v = (double)pj[t] * u[t];
+    mx = fmax(mx, fabs(v));
+    sm += v;
+  }
+  rmax[threadIdx.x] = mx;
+  rsum[threadIdx.x] = sm;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      rmax[threadIdx.x] = fmax(rmax[threadIdx.x], rmax[threadIdx.x + off]);
+      rsum[threadIdx.x] += rsum[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  const double sc = rmax[0] > 0.0 ? rmax[0] / 127.0 : 1.0;
+  for (int64_t t = threadIdx.x; t < n_pad; t += 256) {
+    const double v = (double)pj[t] * u[t];
+    img[j * n_pad + t] = (int8_t)fmin(127.0, fmax(-127.0, rint(v / sc)));
+  }
+  if (threadIdx.x == 0) {
+    sU[j] = sc;
+    dot[j] = rsum[0];
+  }
+}
 __global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= m * (n_pad / 2)) return;
@@ -1867,6 +2152,8 @@ struct Coding {
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
   DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
+  DBuf Lu, sU, uc;                // covariate directions: int8 images of (screen code o u_k) [ncov][m][n_pad],
+                                  // their per-row scales and u_k . code [ncov][m]
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
 };
@@ -1903,6 +2190,10 @@ struct gmat_epi {
   // spectral prefilter: e'Pe >= pf_mu * (|e|^2 - (1'e)^2 / n) - pf_eps * |e|^2 for every e,
   // certified by a Cholesky factorisation of P + pf_mu (11'/n - I); pf_mu = 0: disabled
   double pf_mu = 0, pf_tau = 0, pf_eps = 0;
+  // covariate designs: pf_ncov null directions of P besides 1 enter the certificate with weight pf_ku
+  int pf_ncov = 0;
+  double pf_ku = 0, pf_su[4] = {0, 0, 0, 0};
+  DBuf pf_U;  // [pf_ncov][n_pad] the directions in storage order
   // low-rank screen (lr_screen_kernel): e'Pe >= lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - |Q'e|^2
   // with Q = fp6(bottom eigenvectors x sqrt(d)); lr_R = padded rank (0: disabled)
   int lr_R = 0;
@@ -1924,7 +2215,7 @@ struct gmat_epi {
   double stats[10] = {0};
   // plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition,
   // [3] low-rank certificate, [4] slices + residual bounds, [5] coding builds (side vectors, lazily
-  // in the first scan of a kind), [6] Cholesky factorisations run by the certificates, [7] reserved
+  // in the first scan of a kind), [6] Cholesky factorisations run by the certificates
   double setup[8] = {0};
   hipStream_t s = 0;
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
@@ -2043,6 +2334,17 @@ int build_coding_impl(gmat_epi *e, int which) {
   hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
                      panel, cd.nibI.as<uint32_t>(), cd.nibJ.as<uint32_t>());
   GMAT_HIP(hipGetLastError());
+  if (e->pf_ncov > 0) {  // covariate direction images for the prefilter
+    const int K0 = e->pf_ncov;
+    GMAT_TRY(cd.Lu.alloc((size_t)K0 * m * n_pad));
+    GMAT_TRY(cd.sU.alloc((size_t)K0 * m * sizeof(double)));
+    GMAT_TRY(cd.uc.alloc((size_t)K0 * m * sizeof(double)));
+    for (int k = 0; k < K0; ++k)
+      hipLaunchKernelGGL(cov_image_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel,
+                         e->pf_U.as<double>() + k * n_pad, cd.Lu.as<int8_t>() + (int64_t)k * m * n_pad,
+                         cd.sU.as<double>() + k * m, cd.uc.as<double>() + k * m);
+    GMAT_HIP(hipGetLastError());
+  }
   if (e->lr_R) {  // G = screen codes x B (exact in fp64: fp6 x small integers), kept in fp32
     DBuf g64;
     const int64_t Rp = e->lr_R;
@@ -2103,18 +2405,16 @@ void kind_codings(int kind, int *lc, int *rc) {
 // rounding of A itself (at most (R + 4) u per entry of |P| + lam + 2(lam + tau)/n + |B|D|B'| <=
 // cmax) adds n (R + 4) u (...) in the spectral norm.  Returns GMAT_OK with lr_R = 0 when the
 // screen is disabled (GMAT_LR_RANK=0 / GMAT_NO_LR) or not applicable.
-int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
-  const int64_t n = e->n, n_pad = e->n_pad;
-  const char *renv = getenv("GMAT_LR_RANK"), *kenv = getenv("GMAT_LR_KAPPA");
-  const int R_req = renv ? atoi(renv) : 384;
-  if (R_req <= 0 || getenv("GMAT_NO_LR") || n < 8) return GMAT_OK;
-  const int Re = (int)std::min<int64_t>(R_req, n - 1);
-  const int Rp = (int)cdiv(Re, MXK) * MXK;
-  const int ne = (int)std::min<int64_t>(Re + 1, n);
-  const double kap = kenv ? atof(kenv) : 0.45;
-  double trP = 0.0;
-  for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
-  const double t0 = now();
+// Bottom eigenpairs of P with the intercept direction lifted out of the bottom (P + 4 tr(P)/n
+// 11'/n): rocSOLVER syevd (ascending); lam[r], r < ne, and eigenvector r as row r of Z (natural
+// order).  The screens only need SOME basis and bounds -- every certificate below is checked by its
+// own Cholesky -- so the eigenvectors' accuracy affects tightness, never correctness.
+struct Eigen {
+  int ne = 0;
+  std::vector<double> lam, Z;
+};
+int eigen_bottom(gmat_epi *e, const double *dP, double trP, int ne, Eigen *eg) {
+  const int64_t n = e->n;
   DBuf A, W, E, dinfo;
   GMAT_TRY(A.alloc(n * n * sizeof(double)));
   GMAT_TRY(W.alloc(n * sizeof(double)));
@@ -2127,20 +2427,65 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
   {  // full symmetric eigendecomposition (ascending); column r of the column-major result =
      // eigenvector r = row r of A read row-major
     rocblas_handle hb = nullptr;
-    GMAT_CHECK(rocblas_create_handle(&hb) == rocblas_status_success, GMAT_E_HIP, "lr_setup: rocblas handle");
+    GMAT_CHECK(rocblas_create_handle(&hb) == rocblas_status_success, GMAT_E_HIP, "eigen: rocblas handle");
     const rocblas_status st = rocsolver_dsyevd(hb, rocblas_evect_original, rocblas_fill_lower, (rocblas_int)n,
                                                A.as<double>(), (rocblas_int)n, W.as<double>(), E.as<double>(),
                                                dinfo.as<rocblas_int>());
     GMAT_HIP(hipDeviceSynchronize());
     rocblas_destroy_handle(hb);
-    GMAT_CHECK(st == rocblas_status_success, GMAT_E_HIP, "lr_setup: rocsolver_dsyevd status %d", (int)st);
+    GMAT_CHECK(st == rocblas_status_success, GMAT_E_HIP, "eigen: rocsolver_dsyevd status %d", (int)st);
   }
   int hinfo = 0;
   GMAT_HIP(hipMemcpy(&hinfo, dinfo.p, sizeof(int), hipMemcpyDeviceToHost));
-  GMAT_CHECK(hinfo == 0, GMAT_E_HIP, "lr_setup: syevd info %d", hinfo);
-  std::vector<double> lam_r(ne), Zh((size_t)n * ne);
-  GMAT_HIP(hipMemcpy(lam_r.data(), W.p, ne * sizeof(double), hipMemcpyDeviceToHost));
-  GMAT_HIP(hipMemcpy(Zh.data(), A.p, Zh.size() * sizeof(double), hipMemcpyDeviceToHost));
+  GMAT_CHECK(hinfo == 0, GMAT_E_HIP, "eigen: syevd info %d", hinfo);
+  eg->ne = ne;
+  eg->lam.resize(ne);
+  eg->Z.resize((size_t)n * ne);
+  GMAT_HIP(hipMemcpy(eg->lam.data(), W.p, ne * sizeof(double), hipMemcpyDeviceToHost));
+  GMAT_HIP(hipMemcpy(eg->Z.data(), A.p, eg->Z.size() * sizeof(double), hipMemcpyDeviceToHost));
+  return GMAT_OK;
+}
+
+// Certificate search: the largest x in (0, top] for which ok(x) holds, trying a few candidates just
+// below the eigenvalue estimate first (one Cholesky each; the first success is kept) and bisecting
+// only when all of them fail.  ok returns 1 (certified), 0 (not), < 0 (error).
+template <class F>
+int certify_below(double top, F &&ok, double *best) {
+  static const double fr[] = {1.0 - 2e-3, 1.0 - 2e-2, 0.9, 0.7};
+  double hi = top;
+  for (double f : fr) {
+    const int r = ok(f * top);
+    if (r < 0) return r;
+    if (r) {
+      *best = f * top;
+      return GMAT_OK;
+    }
+    hi = f * top;
+  }
+  double lo = 0.0;
+  for (int it = 0; it < 14; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    const int r = ok(mid);
+    if (r < 0) return r;
+    (r ? lo : hi) = mid;
+  }
+  *best = lo;
+  return GMAT_OK;
+}
+
+int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, const Eigen &eg) {
+  const int64_t n = e->n, n_pad = e->n_pad;
+  const char *renv = getenv("GMAT_LR_RANK"), *kenv = getenv("GMAT_LR_KAPPA");
+  const int R_req = renv ? atoi(renv) : 384;
+  if (R_req <= 0 || getenv("GMAT_NO_LR") || n < 8) return GMAT_OK;
+  const int Re = (int)std::min<int64_t>(std::min<int64_t>(R_req, n - 1), eg.ne - 1);
+  if (Re < 1) return GMAT_OK;
+  const int Rp = (int)cdiv(Re, MXK) * MXK;
+  const int ne = Re + 1;
+  const double kap = kenv ? atof(kenv) : 0.45;
+  double trP = 0.0;
+  for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+  const std::vector<double> &lam_r = eg.lam, &Zh = eg.Z;
   const double t1 = now();
   // Q(lam) = fp6(sqrt(d_r(lam)) u_r), d_r = (lam - lam_r)_+ (1 + kappa): the rows of Q' are the
   // A operand of the screen (tile images) and Q Q' = B D B' enters the certificate exactly.
@@ -2172,7 +2517,8 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
       }
     }
   };
-  DBuf dBn, C, dinv, ld, cinfo;
+  DBuf A, dBn, C, dinv, ld, cinfo;
+  GMAT_TRY(A.alloc(n * n * sizeof(double)));
   GMAT_TRY(dBn.alloc(Bn.size() * sizeof(double)));
   GMAT_TRY(C.alloc(n * n * sizeof(double)));
   GMAT_TRY(dinv.alloc(n * 64 * sizeof(double)));
@@ -2205,21 +2551,15 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax) {
     GMAT_HIP(hipMemcpy(&hi, cinfo.p, sizeof(int), hipMemcpyDeviceToHost));
     return hi == 0 ? 1 : 0;
   };
-  double lo = 0.0, hi = 1.3 * std::max(lam_top, lam_r[Re - 1]);
-  for (int it = 0; it < 20; ++it) {
-    const double mid = 0.5 * (lo + hi);
-    int r = ok(mid);
-    if (r < 0) return r;
-    (r ? lo : hi) = mid;
-  }
+  double lo = 0.0;
+  GMAT_TRY(certify_below(lam_top, ok, &lo));
   quantise(lo, true);  // the certified Q (quantise is deterministic)
-  e->setup[2] = t1 - t0;
   e->setup[3] = now() - t1;
   const double eps = eps_of(lo);
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "lr_setup: R %d (padded %d) lam_0 %.4g lam_R %.4g -> lam %.4g tau %.3g eps %.3g (pf_mu %.4g); "
-                    "eigen %.2f s, certificate %.2f s\n",
-            Re, Rp, lam_r[0], lam_top, lo, tau, eps, e->pf_mu, t1 - t0, now() - t1);
+                    "certificate %.3f s\n",
+            Re, Rp, lam_r[0], lam_top, lo, tau, eps, e->pf_mu, now() - t1);
   if (!(lo > 0.0) || lo <= e->pf_mu || lo < 1e3 * eps) return GMAT_OK;  // no better than the prefilter
   // |c~_r - c_r| <= eta_r = u32 |Q_r|_1 (8 n_pad + 400): fp32 accumulation over n_pad products
   // (w <= 4, one rounding per product, x2 for the MFMA's internal order), the fp32 G' / H and the
@@ -2371,24 +2711,59 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   }
   (void)hipDeviceSynchronize();
   e->setup[4] = now() - t_create;
-  const double t_pf = now();
-  // Spectral prefilter certificate.  If the fp64 Cholesky of A = P + (mu + tau) 11'/n - mu I
+  double trP = 0.0;
+  for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+  // Bottom eigenpairs of P (intercept lifted): the prefilter's covariate directions (P's other null
+  // directions: eigenvalues ~ 0), its mu estimate, and the low-rank screen's basis.
+  Eigen eg;
+  bool have_eig = false;
+  {
+    const double t_eig = now();
+    const char *renv = getenv("GMAT_LR_RANK");
+    const int R_req = renv ? std::max(0, atoi(renv)) : 384;
+    const int ne = (int)std::min<int64_t>(std::max(R_req, 16) + 1, n);
+    have_eig = n >= 8 && !getenv("GMAT_NO_PREFILTER") && eigen_bottom(e, dp.as<double>(), trP, ne, &eg) == GMAT_OK;
+    if (!have_eig && getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: no eigendecomposition (%s)\n", gmat_last_error());
+    e->setup[2] = now() - t_eig;
+  }
+  int K0 = 0;
+  if (have_eig)
+    while (K0 < eg.ne && eg.lam[K0] < 1e-9 * trP / (double)n) ++K0;
+  // Spectral prefilter certificate.  If the fp64 Cholesky of
+  //   A = P + (mu + tau) 11'/n + ku U U' - mu I      (U: the K0 null directions, ku = mu + tau)
   // completes with positive pivots, A + E = LL' with |E| <= gamma_{n+1} |L||L'|, so lambda_min(A)
   // >= -||E||_2 >= -gamma_{n+1} trace(A) (||L||_F^2 = trace(LL')), i.e. for every e
-  //   e'Pe >= mu (|e|^2 - (1'e)^2/n) - tau (1'e)^2/n - eps |e|^2,
-  // eps = 2 gamma_{n+1} trace(A) (x2 margin for the blocked MFMA order).  P 1 = 0 for an
-  // intercept-only model, so tau (a small lift of that direction) keeps A definite; mu is bisected.
-  {
-    DBuf A, dinv, ld, info;
+  //   e'Pe >= mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2,
+  // eps = 2 gamma_{n+1} trace(A) (x2 margin for the blocked MFMA order) + the rounding of forming A.
+  // tau (a small lift) keeps the directions P annihilates definite; mu starts just below the
+  // smallest eigenvalue off those directions.
+  const double t_pf = now();
+  if (have_eig && K0 <= PF_NCOV_MAX && K0 < eg.ne) {
+    DBuf A, dinv, ld, info, dU, C;
     if ((rc = A.alloc(n * n * sizeof(double))) || (rc = dinv.alloc(n * 64 * sizeof(double))) ||
         (rc = ld.alloc(sizeof(double))) || (rc = info.alloc(sizeof(int))))
       return fail(rc);
-    double trP = 0.0;
-    for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+    double cmax = 0.0;
+    if (K0 > 0) {  // C = U'U (n x n) from the eigenvectors, exactly as stored
+      if ((rc = dU.alloc((size_t)K0 * n * sizeof(double))) || (rc = C.alloc(n * n * sizeof(double)))) return fail(rc);
+      if (hipMemcpy(dU.p, eg.Z.data(), (size_t)K0 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("gmat_epi_create: direction upload failed");
+        return fail(GMAT_E_HIP);
+      }
+      if ((rc = dgemm(0, n, n, K0, 1.0, DView{dU.as<double>(), n, 1}, DView{dU.as<double>(), n, 0}, 0.0, C.as<double>(),
+                      n)))
+        return fail(rc);
+      for (int64_t i = 0; i < n; ++i) {
+        double cii = 0.0;
+        for (int k = 0; k < K0; ++k) cii += eg.Z[(size_t)k * n + i] * eg.Z[(size_t)k * n + i];
+        cmax = std::max(cmax, cii);
+      }
+    }
     const double tau0 = 1e-8 * trP / (double)n;
     auto ok = [&](double mu) -> int {  // 1 = certified, 0 = not, < 0 error
-      hipLaunchKernelGGL(pf_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dp.as<double>(), mu,
-                         tau0 + 1e-6 * mu, A.as<double>());
+      const double tau = tau0 + 1e-6 * mu;
+      hipLaunchKernelGGL(pf_shift_u_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dp.as<double>(),
+                         K0 ? C.as<double>() : nullptr, mu, tau, mu + tau, A.as<double>());
       if (hipGetLastError() != hipSuccess) return -1;
       if (cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), info.as<int>()) != GMAT_OK) return -1;
       e->setup[6] += 1;
@@ -2396,26 +2771,47 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
       if (hipMemcpy(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
       return hinfo == 0 ? 1 : 0;
     };
-    double lo = 0.0, hi = 2.0 * trP / (double)n;  // mu above the mean eigenvalue cannot pass
-    for (int it = 0; it < 24; ++it) {
-      const double mid = 0.5 * (lo + hi);
-      const int r = ok(mid);
-      if (r < 0) {
-        set_error("gmat_epi_create: prefilter certificate failed");
-        return fail(GMAT_E_HIP);
-      }
-      (r ? lo : hi) = mid;
+    double lo = 0.0;
+    if (certify_below(eg.lam[K0], ok, &lo) != GMAT_OK) {
+      set_error("gmat_epi_create: prefilter certificate failed");
+      return fail(GMAT_E_HIP);
     }
-    const double eps = 2.0 * (double)(n + 1) * std::ldexp(1.0, -53) * (trP + tau0 + 1e-6 * lo + lo * (1.0 - (double)n)) * 1.01;
+    const double tau = tau0 + 1e-6 * lo, u = std::ldexp(1.0, -53);
+    const double trA = trP + (lo + tau) + (lo + tau) * K0 - (double)n * lo;
+    const double eps = 2.0 * (double)(n + 1) * u * std::fabs(trA) * 1.01 +
+                       (double)n * (K0 + 4) * u * (pmax + lo + 2.0 * (lo + tau) / (double)n + (lo + tau) * cmax);
     if (lo > 0.0 && lo > 1e3 * eps) {
       e->pf_mu = lo;
-      e->pf_tau = tau0 + 1e-6 * lo;
+      e->pf_tau = tau;
       e->pf_eps = eps + 1e-15 * lo;
+      e->pf_ku = lo + tau;
+      e->pf_ncov = K0;
+      if (K0 > 0) {  // the directions in storage order for the codings' images
+        std::vector<double> Us((size_t)K0 * n_pad, 0.0);
+        for (int k = 0; k < K0; ++k) {
+          double su = 0.0;
+          for (int64_t c = 0; c < n; ++c) su += eg.Z[(size_t)k * n + c];
+          e->pf_su[k] = su;
+          for (int64_t q = 0; q < n_pad; ++q) {
+            const int64_t c = (q & ~31LL) + perm_nat((int)(q & 31));
+            if (c < n) Us[(size_t)k * n_pad + q] = eg.Z[(size_t)k * n + c];
+          }
+        }
+        if ((rc = e->pf_U.alloc(Us.size() * sizeof(double)))) return fail(rc);
+        if (hipMemcpy(e->pf_U.p, Us.data(), Us.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+          set_error("gmat_epi_create: direction upload failed");
+          return fail(GMAT_E_HIP);
+        }
+      }
     }
-    if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: prefilter mu %.6g eps %.3g (trace/n %.4g)\n", lo, eps, trP / n);
+    if (getenv("GMAT_DEBUG"))
+      fprintf(stderr, "gmat_epi_create: prefilter mu %.6g (lam %.6g) eps %.3g, %d covariate directions (trace/n %.4g)\n", lo,
+              eg.lam[K0], eps, K0, trP / n);
+  } else if (getenv("GMAT_DEBUG")) {
+    fprintf(stderr, "gmat_epi_create: prefilter off (%d null directions, eigen %d)\n", K0, (int)have_eig);
   }
   e->setup[1] = now() - t_pf;
-  if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax)) != GMAT_OK) {
+  if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax, eg)) != GMAT_OK) {
     // the low-rank screen is an accelerator: without it the MX screen runs
     if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: low-rank screen unavailable: %s\n", gmat_last_error());
     e->lr_R = 0;
@@ -2436,7 +2832,8 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
 
 extern "C" int gmat_epi_setup_stats(const gmat_epi *e, double *out8) {
   GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_setup_stats: bad arguments");
-  for (int k = 0; k < 8; ++k) out8[k] = e->setup[k];
+  for (int k = 0; k < 7; ++k) out8[k] = e->setup[k];
+  out8[7] = e->pf_ncov;
   return GMAT_OK;
 }
 
@@ -2765,6 +3162,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.pf_mu = e->pf_mu;
     sa.pf_eps = e->pf_eps;
     sa.pf_tau = e->pf_tau;
+    sa.pf_ncov = e->pf_ncov;
+    sa.pf_ku = e->pf_ku;
+    for (int k = 0; k < 4; ++k) sa.pf_su[k] = e->pf_su[k];
+    sa.pf_sU = e->pf_ncov ? L.sU.as<double>() : nullptr;
+    sa.pf_ua = e->pf_ncov ? L.uc.as<double>() : nullptr;
+    sa.pf_ub = e->pf_ncov ? R.uc.as<double>() : nullptr;
     sa.n_id = (double)e->n;
     sa.flags = use_pf ? flags[b].as<uint8_t>() : nullptr;
     sa.nJ = (int)nJ;
@@ -2832,11 +3235,22 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.cs[0] = srp;
       x.rs4 = L.p4.as<uint8_t>();
       x.cs4 = R.p4.as<uint8_t>();
-      {  // prefilter pass: 128 x 128 tiles
+      if (e->pf_ncov == 0) {  // prefilter pass: 128 x 128 tiles
         SideArgs xp = x;
         xp.n_rt = (int)cdiv(Rn, PF_T);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_T));
         hipLaunchKernelGGL(prefilter_pass_kernel, dim3(gp), dim3(512), 0, S2, xp);
+      } else {  // covariate designs: 64 x 128 tiles with the direction products
+        SideArgs xp = x;
+        for (int k = 0; k < e->pf_ncov; ++k) xp.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
+        xp.n_rt = (int)cdiv(Rn, PC_TR);
+        const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PC_TC));
+        switch (e->pf_ncov) {
+          case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, dim3(gp), dim3(256), 0, S2, xp); break;
+          case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, dim3(gp), dim3(256), 0, S2, xp); break;
+          case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, dim3(gp), dim3(256), 0, S2, xp); break;
+          default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, dim3(gp), dim3(256), 0, S2, xp); break;
+        }
       }
       GMAT_HIP(hipGetLastError());
       if (x.a.pf_store) {  // the low-rank screen needs nothing else

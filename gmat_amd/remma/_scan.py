@@ -73,7 +73,7 @@ class EpiPlan:
         s = np.zeros(8)
         N.check(self._lib.gmat_epi_setup_stats(self._h, N.ptr(s)), "gmat_epi_setup_stats")
         keys = ("create_s", "prefilter_cert_s", "eigen_s", "lowrank_cert_s", "slices_bounds_s", "coding_s",
-                "cholesky_count")
+                "cholesky_count", "covariate_directions")
         return dict(zip(keys, s.tolist()))
 
     def lowrank_rank(self):

@@ -119,7 +119,7 @@ int gmat_epi_info(const gmat_epi *e, double *out4);
 /* plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition
  * of P, [3] low-rank certificate, [4] slices and residual bounds, [5] coding builds (side vectors;
  * done lazily by the first scan of each coding), [6] Cholesky factorisations the certificates ran,
- * [7] reserved */
+ * [7] covariate directions in the prefilter certificate (null directions of P besides 1) */
 int gmat_epi_setup_stats(const gmat_epi *e, double *out8);
 int gmat_epi_destroy(gmat_epi *e);
 

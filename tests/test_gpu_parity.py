@@ -180,6 +180,27 @@ def test_mouse_scans(mouse_dir, tmp_path):
     _cmp_hits(str(tmp_path / "dd"), os.path.join(MOUSE, "epiDD_1e-5"))
 
 
+def test_mouse_covariates_keep_fast_path(mouse_dir):
+    """The mouse pheno (intercept + 3 covariates): the plan certifies the prefilter with the
+    covariate directions and builds the low-rank screen, so the golden scans above ran on the
+    low-rank level (round 1 fell back to the fp6 quadratic form for every covariate design)."""
+    from gmat_amd.remma._scan import open_plan
+    from gmat_amd.uvlmm.design_matrix import design_matrix_wemai_multi_gmat
+    ref = np.load(os.path.join(MOUSE, "reml.npz"))
+    ka, _ = _mouse_grms(mouse_dir)
+    y, x, z = design_matrix_wemai_multi_gmat(mouse_dir.replace("plink", "pheno"), mouse_dir)
+    assert x.shape[1] == 4
+    plan = open_plan(y, x, z, [ka, ka * ka], ref["var2"], mouse_dir)
+    try:
+        assert plan.setup_stats()["covariate_directions"] == 3
+        assert plan.lowrank_rank() > 0
+        plan.scan("AA", np.arange(plan.geno.m - 1), 1e-5)
+        assert plan.stats()["n_slice"] == -1
+    finally:
+        plan.close()
+        plan.geno.close()
+
+
 def test_mouse_pairs_and_parallel(mouse_dir, tmp_path):
     import gmat_amd.remma as R
     ref = np.load(os.path.join(MOUSE, "reml.npz"))

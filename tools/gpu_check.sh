@@ -16,6 +16,6 @@ if [ "${BENCH:-1}" = "1" ]; then
   cat $OUT/bench.json
 fi
 if [ "${PROF:-1}" = "1" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
   find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -14 {} | cut -c1-180'
 fi
