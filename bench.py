@@ -199,7 +199,7 @@ def e2e_bench(geno, ka, y, var, p_cut, hits_step):
             "what": "remma_epiAA(pheno, bed, [A, AxA], var, p_cut) from files to the hits file"}
 
 
-def covariate_bench(g, ka, n, m, p_cut, seed, steps, ms_intercept):
+def covariate_bench(g, ka, y0, n, m, p_cut, seed, steps, ms_intercept):
     """configs[2] with intercept + 3 covariates (binary, integer-valued, binary: the layout of the
     reference's example pheno): P gains three null directions besides 1; the plan certifies the
     prefilter with them (prefilter_cov_kernel) and keeps the low-rank screen.  Whole-scan time."""
@@ -210,7 +210,7 @@ def covariate_bench(g, ka, n, m, p_cut, seed, steps, ms_intercept):
     lib = N.ensure_device()
     rng = np.random.Generator(np.random.PCG64(seed + 9))
     x = np.column_stack([np.ones(n), rng.integers(0, 2, n), rng.integers(90, 130, n), rng.integers(0, 2, n)])
-    y = 1.0 + 0.3 * x[:, 1] + 0.01 * x[:, 2] + rng.standard_normal(n)
+    y = y0 + 0.3 * x[:, 1] + 0.01 * x[:, 2] - 0.2 * x[:, 3]  # the headline phenotype + covariate effects
     pvp, py = projection(y, x.astype(float), identity(n, format="csr"), [ka, ka * ka], [0.4, 0.2, 0.4])
     rows = np.arange(m - 1, dtype=np.int64)
     t0 = time.perf_counter()
@@ -391,7 +391,7 @@ def main():
             reml = reml_bench(grm_bench.last_k, args.seed)
     cov = None
     if rank == 0 and ws == 1 and not args.no_cov:
-        cov = covariate_bench(g, ka, n, m, args.p_cut, args.seed, 2, t_max / args.steps * 1e3)
+        cov = covariate_bench(g, ka, y, n, m, args.p_cut, args.seed, 2, t_max / args.steps * 1e3)
     e2e = None
     if rank == 0 and ws == 1 and not args.no_e2e:
         e2e = e2e_bench(geno, ka, y, var, args.p_cut, int(round(hits_all)))
