@@ -37,17 +37,18 @@ def log(*a):
 
 
 def build_inputs(n, m, seed, var, rank, ws):
-    """Cohort (deterministic), genotype shards all-gathered over RCCL, P/Py from rank 0."""
+    """Cohort (deterministic, generated shard by shard: rank r makes only its SNP range), the
+    packed shards all-gathered over RCCL, P / Py computed on rank 0 and broadcast."""
     from gmat_amd import dist, synth
     from gmat_amd import _native as N
     nb = (n + 3) // 4
     t0 = time.time()
-    geno = synth.simulate_genotypes(n, m, seed=seed)  # (m, n), identical on every rank
-    body_full = np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8)
     lo, hi = dist.snp_shard(m, rank, ws)
-    body = dist.allgather_packed(body_full.reshape(m, nb)[lo:hi], m, nb)
-    assert np.array_equal(body, body_full), "all-gathered genotype panel differs"
-    log("cohort %d x %d generated + all-gathered in %.1f s" % (n, m, time.time() - t0))
+    shard = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed)  # (hi - lo, n)
+    local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
+    body = dist.allgather_packed(local, m, nb)
+    geno = shard if ws == 1 else None
+    log("cohort %d x %d: shard [%d, %d) generated, panel all-gathered in %.1f s" % (n, m, lo, hi, time.time() - t0))
     import ctypes
     from gmat_amd.plink import Geno
     g = Geno(body=body, n_id=n, n_snp=m)

@@ -52,6 +52,14 @@ _PROTOS = {
     "gmat_float_repr": (_INT, [_D, ctypes.c_char_p, _INT]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
     "gmat_probe_mx_accum": (_INT, [_INT, _P, _P, _P]),
+    "gmat_comm_unique_id": (_INT, [_P]),
+    "gmat_comm_init": (_INT, [_P, _INT, _INT, _P]),
+    "gmat_comm_destroy": (_INT, [_P]),
+    "gmat_comm_allgather": (_INT, [_P, _P, _P, _I64]),
+    "gmat_comm_broadcast": (_INT, [_P, _P, _I64, _INT]),
+    "gmat_comm_allreduce_f64": (_INT, [_P, _P, _I64, _INT]),
+    "gmat_comm_gatherv": (_INT, [_P, _P, _I64, _INT, _P, _P, _I64, _P]),
+    "gmat_comm_barrier": (_INT, [_P]),
     # include/gmat_remma_eff.h: the reference's cffi prototypes (char*, long long, ...)
     "read_plink_bed": (_INT, [ctypes.c_char_p, _I64, _I64, _P]),
     "remma_epiAA_eff_cpu": (_INT, [ctypes.c_char_p, _I64, _I64, _P, _I64, _P, _D, ctypes.c_char_p]),

@@ -1,12 +1,11 @@
 """Multi-GPU sharding of the exhaustive scans.
 
-One process per GPU (torchrun / torch.distributed.run).  Pairs are independent units once
-every rank holds the genotype panel, P and Py, so the scan shards with no collective on
-its hot path:
+One process per GPU (launched by torch.distributed.run / torchrun, which only sets RANK,
+WORLD_SIZE, LOCAL_RANK, MASTER_*).  Pairs are independent units once every rank holds the
+genotype panel, P and Py, so the scan shards with no collective on its hot path:
 
-* genotype panel: each rank reads (or generates) its contiguous shard of SNPs and the
-  packed 2-bit shards are all-gathered -- RCCL over xGMI with the ``nccl`` backend
-  (25 MB at 2,000 x 50,000), gloo on CPU;
+* genotype panel: each rank reads (or generates) its contiguous shard of SNPs and the packed
+  2-bit shards are all-gathered (25 MB at 2,000 x 50,000);
 * P and Py: computed on rank 0 and broadcast (32 MB at n = 2,000);
 * scan: rank r scans the rows of part r+1 of the reference's triangle-folded split
   ``parallel=[N, r+1]`` (remma_epiAA.py:125-139), equal pair counts per rank;
@@ -14,12 +13,20 @@ its hot path:
   single-GPU scan writes, bit-identical values (each pair is computed by one rank with a
   fixed reduction order).
 
-The per-rank compute is injected (``scan_fn``) so the sharding and merge logic is tested
-on CPU with gloo and the oracle; the product path passes the HIP plan's scan.
+Backends.  ``rccl`` (the product path on GPUs): the exchanges run in libgmat_hip on RCCL over
+xGMI (gmat_comm_* in include/gmat_hip.h); no PyTorch is imported.  The 128-byte unique id is
+created by rank 0 and shared through a file in the temp directory keyed by the launcher
+(single-node runs, as bench.py's contract).  ``gloo`` (torch.distributed on CPU) is kept only as
+the test harness of tests/test_dist_cpu.py, with the per-rank compute injected (``scan_fn``).
 """
+import ctypes
 import os
+import tempfile
+import time
 
 import numpy as np
+
+_state = {"backend": None, "comm": None}
 
 
 def world():
@@ -28,56 +35,132 @@ def world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def backend():
+    return _state["backend"]
+
+
+def _id_file():
+    key = "%s_%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "na"), os.getppid())
+    return os.path.join(tempfile.gettempdir(), "gmat_rccl_id_" + key)
+
+
+def _init_rccl(rank, ws):
+    from . import _native as N
+    lib = N.ensure_device()  # binds LOCAL_RANK's GPU before the communicator
+    path = _id_file()
+    uid = (ctypes.c_uint8 * 128)()
+    if rank == 0:
+        N.check(lib.gmat_comm_unique_id(uid), "gmat_comm_unique_id")
+        tmp = path + ".tmp%d" % os.getpid()
+        with open(tmp, "wb") as f:
+            f.write(bytes(uid))
+        os.replace(tmp, path)
+    else:
+        t0 = time.time()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    data = f.read()
+                if len(data) == 128:
+                    break
+            except FileNotFoundError:
+                pass
+            if time.time() - t0 > 120:
+                raise RuntimeError("rank %d: no RCCL unique id from rank 0 at %s" % (rank, path))
+            time.sleep(0.01)
+        ctypes.memmove(uid, data, 128)
+    comm = ctypes.c_void_p()
+    N.check(lib.gmat_comm_init(ctypes.byref(comm), ws, rank, uid), "gmat_comm_init")
+    _state["comm"] = comm
+    N.check(lib.gmat_comm_barrier(comm), "gmat_comm_barrier")
+    if rank == 0:
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+
+
 def init(backend=None):
-    """Initialise torch.distributed when WORLD_SIZE > 1.  Returns the backend used (None
-    for a single process).  ``nccl`` is RCCL on ROCm."""
+    """Set up the process group when WORLD_SIZE > 1.  Returns the backend used (None for a
+    single process).  Default ``rccl`` when a GPU is visible, else ``gloo``; GMAT_DIST_BACKEND
+    overrides."""
     rank, ws, local = world()
     if ws <= 1:
         return None
-    import torch
-    import torch.distributed as dist
-    if dist.is_initialized():
-        return dist.get_backend()
+    if _state["backend"] is not None:
+        return _state["backend"]
     if backend is None:
-        backend = os.environ.get("GMAT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if backend == "nccl":
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend, device_id=torch.device("cuda", local))
-    else:
-        dist.init_process_group(backend)
+        backend = os.environ.get("GMAT_DIST_BACKEND")
+    if backend is None:
+        from . import _native as N
+        lib = N.load(required=False)
+        backend = "rccl" if lib is not None and N.device_count() > 0 else "gloo"
+    if backend == "rccl":
+        try:
+            _init_rccl(rank, ws)
+        except Exception as exc:  # e.g. two ranks on one GPU (RCCL: invalid usage)
+            if os.environ.get("GMAT_DIST_BACKEND") == "rccl":
+                raise
+            import sys
+            print("gmat_amd.dist: RCCL unavailable (%s); exchanging over gloo" % exc, file=sys.stderr)
+            backend = "gloo"
+    if backend == "gloo":
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not tdist.is_initialized():
+            tdist.init_process_group("gloo")
+    elif backend != "rccl":
+        raise ValueError("unknown backend %r (rccl | gloo)" % backend)
+    _state["backend"] = backend
     return backend
 
 
-def _device(backend):
-    import torch
-    return torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+def _require():
+    rank, ws, _ = world()
+    if ws > 1 and _state["backend"] is None:
+        raise RuntimeError("WORLD_SIZE=%d but no process group is initialised: a single rank would "
+                           "see only its own share (call dist.init() first)" % ws)
+    return _state["backend"]
+
+
+def _lib():
+    from . import _native as N
+    return N, N.load()
 
 
 def barrier():
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        dist.barrier()
+    b = _require()
+    if b == "rccl":
+        N, lib = _lib()
+        N.check(lib.gmat_comm_barrier(_state["comm"]), "gmat_comm_barrier")
+    elif b == "gloo":
+        import torch.distributed as tdist
+        tdist.barrier()
+
+
+def _allreduce(x, op):
+    b = _require()
+    if b is None:
+        return float(x)
+    if b == "rccl":
+        N, lib = _lib()
+        v = np.array([float(x)])
+        N.check(lib.gmat_comm_allreduce_f64(_state["comm"], N.ptr(v), 1, 1 if op == "max" else 0),
+                "gmat_comm_allreduce_f64")
+        return float(v[0])
+    import torch
+    import torch.distributed as tdist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX if op == "max" else tdist.ReduceOp.SUM)
+    return float(t.item())
 
 
 def allreduce_max(x):
-    import torch
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()):
-        return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=_device(dist.get_backend()))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _allreduce(x, "max")
 
 
 def allreduce_sum(x):
-    import torch
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()):
-        return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=_device(dist.get_backend()))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _allreduce(x, "sum")
 
 
 def snp_shard(m, rank, ws):
@@ -88,36 +171,43 @@ def snp_shard(m, rank, ws):
 
 def allgather_packed(local_rows, m, nb):
     """All-gather the packed .bed rows (uint8, (hi-lo) x nb) of every rank's SNP shard into
-    the full (m x nb) packed panel (RCCL all_gather on the GPU with nccl)."""
-    import torch
-    import torch.distributed as dist
+    the full (m x nb) packed panel."""
+    b = _require()
     rank, ws, _ = world()
-    if not (dist.is_available() and dist.is_initialized()) or ws == 1:
+    if b is None or ws == 1:
         return np.ascontiguousarray(local_rows).reshape(-1)
     per = (m + ws - 1) // ws
-    dev = _device(dist.get_backend())
     buf = np.zeros((per, nb), dtype=np.uint8)
     buf[: local_rows.shape[0]] = local_rows
-    src = torch.from_numpy(buf).to(dev)
+    if b == "rccl":
+        N, lib = _lib()
+        out = np.empty((ws * per, nb), dtype=np.uint8)
+        N.check(lib.gmat_comm_allgather(_state["comm"], N.ptr(buf), N.ptr(out), buf.nbytes), "gmat_comm_allgather")
+        return np.ascontiguousarray(out[:m]).reshape(-1)
+    import torch
+    import torch.distributed as tdist
+    src = torch.from_numpy(buf)
     outs = [torch.empty_like(src) for _ in range(ws)]
-    dist.all_gather(outs, src)
-    full = torch.cat(outs, dim=0)[:m].cpu().numpy()
-    return np.ascontiguousarray(full).reshape(-1)
+    tdist.all_gather(outs, src)
+    return np.ascontiguousarray(torch.cat(outs, dim=0)[:m].numpy()).reshape(-1)
 
 
 def broadcast_array(arr, src=0, shape=None, dtype=np.float64):
     """Broadcast a numpy array from `src` (other ranks pass arr=None with shape)."""
-    import torch
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()):
+    b = _require()
+    if b is None:
         return arr
-    dev = _device(dist.get_backend())
-    if dist.get_rank() == src:
-        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=dtype)).to(dev)
-    else:
-        t = torch.empty(tuple(shape), dtype=torch.from_numpy(np.zeros(1, dtype)).dtype, device=dev)
-    dist.broadcast(t, src)
-    return t.cpu().numpy()
+    rank, _, _ = world()
+    buf = np.ascontiguousarray(arr, dtype=dtype) if rank == src else np.empty(tuple(shape), dtype=dtype)
+    if b == "rccl":
+        N, lib = _lib()
+        N.check(lib.gmat_comm_broadcast(_state["comm"], N.ptr(buf), buf.nbytes, int(src)), "gmat_comm_broadcast")
+        return buf
+    import torch
+    import torch.distributed as tdist
+    t = torch.from_numpy(buf.copy())
+    tdist.broadcast(t, src)
+    return t.numpy()
 
 
 def rank_rows(kind, num_snp, rank, ws, rows=None):
@@ -140,19 +230,60 @@ def merge_hits(parts):
     return tuple(c[order] for c in cat)
 
 
+_HIT = np.dtype([("i", "<i8"), ("j", "<i8"), ("eff", "<f8"), ("var", "<f8"), ("chi", "<f8"), ("p", "<f8")])
+
+
+def _pack_hits(local):
+    if local is None or not len(local[0]):
+        return np.zeros(0, dtype=_HIT)
+    rec = np.empty(len(local[0]), dtype=_HIT)
+    for name, col in zip(_HIT.names, local):
+        rec[name] = col
+    return rec
+
+
+def _unpack_hits(rec):
+    return tuple(np.ascontiguousarray(rec[name]) for name in _HIT.names)
+
+
+def gather_hits(local, root=0):
+    """Hit tuples of every rank merged on `root` (None elsewhere)."""
+    b = _require()
+    rank, ws, _ = world()
+    if b is None or ws == 1:
+        return merge_hits([local])
+    if b == "rccl":
+        N, lib = _lib()
+        send = _pack_hits(local)
+        sizes = np.zeros(ws)
+        sizes[rank] = send.nbytes
+        N.check(lib.gmat_comm_allreduce_f64(_state["comm"], N.ptr(sizes), ws, 0), "gmat_comm_allreduce_f64")
+        total = int(sizes.sum())
+        recv = np.zeros(total // _HIT.itemsize if rank == root else 0, dtype=_HIT)
+        counts = np.zeros(ws, np.int64)
+        need = ctypes.c_int64()
+        N.check(lib.gmat_comm_gatherv(_state["comm"], N.ptr(send) if send.size else None, send.nbytes, root,
+                                      N.ptr(counts), N.ptr(recv) if recv.size else None, recv.nbytes,
+                                      ctypes.byref(need)), "gmat_comm_gatherv")
+        if rank != root:
+            return None
+        parts, off = [], 0
+        for r in range(ws):
+            k = int(counts[r]) // _HIT.itemsize
+            parts.append(_unpack_hits(recv[off:off + k]))
+            off += k
+        return merge_hits(parts)
+    import torch.distributed as tdist
+    gathered = [None] * ws if rank == root else None
+    tdist.gather_object(None if local is None else tuple(np.asarray(a) for a in local), gathered, dst=root)
+    return merge_hits(gathered) if rank == root else None
+
+
 def distributed_scan(scan_fn, kind, num_snp, p_cut, rows=None):
     """Run ``scan_fn(kind, my_rows, p_cut) -> (i, j, eff, var, chi, p)`` on this rank's
     share and gather the merged hits on rank 0 (other ranks get None)."""
+    _require()
     rank, ws, _ = world()
-    if ws > 1:
-        import torch.distributed as dist
-        if not (dist.is_available() and dist.is_initialized()):
-            raise RuntimeError("WORLD_SIZE=%d but no process group is initialised: a single rank would "
-                               "return only its own share of the hits (call dist.init() first)" % ws)
     mine = rank_rows(kind, num_snp, rank, ws, rows)
     local = scan_fn(kind, mine, p_cut) if mine.size else None
-    if ws == 1:
-        return merge_hits([local])
-    gathered = [None] * ws if rank == 0 else None
-    dist.gather_object(None if local is None else tuple(np.asarray(a) for a in local), gathered, dst=0)
-    return merge_hits(gathered) if rank == 0 else None
+    return gather_hits(local)

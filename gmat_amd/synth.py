@@ -44,6 +44,43 @@ def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, ma
     return geno
 
 
+def simulate_genotype_shard(n_id, n_snp, lo, hi, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01):
+    """SNPs [lo, hi) of a related cohort, generated block by block so that any SNP range is
+    produced on its own (each rank of a sharded run makes only its shard) and the
+    concatenation of any split equals the whole cohort.  The pedigree (parents per generation)
+    comes from `seed`; every block of `block` SNPs has its own stream for the founder
+    frequencies and haplotypes, the per-block inheritance choices and the re-draws of
+    (near-)monomorphic SNPs.  Returns an (hi - lo, n_id) uint8 dosage matrix in {0, 1, 2}."""
+    ss = np.random.SeedSequence([seed, 0x9E3779B9])
+    rng = np.random.Generator(np.random.PCG64(ss.spawn(1)[0]))
+    sizes, parents = [n_founder], []
+    for g in range(n_gen):
+        n_next = n_id if g == n_gen - 1 else max(n_id, sizes[-1])
+        parents.append(rng.integers(0, sizes[-1], size=(2, n_next)))
+        sizes.append(n_next)
+    out = np.empty((max(0, hi - lo), n_id), dtype=np.uint8)
+    for b in range(lo // block, (hi + block - 1) // block if hi > lo else lo // block):
+        b0, b1 = b * block, min(n_snp, (b + 1) * block)
+        brng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, 1, b])))
+        freq = brng.uniform(0.1, 0.9, size=b1 - b0)
+        pop = brng.random((2 * n_founder, b1 - b0)) < freq
+        for g in range(n_gen):
+            pick = brng.integers(0, 2, size=(2, sizes[g + 1]))
+            new = np.empty((2 * sizes[g + 1], b1 - b0), dtype=bool)
+            for side in range(2):
+                par = parents[g][side]
+                new[side::2] = pop[2 * par + pick[side]]
+            pop = new
+        geno = (pop[0::2].astype(np.uint8) + pop[1::2].astype(np.uint8))
+        p = geno.sum(axis=0) / (2.0 * n_id)
+        bad = np.where(np.minimum(p, 1 - p) < maf_min)[0]
+        if bad.size:
+            geno[:, bad] = brng.binomial(2, 0.5, size=(n_id, bad.size)).astype(np.uint8)
+        s0, s1 = max(lo, b0), min(hi, b1)
+        out[s0 - lo:s1 - lo] = geno[:, s0 - b0:s1 - b0].T
+    return out
+
+
 def pack_bed(geno, missing=None):
     """Pack an (n_snp, n_id) dosage matrix into PLINK .bed bytes (with the 3-byte magic)."""
     m, n = geno.shape

@@ -164,6 +164,28 @@ int gmat_snp_test(gmat_geno *g, int kind, const double *pvp, const double *py, d
  * reference's read_plink_bed (_read_plink_bed.c:5-51). */
 int gmat_geno_decode(const gmat_geno *g, double *marker_mat);
 
+/* ---- multi-GPU exchange (RCCL over xGMI; one process per GPU) ----
+ * The sharded scans need one-off exchanges only: the all-gather of the packed
+ * genotype shards, the broadcast of P / Py from rank 0 and the gather of the hit records (the
+ * reference runs separate parallel=[N,k] processes that each write out_file.k,
+ * remma_epiAA.py:109-161).  Host buffers in and out; every call returns when its result is on
+ * the host.  Rank 0 creates the 128-byte unique id, the launcher shares it (gmat_amd/dist.py). */
+typedef struct gmat_comm gmat_comm;
+int gmat_comm_unique_id(uint8_t *out128);
+int gmat_comm_init(gmat_comm **out, int nranks, int rank, const uint8_t *id128);
+int gmat_comm_destroy(gmat_comm *c);
+/* recv (nranks x bytes, rank order) = every rank's send (bytes) */
+int gmat_comm_allgather(gmat_comm *c, const void *send, void *recv, int64_t bytes);
+/* buf (bytes) from root to every rank, in place */
+int gmat_comm_broadcast(gmat_comm *c, void *buf, int64_t bytes, int root);
+/* in place over ranks: op 0 = sum, 1 = max (fp64) */
+int gmat_comm_allreduce_f64(gmat_comm *c, double *v, int64_t count, int op);
+/* variable-length byte records to root: counts[nranks] on every rank; root's recv gets the payloads
+ * back to back in rank order (GMAT_E_OVERFLOW with *needed when recv_cap is too small) */
+int gmat_comm_gatherv(gmat_comm *c, const void *send, int64_t bytes, int root, int64_t *counts, void *recv,
+                      int64_t recv_cap, int64_t *needed);
+int gmat_comm_barrier(gmat_comm *c);
+
 /* ---- diagnostics ----
  * The low-rank screen's accumulation (lr_screen_kernel) on one wave: a chain of n_steps
  * v_mfma_scale_f32_32x32x64_f8f6f4 (A fp6 e2m3 codes[n_steps][32 rows][2 halves][32] with e8m0
