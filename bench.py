@@ -269,6 +269,96 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
             "reference_c_8_threads_pairs_per_s": 3.3e6}
 
 
+def cfg5_main(args):
+    """BASELINE configs[4]: synthetic 5,000 x 100,000 cohort, 5-GRM model [A, D, AxA, AxD, DxD]:
+    GRMs (agmat / dgmat_as products), weighted EM-AI REML (first --reml-iters iterations timed),
+    P / Py, then the exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included)
+    scans at p_cut, rows sharded over the ranks like configs[3].  One JSON line."""
+    import ctypes
+    from gmat_amd import dist, synth
+    from gmat_amd import _native as N
+    from gmat_amd.plink import Geno
+    from gmat_amd.remma._scan import EpiPlan
+    from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat, projection
+    from scipy.sparse import identity
+    backend = dist.init()
+    rank, ws, _ = dist.world()
+    lib = N.ensure_device()
+    n, m = args.n_id, args.n_snp
+    nb = (n + 3) // 4
+    t0 = time.time()
+    lo, hi = dist.snp_shard(m, rank, ws)
+    local = np.frombuffer(synth.pack_bed(synth.simulate_genotype_shard(n, m, lo, hi, seed=args.seed))[3:],
+                          dtype=np.uint8).reshape(hi - lo, nb)
+    g = Geno(body=dist.allgather_packed(local, m, nb), n_id=n, n_snp=m)
+    log("cfg5 cohort %d x %d in %.1f s" % (n, m, time.time() - t0))
+    var = np.array([0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
+    out = {"metric": "SNP-pairs tested/sec (whole node), configs[4]", "unit": "SNP-pairs/s", "n_gpus": ws,
+           "higher_is_better": True, "data": "synthetic", "dtype": "fp6xfp4/fp64",
+           "config": {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP, p_cut=%g"
+                                  % (n, m, args.p_cut), "n_id": n, "n_snp": m, "p_cut": args.p_cut,
+                      "parallelism": "rows folded over %d rank(s), backend %s" % (ws, backend or "single")}}
+    pvp = py = None
+    if rank == 0:
+        mats, grm = [], {}
+        for kind, name in ((0, "A"), (1, "D")):
+            k = np.empty((n, n))
+            sc = ctypes.c_double()
+            t1 = time.perf_counter()
+            N.check(lib.gmat_grm(g.handle, kind, 0.001, N.ptr(k), ctypes.byref(sc)), "gmat_grm")
+            st = np.zeros(4)
+            N.check(lib.gmat_grm_stats(N.ptr(st)), "gmat_grm_stats")
+            grm[name] = {"kernel_ms": st[0] * 1e3, "wall_ms": (time.perf_counter() - t1) * 1e3,
+                         "gflops_kernel": 2.0 * n * n * m / st[0] / 1e9}
+            mats.append(k)
+        a, d = mats
+        gl = [a, d, a * a, a * d, d * d]
+        rng = np.random.Generator(np.random.PCG64(args.seed + 1))
+        y = np.ones(n)
+        for k, s_ in zip(gl, var[:5]):
+            y += np.sqrt(s_) * (np.linalg.cholesky(k + 1e-3 * np.eye(n)) @ rng.standard_normal(n))
+        y += np.sqrt(var[5]) * rng.standard_normal(n)
+        t1 = time.perf_counter()
+        est = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), gl, maxiter=args.reml_iters)
+        st = np.zeros(4)
+        N.check(lib.gmat_reml_stats(N.ptr(st)), "gmat_reml_stats")
+        out["reml"] = {"iters_run": int(st[1]), "ms_per_iter": st[2] * 1e3, "wall_s": time.perf_counter() - t1,
+                       "fp64_tflops": st[3] / st[2] / 1e12 if st[2] else None, "var_after": [float(v) for v in est]}
+        out["grm"] = grm
+        pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), gl, var)
+    pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
+    py = dist.broadcast_array(py, 0, shape=(n,))
+    t1 = time.perf_counter()
+    plan = EpiPlan(g, pvp, py)
+    out["plan_create_s"] = time.perf_counter() - t1
+    out["setup"] = plan.setup_stats()
+    out["lowrank_rank"] = plan.lowrank_rank()
+    total = 0.0
+    t_all = 0.0
+    for kind in ("DD", "AD"):
+        rows = dist.rank_rows(kind, m, rank, ws)
+        plan.scan(kind, rows[:8], args.p_cut)  # builds the coding (side vectors) outside the timing
+        lib.gmat_device_synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        res = plan.scan(kind, rows, args.p_cut)
+        lib.gmat_device_synchronize()
+        dist.barrier()
+        dt = dist.allreduce_max(time.perf_counter() - t1)
+        pairs = float(m) * (m - 1) / 2 if kind == "DD" else float(m) * m
+        st = plan.stats()
+        out["epi" + kind] = {"pairs": pairs, "s": dt, "pairs_per_s": pairs / dt,
+                             "hits": int(dist.allreduce_sum(res[0].size)),
+                             "candidates": int(dist.allreduce_sum(st["candidates"])), "screen_level": int(st["n_slice"])}
+        total += pairs
+        t_all += dt
+    out["value"] = total / t_all
+    plan.close()
+    g.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,8 +375,17 @@ def main():
     ap.add_argument("--no-reml", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cov", action="store_true")
+    ap.add_argument("--config", default="cfg3", choices=["cfg3", "cfg5"],
+                    help="cfg3: the headline (configs[2]/[3]); cfg5: configs[4] (5,000 x 100,000, 5 GRMs, epiDD/epiAD)")
+    ap.add_argument("--reml-iters", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
+    if args.config == "cfg5":
+        if args.n_id == 2000:
+            args.n_id = 5000
+        if args.n_snp == 50000:
+            args.n_snp = 100000
+        return cfg5_main(args)
 
     from gmat_amd import dist
     from gmat_amd import _native as N

@@ -2982,7 +2982,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e2[b].alloc((size_t)SIDE_T * ROWS_PER_LAUNCH * m * sizeof(int)));
   }
   if (e->cand_cap == 0) {
-    e->cand_cap = 1 << 22;
+    const char *cenv = getenv("GMAT_CAND_CAP");  // tests: a small buffer exercises the overflow paths
+    e->cand_cap = cenv ? std::max<int64_t>(1024, atoll(cenv)) : (1 << 22);
     GMAT_TRY(e->cand_i.alloc(e->cand_cap * 8));
     GMAT_TRY(e->cand_j.alloc(e->cand_cap * 8));
     GMAT_TRY(e->ceff.alloc(e->cand_cap * 8));
@@ -3698,11 +3699,19 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       GMAT_HIP(hipStreamSynchronize(sm));
       if (li + 1 < plan.size()) queued[li + 1] = 0;
       if (pending == 0) {
-        GMAT_CHECK(S < e->n_slice, GMAT_E_OVERFLOW,
-                   "one screen launch produced %llu candidates (capacity %lld) with %d slices: p_cut too large "
-                   "for a scan; use the pair test", count, (long long)e->cand_cap, S);
-        S = S == 0 ? std::min(2, e->n_slice) : S + 1;
-        S_max_used = std::max(S_max_used, S);
+        if (S < e->n_slice) {  // thinner candidate band first
+          S = S == 0 ? std::min(2, e->n_slice) : S + 1;
+          S_max_used = std::max(S_max_used, S);
+        } else {  // the finest screen still overflows on one launch (large p_cut): grow the buffer
+          const int64_t cap = std::max<int64_t>(2 * e->cand_cap, (int64_t)(1.25 * (double)count) + 1024);
+          for (DBuf *bf : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp, &e->cand1_i, &e->cand1_j})
+            GMAT_TRY(bf->alloc((size_t)cap * 8));
+          e->cand_cap = cap;
+          sa.cap = cap;
+          sa.cand_i = e->cand_i.as<int64_t>();
+          sa.cand_j = e->cand_j.as<int64_t>();
+          if (getenv("GMAT_DEBUG")) fprintf(stderr, "candidate buffer grown to %lld\n", (long long)cap);
+        }
       }
       GMAT_TRY(flush(pending));
       pending = 0;
