@@ -44,7 +44,9 @@ def build_inputs(n, m, seed, var, rank, ws):
     nb = (n + 3) // 4
     t0 = time.time()
     lo, hi = dist.snp_shard(m, rank, ws)
-    shard = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed)  # (hi - lo, n)
+    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed)  # (hi - lo, n)
+    if dist.allreduce_sum(n_bad) > 0:  # the full generator re-draws (near-)monomorphic SNPs
+        shard = synth.simulate_genotypes(n, m, seed=seed)[lo:hi]
     local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
     body = dist.allgather_packed(local, m, nb)
     geno = shard if ws == 1 else None
@@ -234,7 +236,32 @@ def covariate_bench(g, ka, y0, n, m, p_cut, seed, steps, ms_intercept):
     return out
 
 
-def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
+def eff_cpu_baseline(geno, py, cut, budget_s):
+    """The C++/OpenMP restatement of _remma_epi_eff_cpu.c (oracle/eff_cpu.cpp, bit-identical to
+    the reference's C) timed on the box's host cores on stratified rows of the same cohort."""
+    from oracle import gmat_oracle as O  # checker / CPU baseline only
+    from gmat_amd import synth
+    m, n = geno.shape
+    body = synth.pack_bed(geno)[3:]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    # a probe call sizes the sample so that one call (decode + centring + rows, as the reference's
+    # call does) takes about budget_s
+    probe = np.linspace(0, m - 2, 8).astype(np.int64)
+    t0 = time.perf_counter()
+    O.eff_screen_c("AA", body, n, m, probe, py, [cut], threads=threads)
+    rate = float(np.sum(m - 1 - probe)) / (time.perf_counter() - t0)
+    k = int(min(m - 1, max(8, rate * budget_s / (m / 2))))
+    rows = np.linspace(0, m - 2, k).astype(np.int64)
+    t0 = time.perf_counter()
+    O.eff_screen_c("AA", body, n, m, rows, py, [cut], threads=threads)
+    dt = time.perf_counter() - t0
+    pairs, used = int(np.sum(m - 1 - rows)), rows.size
+    return {"value": pairs / dt, "unit": "SNP-pairs/s", "cores": threads, "kind": "port",
+            "sample": "%d stratified rows of the 2000x50000 cohort (%d pairs, %.1f s incl. decode), C++/OpenMP "
+                      "restatement of _remma_epi_eff_cpu.c:61-137 (oracle/eff_cpu.cpp)" % (used, pairs, dt)}
+
+
+def eff_bench(g, pvp, py, plan, n, m, p_cut, seed, geno=None, cpu_budget=10.0):
     """Effect-only screen (the remma_epiAA_eff_cpu replacement) over the
     same cohort, threshold from the exact variance median of 20,000 random pairs as
     remma_epiAA_approx does.  Algorithmic 2n flop per pair; f64 MFMA roof."""
@@ -262,11 +289,14 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed):
         wall = time.perf_counter() - t0
     N.check(lib.gmat_eff_stats(N.ptr(st)), "gmat_eff_stats")
     pairs = st[0]
+    cpu = eff_cpu_baseline(geno, py, float(eff_cut[0]), cpu_budget) if geno is not None else None
     return {"config": "remma_epiAA_eff over all %d pairs, eff_cut from the median var (p_cut=%g)" % (pairs, p_cut),
             "pairs_per_s_device": pairs / st[2], "pairs_per_s_end_to_end": pairs / wall, "device_s": st[2],
             "text_s": st[3], "hits": int(nh.value),
-            "fp64_tflops_algorithmic": pairs * 2.0 * n / st[2] / 1e12,
-            "reference_c_8_threads_pairs_per_s": 3.3e6}
+            "algorithmic_tflops": pairs * 2.0 * n / st[2] / 1e12,
+            "flop_convention": "2n per pair (SURVEY 8(d)); computed as 2 int8 slices (4n int8 ops) + exact fp64 "
+                               "recompute of the candidates",
+            "cpu_baseline": cpu}
 
 
 def cfg5_main(args):
@@ -288,8 +318,10 @@ def cfg5_main(args):
     nb = (n + 3) // 4
     t0 = time.time()
     lo, hi = dist.snp_shard(m, rank, ws)
-    local = np.frombuffer(synth.pack_bed(synth.simulate_genotype_shard(n, m, lo, hi, seed=args.seed))[3:],
-                          dtype=np.uint8).reshape(hi - lo, nb)
+    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=args.seed)
+    if dist.allreduce_sum(n_bad) > 0:
+        shard = synth.simulate_genotypes(n, m, seed=args.seed)[lo:hi]
+    local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
     g = Geno(body=dist.allgather_packed(local, m, nb), n_id=n, n_snp=m)
     log("cfg5 cohort %d x %d in %.1f s" % (n, m, time.time() - t0))
     var = np.array([0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
@@ -497,7 +529,7 @@ def main():
         e2e = e2e_bench(geno, ka, y, var, args.p_cut, int(round(hits_all)))
     eff = None
     if rank == 0 and ws == 1 and not args.no_eff:
-        eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed)
+        eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed, geno=geno, cpu_budget=args.cpu_budget)
     if rank == 0:
         value = total_pairs * args.steps / t_max
         out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,

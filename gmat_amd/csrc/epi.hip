@@ -2456,8 +2456,16 @@ int certify_below(double top, F &&ok, double *best) {
   for (double f : fr) {
     const int r = ok(f * top);
     if (r < 0) return r;
-    if (r) {
-      *best = f * top;
+    if (r) {  // certified; when a higher candidate failed, bisect a few steps between the two
+      double lo = f * top;
+      if (hi < top)
+        for (int it = 0; it < 4; ++it) {
+          const double mid = 0.5 * (lo + hi);
+          const int q = ok(mid);
+          if (q < 0) return q;
+          (q ? lo : hi) = mid;
+        }
+      *best = lo;
       return GMAT_OK;
     }
     hi = f * top;

@@ -45,40 +45,32 @@ def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, ma
 
 
 def simulate_genotype_shard(n_id, n_snp, lo, hi, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01):
-    """SNPs [lo, hi) of a related cohort, generated block by block so that any SNP range is
-    produced on its own (each rank of a sharded run makes only its shard) and the
-    concatenation of any split equals the whole cohort.  The pedigree (parents per generation)
-    comes from `seed`; every block of `block` SNPs has its own stream for the founder
-    frequencies and haplotypes, the per-block inheritance choices and the re-draws of
-    (near-)monomorphic SNPs.  Returns an (hi - lo, n_id) uint8 dosage matrix in {0, 1, 2}."""
-    ss = np.random.SeedSequence([seed, 0x9E3779B9])
-    rng = np.random.Generator(np.random.PCG64(ss.spawn(1)[0]))
-    sizes, parents = [n_founder], []
+    """SNPs [lo, hi) of ``simulate_genotypes(n_id, n_snp, seed)`` -- the same cohort, bit for bit --
+    with only the shard's columns propagated through the pedigree (the expensive part); every
+    random draw is made in the same order and size as the full generator (they are cheap), so
+    each rank of a sharded run makes just its own SNP range.  Returns ((hi - lo, n_id) uint8,
+    n_bad): n_bad counts this range's (near-)monomorphic SNPs, which the full generator re-draws
+    at the end of its stream -- a caller whose ranks find any must fall back to the full
+    generator (never the case for the bench cohorts)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    freq = rng.uniform(0.1, 0.9, size=n_snp)
+    n_blk = (n_snp + block - 1) // block
+    pop = (rng.random((2 * n_founder, n_snp)) < freq)[:, lo:hi]
+    b_lo, b_hi = lo // block, (max(hi, lo + 1) - 1) // block + 1  # blocks the range touches
+    n_pop = n_founder
     for g in range(n_gen):
-        n_next = n_id if g == n_gen - 1 else max(n_id, sizes[-1])
-        parents.append(rng.integers(0, sizes[-1], size=(2, n_next)))
-        sizes.append(n_next)
-    out = np.empty((max(0, hi - lo), n_id), dtype=np.uint8)
-    for b in range(lo // block, (hi + block - 1) // block if hi > lo else lo // block):
-        b0, b1 = b * block, min(n_snp, (b + 1) * block)
-        brng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, 1, b])))
-        freq = brng.uniform(0.1, 0.9, size=b1 - b0)
-        pop = brng.random((2 * n_founder, b1 - b0)) < freq
-        for g in range(n_gen):
-            pick = brng.integers(0, 2, size=(2, sizes[g + 1]))
-            new = np.empty((2 * sizes[g + 1], b1 - b0), dtype=bool)
-            for side in range(2):
-                par = parents[g][side]
-                new[side::2] = pop[2 * par + pick[side]]
-            pop = new
-        geno = (pop[0::2].astype(np.uint8) + pop[1::2].astype(np.uint8))
-        p = geno.sum(axis=0) / (2.0 * n_id)
-        bad = np.where(np.minimum(p, 1 - p) < maf_min)[0]
-        if bad.size:
-            geno[:, bad] = brng.binomial(2, 0.5, size=(n_id, bad.size)).astype(np.uint8)
-        s0, s1 = max(lo, b0), min(hi, b1)
-        out[s0 - lo:s1 - lo] = geno[:, s0 - b0:s1 - b0].T
-    return out
+        n_next = n_id if g == n_gen - 1 else max(n_id, n_pop)
+        new = np.empty((2 * n_next, hi - lo), dtype=bool)
+        for side in range(2):
+            par = rng.integers(0, n_pop, size=n_next)
+            pick = rng.integers(0, 2, size=(n_next, n_blk), dtype=np.uint8)
+            pick = np.repeat(pick[:, b_lo:b_hi], block, axis=1)[:, lo - b_lo * block:hi - b_lo * block].astype(bool)
+            new[side::2] = np.where(pick, pop[2 * par + 1], pop[2 * par])
+        pop, n_pop = new, n_next
+    geno = (pop[0::2].astype(np.uint8) + pop[1::2].astype(np.uint8)).T.copy()  # (hi - lo, n_id)
+    p = geno.sum(axis=1) / (2.0 * n_id)
+    n_bad = int(np.sum(np.minimum(p, 1 - p) < maf_min))
+    return geno, n_bad
 
 
 def pack_bed(geno, missing=None):

@@ -396,6 +396,38 @@ def epi_eff_screen(kind, snp_mat_dec, py, rows, eff_cut, freq_i=None, freq_j=Non
     return out
 
 
+def eff_screen_c(kind, bed_body, n, m, rows, py, cut, freq_i=None, freq_j=None, threads=None):
+    """The C++/OpenMP restatement of the reference's effect screen (oracle/eff_cpu.cpp, same fp64
+    operation order as _remma_epi_eff_cpu.c:61-574): records (i, j, eff) in the reference's
+    single-thread order.  bed_body: the .bed bytes after the magic."""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libgmat_oracle_eff.so"))
+    fn = lib.oracle_eff_screen
+    P = ctypes.c_void_p
+    fn.restype = ctypes.c_int64
+    fn.argtypes = [ctypes.c_int, P, ctypes.c_int64, ctypes.c_int64, P, ctypes.c_int64, P, P, P, P, ctypes.c_int64, P,
+                   P, P]
+    if threads:
+        os.environ["OMP_NUM_THREADS"] = str(threads)
+    body = np.ascontiguousarray(np.frombuffer(bed_body, dtype=np.uint8))
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    py = np.ascontiguousarray(py, dtype=np.float64).reshape(-1)
+    cut = np.ascontiguousarray(np.atleast_1d(cut), dtype=np.float64)
+    fi = None if freq_i is None else np.ascontiguousarray(freq_i, dtype=np.int64)
+    fj = None if freq_j is None else np.ascontiguousarray(freq_j, dtype=np.int64)
+    ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    kid = {"AA": 0, "AD": 1, "DD": 2}[kind]
+    cap = 1 << 16
+    while True:
+        oi, oj, oe = np.zeros(cap, np.int64), np.zeros(cap, np.int64), np.zeros(cap)
+        k = fn(kid, ptr(body), n, m, ptr(rows), rows.size, ptr(py), ptr(cut), ptr(fi), ptr(fj), cap, ptr(oi), ptr(oj),
+               ptr(oe))
+        if k <= cap:
+            return oi[:k], oj[:k], oe[:k]
+        cap = int(k)
+
+
 def maf_classes(kind, snp_mat):
     """Frequency classes of the _maf_approx pipelines from the (n, m) dosage matrix:
     AA minor-allele frequency (remma_epiAA_maf_approx.py:38-41), DD heterozygosity

@@ -28,7 +28,7 @@ def cfg5():
     from gmat_amd.uvlmm.uvlmm_varcom import projection
     from scipy.sparse import identity
     lib = N.ensure_device()
-    geno = synth.simulate_genotype_shard(N5, M5, 0, M5, seed=SEED5)
+    geno, _ = synth.simulate_genotype_shard(N5, M5, 0, M5, seed=SEED5)
     g = Geno(body=np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8), n_id=N5, n_snp=M5)
     mats = []
     for kind in (0, 1):

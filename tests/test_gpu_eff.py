@@ -135,6 +135,37 @@ def test_eff_symbols_vs_oracle(cohort, kind, tmp_path):
     assert rc < 0
 
 
+@pytest.mark.parametrize("kind", ["AA", "AD", "DD"])
+def test_eff_symbols_bit_identical_to_restatement(cohort, kind, tmp_path):
+    """The GPU screen + exact recompute reproduce the reference's fp64 arithmetic: the written
+    file equals, byte for byte, the C++ restatement's (oracle/eff_cpu.cpp, itself checked
+    bit-for-bit against the reference's own C in the container), single cut and _maf table."""
+    from oracle import gmat_oracle as O
+    from gmat_amd import _native as N
+    prefix, dec, py = cohort
+    lib = N.ensure_device()
+    m, n = dec.shape
+    body = open(prefix + ".bed", "rb").read()[3:]
+    rows = np.array([9, 0, 400, 400, 13, m - 2, 250], dtype=np.longlong)
+    probe = O.epi_eff_screen(kind, dec, py, [0], 0.0)
+    cut = float(np.quantile([abs(e) for _, _, e in probe], 0.8))
+    out = str(tmp_path / "eff")
+    assert getattr(lib, "remma_epi%s_eff_cpu" % kind)(prefix.encode(), n, m, N.ptr(rows), rows.size, N.ptr(py), cut,
+                                                      out.encode()) == 1
+    i, j, e = O.eff_screen_c(kind, body, n, m, rows, py, [cut])
+    assert i.size > 100
+    assert open(out).read() == "snp_0 snp_1 eff\n" + "".join("%d %d %s\n" % (u, v, "%g" % w) for u, v, w in zip(i, j, e))
+    rng = np.random.default_rng(8)
+    fi = rng.integers(0, 11, m).astype(np.longlong)
+    fj = fi if kind != "AD" else rng.integers(0, 11, m).astype(np.longlong)
+    table = np.ascontiguousarray(cut * rng.uniform(0.6, 1.4, 111))
+    msym = getattr(lib, "remma_epi%s_maf_eff_cpu" % kind)
+    args = (N.ptr(fi), N.ptr(fj)) if kind == "AD" else (N.ptr(fi),)
+    assert msym(prefix.encode(), n, m, N.ptr(rows), rows.size, N.ptr(py), *args, N.ptr(table), out.encode()) == 1
+    i, j, e = O.eff_screen_c(kind, body, n, m, rows, py, table, fi, fj)
+    assert open(out).read() == "snp_0 snp_1 eff\n" + "".join("%d %d %s\n" % (u, v, "%g" % w) for u, v, w in zip(i, j, e))
+
+
 @pytest.fixture(scope="module")
 def mouse(tmp_path_factory):
     d = tmp_path_factory.mktemp("mouse_eff")

@@ -75,7 +75,7 @@ def cfg3():
     from gmat_amd.uvlmm.uvlmm_varcom import projection
     from scipy.sparse import identity
     lib = N.ensure_device()
-    geno = synth.simulate_genotype_shard(N3, M3, 0, M3, seed=SEED3)
+    geno = synth.simulate_genotypes(N3, M3, seed=SEED3)
     body = np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8)
     g = Geno(body=body, n_id=N3, n_snp=M3)
     ka = np.empty((N3, N3))

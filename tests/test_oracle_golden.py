@@ -296,3 +296,63 @@ def test_readme_workflow_golden():
     ld = O.ld_filter(anno, open(os.path.join(README, "plink.ld")).read().splitlines(), r2=0.2)
     exp_ld = open(os.path.join(README, "epiAA_a_axa.anno.ld")).read().splitlines()
     assert [l.rstrip() for l in exp_ld] == ld and len(ld) < len(anno)
+
+
+REF_LIB = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "libremma_epi.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LIB), reason="the reference's C is built only in the container")
+@pytest.mark.parametrize("kind", ["AA", "AD", "DD"])
+def test_eff_restatement_is_the_reference_bit_for_bit(kind, tmp_path):
+    """oracle/eff_cpu.cpp against the reference's own _remma_epi_eff_cpu.c (compiled unmodified
+    into oracle/_ref): identical record text ("%lld %lld %g") on a cohort with missing calls,
+    duplicate and unsorted rows, single cut and _maf tables.  The reference runs single-threaded
+    (its OpenMP loop interleaves rows nondeterministically)."""
+    import subprocess
+    import sys
+    from gmat_amd import synth
+    prefix = str(tmp_path / "c")
+    n, m = 301, 420
+    geno = synth.simulate_genotypes(n, m, seed=41, n_founder=20, n_gen=3, block=50)
+    rng = np.random.default_rng(42)
+    synth.write_plink(prefix, geno, missing=rng.random((m, n)) < 0.01, seed=41)
+    py = rng.standard_normal(n)
+    rows = np.array([3, 0, 77, 77, 250, m - 2, 11], dtype=np.int64)
+    body = open(prefix + ".bed", "rb").read()[3:]
+    fi = rng.integers(0, 11, m)
+    fj = fi if kind != "AD" else rng.integers(0, 11, m)
+    table = rng.uniform(0.5, 1.5, 111) * 8.0
+    np.save(str(tmp_path / "py.npy"), py)
+    np.save(str(tmp_path / "rows.npy"), rows)
+    np.save(str(tmp_path / "fi.npy"), fi)
+    np.save(str(tmp_path / "fj.npy"), fj)
+    np.save(str(tmp_path / "table.npy"), table)
+    script = """
+import ctypes, numpy as np, sys
+d, prefix, kind = sys.argv[1], sys.argv[2], sys.argv[3]
+lib = ctypes.CDLL(%r)
+py = np.load(d + '/py.npy'); rows = np.load(d + '/rows.npy'); fi = np.load(d + '/fi.npy'); fj = np.load(d + '/fj.npy')
+table = np.load(d + '/table.npy')
+P, L = ctypes.c_void_p, ctypes.c_longlong
+n, m = %d, %d
+f = getattr(lib, 'remma_epi%%s_eff_cpu' %% kind)
+f.argtypes = [ctypes.c_char_p, L, L, P, L, P, ctypes.c_double, ctypes.c_char_p]
+f(prefix.encode(), n, m, rows.ctypes.data, rows.size, py.ctypes.data, 8.0, (d + '/ref_single').encode())
+g = getattr(lib, 'remma_epi%%s_maf_eff_cpu' %% kind)
+if kind == 'AD':
+    g.argtypes = [ctypes.c_char_p, L, L, P, L, P, P, P, P, ctypes.c_char_p]
+    g(prefix.encode(), n, m, rows.ctypes.data, rows.size, py.ctypes.data, fi.ctypes.data, fj.ctypes.data,
+      table.ctypes.data, (d + '/ref_maf').encode())
+else:
+    g.argtypes = [ctypes.c_char_p, L, L, P, L, P, P, P, ctypes.c_char_p]
+    g(prefix.encode(), n, m, rows.ctypes.data, rows.size, py.ctypes.data, fi.ctypes.data, table.ctypes.data,
+      (d + '/ref_maf').encode())
+""" % (REF_LIB, n, m)
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    subprocess.run([sys.executable, "-c", script, str(tmp_path), prefix, kind], check=True, env=env,
+                   stdout=subprocess.DEVNULL)
+    for name, cut, a, b in (("ref_single", [8.0], None, None), ("ref_maf", table, fi, fj)):
+        i, j, e = O.eff_screen_c(kind, body, n, m, rows, py, cut, a, b)
+        text = "snp_0 snp_1 eff\n" + "".join("%d %d %s\n" % (u, v, "%g" % w) for u, v, w in zip(i, j, e))
+        assert i.size > 20
+        assert open(str(tmp_path / name)).read() == text
