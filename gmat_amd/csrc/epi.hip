@@ -1250,7 +1250,7 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
 template <int SK>
 __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
   constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
-  constexpr int NJC = 2 * 8 * BJ, SI = MX_BI * NB_REC, SJ = 2 * BJ * NB_REC;
+  constexpr int SI = MX_BI * NB_REC, SJ = 2 * BJ * NB_REC;
   __shared__ __attribute__((aligned(16))) uint8_t sA[2][SK * MX_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t sI[2][SK * SI];
   __shared__ __attribute__((aligned(16))) uint8_t sJ[2][SK * SJ];
@@ -1267,9 +1267,6 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   const int half = (PB * w) / (MX_BI / 2);
   const int64_t J0 = (int64_t)Jt[half] * BJ;
   const int nK = x.nK, nC = x.nC;
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
-  const __amdgpu_buffer_rsrc_t rsI = make_rsrc(x.nib_i, x.nib_bytes);
-  const __amdgpu_buffer_rsrc_t rsJ = make_rsrc(x.nib_j, x.nib_bytes);
 
   int64_t ti[PB];
 #pragma unroll
@@ -1277,20 +1274,21 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     const int r = trow[PB * w + t];
     ti[t] = (r >= 0) ? a.rows[r] : -1;
   }
-  const unsigned OOR = 0xFFFFFFF0u;
-  const int jc = tid % NJC, jh = jc >> 8, js = (jc >> 3) & 31, jq = jc & 7, jl = jq ^ ((js >> 1) & 7);
-  const int is = (tid >> 3) & 15;
-  unsigned voffJ = OOR, voffI = OOR;
+  // Every operand of a stage arrives by LDS-DMA (global_load_lds_dwordx4: lane i's 16 bytes land at
+  // M0 + 16 i), so no register round trip and no ds_write: the A tile image (NA wave-instructions
+  // per tile), the j-side records (one per wave: chunk jc = tid of the two column blocks, source
+  // chunk XOR-swizzled by column) and the i-side records (waves 0 and 1: 16 slots x 8 chunks).
+  // Lanes whose column or slot is unused read SNP 0 (finite data in accumulators nobody tests).
+  const int jh = tid >> 8, js = (tid >> 3) & 31, jq = tid & 7, jl = jq ^ ((js >> 1) & 7);
+  const uint8_t *srcJ, *srcI = nullptr;
   {
     const int64_t jj = (int64_t)Jt[jh] * BJ + js;
-    if (Jt[jh] >= 0 && jj < a.m) voffJ = (unsigned)(jj * nK * NB_REC + jl * 16);
+    srcJ = x.nib_j + ((Jt[jh] >= 0 && jj < a.m) ? jj : 0) * nK * NB_REC + jl * 16;
+    if (tid < MX_BI * 8) {
+      const int sl = tid >> 3;
+      srcI = x.nib_i + (trow[sl] >= 0 ? a.rows[trow[sl]] : 0) * nK * NB_REC + jq * 16;
+    }
   }
-  if (trow[is] >= 0) voffI = (unsigned)(a.rows[trow[is]] * nK * NB_REC + jq * 16);
-
-  // the A tile image is a straight copy: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
-  // instruction) into buffer nb, no registers or ds_write; the genotype records go through
-  // registers (the j side is swizzled per lane)
-  v4i rnj[SK], rni[SK];
   auto load = [&](int nb, int ch, int cs2) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < SK; ++s) {
@@ -1299,15 +1297,8 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 #pragma unroll
       for (int u = 0; u < NA; ++u)
         lds_dma16(src + (tid + u * MX_T) * 16, &sA[nb][s * MX_TILE + (w * 64 + u * MX_T) * 16]);
-      rnj[s] = __builtin_amdgcn_raw_buffer_load_b128(rsJ, voffJ, cs * NB_REC, 0);
-      rni[s] = __builtin_amdgcn_raw_buffer_load_b128(rsI, voffI, cs * NB_REC, 0);
-    }
-  };
-  auto store = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < SK; ++s) {
-      *(v4i *)&sJ[b][s * SJ + (jh * BJ + js) * NB_REC + jq * 16] = rnj[s];
-      *(v4i *)&sI[b][s * SI + is * NB_REC + jq * 16] = rni[s];
+      lds_dma16(srcJ + cs * NB_REC, &sJ[nb][s * SJ + w * 1024]);
+      if (w < 2) lds_dma16(srcI + cs * NB_REC, &sI[nb][s * SI + w * 1024]);
     }
   };
 
@@ -1315,8 +1306,17 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   const int sw16 = 16 * ((c >> 3) & 1);
   const int jf = (c >> 1) & 7;
   const int jrow = (half * BJ + c) * NB_REC;
+  // A fragment r of (stage s, half kk): the 6 fp6 dwords + the scale dword of row 32 r + c
+  auto afrag = [&](int b, int s, int kk, int r) __attribute__((always_inline)) {
+    const uint8_t *ar = &sA[b][s * MX_TILE + (2 * kk + h) * 4096 + (32 * r + c) * 32];
+    const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+    return v8i_{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  // Software-pipelined: the next A fragment is read from LDS while the current one's MFMAs run
+  // (the compiler otherwise waits for every fragment right before its MFMAs).
   auto compute = [&](int b, bool first) __attribute__((always_inline)) {
     const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    v8i_ fa = afrag(b, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < SK; ++s)
 #pragma unroll
@@ -1335,12 +1335,13 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
         }
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const uint8_t *ar = &sA[b][s * MX_TILE + (2 * kk + h) * 4096 + (32 * r + c) * 32];
-          const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
-          const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bool last = s == SK - 1 && kk == 1 && r == RB - 1;
+          const int ns = r < RB - 1 ? s : (kk == 1 ? s + 1 : s), nkk = r < RB - 1 ? kk : (kk ^ 1);
+          const v8i_ fn = last ? fa : afrag(b, ns, nkk, (r + 1) % RB);
 #pragma unroll
           for (int t = 0; t < PB; ++t)  // x2 (scale 128): the fp4 codes hold w/2
-            acc[r][t] = mfma_mx(fa, fb[t], (first && s == 0 && kk == 0) ? z : acc[r][t], hi[2], 128);
+            acc[r][t] = mfma_mx(fa, fb[t], (first && s == 0 && kk == 0) ? z : acc[r][t], fa[6], 128);
+          fa = fn;
         }
       }
   };
@@ -1408,13 +1409,11 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     load(b ^ 1, nch, ncs);
     __builtin_amdgcn_sched_barrier(0);
     compute(b, first);
-    store(b ^ 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of the next stage
     __syncthreads();
   };
 
   load(0, 0, 0);
-  store(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   stamp(1);
