@@ -36,7 +36,15 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_inputs(n, m, seed, var, rank, ws):
+def covariate_design(n, seed, y0):
+    """[1, binary, integer 90-129, binary] (the reference's example pheno layout) and the phenotype
+    with covariate effects (shared by --covariates and the covariates leg)."""
+    rng = np.random.Generator(np.random.PCG64(seed + 9))
+    x = np.column_stack([np.ones(n), rng.integers(0, 2, n), rng.integers(90, 130, n), rng.integers(0, 2, n)])
+    return x.astype(float), y0 + 0.3 * x[:, 1] + 0.01 * x[:, 2] - 0.2 * x[:, 3]
+
+
+def build_inputs(n, m, seed, var, rank, ws, covariates=False):
     """Cohort (deterministic, generated shard by shard: rank r makes only its SNP range), the
     packed shards all-gathered over RCCL, P / Py computed on rank 0 and broadcast."""
     from gmat_amd import dist, synth
@@ -67,7 +75,10 @@ def build_inputs(n, m, seed, var, rank, ws):
         y += np.sqrt(var[2]) * rng.standard_normal(n)
         from scipy.sparse import identity
         from gmat_amd.uvlmm.uvlmm_varcom import projection
-        pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), [ka, ka * ka], var)
+        x = np.ones((n, 1))
+        if covariates:
+            x, y = covariate_design(n, seed, y)
+        pvp, py = projection(y, x, identity(n, format="csr"), [ka, ka * ka], var)
     pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
     py = dist.broadcast_array(py, 0, shape=(n,))
     return geno, g, pvp, py, ka, y
@@ -211,10 +222,8 @@ def covariate_bench(g, ka, y0, n, m, p_cut, seed, steps, ms_intercept):
     from gmat_amd.uvlmm.uvlmm_varcom import projection
     from scipy.sparse import identity
     lib = N.ensure_device()
-    rng = np.random.Generator(np.random.PCG64(seed + 9))
-    x = np.column_stack([np.ones(n), rng.integers(0, 2, n), rng.integers(90, 130, n), rng.integers(0, 2, n)])
-    y = y0 + 0.3 * x[:, 1] + 0.01 * x[:, 2] - 0.2 * x[:, 3]  # the headline phenotype + covariate effects
-    pvp, py = projection(y, x.astype(float), identity(n, format="csr"), [ka, ka * ka], [0.4, 0.2, 0.4])
+    x, y = covariate_design(n, seed, y0)
+    pvp, py = projection(y, x, identity(n, format="csr"), [ka, ka * ka], [0.4, 0.2, 0.4])
     rows = np.arange(m - 1, dtype=np.int64)
     t0 = time.perf_counter()
     plan = EpiPlan(g, pvp, py)
@@ -410,6 +419,8 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=["cfg3", "cfg5"],
                     help="cfg3: the headline (configs[2]/[3]); cfg5: configs[4] (5,000 x 100,000, 5 GRMs, epiDD/epiAD)")
     ap.add_argument("--reml-iters", type=int, default=5)
+    ap.add_argument("--covariates", action="store_true",
+                    help="profiling: the timed step uses the covariate design of the covariates leg")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
     if args.config == "cfg5":
@@ -426,7 +437,7 @@ def main():
     N.ensure_device()
     n, m = args.n_id, args.n_snp
     var = np.array([0.4, 0.2, 0.4])
-    geno, g, pvp, py, ka, y = build_inputs(n, m, args.seed, var, rank, ws)
+    geno, g, pvp, py, ka, y = build_inputs(n, m, args.seed, var, rank, ws, covariates=args.covariates)
 
     from gmat_amd.remma._scan import EpiPlan
     lib = N.ensure_device()

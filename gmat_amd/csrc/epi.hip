@@ -515,10 +515,11 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
 // orthonormal null directions, so every pair also needs u_k'e = (a o u_k).b - beta u_k.a - alpha
 // u_k.b + alpha beta 1'u_k for k < NC.  (a o u_k) is a one-slice int8 row image (per-row scale sU):
 // |u_k'e - c~_k| <= sU/2 sum_t b_t = sU csum_r / 2, so |U'e|^2 <= sum_k (|c~_k| + err_k)^2.
-// 64 x 128 (row, column) tiles, 4 waves of 32 x 64 at one wave per SIMD (the NC extra int32
-// accumulator sets per wave need the registers of two); stage image (14 + 4 NC KB, 64 individuals):
+// 64 x 128 (row, column) tiles, 8 waves of 32 x 32 at two waves per SIMD (a 32 x 32 wave tile keeps
+// the NC extra int32 accumulator sets within two waves' registers); stage image (14 + 4 NC KB, 64
+// individuals):
 // L3 slices 0, 1 and the NC direction images (64 rows x 64 B each), fp4 codes of a (64 rows x 32 B)
-// and b (128 columns x 32 B); DMA instruction q (1 KB) lands at q KB, wave w issuing q = w + 4u.
+// and b (128 columns x 32 B); DMA instruction q (1 KB) lands at q KB, wave w issuing q = w + 8u.
 // Five-slot LDS-DMA ring, four stages in flight.
 constexpr int PC_TR = 64, PC_TC = 128, PC_NS = 5, PF_NCOV_MAX = 4;
 template <int NC>
@@ -544,8 +545,9 @@ __device__ __forceinline__ void vm_wait_barrier(int n) {
 #undef VMW
 }
 template <int NC>
-__global__ __launch_bounds__(256, 1) void prefilter_cov_kernel(SideArgs x) {
+__global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   using SH = PcShape<NC>;
+  constexpr int NW = 8;
   const ScreenArgs &a = x.a;
   const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
   const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
@@ -554,15 +556,16 @@ __global__ __launch_bounds__(256, 1) void prefilter_cov_kernel(SideArgs x) {
   const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PC_TC;
   if (r0 >= a.n_rows || c0 >= a.m) return;
   if (a.tri && c0 + PC_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
-  // 4 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
+  // 8 waves at two per SIMD: wave w = rows 32 (w >> 2) .. +32 x columns 32 (w & 3) .. +32
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, h = lane >> 5, c = lane & 31;
   __shared__ __attribute__((aligned(16))) uint8_t ring[PC_NS][SH::ST];
-  const uint8_t *src[SH::QW];
-  int stp[SH::QW];
+  constexpr int QW = (SH::QT + NW - 1) / NW;
+  const uint8_t *src[QW];
+  int stp[QW];
   int nq = 0;  // DMA instructions this wave issues per stage
 #pragma unroll
-  for (int u = 0; u < SH::QW; ++u) {
-    const int q = w + 4 * u;
+  for (int u = 0; u < QW; ++u) {
+    const int q = w + NW * u;
     src[u] = nullptr;
     stp[u] = 0;
     if (q < 4 * SH::NREG) {  // int8 rows: region q / 4, 16 rows x 4 chunks per instruction
@@ -581,70 +584,51 @@ __global__ __launch_bounds__(256, 1) void prefilter_cov_kernel(SideArgs x) {
   }
   auto issue = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < SH::QW; ++u)
-      if (w + 4 * u < SH::QT) lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PC_NS][(w + 4 * u) * 1024]);
+    for (int u = 0; u < QW; ++u)
+      if (w + NW * u < SH::QT) lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PC_NS][(w + NW * u) * 1024]);
   };
-  v16i acc[2][E3_PF], accu[2][NC];
-  v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
+  v16i acc[E3_PF], accu[NC];
+  v16f_ acc4[4];  // a.b, a^2.b, a.b^2, a^2.b^2
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int e = 0; e < 16; ++e) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
+    for (int p = 0; p < E3_PF; ++p) acc[p][e] = 0;
 #pragma unroll
-      for (int p = 0; p < E3_PF; ++p) acc[q][p][e] = 0;
+    for (int k = 0; k < NC; ++k) accu[k][e] = 0;
 #pragma unroll
-      for (int k = 0; k < NC; ++k) accu[q][k][e] = 0;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) acc4[q][p][e] = 0.f;
-    }
+    for (int p = 0; p < 4; ++p) acc4[p][e] = 0.f;
   }
   const int S = (int)(x.n_pad / SG_K);
   const int pre = min(S, PC_NS - 1);
   for (int st = 0; st < pre; ++st) issue(st);
   vm_wait_barrier(nq * (pre - 1));
   const int rrow = 32 * wr + c;
+  const int crow = 32 * wc + c, lcb = h ^ ((crow >> 3) & 1);
   for (int st = 0; st < S; ++st) {
     const uint8_t *bf = ring[st % PC_NS];
     if (st + PC_NS - 1 < S) issue(st + PC_NS - 1);
-    v4i rb4[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
-      rb4[q] = *(const v4i *)&bf[SH::O_B4 + crow * 32 + 16 * lc];
-    }
+    const v4i rb4 = *(const v4i *)&bf[SH::O_B4 + crow * 32 + 16 * lcb];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
-      v4i f[SH::NREG];
+      const v4i fc = i8_of_fp4((unsigned)rb4[2 * kk], (unsigned)rb4[2 * kk + 1]);
 #pragma unroll
-      for (int g = 0; g < SH::NREG; ++g) f[g] = *(const v4i *)&bf[4096 * g + rrow * 64 + 16 * lr];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const v4i fc = i8_of_fp4((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
-#pragma unroll
-        for (int p = 0; p < E3_PF; ++p) acc[q][p] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[p], fc, acc[q][p], 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < NC; ++k)
-          accu[q][k] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[E3_PF + k], fc, accu[q][k], 0, 0, 0);
+      for (int g = 0; g < SH::NREG; ++g) {
+        const v4i f = *(const v4i *)&bf[4096 * g + rrow * 64 + 16 * lr];
+        if (g < E3_PF)
+          acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, fc, acc[g], 0, 0, 0);
+        else
+          accu[g - E3_PF] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, fc, accu[g - E3_PF], 0, 0, 0);
       }
     }
     {
       const int lr = h ^ ((rrow >> 3) & 1);
-      v8i_ fa[2];
-      {
-        const v4i ra4 = *(const v4i *)&bf[SH::O_A4 + rrow * 32 + 16 * lr];
-        fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
-        fa[1] = sq4(ra4);
-      }
+      const v4i ra4 = *(const v4i *)&bf[SH::O_A4 + rrow * 32 + 16 * lr];
+      const v8i_ fa[2] = {v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0}, sq4(ra4)};
+      const v8i_ fb[2] = {v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0}, sq4(rb4)};
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        v8i_ fb[2];
-        fb[0] = v8i_{rb4[q][0], rb4[q][1], rb4[q][2], rb4[q][3], 0, 0, 0, 0};
-        fb[1] = sq4(rb4[q]);
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-          acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
-      }
+      for (int p = 0; p < 4; ++p)
+        acc4[p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[p], 4, 4, 0, 127, 0, 127);
     }
     vm_wait_barrier(nq * (min(st + PC_NS - 1, S - 1) - (st + 1)));
   }
@@ -672,74 +656,71 @@ __global__ __launch_bounds__(256, 1) void prefilter_cov_kernel(SideArgs x) {
   __syncthreads();
   const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
   const double ku = a.pf_ku * (1.0 + 1e-12);
+  const int64_t j = c0 + crow;
+  const int J = (int)(j / 32);
+  const bool jok = j < a.m && j >= a.j_lo;
+  double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int64_t j = c0 + 64 * wc + 32 * q + c;
-    const int J = (int)(j / 32);
-    const bool jok = j < a.m && j >= a.j_lo;
-    double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
+  for (int k = 0; k < NC; ++k) cub[k] = 0.0;
+  bool cmono = true;
+  if (jok) {
+    cbe = a.beta[j];
+    ccb = a.csum_r[j];
+    const double cb2 = a.csq_r[j];
+    cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
+    cnb = n * cbe - ccb;
+    cbsb = cbe * a.spy - a.sb[j];
+    cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+    cmono = a.mono_r[j];
 #pragma unroll
-    for (int k = 0; k < NC; ++k) cub[k] = 0.0;
-    bool cmono = true;
-    if (jok) {
-      cbe = a.beta[j];
-      ccb = a.csum_r[j];
-      const double cb2 = a.csq_r[j];
-      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
-      cnb = n * cbe - ccb;
-      cbsb = cbe * a.spy - a.sb[j];
-      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
-      cmono = a.mono_r[j];
+    for (int k = 0; k < NC; ++k) cub[k] = a.pf_ub[k * a.m + j];
+  }
 #pragma unroll
-      for (int k = 0; k < NC; ++k) cub[k] = a.pf_ub[k * a.m + j];
-    }
+  for (int e = 0; e < 16; ++e) {
+    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+    const bool rok = r < a.n_rows;
+    const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
+    bool live = false;
+    const double iv = rowv[0][rl];
+    if (rok && jok && iv >= 0.0 && !cmono) {
+      const int64_t i = (int64_t)iv;
+      if (!(a.tri && j <= i)) {
+        const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
+        double c3 = 0.0;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
-      const bool rok = r < a.n_rows;
-      const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
-      bool live = false;
-      const double iv = rowv[0][rl];
-      if (rok && jok && iv >= 0.0 && !cmono) {
-        const int64_t i = (int64_t)iv;
-        if (!(a.tri && j <= i)) {
-          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
-          double c3 = 0.0;
+        for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
+        const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
+        const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
+        const double sab = (double)acc4[0][e], sa2b = (double)acc4[1][e], sab2 = (double)acc4[2][e],
+                     sa2b2 = (double)acc4[3][e];
+        const double ee =
+            sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
+        const double se = sab - be * rowv[2][rl] + al * cnb;
+        double u2 = 0.0;
 #pragma unroll
-          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[q][t][e];
-          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
-          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
-          const double sab = (double)acc4[q][0][e], sa2b = (double)acc4[q][1][e], sab2 = (double)acc4[q][2][e],
-                       sa2b2 = (double)acc4[q][3][e];
-          const double ee =
-              sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
-          const double se = sab - be * rowv[2][rl] + al * cnb;
-          double u2 = 0.0;
-#pragma unroll
-          for (int k = 0; k < NC; ++k) {
-            const double sU = rowu[0][k][rl], t1 = sU * (double)accu[q][k][e], t2 = be * rowu[1][k][rl],
-                         t3 = al * cub[k], t4 = al * be * a.pf_su[k];
-            const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sU * ccb * (1.0 + 1e-9) +
-                              1e-12 * (fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4));
-            u2 += ck * ck;
-          }
-          const double vlo = mu_e * ee - k1 * se * se - ku * u2 - k2 * rowv[6][rl] * cmag;
-          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
+        for (int k = 0; k < NC; ++k) {
+          const double sU = rowu[0][k][rl], t1 = sU * (double)accu[k][e], t2 = be * rowu[1][k][rl],
+                       t3 = al * cub[k], t4 = al * be * a.pf_su[k];
+          const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sU * ccb * (1.0 + 1e-9) +
+                            1e-12 * (fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4));
+          u2 += ck * ck;
         }
+        const double vlo = mu_e * ee - k1 * se * se - ku * u2 - k2 * rowv[6][rl] * cmag;
+        live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
       }
-      const unsigned long long bal = __ballot(live);
-      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
-      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
-      if (blk && rok && jok) {
-        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-#pragma unroll
-        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
-        if (a.pf_store)
-#pragma unroll
-          for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
-      }
-      __builtin_amdgcn_sched_barrier(0);
     }
+    const unsigned long long bal = __ballot(live);
+    const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
+    if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+    if (blk && rok && jok) {
+      const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+      for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
+      if (a.pf_store)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[p][e];
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -3254,10 +3235,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         xp.n_rt = (int)cdiv(Rn, PC_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PC_TC));
         switch (e->pf_ncov) {
-          case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, dim3(gp), dim3(256), 0, S2, xp); break;
-          case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, dim3(gp), dim3(256), 0, S2, xp); break;
-          case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, dim3(gp), dim3(256), 0, S2, xp); break;
-          default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, dim3(gp), dim3(256), 0, S2, xp); break;
+          case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, dim3(gp), dim3(512), 0, S2, xp); break;
+          case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, dim3(gp), dim3(512), 0, S2, xp); break;
+          case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, dim3(gp), dim3(512), 0, S2, xp); break;
+          default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, dim3(gp), dim3(512), 0, S2, xp); break;
         }
       }
       GMAT_HIP(hipGetLastError());
