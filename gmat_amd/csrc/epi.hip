@@ -30,6 +30,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 
 #include <rocsolver/rocsolver.h>
@@ -2405,14 +2406,20 @@ int eigen_bottom(gmat_epi *e, const double *dP, double trP, int ne, Eigen *eg) {
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipDeviceSynchronize());
   {  // full symmetric eigendecomposition (ascending); column r of the column-major result =
-     // eigenvector r = row r of A read row-major
-    rocblas_handle hb = nullptr;
-    GMAT_CHECK(rocblas_create_handle(&hb) == rocblas_status_success, GMAT_E_HIP, "eigen: rocblas handle");
-    const rocblas_status st = rocsolver_dsyevd(hb, rocblas_evect_original, rocblas_fill_lower, (rocblas_int)n,
+     // eigenvector r = row r of A read row-major.  The rocBLAS handle is created once per device
+     // and kept (creating one costs more than the decomposition at n = 2,000).
+    static rocblas_handle handles[64] = {nullptr};
+    static std::mutex mu;  // one decomposition at a time per process (the handles are shared)
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    GMAT_HIP(hipGetDevice(&dev));
+    GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_HIP, "eigen: device %d", dev);
+    if (!handles[dev])
+      GMAT_CHECK(rocblas_create_handle(&handles[dev]) == rocblas_status_success, GMAT_E_HIP, "eigen: rocblas handle");
+    const rocblas_status st = rocsolver_dsyevd(handles[dev], rocblas_evect_original, rocblas_fill_lower, (rocblas_int)n,
                                                A.as<double>(), (rocblas_int)n, W.as<double>(), E.as<double>(),
                                                dinfo.as<rocblas_int>());
     GMAT_HIP(hipDeviceSynchronize());
-    rocblas_destroy_handle(hb);
     GMAT_CHECK(st == rocblas_status_success, GMAT_E_HIP, "eigen: rocsolver_dsyevd status %d", (int)st);
   }
   int hinfo = 0;
