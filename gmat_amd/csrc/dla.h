@@ -39,6 +39,11 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
 int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv,
                           double *work, double *ainv);
 
+// The ne smallest eigenpairs of the symmetric n x n matrix a (device, lower triangle read,
+// destroyed): eigenvalues ascending to w_host, eigenvector r to z[r*n .. r*n+n) (device).
+// Synchronous (eig.hip).
+int sym_eig_bottom(int64_t n, double *a, int ne, double *w_host, double *z);
+
 // Small device helpers.
 int fill_sym_upper(hipStream_t s, int64_t n, double *a, int64_t lda);           // upper := lower'
 int dot_rows(hipStream_t s, int64_t rows, int64_t n, const double *a, int64_t lda, const double *b,

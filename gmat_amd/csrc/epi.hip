@@ -30,10 +30,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
-#include <mutex>
 #include <numeric>
 
-#include <rocsolver/rocsolver.h>
 
 #include "dla.h"
 #include "geno.h"
@@ -2393,43 +2391,22 @@ void kind_codings(int kind, int *lc, int *rc) {
 struct Eigen {
   int ne = 0;
   std::vector<double> lam, Z;
+  DBuf dZ;  // Z on the device (ne x n)
 };
 int eigen_bottom(gmat_epi *e, const double *dP, double trP, int ne, Eigen *eg) {
   const int64_t n = e->n;
-  DBuf A, W, E, dinfo;
+  DBuf A;
+  DBuf &Z = eg->dZ;
   GMAT_TRY(A.alloc(n * n * sizeof(double)));
-  GMAT_TRY(W.alloc(n * sizeof(double)));
-  GMAT_TRY(E.alloc(n * sizeof(double)));
-  GMAT_TRY(dinfo.alloc(sizeof(int)));
+  GMAT_TRY(Z.alloc((size_t)n * ne * sizeof(double)));
   hipLaunchKernelGGL(pf_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dP, 0.0, 4.0 * trP / (double)n,
                      A.as<double>());
   GMAT_HIP(hipGetLastError());
-  GMAT_HIP(hipDeviceSynchronize());
-  {  // full symmetric eigendecomposition (ascending); column r of the column-major result =
-     // eigenvector r = row r of A read row-major.  The rocBLAS handle is created once per device
-     // and kept (creating one costs more than the decomposition at n = 2,000).
-    static rocblas_handle handles[64] = {nullptr};
-    static std::mutex mu;  // one decomposition at a time per process (the handles are shared)
-    std::lock_guard<std::mutex> lock(mu);
-    int dev = 0;
-    GMAT_HIP(hipGetDevice(&dev));
-    GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_HIP, "eigen: device %d", dev);
-    if (!handles[dev])
-      GMAT_CHECK(rocblas_create_handle(&handles[dev]) == rocblas_status_success, GMAT_E_HIP, "eigen: rocblas handle");
-    const rocblas_status st = rocsolver_dsyevd(handles[dev], rocblas_evect_original, rocblas_fill_lower, (rocblas_int)n,
-                                               A.as<double>(), (rocblas_int)n, W.as<double>(), E.as<double>(),
-                                               dinfo.as<rocblas_int>());
-    GMAT_HIP(hipDeviceSynchronize());
-    GMAT_CHECK(st == rocblas_status_success, GMAT_E_HIP, "eigen: rocsolver_dsyevd status %d", (int)st);
-  }
-  int hinfo = 0;
-  GMAT_HIP(hipMemcpy(&hinfo, dinfo.p, sizeof(int), hipMemcpyDeviceToHost));
-  GMAT_CHECK(hinfo == 0, GMAT_E_HIP, "eigen: syevd info %d", hinfo);
   eg->ne = ne;
   eg->lam.resize(ne);
   eg->Z.resize((size_t)n * ne);
-  GMAT_HIP(hipMemcpy(eg->lam.data(), W.p, ne * sizeof(double), hipMemcpyDeviceToHost));
-  GMAT_HIP(hipMemcpy(eg->Z.data(), A.p, eg->Z.size() * sizeof(double), hipMemcpyDeviceToHost));
+  GMAT_TRY(sym_eig_bottom(n, A.as<double>(), ne, eg->lam.data(), Z.as<double>()));
+  GMAT_HIP(hipMemcpy(eg->Z.data(), Z.p, eg->Z.size() * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }
 
@@ -2468,6 +2445,32 @@ int certify_below(double top, F &&ok, double *best) {
   return GMAT_OK;
 }
 
+// Q(lam) on the device: block (r, bI) of sqrt(d_r) u_r quantised to fp6 (fp6_block), dequantised
+// into Bn (natural [k][r]) and Bs (storage [q][r]), and the tile images when img is given.
+__global__ void lr_quant_kernel(int64_t n, int64_t n_pad, int nK, int Rp, const double *__restrict__ Z,
+                                const double *__restrict__ sd, double *__restrict__ Bn, double *__restrict__ Bs,
+                                uint32_t *__restrict__ img) {
+  const int64_t nblk = n_pad / 32;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)Rp * nblk) return;
+  const int r = (int)(idx / nblk);
+  const int64_t bI = idx % nblk;
+  const double s = sd[r];
+  double v[32], dq[32];
+  for (int j = 0; j < 32; ++j) {
+    const int64_t c = bI * 32 + perm_nat(j);
+    v[j] = (s > 0.0 && c < n) ? s * Z[(size_t)r * n + c] : 0.0;
+  }
+  uint32_t wds[8];
+  fp6_block(v, wds, dq);
+  if (img) fp6_store(img, nK, r, bI, wds);
+  for (int j = 0; j < 32; ++j) {
+    const int64_t c = bI * 32 + perm_nat(j);
+    if (c < n) Bn[(size_t)c * Rp + r] = dq[j];
+    Bs[(size_t)(bI * 32 + j) * Rp + r] = dq[j];
+  }
+}
+
 int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, const Eigen &eg) {
   const int64_t n = e->n, n_pad = e->n_pad;
   const char *renv = getenv("GMAT_LR_RANK"), *kenv = getenv("GMAT_LR_KAPPA");
@@ -2488,37 +2491,31 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, cons
   const double lam_top = lam_r[ne - 1];
   const char *tenv = getenv("GMAT_LR_TAU");
   const double tau = (tenv ? atof(tenv) : 0.5) * lam_top;
-  std::vector<uint32_t> img((size_t)nC * nK * MX_TILE / 4, 0u);
-  std::vector<double> Bn((size_t)n * Rp, 0.0), Bs((size_t)n_pad * Rp, 0.0);  // natural [k][r], storage [q][r]
-  auto quantise = [&](double lam, bool images) {
-    std::fill(Bn.begin(), Bn.end(), 0.0);
-    std::fill(Bs.begin(), Bs.end(), 0.0);
-    for (int r = 0; r < Rp; ++r) {
-      const double sd = r < Re ? std::sqrt(std::max(lam - lam_r[r], 0.0) * (1.0 + kap)) : 0.0;
-      for (int64_t bI = 0; bI < n_pad / 32; ++bI) {
-        double v[32], dq[32];
-        for (int j = 0; j < 32; ++j) {
-          const int64_t c = bI * 32 + perm_nat(j);
-          v[j] = (sd > 0.0 && c < n) ? sd * Zh[(size_t)r * n + c] : 0.0;
-        }
-        uint32_t wds[8];
-        fp6_block(v, wds, dq);
-        if (images) fp6_store(img.data(), nK, r, bI, wds);
-        for (int j = 0; j < 32; ++j) {
-          const int64_t c = bI * 32 + perm_nat(j);
-          if (c < n) Bn[(size_t)c * Rp + r] = dq[j];
-          Bs[(size_t)(bI * 32 + j) * Rp + r] = dq[j];
-        }
-      }
-    }
-  };
-  DBuf A, dBn, C, dinv, ld, cinfo;
+  const size_t img_words = (size_t)nC * nK * MX_TILE / 4;
+  std::vector<double> Bn((size_t)n * Rp, 0.0);  // natural [k][r] (host copy of the certified Q)
+  DBuf A, dBn, dBs, dsd, C, dinv, ld, cinfo;
   GMAT_TRY(A.alloc(n * n * sizeof(double)));
   GMAT_TRY(dBn.alloc(Bn.size() * sizeof(double)));
+  GMAT_TRY(dBs.alloc((size_t)n_pad * Rp * sizeof(double)));
+  GMAT_TRY(dsd.alloc(Rp * sizeof(double)));
   GMAT_TRY(C.alloc(n * n * sizeof(double)));
   GMAT_TRY(dinv.alloc(n * 64 * sizeof(double)));
   GMAT_TRY(ld.alloc(sizeof(double)));
   GMAT_TRY(cinfo.alloc(sizeof(int)));
+  GMAT_TRY(e->lr_tiles.alloc(img_words * 4));
+  GMAT_HIP(hipMemset(dBn.p, 0, Bn.size() * sizeof(double)));
+  GMAT_HIP(hipMemset(dBs.p, 0, (size_t)n_pad * Rp * sizeof(double)));
+  GMAT_HIP(hipMemset(e->lr_tiles.p, 0, img_words * 4));
+  auto quantise = [&](double lam, bool images) -> int {
+    std::vector<double> sd(Rp, 0.0);
+    for (int r = 0; r < Re; ++r) sd[r] = std::sqrt(std::max(lam - lam_r[r], 0.0) * (1.0 + kap));
+    GMAT_HIP(hipMemcpy(dsd.p, sd.data(), Rp * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(lr_quant_kernel, dim3((unsigned)cdiv((int64_t)Rp * (n_pad / 32), 256)), dim3(256), 0, 0, n, n_pad,
+                       nK, Rp, eg.dZ.as<double>(), dsd.as<double>(), dBn.as<double>(), dBs.as<double>(),
+                       images ? e->lr_tiles.as<uint32_t>() : nullptr);
+    GMAT_HIP(hipGetLastError());
+    return GMAT_OK;
+  };
   auto eps_of = [&](double lam) {  // Bn must be quantise(lam)
     double trC = 0.0, cmax = 0.0;
     for (int64_t k = 0; k < n; ++k) {
@@ -2533,8 +2530,7 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, cons
            (double)n * (Rp + 4) * u * (pmax + 2.0 * lam + 2.0 * (lam + tau) / (double)n + cmax);
   };
   auto ok = [&](double lam) -> int {
-    quantise(lam, false);
-    GMAT_HIP(hipMemcpy(dBn.p, Bn.data(), Bn.size() * sizeof(double), hipMemcpyHostToDevice));
+    GMAT_TRY(quantise(lam, false));
     GMAT_TRY(dgemm(0, n, n, Rp, 1.0, DView{dBn.as<double>(), Rp, 0}, DView{dBn.as<double>(), Rp, 1}, 0.0,
                    C.as<double>(), n));
     hipLaunchKernelGGL(lr_shift_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dP, C.as<double>(), lam,
@@ -2548,7 +2544,8 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, cons
   };
   double lo = 0.0;
   GMAT_TRY(certify_below(lam_top, ok, &lo));
-  quantise(lo, true);  // the certified Q (quantise is deterministic)
+  GMAT_TRY(quantise(lo, true));  // the certified Q (quantise is deterministic)
+  GMAT_HIP(hipMemcpy(Bn.data(), dBn.p, Bn.size() * sizeof(double), hipMemcpyDeviceToHost));
   e->setup[3] = now() - t1;
   const double eps = eps_of(lo);
   if (getenv("GMAT_DEBUG"))
@@ -2571,11 +2568,9 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, cons
     const double eta = u32 * l1 * (8.0 * (double)n_pad + 400.0) * 1.01;
     Esum += eta * eta;
   }
-  GMAT_TRY(e->lr_tiles.alloc(img.size() * 4));
-  GMAT_TRY(e->lr_Bs.alloc(Bs.size() * sizeof(double)));
+  GMAT_TRY(e->lr_Bs.alloc((size_t)n_pad * Rp * sizeof(double)));
   GMAT_TRY(e->lr_q1.alloc(Rp * sizeof(double)));
-  GMAT_HIP(hipMemcpy(e->lr_tiles.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
-  GMAT_HIP(hipMemcpy(e->lr_Bs.p, Bs.data(), Bs.size() * sizeof(double), hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(e->lr_Bs.p, dBs.p, (size_t)n_pad * Rp * sizeof(double), hipMemcpyDeviceToDevice));
   GMAT_HIP(hipMemcpy(e->lr_q1.p, q1.data(), Rp * sizeof(double), hipMemcpyHostToDevice));
   e->lr_lam = lo;
   e->lr_tau = tau;

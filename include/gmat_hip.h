@@ -193,6 +193,9 @@ int gmat_comm_barrier(gmat_comm *c);
  * accumulated in fp32; out[32 x 32] (every column = 4 sum_k A[r][k]).  Lets tests check the
  * screen's fp32 accumulation bound (eta_r) on the hardware. */
 int gmat_probe_mx_accum(int n_steps, const uint8_t *codes, const uint8_t *scales, float *out);
+/* The scan plan's partial symmetric eigensolver on a host matrix (n x n, symmetric): the ne
+ * smallest eigenvalues ascending to w_out, eigenvector r to z_out[r*n .. r*n+n).  Test support. */
+int gmat_probe_eig_bottom(int64_t n, const double *a_host, int ne, double *w_out, double *z_out);
 
 #ifdef __cplusplus
 }
