@@ -161,7 +161,8 @@ def grm_bench(n, m_grm, seed, reps=5):
     return {"config": "configs[1]: agmat GRM %d x %d" % (n, m_grm), "gflops_kernel": flop / kern / 1e9,
             "gflops_end_to_end": flop / wall / 1e9, "kernel_ms": kern * 1e3, "end_to_end_ms": wall * 1e3,
             "flop_convention": "dense-equivalent 2 n^2 m", "int8_ops_issued": float(st[1]),
-            "int8_tops": st[1] / kern / 1e12}
+            "int8_tops": st[1] / kern / 1e12, "int8_frac_of_peak": st[1] / kern / 1e12 / INT8_PEAK_TOPS,
+            "device_ms_all_kernels": float(st[3]) * 1e3}
 
 
 def reml_bench(k, seed):

@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 RAW=gpurun_out/$TAG/raw  # inside gpurun_out so a long pass shows progress; deleted after filtering
 mkdir -p $OUT $RAW
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS="bench.py --n-snp ${NSNP:-10000} --steps 1 --warmup 0 --no-cpu --no-grm --no-eff"
+ARGS=${ARGS:-"bench.py --n-snp ${NSNP:-10000} --steps 1 --warmup 0 --no-cpu --no-grm --no-eff"}
 i=0
 PASSES=${PASSES:-all}
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
