@@ -27,10 +27,10 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // Factor the kb x kb (kb <= 64) diagonal block at a (lda) in LDS with 4 barrier-separated
 // 16-column panels (instead of one barrier group per column): wave 0 factors a panel with its rows
 // in registers (pivot and the panel's column entries broadcast by readlane, no LDS round trips),
-// then all 256 threads apply the panel to the trailing lower triangle.  inv(L) is blocked the same
-// way: the four 16 x 16 diagonal inverses by forward substitution (one thread per column, the
-// column in registers), then the off-diagonal blocks by distance d = i - j as two small products,
-// X_ij = -X_ii (sum_{j<=k<i} L_ik X_kj).  Rows / columns >= kb are an uncoupled identity.  Writes
+// then the four waves apply the panel to the trailing lower 16 x 16 blocks on fp64 MFMA.  inv(L)
+// is blocked the same way: the four 16 x 16 diagonal inverses by forward substitution (one thread
+// per column, the column in registers), then the off-diagonal blocks by distance d = i - j as two
+// small MFMA products, X_ij = -X_ii (sum_{j<=k<i} L_ik X_kj).  Rows / columns >= kb are an uncoupled identity.  Writes
 // L back, inv(L) to dinv (kb rows of NB doubles), adds 2 sum(log diag) to *logdet, flags a bad
 // pivot's block in *info.
 __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv, double *logdet,
@@ -39,6 +39,7 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
   __shared__ double Ls[NB][NB + 1];
   __shared__ double Xs[NB][NB + 1];
   __shared__ double Ts[NP - 1][PW][PW + 1];
+  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int e = tid; e < NB * NB; e += 256) {
     const int rr = e / NB, cc = e % NB;
@@ -47,7 +48,6 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
   }
   __syncthreads();
   bool bad = false;
-  double ld = 0.0;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int c0 = PW * p;
@@ -63,8 +63,12 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
           if (c0 + j < kb) bad = true;
           d = 1.0;
         }
-        const double ljj = sqrt(d), inv = 1.0 / ljj;
-        if (c0 + j < kb) ld += log(ljj);
+        // 1/sqrt(d) from v_rsq_f64 and two Newton steps (to ~1 ulp), L_jj = d / sqrt(d)
+        double inv = __builtin_amdgcn_rsq(d);
+        inv = inv * fma(-0.5 * d * inv, inv, 1.5);
+        inv = inv * fma(-0.5 * d * inv, inv, 1.5);
+        const double ljj = d * inv;
+        if (i == 0) piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
         r[j] = (i > c0 + j) ? r[j] * inv : (i == c0 + j ? ljj : r[j]);
 #pragma unroll
         for (int k = j + 1; k < PW; ++k) r[k] = fma(-r[j], readlane_d(r[j], c0 + k), r[k]);
@@ -74,14 +78,23 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
         for (int q = 0; q < PW; ++q) Ls[i][c0 + q] = (c0 + q <= i) ? r[q] : 0.0;
     }
     __syncthreads();
-    const int t0 = c0 + PW, mt = NB - t0;
-    for (int e = tid; e < mt * mt; e += 256) {
-      const int i = t0 + e / mt, k = t0 + e % mt;
-      if (k <= i) {
-        double sacc = Ls[i][k];
+    // trailing lower blocks (bi >= bk > p) -= L_i,p L_k,p' on v_mfma_f64_16x16x4, one wave per block
+    {
+      const int nb = NP - 1 - p;  // block rows below the panel
+      for (int blk = w; blk < nb * (nb + 1) / 2; blk += 4) {
+        int bi = 0;
+        while ((bi + 1) * (bi + 2) / 2 <= blk) ++bi;
+        const int bk = blk - bi * (bi + 1) / 2;
+        const int ri = PW * (p + 1 + bi), rk = PW * (p + 1 + bk);
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < PW; ++q) sacc = fma(-Ls[i][c0 + q], Ls[k][c0 + q], sacc);
-        Ls[i][k] = sacc;
+        for (int s4 = 0; s4 < PW / 4; ++s4) {
+          const double av = Ls[ri + (lane & 15)][c0 + 4 * s4 + (lane >> 4)];
+          const double bv = Ls[rk + (lane & 15)][c0 + 4 * s4 + (lane >> 4)];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ls[ri + (lane >> 4) + 4 * q][rk + (lane & 15)] -= acc[q];
       }
     }
     __syncthreads();
@@ -102,24 +115,34 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
     for (int q = 0; q < PW; ++q) Xs[o + q][o + c] = x[q];
   }
   __syncthreads();
-  const int rr = tid / PW, cc = tid % PW;
+  // off-diagonal blocks by distance d = i - j on v_mfma_f64_16x16x4 (wave j of the level):
+  // T_j = sum_{k=j}^{i-1} L_ik X_kj, then X_ij = -X_ii T_j
 #pragma unroll
   for (int d = 1; d < NP; ++d) {
-    for (int j = 0; j + d < NP; ++j) {  // T_j = sum_{k=j}^{i-1} L_ik X_kj, i = j + d
-      const int i = j + d;
-      double sacc = 0.0;
+    const int j = w, i = j + d;
+    if (i < NP) {
+      v4d acc = {0.0, 0.0, 0.0, 0.0};
       for (int k = j; k < i; ++k)
 #pragma unroll
-        for (int q = 0; q < PW; ++q) sacc = fma(Ls[PW * i + rr][PW * k + q], Xs[PW * k + q][PW * j + cc], sacc);
-      Ts[j][rr][cc] = sacc;
+        for (int s4 = 0; s4 < PW / 4; ++s4) {
+          const double av = Ls[PW * i + (lane & 15)][PW * k + 4 * s4 + (lane >> 4)];
+          const double bv = Xs[PW * k + 4 * s4 + (lane >> 4)][PW * j + (lane & 15)];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ts[j][(lane >> 4) + 4 * q][lane & 15] = acc[q];
     }
     __syncthreads();
-    for (int j = 0; j + d < NP; ++j) {  // X_ij = -X_ii T_j
-      const int i = j + d;
-      double sacc = 0.0;
+    if (i < NP) {
+      v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < PW; ++q) sacc = fma(Xs[PW * i + rr][PW * i + q], Ts[j][q][cc], sacc);
-      Xs[PW * i + rr][PW * j + cc] = -sacc;
+      for (int s4 = 0; s4 < PW / 4; ++s4) {
+        const double av = Xs[PW * i + (lane & 15)][PW * i + 4 * s4 + (lane >> 4)];
+        const double bv = Ts[j][4 * s4 + (lane >> 4)][lane & 15];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xs[PW * i + (lane >> 4) + 4 * q][PW * j + (lane & 15)] = -acc[q];
     }
     __syncthreads();
   }
@@ -128,9 +151,13 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
     if (c2 < kb) a[(int64_t)r2 * lda + c2] = Ls[r2][c2];
     dinv[r2 * NB + c2] = (c2 < kb) ? Xs[r2][c2] : 0.0;
   }
-  if (tid == 0) {
-    *logdet += 2.0 * ld;
-    if (bad && *info == 0) *info = (int)(k0 + 1);
+  if (w == 0) {  // sum of log L_jj over the block, one log per lane, fixed shuffle tree
+    double lg = log(piv[lane]);
+    for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off);
+    if (lane == 0) {
+      *logdet += 2.0 * lg;
+      if (bad && *info == 0) *info = (int)(k0 + 1);
+    }
   }
 }
 
@@ -168,22 +195,27 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
 
 int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *work,
                           double *ainv) {
-  // work: n*n (Linv, lower) + NB*n (row-panel scratch)
-  double *linv = work, *t = work + n * n;
+  // X = L^-1 by right-looking block forward substitution (work: n*n, lower): block row i of X is
+  // inv(L_ii) times the accumulated right-hand side, then every later block row j subtracts
+  // L_ji X_i in one wide product ((n - i0) x (i0 + 64) x 64) -- the large GEMMs carry the n^3/3
+  // flops instead of 64-row strips.
+  double *linv = work;
   hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s, linv, n * n);
   GMAT_HIP(hipGetLastError());
   for (int64_t i0 = 0; i0 < n; i0 += NB) {
     const int kb = (int)std::min<int64_t>(NB, n - i0);
-    hipLaunchKernelGGL(copy_block_kernel, dim3(kb), dim3(NB), 0, s, kb, dinv + i0 * NB, linv + i0 * n + i0, n);
+    double *xi = linv + i0 * n;
+    // X_i[:, 0:i0] = inv(L_ii) B_i[:, 0:i0]  (in place: each output tile reads only its own columns)
+    if (i0 > 0) GMAT_TRY(dgemm(s, kb, i0, kb, 1.0, DView{dinv + i0 * NB, NB, 0}, DView{xi, n, 0}, 0.0, xi, n));
+    hipLaunchKernelGGL(copy_block_kernel, dim3(kb), dim3(NB), 0, s, kb, dinv + i0 * NB, xi + i0, n);
     GMAT_HIP(hipGetLastError());
-    if (i0 == 0) continue;
-    // T = L[i, 0:i0] * Linv[0:i0, 0:i0]
-    GMAT_TRY(dgemm(s, kb, i0, i0, 1.0, DView{l + i0 * ldl, ldl, 0}, DView{linv, n, 0}, 0.0, t, i0));
-    // Linv[i, 0:i0] = -inv(L_ii) * T
-    GMAT_TRY(dgemm(s, kb, i0, kb, -1.0, DView{dinv + i0 * NB, NB, 0}, DView{t, i0, 0}, 0.0, linv + i0 * n, n));
+    const int64_t rem = n - i0 - kb;
+    if (rem > 0)  // B_j -= L_ji X_i for the block rows below
+      GMAT_TRY(dgemm(s, rem, i0 + kb, kb, -1.0, DView{l + (i0 + kb) * ldl + i0, ldl, 0}, DView{xi, n, 0}, 1.0,
+                     linv + (i0 + kb) * n, n));
   }
   // ainv = Linv' Linv (lower tiles, then mirror)
-  GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{linv, n, 1}, DView{linv, n, 0}, 0.0, ainv, n, 1));
+  GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{linv, n, 1}, DView{linv, n, 0}, 0.0, ainv, n, 2));
   GMAT_TRY(fill_sym_upper(s, n, ainv, n));
   return GMAT_OK;
 }

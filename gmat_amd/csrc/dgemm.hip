@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int64_t M, int64_t N, int64_
                                                     LB lb, double beta, double *__restrict__ C, int64_t ldc,
                                                     int mask) {
   const int64_t bm = (int64_t)blockIdx.y * TM, bn = (int64_t)blockIdx.x * TN;
-  if (mask == 1 && blockIdx.y < blockIdx.x) return;
+  if (mask >= 1 && blockIdx.y < blockIdx.x) return;
   __shared__ double As[2][TK][TM + 1];
   __shared__ double Bs[2][TK][TN + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -68,15 +68,17 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int64_t M, int64_t N, int64_
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
 
+  // mask 2: both operands vanish for k < row (A' A with A lower triangular): start at the tile row
+  const int kt0 = mask == 2 ? (int)(bm / TK) : 0;
   double ra[4], rb[4];
-  fetch(la, bm, 0, tid, ra);
-  fetch(lb, bn, 0, tid, rb);
+  fetch(la, bm, (int64_t)kt0 * TK, tid, ra);
+  fetch(lb, bn, (int64_t)kt0 * TK, tid, rb);
   store(la, As[0], tid, ra);
   store(lb, Bs[0], tid, rb);
   __syncthreads();
   const int nk = (int)((K + TK - 1) / TK);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+  for (int kt = kt0; kt < nk; ++kt) {
+    const int cur = (kt - kt0) & 1;
     if (kt + 1 < nk) {
       fetch(la, bm, (int64_t)(kt + 1) * TK, tid, ra);
       fetch(lb, bn, (int64_t)(kt + 1) * TK, tid, rb);
@@ -115,10 +117,96 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int64_t M, int64_t N, int64_
       }
 }
 
+// Skinny products (N <= 8 with K >= 256, or M * N <= 64): the 64 x 64 tile grid would leave most
+// of the chip idle and read A at a few hundred GB/s.  One wave per output row (A contiguous along
+// k: coalesced row reads, B's N columns shared through the cache) or one thread per row (A stored
+// k-major), fixed reduction order (deterministic).
+template <int NC, class LA, class LB>
+__global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t M, int64_t K, double alpha, LA la, LB lb, double beta,
+                                                        double *__restrict__ C, int64_t ldc, int64_t N) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  double acc[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j] = 0.0;
+  for (int64_t k = lane; k < K; k += 64) {
+    const double a = la.p[r * la.ld + k];
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (j < N) acc[j] = fma(a, lb.at(j, k), acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    double v = acc[j];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0 && j < N) {
+      double o = alpha * v;
+      if (beta != 0.0) o += beta * C[r * ldc + j];
+      C[r * ldc + j] = o;
+    }
+  }
+}
+template <int NC, class LA, class LB>
+__global__ __launch_bounds__(256) void gemv_cols_kernel(int64_t M, int64_t K, double alpha, LA la, LB lb, double beta,
+                                                        double *__restrict__ C, int64_t ldc, int64_t N) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  double acc[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) acc[j] = 0.0;
+  for (int64_t k = 0; k < K; ++k) {
+    const double a = la.p[k * la.ld + r];
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (j < N) acc[j] = fma(a, lb.at(j, k), acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j)
+    if (j < N) {
+      double o = alpha * acc[j];
+      if (beta != 0.0) o += beta * C[r * ldc + j];
+      C[r * ldc + j] = o;
+    }
+}
+// M * N <= 64 outputs, long K: one workgroup per output, 256-way split of k, fixed tree.
+template <class LA, class LB>
+__global__ __launch_bounds__(256) void dot_kernel(int64_t M, int64_t N, int64_t K, double alpha, LA la, LB lb,
+                                                  double beta, double *__restrict__ C, int64_t ldc) {
+  __shared__ double red[4];
+  const int64_t i = blockIdx.x / N, j = blockIdx.x % N;
+  double v = 0.0;
+  for (int64_t k = threadIdx.x; k < K; k += 256) v = fma(la.at(i, k), lb.at(j, k), v);
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double o = alpha * ((red[0] + red[1]) + (red[2] + red[3]));
+    if (beta != 0.0) o += beta * C[i * ldc + j];
+    C[i * ldc + j] = o;
+  }
+}
+
 template <class LA, class LB>
 int launch(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, LA la, LB lb, double beta, double *C,
            int64_t ldc, int mask) {
   if (M <= 0 || N <= 0) return GMAT_OK;
+  if (mask == 0 && K >= 256 && M * N <= 64) {
+    hipLaunchKernelGGL((dot_kernel<LA, LB>), dim3((unsigned)(M * N)), dim3(256), 0, s, M, N, K, alpha, la, lb, beta, C,
+                       ldc);
+    GMAT_HIP(hipGetLastError());
+    return GMAT_OK;
+  }
+  if (mask == 0 && K >= 256 && N <= 8) {
+    if (la.contig_k)
+      hipLaunchKernelGGL((gemv_rows_kernel<8, LA, LB>), dim3((unsigned)cdiv(M, 4)), dim3(256), 0, s, M, K, alpha, la, lb,
+                         beta, C, ldc, N);
+    else
+      hipLaunchKernelGGL((gemv_cols_kernel<8, LA, LB>), dim3((unsigned)cdiv(M, 256)), dim3(256), 0, s, M, K, alpha, la,
+                         lb, beta, C, ldc, N);
+    GMAT_HIP(hipGetLastError());
+    return GMAT_OK;
+  }
   dim3 grid((unsigned)cdiv(N, TN), (unsigned)cdiv(M, TM));
   hipLaunchKernelGGL((dgemm_kernel<LA, LB>), grid, dim3(256), 0, s, M, N, K, alpha, la, lb, beta, C, ldc, mask);
   GMAT_HIP(hipGetLastError());

@@ -19,7 +19,8 @@ struct I8View {
 };
 
 // C[M x N] = alpha * op(A)[M x K] * op(B)[K x N] + beta * C  (row-major C, ldc).
-// mask: 0 = every tile, 1 = only 64x64 tiles with tile_row >= tile_col (lower half).
+// mask: 0 = every tile, 1 = only 64x64 tiles with tile_row >= tile_col (lower half), 2 = as 1 and
+// the k loop starts at the tile's first row (op(A)[r, k] = 0 for k < r: A' A with A lower).
 int dgemm(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DView A, DView B, double beta,
           double *C, int64_t ldc, int mask = 0);
 // Same with an int8 A (values converted exactly to fp64).

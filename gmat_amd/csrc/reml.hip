@@ -133,7 +133,7 @@ struct Model {
     GMAT_TRY(w.alloc((size_t)n * (c + 1) * sizeof(double)));
     GMAT_TRY(pw.alloc((size_t)n * (c + 1) * sizeof(double)));
     GMAT_TRY(small.alloc(4096 * sizeof(double)));
-    GMAT_TRY(rowbuf.alloc((size_t)n * sizeof(double)));
+    GMAT_TRY(rowbuf.alloc((size_t)n * (c + 1) * sizeof(double)));
     GMAT_TRY(col.alloc((size_t)n * sizeof(int64_t)));
     GMAT_HIP(hipMemcpy(x.p, hx, (size_t)n * p * sizeof(double), hipMemcpyHostToDevice));
     GMAT_HIP(hipMemcpy(y.p, hy, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
@@ -194,45 +194,19 @@ struct Model {
     return GMAT_OK;
   }
 
-  double sum_rows(const double *dev_rows) {
-    std::vector<double> h(n);
-    (void)hipMemcpyAsync(h.data(), dev_rows, n * sizeof(double), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    double acc = 0.0;
-    for (double x2 : h) acc += x2;
-    return acc;
-  }
-
-  // gradient fd (c+1) and AI matrix ((c+1)^2) at the current P, Py
+  // gradient fd (c+1) and AI matrix ((c+1)^2) at the current P, Py: every device product is queued
+  // first and the results come back in one transfer (one host synchronisation per call).
   int derivatives(double *fd, double *ai) {
     const int c1 = c + 1;
-    std::vector<double> hpy(n);
-    GMAT_HIP(hipMemcpyAsync(hpy.data(), py.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
     for (int k = 0; k < c; ++k) {
-      // tr(P ZGZ') = sum_ab P_ab (ZGZ')_ab   (both symmetric)
-      GMAT_TRY(dot_rows(s, n, n, pm.as<double>(), n, zg[k].as<double>(), n, rowbuf.as<double>()));
-      const double tr = sum_rows(rowbuf.as<double>());
+      // tr(P ZGZ') = sum_ab P_ab (ZGZ')_ab   (both symmetric): row sums into rowbuf[k]
+      GMAT_TRY(dot_rows(s, n, n, pm.as<double>(), n, zg[k].as<double>(), n, rowbuf.as<double>() + k * n));
       // W[:,k] = ZGZ' Py
       GMAT_TRY(dgemm(s, n, 1, n, 1.0, DView{zg[k].as<double>(), n, 0}, DView{py.as<double>(), 1, 0}, 0.0,
                      w.as<double>() + k, c1));
-      std::vector<double> hw(n * c1);
-      GMAT_HIP(hipMemcpyAsync(hw.data(), w.p, n * c1 * sizeof(double), hipMemcpyDeviceToHost, s));
-      GMAT_HIP(hipStreamSynchronize(s));
-      double q = 0.0;
-      for (int64_t r = 0; r < n; ++r) q += hpy[r] * hw[r * c1 + k];
-      fd[k] = 0.5 * (-tr + q);
     }
-    // residual: -tr(P) + Py'Py
-    {
-      std::vector<double> pd(n);
-      hipLaunchKernelGGL(trace_kernel, dim3(1), dim3(64), 0, s, n, pm.as<double>(), rowbuf.as<double>());
-      GMAT_HIP(hipGetLastError());
-      GMAT_HIP(hipMemcpyAsync(pd.data(), rowbuf.p, sizeof(double), hipMemcpyDeviceToHost, s));
-      GMAT_HIP(hipStreamSynchronize(s));
-      double pp = 0.0;
-      for (int64_t r = 0; r < n; ++r) pp += hpy[r] * hpy[r];
-      fd[c] = 0.5 * (-pd[0] + pp);
-    }
+    hipLaunchKernelGGL(trace_kernel, dim3(1), dim3(64), 0, s, n, pm.as<double>(), rowbuf.as<double>() + c * n);
+    GMAT_HIP(hipGetLastError());
     // W[:,c] = Py
     GMAT_TRY(dgemm(s, n, 1, 1, 1.0, DView{py.as<double>(), 1, 0}, DView{small.as<double>() + 3000, 1, 0}, 0.0,
                    w.as<double>() + c, c1));
@@ -241,8 +215,21 @@ struct Model {
                    pw.as<double>(), c1));
     double *dai = small.as<double>() + 2200;
     GMAT_TRY(dgemm(s, c1, c1, n, 0.5, DView{w.as<double>(), c1, 1}, DView{pw.as<double>(), c1, 0}, 0.0, dai, c1));
+    std::vector<double> rows((size_t)n * c + 1), hw((size_t)n * c1);
+    GMAT_HIP(hipMemcpyAsync(rows.data(), rowbuf.p, ((size_t)n * c + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+    GMAT_HIP(hipMemcpyAsync(hw.data(), w.p, hw.size() * sizeof(double), hipMemcpyDeviceToHost, s));
     GMAT_HIP(hipMemcpyAsync(ai, dai, c1 * c1 * sizeof(double), hipMemcpyDeviceToHost, s));
     GMAT_HIP(hipStreamSynchronize(s));
+    // W[:,c] is Py itself
+    for (int k = 0; k < c; ++k) {
+      double tr = 0.0, q = 0.0;
+      for (int64_t r = 0; r < n; ++r) tr += rows[(size_t)k * n + r];
+      for (int64_t r = 0; r < n; ++r) q += hw[r * c1 + c] * hw[r * c1 + k];
+      fd[k] = 0.5 * (-tr + q);
+    }
+    double pp = 0.0;  // residual: -tr(P) + Py'Py
+    for (int64_t r = 0; r < n; ++r) pp += hw[r * c1 + c] * hw[r * c1 + c];
+    fd[c] = 0.5 * (-rows[(size_t)n * c] + pp);
     return GMAT_OK;
   }
 };

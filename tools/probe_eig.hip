@@ -72,6 +72,17 @@ int main() {
       rocsolver_ssytrd(hb, rocblas_fill_lower, n, Af, n, Wf, Ef, (float *)res);
       hipDeviceSynchronize();
       double t7 = now();
+      // rocSOLVER Cholesky + inverse from the factor (the REML's V^-1)
+      hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice);
+      hipDeviceSynchronize();
+      double tp0 = now();
+      rocsolver_dpotrf(hb, rocblas_fill_lower, n, A, n, info);
+      hipDeviceSynchronize();
+      double tp1 = now();
+      rocsolver_dpotri(hb, rocblas_fill_lower, n, A, n, info);
+      hipDeviceSynchronize();
+      double tp2 = now();
+      if (rep) printf("n %d: rocsolver dpotrf %.2f ms, dpotri %.2f ms\n", n, (tp1 - tp0) * 1e3, (tp2 - tp1) * 1e3);
       // library dgemm n x n x 416 and Cholesky
       double *dinv, *ld;
       int *ci;
