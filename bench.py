@@ -254,13 +254,16 @@ def eff_cpu_baseline(geno, py, cut, budget_s):
     m, n = geno.shape
     body = synth.pack_bed(geno)[3:]
     threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
-    # a probe call sizes the sample so that one call (decode + centring + rows, as the reference's
-    # call does) takes about budget_s
-    probe = np.linspace(0, m - 2, 8).astype(np.int64)
-    t0 = time.perf_counter()
-    O.eff_screen_c("AA", body, n, m, probe, py, [cut], threads=threads)
-    rate = float(np.sum(m - 1 - probe)) / (time.perf_counter() - t0)
-    k = int(min(m - 1, max(8, rate * budget_s / (m / 2))))
+    # two probe calls separate the per-call cost (decode + centring, as the reference's call pays
+    # it) from the per-pair rate, which sizes the sample to about budget_s of pair work
+    t = []
+    for kp in (8, 40):
+        probe = np.linspace(0, m - 2, kp).astype(np.int64)
+        t0 = time.perf_counter()
+        O.eff_screen_c("AA", body, n, m, probe, py, [cut], threads=threads)
+        t.append((float(np.sum(m - 1 - probe)), time.perf_counter() - t0))
+    per_pair = max((t[1][1] - t[0][1]) / (t[1][0] - t[0][0]), 1e-12)
+    k = int(min(m - 1, max(8, budget_s / per_pair / (m / 2))))
     rows = np.linspace(0, m - 2, k).astype(np.int64)
     t0 = time.perf_counter()
     O.eff_screen_c("AA", body, n, m, rows, py, [cut], threads=threads)
