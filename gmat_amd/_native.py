@@ -38,6 +38,8 @@ _PROTOS = {
     "gmat_reml": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _INT, _D, _D, _P, _P, _P]),
     "gmat_projection": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P, _P]),
     "gmat_epi_create": (_INT, [_P, _P, _P, _P, _INT]),
+    "gmat_epi_create_with": (_INT, [_P, _P, _P, _P, _INT, _P, _I64]),
+    "gmat_epi_export": (_INT, [_P, _P, _I64, _P]),
     "gmat_epi_scan": (_INT, [_P, _INT, _P, _I64, _D, _D, _INT, _P]),
     "gmat_epi_hits": (_INT, [_P, _I64, _P, _P, _P, _P, _P, _P]),
     "gmat_epi_pairs": (_INT, [_P, _INT, _P, _I64, _P, _P, _P, _P]),

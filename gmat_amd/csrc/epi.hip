@@ -2196,6 +2196,8 @@ struct gmat_epi {
   // [3] low-rank certificate, [4] slices + residual bounds, [5] coding builds (side vectors, lazily
   // in the first scan of a kind), [6] Cholesky factorisations run by the certificates
   double setup[8] = {0};
+  uint64_t p_hash = 0;  // fingerprint of P (guards imported spectral state)
+  int imported = 0;     // spectral state imported from another plan (gmat_epi_create_with)
   hipStream_t s = 0;
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
   struct ScanBufs {
@@ -2581,7 +2583,13 @@ int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, cons
 }
 }  // namespace
 
-extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
+namespace {
+constexpr uint64_t EPI_STATE_MAGIC = 0x31495045544d4147ULL;  // "GMATEPI1"
+int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes);
+}  // namespace
+
+static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
+                           const uint8_t *state, int64_t state_bytes) {
   GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
   GMAT_CHECK(n_slice >= 1 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 1..4");
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
@@ -2597,13 +2605,19 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   e->nK = (int)(g->n_pad / MXK);
   const int64_t n = e->n, n_pad = e->n_pad;
   double pmax = 0.0, qmax = 0.0;  // max |P|, max |P_kl| off the diagonal
+  uint64_t ph = 0x9e3779b97f4a7c15ULL ^ (uint64_t)n;
   for (int64_t i = 0; i < n; ++i)
     for (int64_t k = 0; k < n; ++k) {
       const double v = std::fabs(pvp[i * n + k]);
       pmax = std::max(pmax, v);
       if (k != i) qmax = std::max(qmax, v);
+      uint64_t b;
+      memcpy(&b, &pvp[i * n + k], 8);
+      ph = (ph ^ b) * 0x100000001b3ULL;
+      ph ^= ph >> 29;
     }
   e->qmax = qmax;
+  e->p_hash = ph;
   double spy = 0.0;
   for (int64_t i = 0; i < n; ++i) spy += py[i];
   e->spy = spy;
@@ -2701,112 +2715,116 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   }
   (void)hipDeviceSynchronize();
   e->setup[4] = now() - t_create;
-  double trP = 0.0;
-  for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
-  // Bottom eigenpairs of P (intercept lifted): the prefilter's covariate directions (P's other null
-  // directions: eigenvalues ~ 0), its mu estimate, and the low-rank screen's basis.
-  Eigen eg;
-  bool have_eig = false;
-  {
-    const double t_eig = now();
-    const char *renv = getenv("GMAT_LR_RANK");
-    const int R_req = renv ? std::max(0, atoi(renv)) : 384;
-    const int ne = (int)std::min<int64_t>(std::max(R_req, 16) + 1, n);
-    have_eig = n >= 8 && !getenv("GMAT_NO_PREFILTER") && eigen_bottom(e, dp.as<double>(), trP, ne, &eg) == GMAT_OK;
-    if (!have_eig && getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: no eigendecomposition (%s)\n", gmat_last_error());
-    e->setup[2] = now() - t_eig;
-  }
-  int K0 = 0;
-  if (have_eig)
-    while (K0 < eg.ne && eg.lam[K0] < 1e-9 * trP / (double)n) ++K0;
-  // Spectral prefilter certificate.  If the fp64 Cholesky of
-  //   A = P + (mu + tau) 11'/n + ku U U' - mu I      (U: the K0 null directions, ku = mu + tau)
-  // completes with positive pivots, A + E = LL' with |E| <= gamma_{n+1} |L||L'|, so lambda_min(A)
-  // >= -||E||_2 >= -gamma_{n+1} trace(A) (||L||_F^2 = trace(LL')), i.e. for every e
-  //   e'Pe >= mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2,
-  // eps = 2 gamma_{n+1} trace(A) (x2 margin for the blocked MFMA order) + the rounding of forming A.
-  // tau (a small lift) keeps the directions P annihilates definite; mu starts just below the
-  // smallest eigenvalue off those directions.
-  const double t_pf = now();
-  if (have_eig && K0 <= PF_NCOV_MAX && K0 < eg.ne) {
-    DBuf A, dinv, ld, info, dU, C;
-    if ((rc = A.alloc(n * n * sizeof(double))) || (rc = dinv.alloc(n * 64 * sizeof(double))) ||
-        (rc = ld.alloc(sizeof(double))) || (rc = info.alloc(sizeof(int))))
-      return fail(rc);
-    double cmax = 0.0;
-    if (K0 > 0) {  // C = U'U (n x n) from the eigenvectors, exactly as stored
-      if ((rc = dU.alloc((size_t)K0 * n * sizeof(double))) || (rc = C.alloc(n * n * sizeof(double)))) return fail(rc);
-      if (hipMemcpy(dU.p, eg.Z.data(), (size_t)K0 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
-        set_error("gmat_epi_create: direction upload failed");
-        return fail(GMAT_E_HIP);
-      }
-      if ((rc = dgemm(0, n, n, K0, 1.0, DView{dU.as<double>(), n, 1}, DView{dU.as<double>(), n, 0}, 0.0, C.as<double>(),
-                      n)))
+  if (state) {  // the spectral state (eigenpairs, certificates, Q images) of another rank's plan
+    if ((rc = import_state(e, state, state_bytes)) != GMAT_OK) return fail(rc);
+  } else {
+    double trP = 0.0;
+    for (int64_t i = 0; i < n; ++i) trP += pvp[i * n + i];
+    // Bottom eigenpairs of P (intercept lifted): the prefilter's covariate directions (P's other null
+    // directions: eigenvalues ~ 0), its mu estimate, and the low-rank screen's basis.
+    Eigen eg;
+    bool have_eig = false;
+    {
+      const double t_eig = now();
+      const char *renv = getenv("GMAT_LR_RANK");
+      const int R_req = renv ? std::max(0, atoi(renv)) : 384;
+      const int ne = (int)std::min<int64_t>(std::max(R_req, 16) + 1, n);
+      have_eig = n >= 8 && !getenv("GMAT_NO_PREFILTER") && eigen_bottom(e, dp.as<double>(), trP, ne, &eg) == GMAT_OK;
+      if (!have_eig && getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: no eigendecomposition (%s)\n", gmat_last_error());
+      e->setup[2] = now() - t_eig;
+    }
+    int K0 = 0;
+    if (have_eig)
+      while (K0 < eg.ne && eg.lam[K0] < 1e-9 * trP / (double)n) ++K0;
+    // Spectral prefilter certificate.  If the fp64 Cholesky of
+    //   A = P + (mu + tau) 11'/n + ku U U' - mu I      (U: the K0 null directions, ku = mu + tau)
+    // completes with positive pivots, A + E = LL' with |E| <= gamma_{n+1} |L||L'|, so lambda_min(A)
+    // >= -||E||_2 >= -gamma_{n+1} trace(A) (||L||_F^2 = trace(LL')), i.e. for every e
+    //   e'Pe >= mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2,
+    // eps = 2 gamma_{n+1} trace(A) (x2 margin for the blocked MFMA order) + the rounding of forming A.
+    // tau (a small lift) keeps the directions P annihilates definite; mu starts just below the
+    // smallest eigenvalue off those directions.
+    const double t_pf = now();
+    if (have_eig && K0 <= PF_NCOV_MAX && K0 < eg.ne) {
+      DBuf A, dinv, ld, info, dU, C;
+      if ((rc = A.alloc(n * n * sizeof(double))) || (rc = dinv.alloc(n * 64 * sizeof(double))) ||
+          (rc = ld.alloc(sizeof(double))) || (rc = info.alloc(sizeof(int))))
         return fail(rc);
-      for (int64_t i = 0; i < n; ++i) {
-        double cii = 0.0;
-        for (int k = 0; k < K0; ++k) cii += eg.Z[(size_t)k * n + i] * eg.Z[(size_t)k * n + i];
-        cmax = std::max(cmax, cii);
-      }
-    }
-    const double tau0 = 1e-8 * trP / (double)n;
-    auto ok = [&](double mu) -> int {  // 1 = certified, 0 = not, < 0 error
-      const double tau = tau0 + 1e-6 * mu;
-      hipLaunchKernelGGL(pf_shift_u_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dp.as<double>(),
-                         K0 ? C.as<double>() : nullptr, mu, tau, mu + tau, A.as<double>());
-      if (hipGetLastError() != hipSuccess) return -1;
-      if (cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), info.as<int>()) != GMAT_OK) return -1;
-      e->setup[6] += 1;
-      int hinfo = 1;
-      if (hipMemcpy(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-      return hinfo == 0 ? 1 : 0;
-    };
-    double lo = 0.0;
-    if (certify_below(eg.lam[K0], ok, &lo) != GMAT_OK) {
-      set_error("gmat_epi_create: prefilter certificate failed");
-      return fail(GMAT_E_HIP);
-    }
-    const double tau = tau0 + 1e-6 * lo, u = std::ldexp(1.0, -53);
-    const double trA = trP + (lo + tau) + (lo + tau) * K0 - (double)n * lo;
-    const double eps = 2.0 * (double)(n + 1) * u * std::fabs(trA) * 1.01 +
-                       (double)n * (K0 + 4) * u * (pmax + lo + 2.0 * (lo + tau) / (double)n + (lo + tau) * cmax);
-    if (lo > 0.0 && lo > 1e3 * eps) {
-      e->pf_mu = lo;
-      e->pf_tau = tau;
-      e->pf_eps = eps + 1e-15 * lo;
-      e->pf_ku = lo + tau;
-      e->pf_ncov = K0;
-      if (K0 > 0) {  // the directions in storage order for the codings' images
-        std::vector<double> Us((size_t)K0 * n_pad, 0.0);
-        for (int k = 0; k < K0; ++k) {
-          double su = 0.0;
-          for (int64_t c = 0; c < n; ++c) su += eg.Z[(size_t)k * n + c];
-          e->pf_su[k] = su;
-          for (int64_t q = 0; q < n_pad; ++q) {
-            const int64_t c = (q & ~31LL) + perm_nat((int)(q & 31));
-            if (c < n) Us[(size_t)k * n_pad + q] = eg.Z[(size_t)k * n + c];
-          }
-        }
-        if ((rc = e->pf_U.alloc(Us.size() * sizeof(double)))) return fail(rc);
-        if (hipMemcpy(e->pf_U.p, Us.data(), Us.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+      double cmax = 0.0;
+      if (K0 > 0) {  // C = U'U (n x n) from the eigenvectors, exactly as stored
+        if ((rc = dU.alloc((size_t)K0 * n * sizeof(double))) || (rc = C.alloc(n * n * sizeof(double)))) return fail(rc);
+        if (hipMemcpy(dU.p, eg.Z.data(), (size_t)K0 * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
           set_error("gmat_epi_create: direction upload failed");
           return fail(GMAT_E_HIP);
         }
+        if ((rc = dgemm(0, n, n, K0, 1.0, DView{dU.as<double>(), n, 1}, DView{dU.as<double>(), n, 0}, 0.0, C.as<double>(),
+                        n)))
+          return fail(rc);
+        for (int64_t i = 0; i < n; ++i) {
+          double cii = 0.0;
+          for (int k = 0; k < K0; ++k) cii += eg.Z[(size_t)k * n + i] * eg.Z[(size_t)k * n + i];
+          cmax = std::max(cmax, cii);
+        }
       }
+      const double tau0 = 1e-8 * trP / (double)n;
+      auto ok = [&](double mu) -> int {  // 1 = certified, 0 = not, < 0 error
+        const double tau = tau0 + 1e-6 * mu;
+        hipLaunchKernelGGL(pf_shift_u_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, 0, n, dp.as<double>(),
+                           K0 ? C.as<double>() : nullptr, mu, tau, mu + tau, A.as<double>());
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (cholesky(0, n, A.as<double>(), n, dinv.as<double>(), ld.as<double>(), info.as<int>()) != GMAT_OK) return -1;
+        e->setup[6] += 1;
+        int hinfo = 1;
+        if (hipMemcpy(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return hinfo == 0 ? 1 : 0;
+      };
+      double lo = 0.0;
+      if (certify_below(eg.lam[K0], ok, &lo) != GMAT_OK) {
+        set_error("gmat_epi_create: prefilter certificate failed");
+        return fail(GMAT_E_HIP);
+      }
+      const double tau = tau0 + 1e-6 * lo, u = std::ldexp(1.0, -53);
+      const double trA = trP + (lo + tau) + (lo + tau) * K0 - (double)n * lo;
+      const double eps = 2.0 * (double)(n + 1) * u * std::fabs(trA) * 1.01 +
+                         (double)n * (K0 + 4) * u * (pmax + lo + 2.0 * (lo + tau) / (double)n + (lo + tau) * cmax);
+      if (lo > 0.0 && lo > 1e3 * eps) {
+        e->pf_mu = lo;
+        e->pf_tau = tau;
+        e->pf_eps = eps + 1e-15 * lo;
+        e->pf_ku = lo + tau;
+        e->pf_ncov = K0;
+        if (K0 > 0) {  // the directions in storage order for the codings' images
+          std::vector<double> Us((size_t)K0 * n_pad, 0.0);
+          for (int k = 0; k < K0; ++k) {
+            double su = 0.0;
+            for (int64_t c = 0; c < n; ++c) su += eg.Z[(size_t)k * n + c];
+            e->pf_su[k] = su;
+            for (int64_t q = 0; q < n_pad; ++q) {
+              const int64_t c = (q & ~31LL) + perm_nat((int)(q & 31));
+              if (c < n) Us[(size_t)k * n_pad + q] = eg.Z[(size_t)k * n + c];
+            }
+          }
+          if ((rc = e->pf_U.alloc(Us.size() * sizeof(double)))) return fail(rc);
+          if (hipMemcpy(e->pf_U.p, Us.data(), Us.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("gmat_epi_create: direction upload failed");
+            return fail(GMAT_E_HIP);
+          }
+        }
+      }
+      if (getenv("GMAT_DEBUG"))
+        fprintf(stderr, "gmat_epi_create: prefilter mu %.6g (lam %.6g) eps %.3g, %d covariate directions (trace/n %.4g)\n", lo,
+                eg.lam[K0], eps, K0, trP / n);
+    } else if (getenv("GMAT_DEBUG")) {
+      fprintf(stderr, "gmat_epi_create: prefilter off (%d null directions, eigen %d)\n", K0, (int)have_eig);
     }
-    if (getenv("GMAT_DEBUG"))
-      fprintf(stderr, "gmat_epi_create: prefilter mu %.6g (lam %.6g) eps %.3g, %d covariate directions (trace/n %.4g)\n", lo,
-              eg.lam[K0], eps, K0, trP / n);
-  } else if (getenv("GMAT_DEBUG")) {
-    fprintf(stderr, "gmat_epi_create: prefilter off (%d null directions, eigen %d)\n", K0, (int)have_eig);
-  }
-  e->setup[1] = now() - t_pf;
-  if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax, eg)) != GMAT_OK) {
-    // the low-rank screen is an accelerator: without it the MX screen runs
-    if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: low-rank screen unavailable: %s\n", gmat_last_error());
-    e->lr_R = 0;
-    rc = GMAT_OK;
-  }
+    e->setup[1] = now() - t_pf;
+    if (e->pf_mu > 0.0 && (rc = lr_setup(e, dp.as<double>(), pvp, pmax, eg)) != GMAT_OK) {
+      // the low-rank screen is an accelerator: without it the MX screen runs
+      if (getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: low-rank screen unavailable: %s\n", gmat_last_error());
+      e->lr_R = 0;
+      rc = GMAT_OK;
+    }
+  }  // spectral state computed here
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
     set_error("gmat_epi_create: z download failed");
@@ -2817,6 +2835,108 @@ extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, 
   e->zz = zz;
   e->setup[0] = now() - t_create;
   *out = e;
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
+  return epi_create_impl(out, g, pvp, py, n_slice, nullptr, 0);
+}
+
+extern "C" int gmat_epi_create_with(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
+                                    const uint8_t *state, int64_t state_bytes) {
+  GMAT_CHECK(state && state_bytes > 0, GMAT_E_ARG, "gmat_epi_create_with: no state");
+  return epi_create_impl(out, g, pvp, py, n_slice, state, state_bytes);
+}
+
+namespace {
+struct StateHead {
+  uint64_t magic, n, n_pad, p_hash;
+  double d[12];  // pf_mu, pf_tau, pf_eps, pf_ku, pf_su[4], lr_lam, lr_tau, lr_eps, lr_E
+  int64_t pf_ncov, lr_R, tiles_bytes, pad;
+};
+int64_t state_size(const gmat_epi *e) {
+  return (int64_t)sizeof(StateHead) + (int64_t)e->pf_ncov * e->n_pad * 8 + (e->lr_R ? (int64_t)e->lr_tiles.bytes : 0) +
+         (int64_t)e->n_pad * e->lr_R * 8 + (int64_t)e->lr_R * 8;
+}
+int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes) {
+  StateHead h;
+  GMAT_CHECK(bytes >= (int64_t)sizeof(h), GMAT_E_ARG, "plan state: %lld bytes", (long long)bytes);
+  memcpy(&h, st, sizeof(h));
+  GMAT_CHECK(h.magic == EPI_STATE_MAGIC && (int64_t)h.n == e->n && (int64_t)h.n_pad == e->n_pad, GMAT_E_ARG,
+             "plan state: not a state of an n = %lld plan", (long long)e->n);
+  GMAT_CHECK(h.p_hash == e->p_hash, GMAT_E_ARG, "plan state: computed for a different P");
+  GMAT_CHECK(h.pf_ncov >= 0 && h.pf_ncov <= PF_NCOV_MAX && h.lr_R >= 0 && h.tiles_bytes >= 0, GMAT_E_ARG,
+             "plan state: corrupt header");
+  e->pf_mu = h.d[0];
+  e->pf_tau = h.d[1];
+  e->pf_eps = h.d[2];
+  e->pf_ku = h.d[3];
+  for (int k = 0; k < 4; ++k) e->pf_su[k] = h.d[4 + k];
+  e->lr_lam = h.d[8];
+  e->lr_tau = h.d[9];
+  e->lr_eps = h.d[10];
+  e->lr_E = h.d[11];
+  e->pf_ncov = (int)h.pf_ncov;
+  e->lr_R = (int)h.lr_R;
+  int64_t off = sizeof(h);
+  const int64_t nU = (int64_t)e->pf_ncov * e->n_pad * 8, nB = e->n_pad * (int64_t)e->lr_R * 8, nq = e->lr_R * 8LL;
+  GMAT_CHECK(bytes == off + nU + (e->lr_R ? h.tiles_bytes : 0) + nB + nq, GMAT_E_ARG, "plan state: %lld bytes, "
+             "header describes %lld", (long long)bytes, (long long)(off + nU + h.tiles_bytes + nB + nq));
+  if (nU) {
+    GMAT_TRY(e->pf_U.alloc(nU));
+    GMAT_HIP(hipMemcpy(e->pf_U.p, st + off, nU, hipMemcpyHostToDevice));
+    off += nU;
+  }
+  if (e->lr_R) {
+    GMAT_TRY(e->lr_tiles.alloc(h.tiles_bytes));
+    GMAT_HIP(hipMemcpy(e->lr_tiles.p, st + off, h.tiles_bytes, hipMemcpyHostToDevice));
+    off += h.tiles_bytes;
+    GMAT_TRY(e->lr_Bs.alloc(nB));
+    GMAT_HIP(hipMemcpy(e->lr_Bs.p, st + off, nB, hipMemcpyHostToDevice));
+    off += nB;
+    GMAT_TRY(e->lr_q1.alloc(nq));
+    GMAT_HIP(hipMemcpy(e->lr_q1.p, st + off, nq, hipMemcpyHostToDevice));
+  }
+  e->imported = 1;
+  return GMAT_OK;
+}
+}  // namespace
+
+// The plan's spectral state -- the prefilter and low-rank certificates (P's covariate directions,
+// mu, lam, tau, eps and the certified Q's tile images and fp64 copy) -- serialised so that one
+// rank computes it and every other rank imports it (gmat_epi_create_with): the eigendecomposition
+// and the certificate searches run once per job.  *needed = the size; buf may be null.
+extern "C" int gmat_epi_export(const gmat_epi *e, uint8_t *buf, int64_t cap, int64_t *needed) {
+  GMAT_CHECK(e && needed, GMAT_E_ARG, "gmat_epi_export: bad arguments");
+  const int64_t sz = state_size(e);
+  *needed = sz;
+  if (!buf) return GMAT_OK;
+  GMAT_CHECK(cap >= sz, GMAT_E_OVERFLOW, "gmat_epi_export: %lld bytes needed", (long long)sz);
+  StateHead h{};
+  h.magic = EPI_STATE_MAGIC;
+  h.n = e->n;
+  h.n_pad = e->n_pad;
+  h.p_hash = e->p_hash;
+  const double d[12] = {e->pf_mu, e->pf_tau, e->pf_eps, e->pf_ku, e->pf_su[0], e->pf_su[1],
+                        e->pf_su[2], e->pf_su[3], e->lr_lam, e->lr_tau, e->lr_eps, e->lr_E};
+  memcpy(h.d, d, sizeof(d));
+  h.pf_ncov = e->pf_ncov;
+  h.lr_R = e->lr_R;
+  h.tiles_bytes = e->lr_R ? (int64_t)e->lr_tiles.bytes : 0;
+  memcpy(buf, &h, sizeof(h));
+  int64_t off = sizeof(h);
+  const int64_t nU = (int64_t)e->pf_ncov * e->n_pad * 8;
+  if (nU) {
+    GMAT_HIP(hipMemcpy(buf + off, e->pf_U.p, nU, hipMemcpyDeviceToHost));
+    off += nU;
+  }
+  if (e->lr_R) {
+    GMAT_HIP(hipMemcpy(buf + off, e->lr_tiles.p, h.tiles_bytes, hipMemcpyDeviceToHost));
+    off += h.tiles_bytes;
+    GMAT_HIP(hipMemcpy(buf + off, e->lr_Bs.p, e->n_pad * (int64_t)e->lr_R * 8, hipMemcpyDeviceToHost));
+    off += e->n_pad * (int64_t)e->lr_R * 8;
+    GMAT_HIP(hipMemcpy(buf + off, e->lr_q1.p, e->lr_R * 8LL, hipMemcpyDeviceToHost));
+  }
   return GMAT_OK;
 }
 

@@ -7,6 +7,8 @@ genotype panel, P and Py, so the scan shards with no collective on its hot path:
 * genotype panel: each rank reads (or generates) its contiguous shard of SNPs and the packed
   2-bit shards are all-gathered (25 MB at 2,000 x 50,000);
 * P and Py: computed on rank 0 and broadcast (32 MB at n = 2,000);
+* scan plan: its spectral state (eigendecomposition, certificates, low-rank basis) computed on
+  rank 0 and broadcast (shared_plan), the slices and codings built locally;
 * scan: rank r scans the rows of part r+1 of the reference's triangle-folded split
   ``parallel=[N, r+1]`` (remma_epiAA.py:125-139), equal pair counts per rank;
 * hits: gathered to rank 0 and merged in (i, j) order -- the same rows and order a
@@ -277,6 +279,26 @@ def gather_hits(local, root=0):
     gathered = [None] * ws if rank == root else None
     tdist.gather_object(None if local is None else tuple(np.asarray(a) for a in local), gathered, dst=root)
     return merge_hits(gathered) if rank == root else None
+
+
+def shared_plan(geno, pvp, py, **kw):
+    """EpiPlan on every rank with the spectral state (eigendecomposition and certificate
+    searches, the plan setup's dominant cost) computed once on rank 0 and broadcast: the other
+    ranks import it (gmat_epi_create_with), so the certificates are identical on every rank."""
+    from .remma._scan import EpiPlan
+    b = _require()
+    rank, ws, _ = world()
+    if b is None or ws == 1:
+        return EpiPlan(geno, pvp, py, **kw)
+    if rank == 0:
+        plan = EpiPlan(geno, pvp, py, **kw)
+        st = plan.export_state()
+        allreduce_max(st.size)
+        broadcast_array(st, 0, dtype=np.uint8)
+        return plan
+    size = int(allreduce_max(0))
+    st = broadcast_array(None, 0, shape=(size,), dtype=np.uint8)
+    return EpiPlan(geno, pvp, py, state=st, **kw)
 
 
 def distributed_scan(scan_fn, kind, num_snp, p_cut, rows=None):

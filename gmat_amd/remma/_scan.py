@@ -25,7 +25,9 @@ N_SLICE = 3  # slices kept; each scan uses 1, 2 or 3 by p_cut (gmat_epi_scan n_s
 class EpiPlan:
     """gmat_epi handle: a genotype panel plus Z'PZ and Z'Py resident on the device."""
 
-    def __init__(self, geno, pvp, py, n_slice=N_SLICE):
+    def __init__(self, geno, pvp, py, n_slice=N_SLICE, state=None):
+        """state: the spectral state of a plan for the same P (export_state() of another rank's
+        plan); the eigendecomposition and certificate searches are then skipped."""
         self._lib = N.ensure_device()
         self.geno = geno
         pvp = N.f64(pvp)
@@ -34,9 +36,22 @@ class EpiPlan:
             raise ValueError("P is %s and Py has %d entries for %d genotyped individuals"
                              % (pvp.shape, py.size, geno.n))
         h = ctypes.c_void_p()
-        N.check(self._lib.gmat_epi_create(ctypes.byref(h), geno.handle, N.ptr(pvp), N.ptr(py), int(n_slice)),
-                "gmat_epi_create")
+        if state is None:
+            N.check(self._lib.gmat_epi_create(ctypes.byref(h), geno.handle, N.ptr(pvp), N.ptr(py), int(n_slice)),
+                    "gmat_epi_create")
+        else:
+            st = np.ascontiguousarray(state, dtype=np.uint8)
+            N.check(self._lib.gmat_epi_create_with(ctypes.byref(h), geno.handle, N.ptr(pvp), N.ptr(py), int(n_slice),
+                                                   N.ptr(st), st.size), "gmat_epi_create_with")
         self._h = h
+
+    def export_state(self):
+        """The plan's spectral state as bytes (uint8 array) for EpiPlan(..., state=...)."""
+        need = ctypes.c_int64()
+        N.check(self._lib.gmat_epi_export(self._h, None, 0, ctypes.byref(need)), "gmat_epi_export")
+        buf = np.zeros(need.value, dtype=np.uint8)
+        N.check(self._lib.gmat_epi_export(self._h, N.ptr(buf), buf.size, ctypes.byref(need)), "gmat_epi_export")
+        return buf
 
     def scan(self, kind, rows, p_cut, n_slice=0):
         """Hits (i, j, eff, var, chi, p) with p < p_cut over first-SNP rows `rows`

@@ -93,6 +93,14 @@ int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, cons
 typedef struct gmat_epi gmat_epi;
 /* n_slice (1..4): int8 slices of P (off the diagonal) kept for the screen (see gmat_epi_scan). */
 int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice);
+/* Multi-GPU: the plan's spectral state (P's covariate directions, the certified prefilter and
+ * low-rank bounds, the low-rank basis' tile images) computed once and shared.  gmat_epi_export
+ * writes it to buf (cap bytes; *needed = its size, buf may be NULL to query); gmat_epi_create_with
+ * builds a plan for the same P from it (checked against a fingerprint of P) instead of
+ * recomputing the eigendecomposition and the certificate searches. */
+int gmat_epi_export(const gmat_epi *e, uint8_t *buf, int64_t cap, int64_t *needed);
+int gmat_epi_create_with(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
+                         const uint8_t *state, int64_t state_bytes);
 /* Exhaustive exact scan over first-SNP rows `rows` (sorted ascending): AA/DD test pairs
  * (i, j>i) (remma_epiAA.py:71-82, remma_epiDD.py:75-86), AD tests (i, all j) including i==j
  * (remma_epiAD.py:76-87).  A pair is a hit when p < p_cut with p = chi2.sf(eff^2/var, 1);

@@ -50,9 +50,28 @@ def main():
         merged = dist.distributed_scan(scan_fn, kind, m, 0.05)
         if rank == 0:
             results[kind] = merged
+    # shared_plan: rank 0's plan state reaches every rank byte for byte (plan stubbed: no GPU here)
+    from gmat_amd.remma import _scan
+
+    class StubPlan:
+        def __init__(self, geno, pvp_, py_, state=None):
+            self.state = state
+
+        def export_state(self):
+            return (np.arange(100003, dtype=np.int64) * 7919 % 251).astype(np.uint8)
+
+    real = _scan.EpiPlan
+    _scan.EpiPlan = StubPlan
+    try:
+        plan = dist.shared_plan(None, pvp, py)
+    finally:
+        _scan.EpiPlan = real
+    want = StubPlan(None, None, None).export_state()
+    state_ok = float(plan.state is None) if rank == 0 else float(np.array_equal(plan.state, want))
+    state_ok = -dist.allreduce_max(-state_ok)  # min over ranks
     mx = dist.allreduce_max(float(rank))
     if rank == 0:
-        np.savez(out_path, mx=mx, **{k + "_" + str(t): v[t] for k, v in results.items() for t in range(6)})
+        np.savez(out_path, mx=mx, state_ok=state_ok, **{k + "_" + str(t): v[t] for k, v in results.items() for t in range(6)})
     dist.barrier()
 
 

@@ -36,6 +36,7 @@ def test_sharded_scan_equals_single_process(tmp_path, ws):
     assert rcs == [0] * ws
     res = np.load(out)
     assert float(res["mx"]) == ws - 1
+    assert float(res["state_ok"]) == 1.0  # shared_plan broadcast rank 0's plan state
     snp = O.read_plink(TINY)
     ref = np.load(os.path.join(REPO, "tests", "golden", "tiny", "tiny_ref.npz"))
     y, x, col, nid = O.design_matrix(TINY + ".pheno", TINY)
