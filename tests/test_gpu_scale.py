@@ -187,3 +187,31 @@ def test_cfg3_covariates_vs_oracle(cfg3):
             hi, hj, eff, var, chi, p = plan.scan(kind, rows[:4], 1e-3, n_slice=-2)
             assert hi.size == exp.shape[0], (kind, hi.size, exp.shape)
             np.testing.assert_array_equal(np.column_stack([hi, hj]), exp[:, :2].astype(np.int64))
+
+
+def test_grm_and_inverse_at_cfg5_n():
+    """n = 5,000 (configs[4]'s individuals; ceil(n/4) = 1,250 bytes per SNP row: unaligned dword
+    reads of the packed rows): agmat / dgmat_as against the oracle on 3,000 SNPs, and the SPD
+    inverse of V-like matrices at n = 2,049 and 5,000 against numpy."""
+    import ctypes
+    from oracle import gmat_oracle as O
+    from gmat_amd import _native as N, synth
+    from gmat_amd.gmatrix import spd_inverse
+    from gmat_amd.plink import Geno
+    lib = N.ensure_device()
+    n, m = 5000, 3000
+    geno = synth.simulate_genotypes(n, m, seed=21)
+    body = np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8)
+    snp = np.ascontiguousarray(geno.T, dtype=np.float64)
+    with Geno(body=body, n_id=n, n_snp=m) as g:
+        for kind, ref in ((0, O.agmat), (1, O.dgmat_as)):
+            k = np.empty((n, n))
+            sc = ctypes.c_double()
+            N.check(lib.gmat_grm(g.handle, kind, 0.001, N.ptr(k), ctypes.byref(sc)), "gmat_grm")
+            np.testing.assert_allclose(k, ref(snp), rtol=1e-10, atol=1e-12)
+    rng = np.random.default_rng(2)
+    for nn in (2049, 5000):
+        a = rng.standard_normal((nn, 300))
+        v = a @ a.T / 300 + 0.5 * np.eye(nn)
+        vi = spd_inverse(v)
+        np.testing.assert_allclose(vi, np.linalg.inv(v), rtol=1e-8, atol=1e-10)
