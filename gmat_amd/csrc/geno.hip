@@ -165,6 +165,13 @@ __global__ __launch_bounds__(256) void grm_rowdot_reduce_kernel(const double *__
   if (lane == 0) r[a] = s;
 }
 
+// rows of the packed panel copied to a 4-byte-aligned stride (the SYRK reads dwords of rows)
+__global__ __launch_bounds__(256) void pad_rows_kernel(const uint8_t *__restrict__ src, int64_t nb, int64_t m, int64_t nb4,
+                                                       uint8_t *__restrict__ dst) {
+  const int64_t j = blockIdx.y, b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < m && b < nb4) dst[j * nb4 + b] = b < nb ? src[j * nb + b] : 0;
+}
+
 struct GrmWork {
   const int *seg0;   // [W + 1]: the segments of workgroup w are [seg0[w], seg0[w+1])
   const int *stile;  // per segment: tile, first and end stage (the segment's slot = its index)
@@ -182,7 +189,10 @@ __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restr
   // positions (rows 2 apart) x eight SNP quads; each lane loads its dword of four stage rows
   const int op = w >> 2, wv = w & 3;
   const int dpos = (lane & 3) + 4 * (lane >> 5) + 8 * (wv & 1), qd = (wv >> 1) * 8 + ((lane >> 2) & 7);
-  const int s0 = wk.seg0[blockIdx.x], s1 = wk.seg0[blockIdx.x + 1];
+  // XCD-aware: workgroup b runs on XCD b mod 8, so the work ranges are dealt in 8 contiguous
+  // groups -- the workgroups of one XCD stream neighbouring tiles (shared row panels) in its L2
+  const int nx = gridDim.x % 8 == 0 ? 8 : 1, bl = (blockIdx.x % nx) * (gridDim.x / nx) + blockIdx.x / nx;
+  const int s0 = wk.seg0[bl], s1 = wk.seg0[bl + 1];
   const __amdgpu_buffer_rsrc_t rs = grm_rsrc(packed, m * nb + 256);  // + the zeroed tail of the panel
   for (int sg = s0; sg < s1; ++sg) {
     const int t = wk.stile[sg], it0 = wk.sit0[sg], it1 = wk.sit1[sg];
@@ -420,7 +430,7 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_grm: panel has %lld missing genotypes (impute first)",
              (long long)g->total_missing);
   const int64_t n = g->n, m = g->m, nb = g->nb;
-  GMAT_CHECK(m <= 2000000 && (m + 2 * GS * GD) * nb + 256 < (1LL << 31), GMAT_E_ARG,
+  GMAT_CHECK(m <= 2000000 && (m + 2 * GS * GD) * round_up(nb, 4) + 256 < (1LL << 31), GMAT_E_ARG,
              "gmat_grm: at most 2,000,000 SNPs and 2 GB of packed codes (int32 accumulation, 32-bit offsets)");
   // centring vector and scale exactly as gmatrix.py:53-57 (additive) / :116-120 (dominance)
   std::vector<double> c(m);
@@ -494,18 +504,31 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   hipEvent_t ev[4];
   for (auto &x : ev) GMAT_HIP(hipEventCreate(&x));
   GMAT_HIP(hipEventRecord(ev[0], 0));
-  const bool al = nb % 4 == 0;
+  // rows at a 4-byte-aligned stride: dword buffer loads instead of four byte loads per dword
+  const uint8_t *pk = g->packed.as<uint8_t>();
+  int64_t nbs = nb;
+  DBuf aligned;
+  if (nb % 4) {
+    nbs = round_up(nb, 4);
+    GMAT_TRY(aligned.alloc((size_t)m * nbs + 256));
+    GMAT_HIP(hipMemsetAsync(aligned.as<uint8_t>() + (size_t)m * nbs, 0, 256, 0));
+    hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)cdiv(nbs, 256), (unsigned)m), dim3(256), 0, 0, pk, nb, m, nbs,
+                       aligned.as<uint8_t>());
+    GMAT_HIP(hipGetLastError());
+    pk = aligned.as<uint8_t>();
+  }
+  const bool al = nbs % 4 == 0;  // always: the rows were padded above
   const dim3 rg((unsigned)cdiv(nd, 64), (unsigned)nch);
   auto rk = kind == GMAT_GRM_ADD ? (al ? grm_rowdot_kernel<GMAT_GRM_ADD, true> : grm_rowdot_kernel<GMAT_GRM_ADD, false>)
                                  : (al ? grm_rowdot_kernel<GMAT_GRM_DOM, true> : grm_rowdot_kernel<GMAT_GRM_DOM, false>);
-  hipLaunchKernelGGL(rk, rg, dim3(64), 0, 0, g->packed.as<uint8_t>(), nb, m, dc.as<double>(), nd, dpar.as<double>());
+  hipLaunchKernelGGL(rk, rg, dim3(64), 0, 0, pk, nbs, m, dc.as<double>(), nd, dpar.as<double>());
   hipLaunchKernelGGL(grm_rowdot_reduce_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, 0, dpar.as<double>(), nd, n,
                      nch, dr.as<double>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[1], 0));
   auto kern = kind == GMAT_GRM_ADD ? (al ? grm_partial_kernel<GMAT_GRM_ADD, true> : grm_partial_kernel<GMAT_GRM_ADD, false>)
                                    : (al ? grm_partial_kernel<GMAT_GRM_DOM, true> : grm_partial_kernel<GMAT_GRM_DOM, false>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)W), dim3(GNT), 0, 0, g->packed.as<uint8_t>(), nb, m, wk, dpart.as<int>());
+  hipLaunchKernelGGL(kern, dim3((unsigned)W), dim3(GNT), 0, 0, pk, nbs, m, wk, dpart.as<int>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[2], 0));
   hipLaunchKernelGGL(grm_epilogue_kernel, dim3((unsigned)ntile, 8, 2), dim3(256), 0, 0, dpart.as<int>(), dslot0, wk.ta, wk.tb, n,
