@@ -2119,6 +2119,98 @@ double now() {
 
 // ------------------------------------------------------------------ plan object
 
+// ---- tile lists of the low-rank screen built on the device from the prefilter's flags (the host
+// builder of build_mx, restated): per 32-column block J the flagged band rows in row order, packed
+// into half-tiles of MX_BI/2 rows, consecutive half-tiles (J-major) paired into MX tiles, tile t
+// dealt to entry 8 (t mod C) + t / C (C = ceil(tiles / 8): the 8 XCDs get contiguous chunks),
+// padding entries -1.  Thread (jl, rg) of a 256-thread workgroup: column block 64 b + jl, rows
+// [128 rg, 128 rg + 128).
+constexpr int TL_R = 128;  // band rows per thread (ROWS_PER_LAUNCH / 4)
+__global__ __launch_bounds__(256) void tl_count_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
+                                                       int *__restrict__ cnt4) {
+  const int jl = threadIdx.x & 63, rg = threadIdx.x >> 6, J = blockIdx.x * 64 + jl;
+  if (J >= nJ) return;
+  int c = 0;
+  const int r1 = min(Rn, TL_R * (rg + 1));
+  for (int r = TL_R * rg; r < r1; ++r) c += flags[(size_t)r * nJ + J] != 0;
+  cnt4[4 * J + rg] = c;
+}
+// one workgroup: exclusive scan of the half-tile counts over J; info = {halves, tiles, entries}
+__global__ __launch_bounds__(1024) void tl_scan_kernel(const int *__restrict__ cnt4, int nJ, int *__restrict__ H,
+                                                       int *__restrict__ info, int *__restrict__ mxt,
+                                                       int *__restrict__ mxr) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, per = (nJ + 1023) / 1024, j0 = t * per, j1 = min(nJ, j0 + per);
+  int sum = 0;
+  for (int J = j0; J < j1; ++J) {
+    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    sum += (c + MX_BI / 2 - 1) / (MX_BI / 2);
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int J = j0; J < j1; ++J) {
+    H[J] = run;
+    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    run += (c + MX_BI / 2 - 1) / (MX_BI / 2);
+  }
+  if (t == 0) {
+    const int halves = part[1023], tiles = (halves + 1) / 2, C = (tiles + 7) / 8;
+    info[0] = halves;
+    info[1] = tiles;
+    info[2] = 8 * C;
+    for (int q = tiles; q < 8 * C; ++q) {  // padding entries
+      const int bb = 8 * (q % C) + q / C;
+      for (int k = 0; k < MX_TE; ++k) mxt[MX_TE * bb + k] = -1;
+    }
+    if (halves % 2) {  // the last tile has one half
+      const int tl = tiles - 1, bb = 8 * (tl % C) + tl / C;
+      mxt[MX_TE * bb + 2] = -1;
+      for (int q = 0; q < MX_BI / 2; ++q) mxr[tl * MX_BI + MX_BI / 2 + q] = -1;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
+                                                      const int *__restrict__ cnt4, const int *__restrict__ H,
+                                                      const int *__restrict__ info, int *__restrict__ mxt,
+                                                      int *__restrict__ mxr) {
+  const int jl = threadIdx.x & 63, rg = threadIdx.x >> 6, J = blockIdx.x * 64 + jl;
+  if (J >= nJ) return;
+  const int C = info[2] / 8, h0 = H[J];
+  int idx = 0;
+  for (int g = 0; g < rg; ++g) idx += cnt4[4 * J + g];
+  const int r1 = min(Rn, TL_R * (rg + 1));
+  for (int r = TL_R * rg; r < r1; ++r)
+    if (flags[(size_t)r * nJ + J]) {
+      const int k = h0 + idx / (MX_BI / 2);
+      mxr[(k / 2) * MX_BI + (k % 2) * (MX_BI / 2) + idx % (MX_BI / 2)] = r;
+      ++idx;
+    }
+  if (rg == 0) {  // the tile entries of J's half-tiles and the empty slots of its last one
+    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    const int nh = (c + MX_BI / 2 - 1) / (MX_BI / 2);
+    for (int q = c; q < nh * (MX_BI / 2); ++q) {
+      const int k = h0 + q / (MX_BI / 2);
+      mxr[(k / 2) * MX_BI + (k % 2) * (MX_BI / 2) + q % (MX_BI / 2)] = -1;
+    }
+    for (int u = 0; u < nh; ++u) {
+      const int k = h0 + u, tl = k / 2, bb = 8 * (tl % C) + tl / C;
+      if (k % 2 == 0) {
+        mxt[MX_TE * bb] = tl;
+        mxt[MX_TE * bb + 1] = J;
+      } else {
+        mxt[MX_TE * bb + 2] = J;
+      }
+    }
+  }
+}
+
 struct Coding {
   bool ready = false;
   DBuf U;                         // P * screen code panel  [m][n_pad]
@@ -3077,6 +3169,15 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // (7x fewer refined pairs, but the sparse (row, block) slots fill MX tiles poorly: slower end to
   // end at the bench configuration, kept for study)
   const bool use_stage2 = use_lr && getenv("GMAT_STAGE2") != nullptr;
+  // low-rank screen tile lists built on the device right behind the prefilter (tl_*_kernel): the
+  // host waits only for the tile count, not for the flags and a host-side build
+  const bool dev_tiles = use_lr && !use_stage2 && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
+  DBuf tl_cnt, tl_h, tl_info;
+  if (dev_tiles) {
+    GMAT_TRY(tl_cnt.alloc((size_t)4 * nJ * sizeof(int)));
+    GMAT_TRY(tl_h.alloc((size_t)nJ * sizeof(int)));
+    GMAT_TRY(tl_info.alloc(2 * 4 * sizeof(int)));
+  }
   for (int b = 0; b < 2; ++b) {
     GMAT_TRY(drows[b].alloc(ROWS_PER_LAUNCH * 8));
     GMAT_TRY(dtiles[b].alloc((size_t)max_tiles * 2 * sizeof(int)));
@@ -3365,8 +3466,22 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       GMAT_HIP(hipGetLastError());
       if (x.a.pf_store) {  // the low-rank screen needs nothing else
-        GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
-        GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, flags[b].p, (size_t)Rn * nJ, hipMemcpyDeviceToHost, S2));
+        if (dev_tiles) {
+          const unsigned gj = (unsigned)cdiv(nJ, 64);
+          int *info = tl_info.as<int>() + 4 * b;
+          hipLaunchKernelGGL(tl_count_kernel, dim3(gj), dim3(256), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+                             tl_cnt.as<int>());
+          hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, S2, tl_cnt.as<int>(), (int)nJ, tl_h.as<int>(), info,
+                             mxt[b].as<int>(), mxr[b].as<int>());
+          hipLaunchKernelGGL(tl_fill_kernel, dim3(gj), dim3(256), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+                             tl_cnt.as<int>(), tl_h.as<int>(), info, mxt[b].as<int>(), mxr[b].as<int>());
+          GMAT_HIP(hipGetLastError());
+          GMAT_TRY(pin_flags[b].reserve(16));
+          GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, info, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
+        } else {
+          GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
+          GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, flags[b].p, (size_t)Rn * nJ, hipMemcpyDeviceToHost, S2));
+        }
         GMAT_HIP(hipEventRecord(side_end[b], S2));
         return GMAT_OK;
       }
@@ -3426,7 +3541,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     // J-major, dealt to the 8 XCDs (workgroup b runs on XCD b mod 8) in contiguous chunks so a
     // J's j-side records are re-read from one L2; padding entries (-1) exit at once
   std::vector<int> mxT[2], mxR[2];
-  int64_t nMX[2] = {0, 0};
+  int64_t nMX[2] = {0, 0}, gT[2] = {0, 0};  // tiles, tile entries (= workgroups, padding included)
   size_t built_for[2] = {SIZE_MAX, SIZE_MAX};
   double t_build = 0.0;  // host seconds spent building MX / low-rank tile lists (diagnostics)
   auto build_mx = [&](size_t li, int b) -> int {
@@ -3441,6 +3556,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     std::vector<int> &mx_tiles = mxT[b], &mx_rows = mxR[b];
     int64_t &n_mx = nMX[b];
     built_for[b] = li;
+    if (dev_tiles) {  // the lists are on the device already: the tile count is all the host needs
+      GMAT_HIP(hipEventSynchronize(side_end[b]));
+      const int *info = pin_flags[b].as<int>();
+      n_mx = info[1];
+      gT[b] = info[2];
+      return GMAT_OK;
+    }
     {
       const uint8_t *fl = nullptr;  // flags of launch li (copied to pinned memory by its side pass)
       if (use_pf) {
@@ -3519,6 +3641,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         for (int k = 0; k < MX_TE; ++k) mx_tiles[MX_TE * bb + k] = lst[MX_TE * p + k];
       }
       mx_rows.swap(rl);
+      gT[b] = (int64_t)(mx_tiles.size() / MX_TE);
       if (!mx_tiles.empty()) {  // sm is past screen li-1, the last reader of mxt[b] / mxr[b]
         GMAT_TRY(pin_mxt[b].reserve(mx_tiles.size() * sizeof(int)));
         GMAT_TRY(pin_mxr[b].reserve(mx_rows.size() * sizeof(int)));
@@ -3703,8 +3826,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     const LrArgs lx = lr_args(li);
     GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
     GMAT_HIP(hipEventRecord(evs7[b], sm));
-    if (!mxT[b].empty())
-      launch_lr_kernel((unsigned)(mxT[b].size() / MX_TE), sa, lx);
+    if (gT[b] > 0) launch_lr_kernel((unsigned)gT[b], sa, lx);
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipEventRecord(evs2[b], sm));
     GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
@@ -3749,8 +3871,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         sa.e3_eps = 0.5 * std::pow(128.0, -(sa.e3_t - 1)) + 1e-12;
       }
       ntiles = (int64_t)plan[li].tiles.size() / 2;
-      if (S == 0 && use_lr && !mx_tiles.empty()) {
-        const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
+      if (S == 0 && use_lr && gT[b] > 0) {
+        const unsigned g = (unsigned)gT[b];
         ScreenArgs s1 = sa;  // with stage 2 the low-rank candidates go to cand1
         if (two_stage) {
           s1.counter = e->counter1.as<unsigned long long>();
