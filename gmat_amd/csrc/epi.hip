@@ -1676,6 +1676,198 @@ __global__ void pvalue_kernel(int64_t np, const double *eff, const double *var, 
   p[t] = (c < 0.0) ? 1.0 : erfc(sqrt(0.5 * c));
 }
 
+// ------------------------------------------------------------------ pair screen
+// The screens' candidates re-tested one pair at a time before the fp64 refine (the low-rank
+// screen's bound is loose by design: most of its candidates fail a sharper test).  With screen
+// codes a, b, offsets alpha, beta, w = a o b and v = -beta a - alpha b + alpha beta 1, e = w + v and
+//   e'Pe = w'P_off w + sum_q P_qq w_q^2 + 2 v'Pw + v'Pv,
+//   v'Pw = w.(-beta Pa - alpha Pb + alpha beta z),
+//   v'Pv = beta^2 a'Pa + alpha^2 b'Pb + alpha^2 beta^2 1'P1 + 2 alpha beta a'Pb - 2 alpha beta^2 a'P1
+//          - 2 alpha^2 beta b'P1.
+// pair_side_kernel forms every term but the first in fp64 from U = P x codes (the side vectors of
+// the screens), and eff = e'Py; pair_mx_kernel evaluates w'P_off w on the MX screen's fp6 tile
+// images with w in fp4 (the error bound rho_mx |w|^2 of mx_screen_kernel: the same operands,
+// stage order and fp32 accumulation) and keeps the pair unless its p-value is certainly >= p_cut.
+struct PairArgs {
+  const int64_t *ci, *cj;  // candidates [np]
+  int64_t np, n_pad;
+  const int8_t *a, *b;        // screen panels (left, right coding) [m][n_pad]
+  const double *Ua, *Ub;      // P x panel [m][n_pad]
+  const double *alpha, *beta;  // screen-code offsets
+  const double *qa, *ra, *qb, *rb;
+  const double *z, *dg, *py;
+  double zz;
+  double *side;  // [5][np]: v-terms of var, their rounding slack, eff, sum |e py|, sum w^2
+  const uint8_t *tiles, *nib_i, *nib_j;
+  int64_t tiles_bytes;
+  int nK;
+  double rho, chi_cut;
+  unsigned long long *counter;
+  int64_t *oi, *oj;  // surviving pairs
+};
+
+// one wave per pair, 8 individuals per lane and step
+__global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= x.np) return;
+  const int64_t i = x.ci[p], j = x.cj[p], n_pad = x.n_pad;
+  const double al = x.alpha[i], be = x.beta[j], ab = al * be;
+  const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
+  const double *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
+  double s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
+  for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
+    const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
+    const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      const v2d_ u2 = *(const v2d_ *)(ua + q0 + k), v2 = *(const v2d_ *)(ub + q0 + k),
+                 z2 = *(const v2d_ *)(x.z + q0 + k), d2 = *(const v2d_ *)(x.dg + q0 + k),
+                 y2 = *(const v2d_ *)(x.py + q0 + k);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double av = (double)ca[k + h], bv = (double)cb[k + h], w = av * bv;
+        const double tu = be * u2[h], tv = al * v2[h], tz = ab * z2[h];
+        s1 += w * ((tz - tu) - tv);
+        s1a += w * ((fabs(tu) + fabs(tv)) + fabs(tz));
+        s2 += av * v2[h];
+        s2a += fabs(av * v2[h]);
+        s3 += d2[h] * (w * w);
+        s3a += fabs(d2[h]) * (w * w);
+        const double e = (av - al) * (bv - be), ey = e * y2[h];
+        ef += ey;
+        efa += fabs(ey);
+        sw += w * w;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s1a += __shfl_xor(s1a, off);
+    s2 += __shfl_xor(s2, off);
+    s2a += __shfl_xor(s2a, off);
+    s3 += __shfl_xor(s3, off);
+    s3a += __shfl_xor(s3a, off);
+    ef += __shfl_xor(ef, off);
+    efa += __shfl_xor(efa, off);
+    sw += __shfl_xor(sw, off);
+  }
+  if (lane != 0) return;
+  const double t3 = be * be * x.qa[i], t5 = al * al * x.qb[j], t7 = ab * ab * x.zz, t8 = 2.0 * ab * s2,
+               t4 = -2.0 * ab * be * x.ra[i], t6 = -2.0 * ab * al * x.rb[j];
+  x.side[p] = s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
+  // fp64 rounding of the dots and of U = P x codes (n u |P||a| per entry): far inside 1e-10 of
+  // the magnitudes summed
+  x.side[x.np + p] = 1e-10 * (s3a + 2.0 * s1a + fabs(t3) + fabs(t5) + fabs(t7) + 2.0 * fabs(ab) * s2a + fabs(t4) +
+                              fabs(t6));
+  x.side[2 * x.np + p] = ef;
+  x.side[3 * x.np + p] = efa;
+  x.side[4 * x.np + p] = sw;
+}
+
+// PP pairs per workgroup (PP / 32 column tiles x four 32-row tiles, one wave each); the pairs' w
+// codes for all individuals stay in LDS (pitch nK * 64 + 16 bytes: conflict-free fragment reads),
+// the tile images stream through a double buffer in the block-upper stage order of mx_screen.
+template <int PP>
+__global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
+  constexpr int T = PP * 8, NA = MX_TILE / 16 / T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+  uint8_t *sA = dyn;                        // [2][MX_TILE]
+  uint8_t *wpl = dyn + 2 * MX_TILE;         // [PP][pitch]
+  const int nK = x.nK, pitch = nK * 64 + 16;
+  double *red = (double *)(wpl + PP * pitch);  // [4][PP]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int r = w & 3, t = w >> 2;
+  const int64_t p0 = (int64_t)blockIdx.x * PP;
+  // w planes: w = (M1 & S1) | (M2 & 2 S1) per 16-byte chunk (the MX screen's fp4 codes of w / 2)
+  for (int k = tid; k < PP * nK * 4; k += T) {
+    const int pl = k / (nK * 4), s = (k >> 2) % nK, q = k & 3;
+    const int64_t gp = p0 + pl;
+    v4i wv = {0, 0, 0, 0};
+    if (gp < x.np) {
+      const uint8_t *ri = x.nib_i + (x.ci[gp] * nK + s) * NB_REC + 16 * q;
+      const v4i m1 = *(const v4i *)ri, m2 = *(const v4i *)(ri + 64);
+      const v4i s1 = *(const v4i *)(x.nib_j + (x.cj[gp] * nK + s) * NB_REC + 16 * q);
+      wv = (m1 & s1) | (m2 & (s1 << 1));
+    }
+    *(v4i *)&wpl[pl * pitch + s * 64 + 16 * q] = wv;
+  }
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(x.tiles, x.tiles_bytes);
+  v4i ra[NA];
+  auto load = [&](int kb, int cs) __attribute__((always_inline)) {
+    const int soffA = (kb * nK + cs) * MX_TILE;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * T) * 16, soffA, 0);
+  };
+  auto store = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b * MX_TILE + (tid + u * T) * 16] = ra[u];
+  };
+  const uint8_t *wrow = wpl + (32 * t + c) * pitch;
+  const int sw16 = 16 * ((c >> 3) & 1);
+  v16f_ acc;
+  auto compute = [&](int b, int cs, bool diag) __attribute__((always_inline)) {
+    const int bscale = diag ? 128 : 129;
+    const v16f_ zv = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v4i wb = *(const v4i *)(wrow + cs * 64 + 16 * (2 * kk + h));
+      const v8i_ fb = {wb[0], wb[1], wb[2], wb[3], 0, 0, 0, 0};
+      const uint8_t *ar = &sA[b * MX_TILE + (2 * kk + h) * 4096 + (32 * r + c) * 32];
+      const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+      const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      acc = mfma_mx(fa, fb, (diag && kk == 0) ? zv : acc, hi[2], bscale);
+    }
+  };
+  double tot = 0.0;
+  load(0, 0);
+  store(0);
+  __syncthreads();
+  int b = 0;
+  for (int kb = 0; kb < nK; ++kb) {
+#pragma unroll 1
+    for (int cs = kb; cs < nK; ++cs) {
+      const bool more = cs + 1 < nK || kb + 1 < nK;
+      if (more) load(cs + 1 < nK ? kb : kb + 1, cs + 1 < nK ? cs + 1 : kb + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(b, cs, cs == kb);
+      if (more) store(b ^ 1);
+      __syncthreads();
+      b ^= 1;
+    }
+    // sum_rows w[row] acc[row]: register e of this lane <-> storage slot 16h + e of row tile r
+    const v2i_ m = *(const v2i_ *)(wrow + kb * 64 + 16 * r + 8 * h);
+    v2f_ s2 = {0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const unsigned wd = (unsigned)m[d];
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const v2f_ wf = bb == 0 ? fp4_pair<0>(wd) : bb == 1 ? fp4_pair<1>(wd) : bb == 2 ? fp4_pair<2>(wd) : fp4_pair<3>(wd);
+        const v2f_ av = {acc[8 * d + 2 * bb], acc[8 * d + 2 * bb + 1]};
+        s2 = __builtin_elementwise_fma(wf, av, s2);
+      }
+    }
+    tot += (double)s2[0] + (double)s2[1];
+  }
+  tot += __shfl_xor(tot, 32);
+  if (h == 0) red[r * PP + 32 * t + c] = tot;
+  __syncthreads();
+  if (tid >= PP) return;
+  const int64_t p = p0 + tid;
+  if (p >= x.np) return;
+  const double M = (red[tid] + red[PP + tid]) + (red[2 * PP + tid] + red[3 * PP + tid]);
+  const double var = M + x.side[p], sw = x.side[4 * x.np + p];
+  const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
+  const double eff_hi = fabs(x.side[2 * x.np + p]) + 1e-10 * x.side[3 * x.np + p];
+  if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
+    const unsigned long long k = atomicAdd(x.counter, 1ULL);
+    x.oi[k] = x.ci[p];
+    x.oj[k] = x.cj[p];
+  }
+}
+
 // ------------------------------------------------------------------ setup kernels
 
 // P_store[q][q'] = P[nat(q)][nat(q')], zero padded; z = P_store 1 computed later.
@@ -2280,6 +2472,7 @@ struct gmat_epi {
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
   DBuf cand1_i, cand1_j, counter1;  // low-rank screen's candidates (stage 1; the MX screen re-tests them)
+  DBuf cand2_i, cand2_j, counter2, ps_side;  // pair screen survivors; its per-pair side terms
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
@@ -2298,7 +2491,7 @@ struct gmat_epi {
   } sb;
   // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
   struct ScanPins {
-    Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2];
+    Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2], count2;
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   ~gmat_epi() {
@@ -2434,8 +2627,7 @@ int build_coding_impl(gmat_epi *e, int which) {
     GMAT_HIP(hipStreamSynchronize(e->s));
   }
   GMAT_HIP(hipStreamSynchronize(e->s));
-  cd.U.release();
-  cd.ready = true;
+  cd.ready = true;  // U stays: the pair screen's side terms read its rows
   return GMAT_OK;
 }
 
@@ -2461,6 +2653,76 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
   }
   hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
   GMAT_HIP(hipGetLastError());
+  return GMAT_OK;
+}
+
+// pair screen of np candidates (pi, pj) on stream st: the survivors go to e->cand2_i / cand2_j,
+// their number to *n_out (the stream is synchronised).  Needs the w planes of a workgroup's pairs
+// in LDS: nK <= 63 (n_pad <= 8064); the caller checks pair_screen_fits.
+bool pair_screen_fits(const gmat_epi *e) { return e->nK <= 63; }
+int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *slp, const int8_t *srp,
+                const int64_t *pi, const int64_t *pj, int64_t np, double chi_cut, int64_t *n_out) {
+  *n_out = 0;
+  if (np <= 0) return GMAT_OK;
+  const int nK = e->nK, pp = nK <= 31 ? 64 : 32;
+  GMAT_CHECK(nK <= 63, GMAT_E_ARG, "pair screen: %d stages exceed the LDS", nK);
+  GMAT_CHECK(L.U.p && R.U.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
+                 R.qb.p && e->cand2_i.p && e->cand2_j.p && e->counter2.p &&
+                 e->cand2_i.bytes >= (size_t)np * 8 && L.U.bytes >= (size_t)e->m * e->n_pad * 8 &&
+                 R.U.bytes >= (size_t)e->m * e->n_pad * 8 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
+             GMAT_E_ARG, "pair screen: plan buffers missing");
+  GMAT_TRY(e->ps_side.alloc((size_t)5 * np * sizeof(double)));
+  GMAT_TRY(e->pins.count2.reserve(8));
+  PairArgs x;
+  x.ci = pi;
+  x.cj = pj;
+  x.np = np;
+  x.n_pad = e->n_pad;
+  x.a = slp;
+  x.b = srp;
+  x.Ua = L.U.as<double>();
+  x.Ub = R.U.as<double>();
+  x.alpha = L.soff.as<double>();
+  x.beta = R.soff.as<double>();
+  x.qa = L.qa.as<double>();
+  x.ra = L.ra.as<double>();
+  x.qb = R.qb.as<double>();
+  x.rb = R.rb.as<double>();
+  x.z = e->z.as<double>();
+  x.dg = e->dg.as<double>();
+  x.py = e->py.as<double>();
+  x.zz = e->zz;
+  x.side = e->ps_side.as<double>();
+  x.tiles = e->mx_tiles.as<uint8_t>();
+  x.nib_i = L.nibI.as<uint8_t>();
+  x.nib_j = R.nibJ.as<uint8_t>();
+  x.tiles_bytes = (int64_t)e->mx_tiles.bytes;
+  x.nK = nK;
+  x.rho = e->rho_mx;
+  x.chi_cut = chi_cut;
+  x.counter = e->counter2.as<unsigned long long>();
+  x.oi = e->cand2_i.as<int64_t>();
+  x.oj = e->cand2_j.as<int64_t>();
+  GMAT_HIP(hipMemsetAsync(e->counter2.p, 0, 8, st));
+  hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, x);
+  GMAT_HIP(hipGetLastError());
+  const size_t lds = 2 * MX_TILE + (size_t)pp * (nK * 64 + 16) + 4 * pp * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 256));
+    GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 256));
+    attr = true;
+  }
+  if (pp == 64)
+    hipLaunchKernelGGL(pair_mx_kernel<64>, dim3((unsigned)cdiv(np, 64)), dim3(512), lds, st, x);
+  else
+    hipLaunchKernelGGL(pair_mx_kernel<32>, dim3((unsigned)cdiv(np, 32)), dim3(256), lds, st, x);
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipMemcpyAsync(e->pins.count2.p, e->counter2.p, 8, hipMemcpyDeviceToHost, st));
+  GMAT_HIP(hipStreamSynchronize(st));
+  *n_out = (int64_t)*e->pins.count2.as<unsigned long long>();
   return GMAT_OK;
 }
 
@@ -3208,6 +3470,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e->cand1_j.alloc(e->cand_cap * 8));
     GMAT_TRY(e->counter1.alloc(8));
   }
+  // pair screen between the screens and the refine (GMAT_NO_PAIR_SCREEN: off, for A/B runs)
+  const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
+  if (use_ps && e->cand2_i.bytes < (size_t)e->cand_cap * 8) {
+    GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->counter2.alloc(8));
+  }
   // scan-private streams (the null stream would serialise them): screen + refine on sm,
   // side terms on S2; ordered after the coding setup by a device synchronisation
   if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
@@ -3245,42 +3514,50 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // exact refine of candidates [0, count) and collection of the hits
   // The exact refine runs on its own stream (s3) when the candidate buffer is flushed.  (Refining
   // launch by launch beside the screens was measured 2.7x slower overall: refine waves occupy
-  // CUs that a screen workgroup, which needs a whole CU, then waits for.)  Candidates [0, issued)
-  // of the device buffer have their refine enqueued.
+  // CUs that a screen workgroup, which needs a whole CU, then waits for.)
   if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
   const hipStream_t S3 = e->s3;
-  int64_t issued = 0;
-  auto enqueue_refine = [&](int64_t upto) -> int {
-    if (upto <= issued) return GMAT_OK;
-    if (issued == 0) GMAT_HIP(hipEventRecord(ev[3], S3));
-    GMAT_TRY(refine(e, S3, L, R, lp, rp, e->cand_i.as<int64_t>() + issued, e->cand_j.as<int64_t>() + issued,
-                    upto - issued, e->ceff.as<double>() + issued, e->cvar.as<double>() + issued,
-                    e->cchi.as<double>() + issued, e->cp.as<double>() + issued));
+  double n_refined = 0;
+  // pair screen (use_ps) and exact refine of candidates [0, count) on S3
+  auto enqueue_refine = [&](int64_t count, const int64_t **fi, const int64_t **fj, int64_t *nf) -> int {
+    *fi = e->cand_i.as<int64_t>();
+    *fj = e->cand_j.as<int64_t>();
+    *nf = count;
+    GMAT_HIP(hipEventRecord(ev[3], S3));
+    if (use_ps) {
+      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, *fi, *fj, count, chi_cut, nf));
+      *fi = e->cand2_i.as<int64_t>();
+      *fj = e->cand2_j.as<int64_t>();
+    }
+    GMAT_TRY(refine(e, S3, L, R, lp, rp, *fi, *fj, *nf, e->ceff.as<double>(), e->cvar.as<double>(),
+                    e->cchi.as<double>(), e->cp.as<double>()));
     GMAT_HIP(hipEventRecord(ev[4], S3));
-    issued = upto;
     return GMAT_OK;
   };
   Pinned &pin_res = e->pins.res;
   // refine what is left of [0, count), collect the hits; the buffer is free afterwards
   auto flush = [&](int64_t count) -> int {
     if (count <= 0) return GMAT_OK;
-    GMAT_TRY(enqueue_refine(count));
-    GMAT_TRY(pin_res.reserve((size_t)count * 48));
-    int64_t *ci = pin_res.as<int64_t>(), *cj = ci + count;
-    double *ce = (double *)(cj + count), *cv = ce + count, *cc = cv + count, *cp = cc + count;
-    GMAT_HIP(hipMemcpyAsync(ci, e->cand_i.p, count * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cj, e->cand_j.p, count * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, count * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, count * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, count * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cp, e->cp.p, count * 8, hipMemcpyDeviceToHost, S3));
+    const int64_t *fi, *fj;
+    int64_t nf;
+    GMAT_TRY(enqueue_refine(count, &fi, &fj, &nf));
+    ncand_total += (double)count;
+    n_refined += (double)nf;
+    if (nf <= 0) return GMAT_OK;
+    GMAT_TRY(pin_res.reserve((size_t)nf * 48));
+    int64_t *ci = pin_res.as<int64_t>(), *cj = ci + nf;
+    double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cp = cc + nf;
+    GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, S3));
+    GMAT_HIP(hipMemcpyAsync(cp, e->cp.p, nf * 8, hipMemcpyDeviceToHost, S3));
     GMAT_HIP(hipStreamSynchronize(S3));
     float ms34;
     GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
     t_ref += ms34 * 1e-3;  // span of the refine stream's work (it shares the GPU with the screens)
-    ncand_total += (double)count;
-    issued = 0;
-    for (int64_t k = 0; k < count; ++k) {
+    for (int64_t k = 0; k < nf; ++k) {
       if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
         e->hit_i.push_back(ci[k]);
         e->hit_j.push_back(cj[k]);
@@ -3938,6 +4215,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
           const int64_t cap = std::max<int64_t>(2 * e->cand_cap, (int64_t)(1.25 * (double)count) + 1024);
           for (DBuf *bf : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp, &e->cand1_i, &e->cand1_j})
             GMAT_TRY(bf->alloc((size_t)cap * 8));
+          if (use_ps)
+            for (DBuf *bf : {&e->cand2_i, &e->cand2_j}) GMAT_TRY(bf->alloc((size_t)cap * 8));
           e->cand_cap = cap;
           sa.cap = cap;
           sa.cand_i = e->cand_i.as<int64_t>();
@@ -4031,6 +4310,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "gmat_epi_scan: %lld launches, tile-list building %.3f s on the host, total %.3f s\n",
             (long long)launches_done, t_build, e->stats[6]);
+  if (getenv("GMAT_DEBUG"))
+    fprintf(stderr, "gmat_epi_scan: %.0f screen candidates, %.0f refined%s\n", ncand_total, n_refined,
+            use_ps ? " (pair screen)" : "");
   if (getenv("GMAT_DEBUG") && use_stage2)
     fprintf(stderr, "gmat_epi_scan: low-rank screen candidates %.0f -> MX re-screen %.0f (%.3f s)\n", n_stage1,
             ncand_total, t_stage2);
