@@ -1692,7 +1692,7 @@ struct PairArgs {
   const int64_t *ci, *cj;  // candidates [np]
   int64_t np, n_pad;
   const int8_t *a, *b;        // screen panels (left, right coding) [m][n_pad]
-  const double *Ua, *Ub;      // P x panel [m][n_pad]
+  const float *Ua, *Ub;       // P x panel rounded to fp32 [m][n_pad]
   const double *alpha, *beta;  // screen-code offsets
   const double *qa, *ra, *qb, *rb;
   const double *z, *dg, *py;
@@ -1714,24 +1714,24 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
   const int64_t i = x.ci[p], j = x.cj[p], n_pad = x.n_pad;
   const double al = x.alpha[i], be = x.beta[j], ab = al * be;
   const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
-  const double *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
+  const float *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
   double s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
   for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
     const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
     const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
 #pragma unroll
     for (int k = 0; k < 8; k += 2) {
-      const v2d_ u2 = *(const v2d_ *)(ua + q0 + k), v2 = *(const v2d_ *)(ub + q0 + k),
-                 z2 = *(const v2d_ *)(x.z + q0 + k), d2 = *(const v2d_ *)(x.dg + q0 + k),
+      const v2f_ u2 = *(const v2f_ *)(ua + q0 + k), v2 = *(const v2f_ *)(ub + q0 + k);
+      const v2d_ z2 = *(const v2d_ *)(x.z + q0 + k), d2 = *(const v2d_ *)(x.dg + q0 + k),
                  y2 = *(const v2d_ *)(x.py + q0 + k);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const double av = (double)ca[k + h], bv = (double)cb[k + h], w = av * bv;
-        const double tu = be * u2[h], tv = al * v2[h], tz = ab * z2[h];
+        const double tu = be * (double)u2[h], tv = al * (double)v2[h], tz = ab * z2[h];
         s1 += w * ((tz - tu) - tv);
         s1a += w * ((fabs(tu) + fabs(tv)) + fabs(tz));
-        s2 += av * v2[h];
-        s2a += fabs(av * v2[h]);
+        s2 += av * (double)v2[h];
+        s2a += fabs(av * (double)v2[h]);
         s3 += d2[h] * (w * w);
         s3a += fabs(d2[h]) * (w * w);
         const double e = (av - al) * (bv - be), ey = e * y2[h];
@@ -1757,10 +1757,11 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
   const double t3 = be * be * x.qa[i], t5 = al * al * x.qb[j], t7 = ab * ab * x.zz, t8 = 2.0 * ab * s2,
                t4 = -2.0 * ab * be * x.ra[i], t6 = -2.0 * ab * al * x.rb[j];
   x.side[p] = s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
-  // fp64 rounding of the dots and of U = P x codes (n u |P||a| per entry): far inside 1e-10 of
-  // the magnitudes summed
-  x.side[x.np + p] = 1e-10 * (s3a + 2.0 * s1a + fabs(t3) + fabs(t5) + fabs(t7) + 2.0 * fabs(ab) * s2a + fabs(t4) +
-                              fabs(t6));
+  // U in fp32: |U32 - U| <= 2^-24 |U| per entry, i.e. 2^-24 (1 + 2^-23) of the s1 / s2 magnitudes;
+  // the fp64 rounding of the dots and of U = P x codes itself (n u |P||a| per entry): far inside
+  // 1e-10 of the magnitudes summed
+  const double su = 2.0 * s1a + 2.0 * fabs(ab) * s2a;
+  x.side[x.np + p] = 6.0e-8 * su + 1e-10 * (s3a + su + fabs(t3) + fabs(t5) + fabs(t7) + fabs(t4) + fabs(t6));
   x.side[2 * x.np + p] = ef;
   x.side[3 * x.np + p] = efa;
   x.side[4 * x.np + p] = sw;
@@ -2324,6 +2325,7 @@ __global__ __launch_bounds__(256) void tl_count_kernel(const uint8_t *__restrict
   if (J >= nJ) return;
   int c = 0;
   const int r1 = min(Rn, TL_R * (rg + 1));
+#pragma unroll 16
   for (int r = TL_R * rg; r < r1; ++r) c += flags[(size_t)r * nJ + J] != 0;
   cnt4[4 * J + rg] = c;
 }
@@ -2378,6 +2380,7 @@ __global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict_
   int idx = 0;
   for (int g = 0; g < rg; ++g) idx += cnt4[4 * J + g];
   const int r1 = min(Rn, TL_R * (rg + 1));
+#pragma unroll 16
   for (int r = TL_R * rg; r < r1; ++r)
     if (flags[(size_t)r * nJ + J]) {
       const int k = h0 + idx / (MX_BI / 2);
@@ -2405,7 +2408,8 @@ __global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict_
 
 struct Coding {
   bool ready = false;
-  DBuf U;                         // P * screen code panel  [m][n_pad]
+  DBuf U;                         // P * screen code panel  [m][n_pad] (fp64, while the coding is built)
+  DBuf U32;                       // the same rounded to fp32 (pair screen side terms)
   DBuf off;                       // alpha/beta of the reference codes (refine) [m]
   DBuf soff;                      // centring offsets of the screen codes [m]
   DBuf sq;                        // squared screen codes (additive coding only) [m][n_pad]
@@ -2626,8 +2630,13 @@ int build_coding_impl(gmat_epi *e, int which) {
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipStreamSynchronize(e->s));
   }
+  GMAT_TRY(cd.U32.alloc((size_t)m * n_pad * sizeof(float)));
+  hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)cdiv(m * n_pad, 256)), dim3(256), 0, e->s, m * n_pad,
+                     cd.U.as<double>(), cd.U32.as<float>());
+  GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipStreamSynchronize(e->s));
-  cd.ready = true;  // U stays: the pair screen's side terms read its rows
+  cd.U.release();
+  cd.ready = true;
   return GMAT_OK;
 }
 
@@ -2660,16 +2669,20 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
 // their number to *n_out (the stream is synchronised).  Needs the w planes of a workgroup's pairs
 // in LDS: nK <= 63 (n_pad <= 8064); the caller checks pair_screen_fits.
 bool pair_screen_fits(const gmat_epi *e) { return e->nK <= 63; }
+// Rank of the low-rank screen: with the pair screen behind it a looser, cheaper bound pays (one
+// 128-deep basis chunk: 4.5x the candidates of rank 384, 0.55x the screen time at the bench
+// configuration); without it the refine of those candidates would dominate.
+int default_lr_rank(const gmat_epi *e) { return pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN") ? 128 : 384; }
 int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *slp, const int8_t *srp,
                 const int64_t *pi, const int64_t *pj, int64_t np, double chi_cut, int64_t *n_out) {
   *n_out = 0;
   if (np <= 0) return GMAT_OK;
   const int nK = e->nK, pp = nK <= 31 ? 64 : 32;
   GMAT_CHECK(nK <= 63, GMAT_E_ARG, "pair screen: %d stages exceed the LDS", nK);
-  GMAT_CHECK(L.U.p && R.U.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
+  GMAT_CHECK(L.U32.p && R.U32.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
                  R.qb.p && e->cand2_i.p && e->cand2_j.p && e->counter2.p &&
-                 e->cand2_i.bytes >= (size_t)np * 8 && L.U.bytes >= (size_t)e->m * e->n_pad * 8 &&
-                 R.U.bytes >= (size_t)e->m * e->n_pad * 8 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
+                 e->cand2_i.bytes >= (size_t)np * 8 && L.U32.bytes >= (size_t)e->m * e->n_pad * 4 &&
+                 R.U32.bytes >= (size_t)e->m * e->n_pad * 4 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
              GMAT_E_ARG, "pair screen: plan buffers missing");
   GMAT_TRY(e->ps_side.alloc((size_t)5 * np * sizeof(double)));
   GMAT_TRY(e->pins.count2.reserve(8));
@@ -2680,8 +2693,8 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   x.n_pad = e->n_pad;
   x.a = slp;
   x.b = srp;
-  x.Ua = L.U.as<double>();
-  x.Ub = R.U.as<double>();
+  x.Ua = L.U32.as<float>();
+  x.Ub = R.U32.as<float>();
   x.alpha = L.soff.as<double>();
   x.beta = R.soff.as<double>();
   x.qa = L.qa.as<double>();
@@ -2830,7 +2843,7 @@ __global__ void lr_quant_kernel(int64_t n, int64_t n_pad, int nK, int Rp, const 
 int lr_setup(gmat_epi *e, const double *dP, const double *pvp, double pmax, const Eigen &eg) {
   const int64_t n = e->n, n_pad = e->n_pad;
   const char *renv = getenv("GMAT_LR_RANK"), *kenv = getenv("GMAT_LR_KAPPA");
-  const int R_req = renv ? atoi(renv) : 384;
+  const int R_req = renv ? atoi(renv) : default_lr_rank(e);
   if (R_req <= 0 || getenv("GMAT_NO_LR") || n < 8) return GMAT_OK;
   const int Re = (int)std::min<int64_t>(std::min<int64_t>(R_req, n - 1), eg.ne - 1);
   if (Re < 1) return GMAT_OK;
@@ -3081,7 +3094,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
     {
       const double t_eig = now();
       const char *renv = getenv("GMAT_LR_RANK");
-      const int R_req = renv ? std::max(0, atoi(renv)) : 384;
+      const int R_req = renv ? std::max(0, atoi(renv)) : default_lr_rank(e);
       const int ne = (int)std::min<int64_t>(std::max(R_req, 16) + 1, n);
       have_eig = n >= 8 && !getenv("GMAT_NO_PREFILTER") && eigen_bottom(e, dp.as<double>(), trP, ne, &eg) == GMAT_OK;
       if (!have_eig && getenv("GMAT_DEBUG")) fprintf(stderr, "gmat_epi_create: no eigendecomposition (%s)\n", gmat_last_error());
