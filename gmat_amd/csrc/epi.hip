@@ -1186,20 +1186,26 @@ struct LrArgs {
   unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0, 1, 4, 5 per workgroup
 };
 
+// Every operand is loaded up front from clamped indices (independent loads issued together; the
+// validity checks only gate the atomic), so a lane's test costs one memory latency.
 __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, int ri, int64_t i, int64_t j,
                                         double lowrank) {
-  if (j >= a.m || (a.tri && j <= i)) return;
-  if (a.mono_l[i] || a.mono_r[j]) return;
-  const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-  double c3 = 0.0;
+  const bool ok = i >= 0 && ri >= 0 && j >= a.j_lo && j < a.m && !(a.tri && j <= i);
+  const int64_t ic = ok ? i : 0, jc = ok ? j : a.j_lo;
+  const int64_t o1 = (int64_t)(ok ? ri : 0) * a.ld_e + (jc - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+  int c3i[SIDE_T];
 #pragma unroll
-  for (int t = a.e3_t - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)a.c13[t * a.c13_stride + o3];
-  const double al = a.alpha[i], be = a.beta[j], ca = a.csum_l[i], ca2 = a.csq_l[i], cb = a.csum_r[j],
-               cb2 = a.csq_r[j], n = a.n_id;
-  const double eff = a.sL3[i] * c3 - be * a.sa[i] - al * a.sb[j] + al * be * a.spy;
-  const double eff_hi = fabs(eff) + a.e3_eps * a.sL3[i] * cb;
+  for (int t = 0; t < SIDE_T; ++t) c3i[t] = t < a.e3_t ? a.c13[t * a.c13_stride + o3] : 0;
+  const bool mono = a.mono_l[ic] || a.mono_r[jc];
+  const double al = a.alpha[ic], be = a.beta[jc], ca = a.csum_l[ic], ca2 = a.csq_l[ic], cb = a.csum_r[jc],
+               cb2 = a.csq_r[jc], n = a.n_id, sl3 = a.sL3[ic], sai = a.sa[ic], sbj = a.sb[jc];
   const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
                sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+  double c3 = 0.0;
+#pragma unroll
+  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)c3i[t];  // zeros beyond e3_t
+  const double eff = sl3 * c3 - be * sai - al * sbj + al * be * a.spy;
+  const double eff_hi = fabs(eff) + a.e3_eps * sl3 * cb;
   const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
                           -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
   double ee = 0.0, mag = 0.0;
@@ -1213,7 +1219,7 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
   const double qb = sqrt(lowrank * (1.0 + 1e-4)) + sqrt(x.E);
   const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - qb * qb -
                      1e-12 * (x.lam + x.tau) * (mag + se * se / n);
-  if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) {
+  if (ok && !mono && (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo)) {
     const unsigned long long k = atomicAdd(a.counter, 1ULL);
     if ((int64_t)k < a.cap) {
       a.cand_i[k] = i;
@@ -1417,12 +1423,12 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     epilogue();
   }
   stamp(4);
+  // lane half h tests slot PB w + h of column c (both halves hold the sums after the exchange)
+  static_assert(PB == 2, "one slot per lane half");
+  double tot[PB];
 #pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    const double other = __shfl_xor(lowrank[t], 32);
-    if (h != 0 || ti[t] < 0) continue;
-    lr_test(a, x, trow[PB * w + t], ti[t], J0 + c, lowrank[t] + other);
-  }
+  for (int t = 0; t < PB; ++t) tot[t] = lowrank[t] + __shfl_xor(lowrank[t], 32);
+  lr_test(a, x, trow[PB * w + h], h ? ti[1] : ti[0], J0 + c, h ? tot[1] : tot[0]);
   if (x.stamp) {
     __syncthreads();
     stamp(5);
