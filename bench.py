@@ -262,7 +262,9 @@ def eff_cpu_baseline(geno, py, cut, budget_s):
         t0 = time.perf_counter()
         O.eff_screen_c("AA", body, n, m, probe, py, [cut], threads=threads)
         t.append((float(np.sum(m - 1 - probe)), time.perf_counter() - t0))
-    per_pair = max((t[1][1] - t[0][1]) / (t[1][0] - t[0][0]), 1e-12)
+    # the difference of the two probes is noisy when the per-call decode dominates them: bound the
+    # per-pair cost below by a quarter of the larger probe's average (sample <= 4 x budget_s)
+    per_pair = max((t[1][1] - t[0][1]) / (t[1][0] - t[0][0]), t[1][1] / t[1][0] / 4.0)
     k = int(min(m - 1, max(8, budget_s / per_pair / (m / 2))))
     rows = np.linspace(0, m - 2, k).astype(np.int64)
     t0 = time.perf_counter()
@@ -302,6 +304,7 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed, geno=None, cpu_budget=10.0):
         wall = time.perf_counter() - t0
     N.check(lib.gmat_eff_stats(N.ptr(st)), "gmat_eff_stats")
     pairs = st[0]
+    log("effect screen cpu baseline")
     cpu = eff_cpu_baseline(geno, py, float(eff_cut[0]), cpu_budget) if geno is not None else None
     return {"config": "remma_epiAA_eff over all %d pairs, eff_cut from the median var (p_cut=%g)" % (pairs, p_cut),
             "pairs_per_s_device": pairs / st[2], "pairs_per_s_end_to_end": pairs / wall, "device_s": st[2],
@@ -537,21 +540,28 @@ def main():
 
     cpu = parity = None
     if rank == 0 and ws == 1 and not args.no_cpu:
+        log("cpu baseline (oracle port) on stratified rows, %.0f s budget" % args.cpu_budget)
         cpu, used_rows, exp_hits = cpu_baseline(geno, pvp, py, args.cpu_budget)
+        log("parity of the sampled rows against the oracle")
         parity = parity_check(plan, used_rows, exp_hits, args.p_cut)
     grm = reml = None
     if rank == 0 and not args.no_grm:
+        log("configs[1] GRM")
         grm = grm_bench(n, 20000, args.seed)
         if not args.no_reml:
+            log("configs[1] REML")
             reml = reml_bench(grm_bench.last_k, args.seed)
     cov = None
     if rank == 0 and ws == 1 and not args.no_cov:
+        log("covariate design")
         cov = covariate_bench(g, ka, y, n, m, args.p_cut, args.seed, 2, t_max / args.steps * 1e3)
     e2e = None
     if rank == 0 and ws == 1 and not args.no_e2e:
+        log("end to end remma_epiAA")
         e2e = e2e_bench(geno, ka, y, var, args.p_cut, int(round(hits_all)))
     eff = None
     if rank == 0 and ws == 1 and not args.no_eff:
+        log("effect screen")
         eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed, geno=geno, cpu_budget=args.cpu_budget)
     if rank == 0:
         value = total_pairs * args.steps / t_max

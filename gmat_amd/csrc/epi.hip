@@ -1184,6 +1184,7 @@ struct LrArgs {
   const float *G, *H;      // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
   double lam, tau, eps, E;  // E = sum_r eta_r^2
   unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0, 1, 4, 5 per workgroup
+  int diag;                   // diagnostics (GMAT_LR_DIAG, timing only, no candidates): 1 no stage loads, 2 no MFMAs
 };
 
 // Every operand is loaded up front from clamped indices (independent loads issued together; the
@@ -1233,7 +1234,8 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
 // K-sweep step (no symmetry), with the chunk's epilogue after its last stage.
 // SK tile images (128 individuals each) per LDS stage and barrier (SK = 2: 256-deep stages, half
 // the barriers, 144 KB of LDS)
-template <int SK>
+// DIAG (timing diagnostics, GMAT_LR_DIAG; no candidates): 1 = no stage loads, 2 = no MFMAs
+template <int SK, int DIAG = 0>
 __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
   constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
   constexpr int SI = MX_BI * NB_REC, SJ = 2 * BJ * NB_REC;
@@ -1392,9 +1394,9 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
   };
   auto iter = [&](int b, bool first, int nch, int ncs) __attribute__((always_inline)) {
-    load(b ^ 1, nch, ncs);
+    if (!(DIAG & 1)) load(b ^ 1, nch, ncs);
     __builtin_amdgcn_sched_barrier(0);
-    compute(b, first);
+    if (!(DIAG & 2)) compute(b, first);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of the next stage
     __syncthreads();
   };
@@ -1428,6 +1430,10 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   double tot[PB];
 #pragma unroll
   for (int t = 0; t < PB; ++t) tot[t] = lowrank[t] + __shfl_xor(lowrank[t], 32);
+  if (DIAG) {  // timing diagnostics: keep the sums alive, report nothing
+    if (tot[0] + tot[1] == -1.0) a.cand_i[0] = -1;
+    return;
+  }
   lr_test(a, x, trow[PB * w + h], h ? ti[1] : ti[0], J0 + c, h ? tot[1] : tot[0]);
   if (x.stamp) {
     __syncthreads();
@@ -4089,7 +4095,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
   const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
   auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, const LrArgs &lx_) {
-    if (lr_sk == 2)
+    if (lx_.diag == 1)
+      hipLaunchKernelGGL((lr_screen_kernel<2, 1>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    else if (lx_.diag == 2)
+      hipLaunchKernelGGL((lr_screen_kernel<2, 2>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    else if (lx_.diag == 3)
+      hipLaunchKernelGGL((lr_screen_kernel<2, 3>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    else if (lr_sk == 2)
       hipLaunchKernelGGL(lr_screen_kernel<2>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
     else
       hipLaunchKernelGGL(lr_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
@@ -4111,6 +4123,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     lx.tau = e->lr_tau;
     lx.eps = e->lr_eps;
     lx.stamp = (stamps_on && li == 5) ? dstamp.as<unsigned long long>() : nullptr;
+    lx.diag = getenv("GMAT_LR_DIAG") ? atoi(getenv("GMAT_LR_DIAG")) : 0;
     return lx;
   };
   // queue the low-rank screen of launch li (level 0) on sm: waits for its side pass, counts after it
