@@ -1181,30 +1181,44 @@ struct LrArgs {
   const uint8_t *nib_i, *nib_j;
   int64_t tiles_bytes, nib_bytes;
   int nK, nC, R;           // stages, 128-row chunks, padded rank
+  int n_tiles;             // tile entries of the launch: workgroup b takes entries b, b + grid, ...
   const float *G, *H;      // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
+  const double *recL, *recR;  // per-SNP test records (LR_REC doubles each, lr_rec_kernel)
   double lam, tau, eps, E;  // E = sum_r eta_r^2
-  unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0, 1, 4, 5 per workgroup
-  int diag;                   // diagnostics (GMAT_LR_DIAG, timing only, no candidates): 1 no stage loads, 2 no MFMAs
+  unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0 .. 5 per tile entry
 };
+// Test records: left {alpha, csum, csq, sL3, sa, mono}, right {beta, csum, csq, sb, mono}, padded to
+// 64 bytes (four 16-byte DMA chunks)
+constexpr int LR_REC = 8;
+// Test operands staged in LDS while a tile's stages run: planes [LR_NPL][16 slots][32 columns] of
+// int32 (the E3 slices c13_0 .. c13_{SIDE_T-1}, then the code products Sab, Sa2b, Sab2, Sa2b2), the
+// 16 slots' left records and the 64 columns' right records.
+constexpr int LR_NPL = SIDE_T + 4, LR_PLANE = MX_BI * BJ * 4;
+constexpr int LR_OFF_RL = LR_NPL * LR_PLANE, LR_OFF_RR = LR_OFF_RL + MX_BI * LR_REC * 8;
+constexpr int LR_ST_BYTES = LR_OFF_RR + 2 * BJ * LR_REC * 8;
 
-// Every operand is loaded up front from clamped indices (independent loads issued together; the
-// validity checks only gate the atomic), so a lane's test costs one memory latency.
-__device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, int ri, int64_t i, int64_t j,
-                                        double lowrank) {
-  const bool ok = i >= 0 && ri >= 0 && j >= a.j_lo && j < a.m && !(a.tri && j <= i);
-  const int64_t ic = ok ? i : 0, jc = ok ? j : a.j_lo;
-  const int64_t o1 = (int64_t)(ok ? ri : 0) * a.ld_e + (jc - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-  int c3i[SIDE_T];
-#pragma unroll
-  for (int t = 0; t < SIDE_T; ++t) c3i[t] = t < a.e3_t ? a.c13[t * a.c13_stride + o3] : 0;
-  const bool mono = a.mono_l[ic] || a.mono_r[jc];
-  const double al = a.alpha[ic], be = a.beta[jc], ca = a.csum_l[ic], ca2 = a.csq_l[ic], cb = a.csum_r[jc],
-               cb2 = a.csq_r[jc], n = a.n_id, sl3 = a.sL3[ic], sai = a.sa[ic], sbj = a.sb[jc];
-  const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
-               sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+__device__ __forceinline__ void lds_dma4(const void *g, const void *lds) {
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)lds);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" : : "v"(g), "{m0}"(m) : "memory");
+}
+
+// Candidate test of the lane's pair (slot s, column col of column block `half`) from the operands
+// staged in sT: every pair whose p-value could be below p_cut is kept.
+__device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, const uint8_t *sT, int s, int col,
+                                        int half, bool ok, int64_t i, int64_t j, double lowrank) {
+  const int *pl = (const int *)sT + s * BJ + col;
+  const double *rl = (const double *)(sT + LR_OFF_RL) + s * LR_REC;
+  const double *rr = (const double *)(sT + LR_OFF_RR) + (half * BJ + col) * LR_REC;
   double c3 = 0.0;
 #pragma unroll
-  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)c3i[t];  // zeros beyond e3_t
+  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (t < a.e3_t ? (double)pl[t * MX_BI * BJ] : 0.0);
+  const double sab = (double)pl[SIDE_T * MX_BI * BJ], sa2b = (double)pl[(SIDE_T + 1) * MX_BI * BJ],
+               sab2 = (double)pl[(SIDE_T + 2) * MX_BI * BJ], sa2b2 = (double)pl[(SIDE_T + 3) * MX_BI * BJ];
+  const double al = rl[0], ca = rl[1], ca2 = rl[2], sl3 = rl[3], sai = rl[4];
+  const double be = rr[0], cb = rr[1], cb2 = rr[2], sbj = rr[3];
+  const bool mono = rl[5] != 0.0 || rr[4] != 0.0;
+  const double n = a.n_id;
   const double eff = sl3 * c3 - be * sai - al * sbj + al * be * a.spy;
   const double eff_hi = fabs(eff) + a.e3_eps * sl3 * cb;
   const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
@@ -1229,55 +1243,67 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, in
   }
 }
 
-// Workgroup / wave layout, tile list, staging and LDS images as mx_screen_kernel (MxShape<1>);
-// the loop is chunk ch (128 eigen-directions) -> stage cs (128 individuals), every stage a full
-// K-sweep step (no symmetry), with the chunk's epilogue after its last stage.
-// SK tile images (128 individuals each) per LDS stage and barrier (SK = 2: 256-deep stages, half
-// the barriers, 144 KB of LDS)
-// DIAG (timing diagnostics, GMAT_LR_DIAG; no candidates): 1 = no stage loads, 2 = no MFMAs
-template <int SK, int DIAG = 0>
+// Workgroup / wave layout, tile entries, staging and LDS images as mx_screen_kernel (MxShape<1>);
+// per tile the loop is chunk ch (128 eigen-directions) -> stage (SK x 128 individuals, one barrier),
+// every stage a full K-sweep step (no symmetry), with the chunk's epilogue after its last stage.
+// Each workgroup works through several tile entries (b, b + grid, ...; the grid is a multiple of 8,
+// so an entry keeps the XCD it was dealt to), and a tile's fixed costs run beside its stages:
+//  * the first stage of the next chunk / tile is loaded during the last stage of this one and lands
+//    during the epilogue and the test;
+//  * the chunk's epilogue operands (G' rows of the 16 slots, H rows of the 64 columns) and, with the
+//    first chunk, every test operand (E3 slices, code products, per-SNP records: a lane fetches those
+//    of its own pair) are fetched by LDS-DMA as the youngest operations of the second-to-last stage,
+//    whose wait (a counted vmcnt: VMEM operations retire in order) lets them land during the last
+//    stage.  Every wait is one asm statement with the barrier (vm_wait_barrier): the compiler does
+//    not know that the DMA asm writes LDS.
+template <int SK>
 __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
   constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
-  constexpr int SI = MX_BI * NB_REC, SJ = 2 * BJ * NB_REC;
+  // j side: only the S1 plane (first 64 bytes of a record: b as fp4 codes) is staged, S2 = S1 << 1
+  constexpr int JB = NB_REC / 2, SI = MX_BI * NB_REC, SJ = 2 * BJ * JB;
+  static_assert(PB == 2, "one slot per lane half");
   __shared__ __attribute__((aligned(16))) uint8_t sA[2][SK * MX_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t sI[2][SK * SI];
   __shared__ __attribute__((aligned(16))) uint8_t sJ[2][SK * SJ];
-  __shared__ __attribute__((aligned(16))) uint8_t sE[40 * 1024];  // chunk epilogue operands (LDS-DMA)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
-  const int tl = a.tiles[MX_TE * blockIdx.x];
-  if (tl < 0) return;
-  auto stamp = [&](int k) __attribute__((always_inline)) {
-    if (x.stamp && tid == 0) x.stamp[6 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+  __shared__ __attribute__((aligned(16))) uint8_t sE[40 * 1024];    // chunk epilogue operands
+  __shared__ __attribute__((aligned(16))) uint8_t sT[LR_ST_BYTES];  // test operands
+  // per-lane DMA source offsets parked in LDS (registers are the loop's): [tile parity][thread] the
+  // stage record offset (i side for waves 0, 1, j side for waves 4..7), [tile parity][lane] wave 0's
+  // slot record offset
+  __shared__ unsigned sO[2][MxShape<1>::T], sRo[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = (PB * w) / (MX_BI / 2);  // this wave's column block
+  const int nK = x.nK, nC = x.nC, nS = nK / SK, G = (int)gridDim.x;
+  const int64_t R = x.R;
+  auto next_entry = [&](int e) __attribute__((always_inline)) {
+    while (e < x.n_tiles && a.tiles[MX_TE * e] < 0) e += G;
+    return e < x.n_tiles ? e : -1;
   };
-  stamp(0);
-  const int Jt[2] = {a.tiles[MX_TE * blockIdx.x + 1], a.tiles[MX_TE * blockIdx.x + 2]};
-  const int *trow = a.tile_rows + (int64_t)tl * MX_BI;
-  const int half = (PB * w) / (MX_BI / 2);
-  const int64_t J0 = (int64_t)Jt[half] * BJ;
-  const int nK = x.nK, nC = x.nC;
-
-  int64_t ti[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    const int r = trow[PB * w + t];
-    ti[t] = (r >= 0) ? a.rows[r] : -1;
-  }
-  // Every operand of a stage arrives by LDS-DMA (global_load_lds_dwordx4: lane i's 16 bytes land at
-  // M0 + 16 i), so no register round trip and no ds_write: the A tile image (NA wave-instructions
-  // per tile), the j-side records (one per wave: chunk jc = tid of the two column blocks, source
-  // chunk XOR-swizzled by column) and the i-side records (waves 0 and 1: 16 slots x 8 chunks).
-  // Lanes whose column or slot is unused read SNP 0 (finite data in accumulators nobody tests).
-  const int jh = tid >> 8, js = (tid >> 3) & 31, jq = tid & 7, jl = jq ^ ((js >> 1) & 7);
-  const uint8_t *srcJ, *srcI = nullptr;
-  {
-    const int64_t jj = (int64_t)Jt[jh] * BJ + js;
-    srcJ = x.nib_j + ((Jt[jh] >= 0 && jj < a.m) ? jj : 0) * nK * NB_REC + jl * 16;
-    if (tid < MX_BI * 8) {
-      const int sl = tid >> 3;
-      srcI = x.nib_i + (trow[sl] >= 0 ? a.rows[trow[sl]] : 0) * nK * NB_REC + jq * 16;
+  int e = next_entry((int)blockIdx.x);
+  if (e < 0) return;
+  auto stamp = [&](int ent, int k) __attribute__((always_inline)) {
+    if (x.stamp && tid == 0) x.stamp[6 * ent + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  // Stage operands by LDS-DMA (global_load_lds_dwordx4: lane i's 16 bytes land at M0 + 16 i): the A
+  // tile image (NA wave-instructions per image), the j-side S1 planes (waves 4..7: 16 columns x 4
+  // chunks each, physical chunk p of column js holding logical chunk p ^ (js & 3): conflict-free
+  // fragment reads) and the i-side records (waves 0 and 1: 16 slots x 8 chunks).  Lanes whose
+  // column or slot is unused read SNP 0 (finite data in accumulators nobody tests).
+  auto src_offsets = [&](int tl, int J0t, int J1t, unsigned &oI, unsigned &oJ) __attribute__((always_inline)) {
+    oI = oJ = 0;
+    if (w >= 4) {
+      const int jc = tid - 256, jh = jc >> 7, js = (jc >> 2) & 31, jq = jc & 3;
+      const int Jh = jh ? J1t : J0t;
+      const int64_t jj = (int64_t)Jh * BJ + js;
+      oJ = (unsigned)(((Jh >= 0 && jj < a.m) ? jj : 0) * nK * NB_REC + (jq ^ (js & 3)) * 16);
     }
-  }
-  auto load = [&](int nb, int ch, int cs2) __attribute__((always_inline)) {
+    if (w < 2) {
+      const int r = a.tile_rows[(int64_t)tl * MX_BI + (tid >> 3)];
+      oI = (unsigned)((r >= 0 ? a.rows[r] : 0) * nK * NB_REC + (tid & 7) * 16);
+    }
+  };
+  auto load = [&](int nb, int ch, int cs2, unsigned oI, unsigned oJ) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < SK; ++s) {
       const int cs = cs2 * SK + s;
@@ -1285,15 +1311,16 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 #pragma unroll
       for (int u = 0; u < NA; ++u)
         lds_dma16(src + (tid + u * MX_T) * 16, &sA[nb][s * MX_TILE + (w * 64 + u * MX_T) * 16]);
-      lds_dma16(srcJ + cs * NB_REC, &sJ[nb][s * SJ + w * 1024]);
-      if (w < 2) lds_dma16(srcI + cs * NB_REC, &sI[nb][s * SI + w * 1024]);
+      if (w >= 4) lds_dma16(x.nib_j + oJ + cs * NB_REC, &sJ[nb][s * SJ + (w - 4) * 1024]);
+      if (w < 2) lds_dma16(x.nib_i + oI + cs * NB_REC, &sI[nb][s * SI + w * 1024]);
     }
   };
+  const int NL = SK * (NA + (w >= 4 ? 1 : 0) + (w < 2 ? 1 : 0));  // this wave's DMAs per stage load
 
   v16f_ acc[RB][PB];
   const int sw16 = 16 * ((c >> 3) & 1);
-  const int jf = (c >> 1) & 7;
-  const int jrow = (half * BJ + c) * NB_REC;
+  const int jf = c & 3;
+  const int jrow = (half * BJ + c) * JB;
   // A fragment r of (stage s, half kk): the 6 fp6 dwords + the scale dword of row 32 r + c
   auto afrag = [&](int b, int s, int kk, int r) __attribute__((always_inline)) {
     const uint8_t *ar = &sA[b][s * MX_TILE + (2 * kk + h) * 4096 + (32 * r + c) * 32];
@@ -1333,44 +1360,65 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
         }
       }
   };
-  // Chunk epilogue operands staged in LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
-  // instruction q, written linearly at sE + q KB): q 0..7 = G' rows of the 16 slots (512 B each),
-  // q 8..39 = H rows of the 64 columns (physical 16-byte chunk p of column row holds logical chunk
-  // p ^ (row & 15): conflict-free reads).  Wave w issues q = w, 8+w, .., 32+w; the per-lane source
-  // offsets are fixed per tile.
-  const int64_t jcol = max((int64_t)0, min(J0 + c, a.m - 1));  // J0 < 0 for an unused tile half
-  const float be = (float)a.beta[jcol];
-  float al[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) al[t] = (float)a.alpha[ti[t] < 0 ? 0 : ti[t]];
-  int offG, offH[4];
-  {
-    const int sl = 2 * w + (lane >> 5), r = trow[sl];
-    offG = (int)((r >= 0 ? a.rows[r] : 0) * x.R) + 4 * (lane & 31);
+  // Chunk epilogue operands (1 KB per wave instruction q, written linearly at sE + q KB): q 0..7 =
+  // G' rows of the 16 slots (512 B each), q 8..39 = H rows of the 64 columns (physical 16-byte chunk
+  // p of column row holds logical chunk p ^ (row & 15): conflict-free reads).  Wave w issues q = w,
+  // 8 + w, .., 32 + w.
+  // The fetches' pointers and lane indices are laundered through empty asm at the point of use: the
+  // compiler would otherwise hoist their address arithmetic out of the stage loop and keep it in
+  // registers the accumulators need.
+  auto fetch_epi = [&](int ch, int J0t, int J1t, int64_t i0, int64_t i1) __attribute__((always_inline)) {
+    const float *Gp = x.G, *Hp = x.H;
+    int ln = lane;
+    asm volatile("" : "+s"(Gp), "+s"(Hp), "+v"(ln));
+    const int hh = ln >> 5, cc = ln & 31;
+    const int64_t ig = hh ? i1 : i0;
+    lds_dma16(Gp + (ig < 0 ? 0 : ig) * R + ch * MXK + 4 * cc, &sE[w * 1024]);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int row = 2 * (w + 8 * u) + (lane >> 5);
-      const int Jh = Jt[row >> 5];
+      const int row = 2 * (w + 8 * u) + hh;
+      const int Jh = (row >> 5) ? J1t : J0t;
       const int64_t jj = Jh < 0 ? 0 : min((int64_t)Jh * BJ + (row & 31), a.m - 1);
-      offH[u] = (int)(jj * x.R) + 4 * ((lane & 31) ^ (row & 15));
+      lds_dma16(Hp + jj * R + ch * MXK + 4 * (cc ^ (row & 15)), &sE[(8 + w + 8 * u) * 1024]);
     }
-  }
-  auto fetch_epi = [&](int ch) __attribute__((always_inline)) {
-    lds_dma16(x.G + offG + ch * MXK, &sE[w * 1024]);
+  };
+  // Test operands of the lane's own pair (slot 2w + h, column c of the wave's block): SIDE_T + 4
+  // planes by global_load_lds_dword (lane i's 4 bytes at M0 + 4 i); wave 0 fetches the 16 slot
+  // records (lane: slot lane / 4, quarter lane % 4), waves 1..4 the 64 column records (16 each).
+  // Unused slots / columns read offset 0 (SNP 0, band row 0, column j_lo).
+  auto fetch_test = [&](int J0t, int J1t, int ri, unsigned orec) __attribute__((always_inline)) {
+    const int *c13 = a.c13, *pfc = a.pfc;
+    const double *recL = x.recL, *recR = x.recR;
+    int ln = lane;
+    asm volatile("" : "+s"(c13), "+s"(pfc), "+s"(recL), "+s"(recR), "+v"(ln));
+    const int Jh = half ? J1t : J0t;
+    const int64_t j = (int64_t)Jh * BJ + (ln & 31);
+    const bool ok = ri >= 0 && Jh >= 0 && j >= a.j_lo && j < a.m;
+    const int64_t o1 = ok ? (int64_t)ri * a.ld_e + (j - a.j_lo) : 0;
+    const int64_t o3 = ok ? o1 + (int64_t)a.n_rows * a.ld_e : 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      lds_dma16(x.H + offH[u] + ch * MXK, &sE[(8 + w + 8 * u) * 1024]);
+    for (int t = 0; t < SIDE_T; ++t)
+      lds_dma4(c13 + (t < a.e3_t ? t * a.c13_stride + o3 : 0), sT + t * LR_PLANE + 2 * w * BJ * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lds_dma4(pfc + k * a.pfc_stride + o1, sT + (SIDE_T + k) * LR_PLANE + 2 * w * BJ * 4);
+    if (w == 0) lds_dma16(recL + orec, sT + LR_OFF_RL);
+    if (w >= 1 && w <= 4) {
+      const int col = 16 * (w - 1) + (ln >> 2);
+      const int Jc = (col >> 5) ? J1t : J0t;
+      const int64_t jj = Jc < 0 ? 0 : min((int64_t)Jc * BJ + (col & 31), a.m - 1);
+      lds_dma16(recR + jj * LR_REC + 2 * (ln & 3), sT + LR_OFF_RR + (w - 1) * 1024);
+    }
   };
   // sum of c~_r^2 over the chunk's rows: c~ = acc - beta G' - alpha H, two rows per v_pk_fma_f32
-  double lowrank[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) lowrank[t] = 0.0;
   const int hrow = half * BJ + c;
-  auto epilogue = [&]() __attribute__((always_inline)) {
+  auto epilogue = [&](double *lowrank) __attribute__((always_inline)) {
+    const float be = (float)((const double *)(sT + LR_OFF_RR))[hrow * LR_REC];
     const v2f_ nbe = {-be, -be};
 #pragma unroll
     for (int t = 0; t < PB; ++t) {
-      const v2f_ nal = {-al[t], -al[t]};
+      const float al = (float)((const double *)(sT + LR_OFF_RL))[(PB * w + t) * LR_REC];
+      const v2f_ nal = {-al, -al};
       v2f_ s2 = {0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
@@ -1393,51 +1441,111 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       lowrank[t] += (double)s2[0] + (double)s2[1];
     }
   };
-  auto iter = [&](int b, bool first, int nch, int ncs) __attribute__((always_inline)) {
-    if (!(DIAG & 1)) load(b ^ 1, nch, ncs);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!(DIAG & 2)) compute(b, first);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of the next stage
-    __syncthreads();
-  };
 
-  load(0, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  stamp(1);
-  int b = 0;
-  const int nS = nK / SK;  // stages per chunk
-  for (int ch = 0; ch < nC; ++ch) {
-    const bool lastch = ch + 1 == nC;
-    if (ch > 0) __syncthreads();  // every wave is past the previous chunk's epilogue reads of sE
-    fetch_epi(ch);                // lands during this chunk's stages
-    if (nS > 1) iter(b, true, ch, 1);
-    else iter(b, true, lastch ? ch : ch + 1, 0);
-    b ^= 1;
-#pragma unroll 1
-    for (int cs = 1; cs < nS; ++cs) {
-      const bool lastc = cs + 1 == nS;
-      iter(b, false, lastc ? (lastch ? ch : ch + 1) : ch, lastc ? 0 : cs + 1);
-      b ^= 1;
+  int tl = a.tiles[MX_TE * e], J0t = a.tiles[MX_TE * e + 1], J1t = a.tiles[MX_TE * e + 2];
+  {
+    unsigned oI, oJ;
+    src_offsets(tl, J0t, J1t, oI, oJ);
+    sO[0][tid] = w < 2 ? oI : oJ;
+    stamp(e, 0);
+    load(0, 0, 0, oI, oJ);
+  }
+  int b = 0, par = 0;
+  for (;;) {
+    // this tile's slots (wave-uniform: slots 2w, 2w + 1) and the next entry's stage sources
+    const int *trow = a.tile_rows + (int64_t)tl * MX_BI;
+    const int r0 = trow[PB * w], r1 = trow[PB * w + 1];
+    const int64_t i0 = r0 >= 0 ? a.rows[r0] : -1, i1 = r1 >= 0 ? a.rows[r1] : -1;
+    const int en = next_entry(e + G);
+    int tln = 0, J0n = -1, J1n = -1;
+    if (en >= 0) {
+      tln = a.tiles[MX_TE * en];
+      J0n = a.tiles[MX_TE * en + 1];
+      J1n = a.tiles[MX_TE * en + 2];
+      unsigned oIn, oJn;
+      src_offsets(tln, J0n, J1n, oIn, oJn);
+      sO[par ^ 1][tid] = w < 2 ? oIn : oJn;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA of sE has landed
-    __syncthreads();                                   // ... and every other wave's
-    epilogue();
+    if (w == 0) {  // the slot record quarter this lane fetches
+      const int r = trow[lane >> 2];
+      sRo[par][lane] = (unsigned)((r >= 0 ? a.rows[r] : 0) * LR_REC + 2 * (lane & 3));
+    }
+    vm_wait_barrier(0);  // the tile's first stage (and every wave is past the last tile's test)
+    stamp(e, 1);
+    double lowrank[PB] = {0.0, 0.0};
+    for (int ch = 0; ch < nC; ++ch) {
+      const bool lastch = ch + 1 == nC;
+      if (ch > 0) __syncthreads();  // every wave is past the last chunk's epilogue reads of sE
+      // the DMAs after a stage's MFMAs: its successor, or the first stage of the next chunk / tile
+      auto load_after = [&](int cs2) __attribute__((always_inline)) {
+        if (cs2 + 1 < nS) {
+          const unsigned o = sO[par][tid];
+          load(b ^ 1, ch, cs2 + 1, o, o);
+        } else if (!lastch || en >= 0) {
+          const unsigned o = sO[lastch ? par ^ 1 : par][tid];
+          load(b ^ 1, lastch ? 0 : ch + 1, 0, o, o);
+        }
+      };
+      // first stage (peeled): its load, then the epilogue (and with the first chunk the test)
+      // operands as the youngest DMAs, so its wait leaves them in flight over the next stage; the
+      // fetch code stays out of the stage loop, whose accumulators need every register
+      load_after(0);
+      fetch_epi(ch, J0t, J1t, i0, i1);
+      int nf = 5;
+      if (ch == 0) {
+        fetch_test(J0t, J1t, h ? r1 : r0, w == 0 ? sRo[par][lane] : 0u);
+        nf += SIDE_T + 4 + (w <= 4 ? 1 : 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      compute(b, true);
+      vm_wait_barrier(nS > 1 ? nf : 0);
+      b ^= 1;
+      if (ch == 0) stamp(e, 2);
+#pragma unroll 1
+      for (int cs2 = 1; cs2 < nS; ++cs2) {
+        load_after(cs2);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(b, false);
+        vm_wait_barrier(0);
+        b ^= 1;
+      }
+      stamp(e, 3);
+      epilogue(lowrank);
+    }
+    stamp(e, 4);
+    // lane half h tests slot PB w + h of column c (both halves hold the sums after the exchange)
+    {
+      const double tot = (h ? lowrank[1] : lowrank[0]) + __shfl_xor(h ? lowrank[0] : lowrank[1], 32);
+      const int ri = h ? r1 : r0;
+      const int64_t i = h ? i1 : i0;
+      const int Jh = half ? J1t : J0t;
+      const int64_t j = (int64_t)Jh * BJ + c;
+      const bool ok = i >= 0 && ri >= 0 && Jh >= 0 && j >= a.j_lo && j < a.m && !(a.tri && j <= i);
+      lr_test(a, x, sT, PB * w + h, c, half, ok, i, j, tot);
+    }
+    stamp(e, 5);
+    if (en < 0) break;
+    e = en;
+    tl = tln;
+    J0t = J0n;
+    J1t = J1n;
+    par ^= 1;
   }
-  stamp(4);
-  // lane half h tests slot PB w + h of column c (both halves hold the sums after the exchange)
-  static_assert(PB == 2, "one slot per lane half");
-  double tot[PB];
+}
+
+// Left / right test records of a coding (lr_screen_kernel's per-SNP test operands in one 64-byte
+// record each: one LDS-DMA chunk per quarter)
+__global__ void lr_rec_kernel(int64_t m, const double *soff, const double *csum, const double *csq, const double *sL3,
+                              const double *sa, const double *sb, const uint8_t *mono, double *recL, double *recR) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const double mo = mono[j] ? 1.0 : 0.0;
+  const double l[LR_REC] = {soff[j], csum[j], csq[j], sL3[j], sa[j], mo, 0.0, 0.0};
+  const double r[LR_REC] = {soff[j], csum[j], csq[j], sb[j], mo, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int t = 0; t < PB; ++t) tot[t] = lowrank[t] + __shfl_xor(lowrank[t], 32);
-  if (DIAG) {  // timing diagnostics: keep the sums alive, report nothing
-    if (tot[0] + tot[1] == -1.0) a.cand_i[0] = -1;
-    return;
-  }
-  lr_test(a, x, trow[PB * w + h], h ? ti[1] : ti[0], J0 + c, h ? tot[1] : tot[0]);
-  if (x.stamp) {
-    __syncthreads();
-    stamp(5);
+  for (int k = 0; k < LR_REC; ++k) {
+    recL[j * LR_REC + k] = l[k];
+    recR[j * LR_REC + k] = r[k];
   }
 }
 
@@ -2435,6 +2543,7 @@ struct Coding {
                                   // their per-row scales and u_k . code [ncov][m]
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
+  DBuf lrRecL, lrRecR;            // low-rank screen test records [m][LR_REC] (left / right roles)
 };
 
 // pinned host staging buffer (grown on demand, kept by the plan across scans)
@@ -2639,6 +2748,12 @@ int build_coding_impl(gmat_epi *e, int which) {
     GMAT_TRY(cd.lrGa.alloc((size_t)m * Rp * sizeof(float)));
     hipLaunchKernelGGL(lr_adjust_kernel, dim3((unsigned)cdiv(m * Rp, 256)), dim3(256), 0, e->s, m, Rp, g64.as<double>(),
                        cd.soff.as<double>(), e->lr_q1.as<double>(), cd.lrGa.as<float>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_TRY(cd.lrRecL.alloc((size_t)m * LR_REC * sizeof(double)));
+    GMAT_TRY(cd.lrRecR.alloc((size_t)m * LR_REC * sizeof(double)));
+    hipLaunchKernelGGL(lr_rec_kernel, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, e->s, m, cd.soff.as<double>(),
+                       cd.csum.as<double>(), cd.csq.as<double>(), cd.sL3.as<double>(), cd.sa.as<double>(),
+                       cd.sb.as<double>(), cd.mono.as<uint8_t>(), cd.lrRecL.as<double>(), cd.lrRecR.as<double>());
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipStreamSynchronize(e->s));
   }
@@ -4094,18 +4209,18 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_TRY(pin_cnt[1].reserve(8));
   // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
   const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
-  auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, const LrArgs &lx_) {
-    if (lx_.diag == 1)
-      hipLaunchKernelGGL((lr_screen_kernel<2, 1>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
-    else if (lx_.diag == 2)
-      hipLaunchKernelGGL((lr_screen_kernel<2, 2>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
-    else if (lx_.diag == 3)
-      hipLaunchKernelGGL((lr_screen_kernel<2, 3>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
-    else if (lr_sk == 2)
-      hipLaunchKernelGGL(lr_screen_kernel<2>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+  // tile entries per workgroup (GMAT_LR_TPW): the grid strides over the entries in multiples of 8
+  const int lr_tpw = getenv("GMAT_LR_TPW") ? std::max(1, atoi(getenv("GMAT_LR_TPW"))) : 2;
+  auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, LrArgs lx_) {
+    lx_.n_tiles = (int)g;
+    unsigned grid = (unsigned)cdiv((int64_t)g, lr_tpw);
+    grid = std::min<unsigned>((unsigned)cdiv(grid, 8) * 8, g);
+    if (lr_sk == 2)
+      hipLaunchKernelGGL(lr_screen_kernel<2>, dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
     else
-      hipLaunchKernelGGL(lr_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+      hipLaunchKernelGGL(lr_screen_kernel<1>, dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
   };
+
   auto lr_args = [&](size_t li) {
     LrArgs lx;
     lx.tiles = e->lr_tiles.as<uint8_t>();
@@ -4123,7 +4238,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     lx.tau = e->lr_tau;
     lx.eps = e->lr_eps;
     lx.stamp = (stamps_on && li == 5) ? dstamp.as<unsigned long long>() : nullptr;
-    lx.diag = getenv("GMAT_LR_DIAG") ? atoi(getenv("GMAT_LR_DIAG")) : 0;
+    lx.recL = L.lrRecL.as<double>();
+    lx.recR = R.lrRecR.as<double>();
+    lx.n_tiles = 0;
     return lx;
   };
   // queue the low-rank screen of launch li (level 0) on sm: waits for its side pass, counts after it
@@ -4272,12 +4389,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         if (mx_tiles[MX_TE * q] < 0) continue;
         const unsigned long long *st = &hs[6 * q];
         ph[0].push_back((double)(st[1] - st[0]) * 10.0);  // 100 MHz -> ns
-        ph[3].push_back((double)(st[4] - st[1]) * 10.0);
+        ph[1].push_back((double)(st[2] - st[1]) * 10.0);
+        ph[2].push_back((double)(st[3] - st[2]) * 10.0);
+        ph[3].push_back((double)(st[4] - st[3]) * 10.0);
         ph[4].push_back((double)(st[5] - st[4]) * 10.0);
         t_min = std::min(t_min, st[0]);
         t_max = std::max(t_max, st[5]);
       }
-      const char *nm[5] = {"prologue", "-", "-", "chunks", "tests"};
+      const char *nm[5] = {"prologue", "first stage", "other stages", "epilogue", "tests"};
       for (int k = 0; k < 5; ++k) {
         std::sort(ph[k].begin(), ph[k].end());
         if (!ph[k].empty())

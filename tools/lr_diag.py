@@ -24,7 +24,7 @@ def main():
     from gmat_amd import _native as N
     from gmat_amd.remma._scan import EpiPlan
     N.ensure_device()
-    geno, g, pvp, py = bench.build_inputs(args.n_id, args.n_snp, 1, np.array([0.4, 0.2, 0.4]), 0, 1)
+    geno, g, pvp, py = bench.build_inputs(args.n_id, args.n_snp, 1, np.array([0.4, 0.2, 0.4]), 0, 1)[:4]
     plan = EpiPlan(g, pvp, py)
     rows = np.arange(args.n_snp - 1)
     modes = [int(v) for v in args.modes.split(",")]
