@@ -1287,8 +1287,9 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   };
   // Stage operands by LDS-DMA (global_load_lds_dwordx4: lane i's 16 bytes land at M0 + 16 i): the A
   // tile image (NA wave-instructions per image), the j-side S1 planes (waves 4..7: 16 columns x 4
-  // chunks each, physical chunk p of column js holding logical chunk p ^ (js & 3): conflict-free
-  // fragment reads) and the i-side records (waves 0 and 1: 16 slots x 8 chunks).  Lanes whose
+  // chunks each, physical chunk p of column js holding logical chunk p ^ ((js >> 2) & 3): the 16
+  // lanes of a ds_read_b128 group hit 16 distinct 16-byte bank slots) and the i-side records (waves
+  // 0 and 1: 16 slots x 8 chunks).  Lanes whose
   // column or slot is unused read SNP 0 (finite data in accumulators nobody tests).
   auto src_offsets = [&](int tl, int J0t, int J1t, unsigned &oI, unsigned &oJ) __attribute__((always_inline)) {
     oI = oJ = 0;
@@ -1296,7 +1297,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       const int jc = tid - 256, jh = jc >> 7, js = (jc >> 2) & 31, jq = jc & 3;
       const int Jh = jh ? J1t : J0t;
       const int64_t jj = (int64_t)Jh * BJ + js;
-      oJ = (unsigned)(((Jh >= 0 && jj < a.m) ? jj : 0) * nK * NB_REC + (jq ^ (js & 3)) * 16);
+      oJ = (unsigned)(((Jh >= 0 && jj < a.m) ? jj : 0) * nK * NB_REC + (jq ^ ((js >> 2) & 3)) * 16);
     }
     if (w < 2) {
       const int r = a.tile_rows[(int64_t)tl * MX_BI + (tid >> 3)];
@@ -1319,7 +1320,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 
   v16f_ acc[RB][PB];
   const int sw16 = 16 * ((c >> 3) & 1);
-  const int jf = c & 3;
+  const int jf = (c >> 2) & 3;
   const int jrow = (half * BJ + c) * JB;
   // A fragment r of (stage s, half kk): the 6 fp6 dwords + the scale dword of row 32 r + c
   auto afrag = [&](int b, int s, int kk, int r) __attribute__((always_inline)) {
@@ -2436,18 +2437,24 @@ double now() {
 // builder of build_mx, restated): per 32-column block J the flagged band rows in row order, packed
 // into half-tiles of MX_BI/2 rows, consecutive half-tiles (J-major) paired into MX tiles, tile t
 // dealt to entry 8 (t mod C) + t / C (C = ceil(tiles / 8): the 8 XCDs get contiguous chunks),
-// padding entries -1.  Thread (jl, rg) of a 256-thread workgroup: column block 64 b + jl, rows
-// [128 rg, 128 rg + 128).
-constexpr int TL_R = 128;  // band rows per thread (ROWS_PER_LAUNCH / 4)
-__global__ __launch_bounds__(256) void tl_count_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
-                                                       int *__restrict__ cnt4) {
+// padding entries -1.  Thread (jl, rg) of a 1024-thread workgroup: column block 64 b + jl, rows
+// [TL_R rg, TL_R rg + TL_R) (16 row groups: short load chains, 16 waves per column group).
+constexpr int TL_G = 16, TL_R = ROWS_PER_LAUNCH / TL_G;  // row groups, band rows per thread
+__global__ __launch_bounds__(1024) void tl_count_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
+                                                        int *__restrict__ cnt4) {
   const int jl = threadIdx.x & 63, rg = threadIdx.x >> 6, J = blockIdx.x * 64 + jl;
   if (J >= nJ) return;
   int c = 0;
   const int r1 = min(Rn, TL_R * (rg + 1));
 #pragma unroll 16
   for (int r = TL_R * rg; r < r1; ++r) c += flags[(size_t)r * nJ + J] != 0;
-  cnt4[4 * J + rg] = c;
+  cnt4[TL_G * J + rg] = c;
+}
+__device__ __forceinline__ int tl_total(const int *cnt, int J) {
+  int c = 0;
+#pragma unroll
+  for (int g = 0; g < TL_G; ++g) c += cnt[TL_G * J + g];
+  return c;
 }
 // one workgroup: exclusive scan of the half-tile counts over J; info = {halves, tiles, entries}
 __global__ __launch_bounds__(1024) void tl_scan_kernel(const int *__restrict__ cnt4, int nJ, int *__restrict__ H,
@@ -2457,7 +2464,7 @@ __global__ __launch_bounds__(1024) void tl_scan_kernel(const int *__restrict__ c
   const int t = threadIdx.x, per = (nJ + 1023) / 1024, j0 = t * per, j1 = min(nJ, j0 + per);
   int sum = 0;
   for (int J = j0; J < j1; ++J) {
-    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    const int c = tl_total(cnt4, J);
     sum += (c + MX_BI / 2 - 1) / (MX_BI / 2);
   }
   part[t] = sum;
@@ -2471,7 +2478,7 @@ __global__ __launch_bounds__(1024) void tl_scan_kernel(const int *__restrict__ c
   int run = part[t] - sum;
   for (int J = j0; J < j1; ++J) {
     H[J] = run;
-    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    const int c = tl_total(cnt4, J);
     run += (c + MX_BI / 2 - 1) / (MX_BI / 2);
   }
   if (t == 0) {
@@ -2490,7 +2497,7 @@ __global__ __launch_bounds__(1024) void tl_scan_kernel(const int *__restrict__ c
     }
   }
 }
-__global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
+__global__ __launch_bounds__(1024) void tl_fill_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ,
                                                       const int *__restrict__ cnt4, const int *__restrict__ H,
                                                       const int *__restrict__ info, int *__restrict__ mxt,
                                                       int *__restrict__ mxr) {
@@ -2498,7 +2505,7 @@ __global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict_
   if (J >= nJ) return;
   const int C = info[2] / 8, h0 = H[J];
   int idx = 0;
-  for (int g = 0; g < rg; ++g) idx += cnt4[4 * J + g];
+  for (int g = 0; g < rg; ++g) idx += cnt4[TL_G * J + g];
   const int r1 = min(Rn, TL_R * (rg + 1));
 #pragma unroll 16
   for (int r = TL_R * rg; r < r1; ++r)
@@ -2508,7 +2515,7 @@ __global__ __launch_bounds__(256) void tl_fill_kernel(const uint8_t *__restrict_
       ++idx;
     }
   if (rg == 0) {  // the tile entries of J's half-tiles and the empty slots of its last one
-    const int c = cnt4[4 * J] + cnt4[4 * J + 1] + cnt4[4 * J + 2] + cnt4[4 * J + 3];
+    const int c = tl_total(cnt4, J);
     const int nh = (c + MX_BI / 2 - 1) / (MX_BI / 2);
     for (int q = c; q < nh * (MX_BI / 2); ++q) {
       const int k = h0 + q / (MX_BI / 2);
@@ -2574,6 +2581,8 @@ struct gmat_epi {
   int n_slice = 3;
   double qmax = 0, zz = 0, spy = 0;
   double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2
+                                    // (0: not computed yet, ensure_rho)
+  double pmax = 0;                  // max |P|
   double rho_mx = 0;                // the MX screen's bound: ||P_off - E||_2 + fp32 accumulation term
   // spectral prefilter: e'Pe >= pf_mu * (|e|^2 - (1'e)^2 / n) - pf_eps * |e|^2 for every e,
   // certified by a Cholesky factorisation of P + pf_mu (11'/n - I); pf_mu = 0: disabled
@@ -2800,10 +2809,14 @@ bool pair_screen_fits(const gmat_epi *e) { return e->nK <= 63; }
 // 128-deep basis chunk: 4.5x the candidates of rank 384, 0.55x the screen time at the bench
 // configuration); without it the refine of those candidates would dominate.
 int default_lr_rank(const gmat_epi *e) { return pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN") ? 128 : 384; }
+// Survivors are appended to cand2 at counter2: `reset` zeroes the counter first, `n_out` (when given)
+// receives its value after a stream synchronisation; without it the call only enqueues (the scan
+// screens candidate ranges in chunks beside the later launches and reads the total at flush time).
 int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *slp, const int8_t *srp,
-                const int64_t *pi, const int64_t *pj, int64_t np, double chi_cut, int64_t *n_out) {
-  *n_out = 0;
-  if (np <= 0) return GMAT_OK;
+                const int64_t *pi, const int64_t *pj, int64_t np, double chi_cut, int64_t *n_out, bool reset = true) {
+  if (n_out) *n_out = 0;
+  if (np <= 0 && !n_out) return GMAT_OK;
+  if (np <= 0 && reset) return GMAT_OK;
   const int nK = e->nK, pp = nK <= 31 ? 64 : 32;
   GMAT_CHECK(nK <= 63, GMAT_E_ARG, "pair screen: %d stages exceed the LDS", nK);
   GMAT_CHECK(L.U32.p && R.U32.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
@@ -2811,7 +2824,11 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
                  e->cand2_i.bytes >= (size_t)np * 8 && L.U32.bytes >= (size_t)e->m * e->n_pad * 4 &&
                  R.U32.bytes >= (size_t)e->m * e->n_pad * 4 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
              GMAT_E_ARG, "pair screen: plan buffers missing");
-  GMAT_TRY(e->ps_side.alloc((size_t)5 * np * sizeof(double)));
+  // the side-term buffer is sized for the largest call once (calls queued on one stream share it)
+  if (e->ps_side.bytes < (size_t)5 * np * sizeof(double)) {
+    GMAT_HIP(hipStreamSynchronize(st));
+    GMAT_TRY(e->ps_side.alloc((size_t)5 * std::max<int64_t>(np, e->cand_cap) * sizeof(double)));
+  }
   GMAT_TRY(e->pins.count2.reserve(8));
   PairArgs x;
   x.ci = pi;
@@ -2843,7 +2860,8 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   x.counter = e->counter2.as<unsigned long long>();
   x.oi = e->cand2_i.as<int64_t>();
   x.oj = e->cand2_j.as<int64_t>();
-  GMAT_HIP(hipMemsetAsync(e->counter2.p, 0, 8, st));
+  if (reset) GMAT_HIP(hipMemsetAsync(e->counter2.p, 0, 8, st));
+  if (np > 0) {
   hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, x);
   GMAT_HIP(hipGetLastError());
   const size_t lds = 2 * MX_TILE + (size_t)pp * (nK * 64 + 16) + 4 * pp * sizeof(double);
@@ -2860,6 +2878,8 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   else
     hipLaunchKernelGGL(pair_mx_kernel<32>, dim3((unsigned)cdiv(np, 32)), dim3(256), lds, st, x);
   GMAT_HIP(hipGetLastError());
+  }
+  if (!n_out) return GMAT_OK;
   GMAT_HIP(hipMemcpyAsync(e->pins.count2.p, e->counter2.p, 8, hipMemcpyDeviceToHost, st));
   GMAT_HIP(hipStreamSynchronize(st));
   *n_out = (int64_t)*e->pins.count2.as<unsigned long long>();
@@ -3082,6 +3102,45 @@ constexpr uint64_t EPI_STATE_MAGIC = 0x31495045544d4147ULL;  // "GMATEPI1"
 int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes);
 }  // namespace
 
+// ||R^16||_F^(1/16) >= ||R||_2 (R symmetric) from a residual in r1 scaled to entries of order one:
+// four fp64 MFMA squarings (r1, r2 are overwritten)
+static int fro16_root(int64_t n_pad, DBuf &r1, DBuf &r2, DBuf &rrows, double *fro_root) {
+  double *src = r1.as<double>(), *dst = r2.as<double>();
+  for (int q = 0; q < 4; ++q) {
+    GMAT_TRY(dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad));
+    std::swap(src, dst);
+  }
+  GMAT_TRY(dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rrows.as<double>()));
+  std::vector<double> hr(n_pad);
+  GMAT_HIP(hipMemcpy(hr.data(), rrows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost));
+  double fro2 = 0.0;
+  for (double v : hr) fro2 += v;
+  *fro_root = std::pow(std::sqrt(fro2), 1.0 / 16.0);
+  return GMAT_OK;
+}
+
+// rho[S], the int8 screen's bound ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2 for S slices, computed
+// when a scan first uses that level (the low-rank and MX levels never do): the residual of the
+// slicing of P in storage order (a symmetric permutation of the natural one: same spectrum)
+static int ensure_rho(gmat_epi *e, int S) {
+  if (S < 1 || S > e->n_slice || e->rho[S] > 0.0) return GMAT_OK;
+  const int64_t n_pad = e->n_pad;
+  DBuf r1, r2, rrows;
+  GMAT_TRY(r1.alloc(n_pad * n_pad * sizeof(double)));
+  GMAT_TRY(r2.alloc(n_pad * n_pad * sizeof(double)));
+  GMAT_TRY(rrows.alloc(n_pad * sizeof(double)));
+  const double unit = e->qmax > 0 ? 127.0 / e->qmax : 1.0;
+  const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
+  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)cdiv(n_pad * n_pad, 256)), dim3(256), 0, 0, n_pad, n_pad,
+                     e->Ps.as<double>(), unit, S, 1.0 / 64.0, r1.as<double>());  // residual in [-64, 64] units
+  GMAT_HIP(hipGetLastError());
+  double fr;
+  GMAT_TRY(fro16_root(n_pad, r1, r2, rrows, &fr));
+  // 5% margin for the fp64 rounding of the squarings, plus the rounding of P*unit itself
+  e->rho[S] = 1.05 * rmax * fr + 1e-15 * e->pmax * (double)e->n;
+  return GMAT_OK;
+}
+
 static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
                            const uint8_t *state, int64_t state_bytes) {
   GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
@@ -3098,18 +3157,36 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   e->n_slice = n_slice;
   e->nK = (int)(g->n_pad / MXK);
   const int64_t n = e->n, n_pad = e->n_pad;
-  double pmax = 0.0, qmax = 0.0;  // max |P|, max |P_kl| off the diagonal
-  uint64_t ph = 0x9e3779b97f4a7c15ULL ^ (uint64_t)n;
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = 0; k < n; ++k) {
-      const double v = std::fabs(pvp[i * n + k]);
-      pmax = std::max(pmax, v);
-      if (k != i) qmax = std::max(qmax, v);
+  // max |P|, max |P_kl| off the diagonal (contiguous row pieces: vectorised) and the fingerprint of
+  // P as 8 interleaved hash lanes (independent multiply chains; one chain ran 11 ms at n = 2,000)
+  double pmax = 0.0, qmax = 0.0, dmax = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double *row = pvp + i * n;
+    double q = 0.0;
+    for (int64_t k = 0; k < i; ++k) q = std::max(q, std::fabs(row[k]));
+    for (int64_t k = i + 1; k < n; ++k) q = std::max(q, std::fabs(row[k]));
+    qmax = std::max(qmax, q);
+    dmax = std::max(dmax, std::fabs(row[i]));
+  }
+  pmax = std::max(qmax, dmax);
+  uint64_t hl[8];
+  for (int l = 0; l < 8; ++l) hl[l] = (0x9e3779b97f4a7c15ULL ^ (uint64_t)n) + 0x632be59bd9b4e019ULL * (uint64_t)l;
+  const int64_t nn = n * n, n8 = nn / 8 * 8;
+  for (int64_t k = 0; k < n8; k += 8)
+    for (int l = 0; l < 8; ++l) {
       uint64_t b;
-      memcpy(&b, &pvp[i * n + k], 8);
-      ph = (ph ^ b) * 0x100000001b3ULL;
-      ph ^= ph >> 29;
+      memcpy(&b, &pvp[k + l], 8);
+      hl[l] = (hl[l] ^ b) * 0x100000001b3ULL;
+      hl[l] ^= hl[l] >> 29;
     }
+  for (int64_t k = n8; k < nn; ++k) {
+    uint64_t b;
+    memcpy(&b, &pvp[k], 8);
+    hl[0] = (hl[0] ^ b) * 0x100000001b3ULL;
+    hl[0] ^= hl[0] >> 29;
+  }
+  uint64_t ph = 0;
+  for (int l = 0; l < 8; ++l) ph = (ph ^ hl[l]) * 0x100000001b3ULL ^ (ph >> 31);
   e->qmax = qmax;
   e->p_hash = ph;
   double spy = 0.0;
@@ -3146,36 +3223,12 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
     set_error("gmat_epi_create: setup kernels failed");
     return fail(GMAT_E_HIP);
   }
-  // ||R||_2 <= ||R^16||_F^(1/16) (R symmetric): four fp64 MFMA squarings of R scaled to
-  // unit max entry (|R_kl| <= 0.5 * 128^-(S-1) / unit), for every usable slice count S
-  // ||R^16||_F from a residual already scaled to entries of order one (four fp64 squarings)
+  // the int8 levels' bounds rho[S] are computed on first use (ensure_rho)
+  e->pmax = pmax;
   DBuf r1, r2, rrows;
   if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
       (rc = rrows.alloc(n_pad * sizeof(double))))
     return fail(rc);
-  auto fro16 = [&](double *fro_root) -> int {
-    double *src = r1.as<double>(), *dst = r2.as<double>();
-    for (int q = 0; q < 4; ++q) {
-      GMAT_TRY(dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad));
-      std::swap(src, dst);
-    }
-    GMAT_TRY(dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rrows.as<double>()));
-    std::vector<double> hr(n_pad);
-    GMAT_HIP(hipMemcpy(hr.data(), rrows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost));
-    double fro2 = 0.0;
-    for (double v : hr) fro2 += v;
-    *fro_root = std::pow(std::sqrt(fro2), 1.0 / 16.0);
-    return GMAT_OK;
-  };
-  for (int S = 1; S <= n_slice; ++S) {
-    const double rmax = 0.5 * std::pow(128.0, -(S - 1)) / unit;
-    hipLaunchKernelGGL(residual_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, S,
-                       1.0 / 64.0, r1.as<double>());  // final residual in [-64, 64] scaled units
-    double fr;
-    if ((rc = fro16(&fr))) return fail(rc);
-    // 5% margin for the fp64 rounding of the squarings, plus the rounding of P*unit itself
-    e->rho[S] = 1.05 * rmax * fr + 1e-15 * pmax * (double)n;
-  }
   // MX screen: fp6 records + scales, the residual of the matrix it evaluates, and the fp32
   // accumulation bound: every acc_k is a sum of at most n_pad products (each exact in fp32)
   // accumulated with at most one rounding per product (x2 margin for the MFMA's internal
@@ -3196,7 +3249,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
       return fail(GMAT_E_HIP);
     }
     double fr;
-    if ((rc = fro16(&fr))) return fail(rc);
+    if ((rc = fro16_root(n_pad, r1, r2, rrows, &fr))) return fail(rc);
     std::vector<double> ha(n_pad);
     if (hipMemcpy(ha.data(), rabs.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
       set_error("gmat_epi_create: MX row sums download failed");
@@ -3576,7 +3629,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const bool dev_tiles = use_lr && !use_stage2 && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
   DBuf tl_cnt, tl_h, tl_info;
   if (dev_tiles) {
-    GMAT_TRY(tl_cnt.alloc((size_t)4 * nJ * sizeof(int)));
+    GMAT_TRY(tl_cnt.alloc((size_t)TL_G * nJ * sizeof(int)));
     GMAT_TRY(tl_h.alloc((size_t)nJ * sizeof(int)));
     GMAT_TRY(tl_info.alloc(2 * 4 * sizeof(int)));
   }
@@ -3659,13 +3712,19 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const hipStream_t S3 = e->s3;
   double n_refined = 0;
   // pair screen (use_ps) and exact refine of candidates [0, count) on S3
+  // pair screen of the candidates [ps_done, ...) already queued on S3 beside the screens (chunks of
+  // GMAT_PS_CHUNK, default 65,536 candidates); the flush screens the rest and reads the survivors
+  int64_t ps_done = 0;
+  const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 65536;
   auto enqueue_refine = [&](int64_t count, const int64_t **fi, const int64_t **fj, int64_t *nf) -> int {
     *fi = e->cand_i.as<int64_t>();
     *fj = e->cand_j.as<int64_t>();
     *nf = count;
     GMAT_HIP(hipEventRecord(ev[3], S3));
     if (use_ps) {
-      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, *fi, *fj, count, chi_cut, nf));
+      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, *fi + ps_done, *fj + ps_done, count - ps_done, chi_cut, nf,
+                           ps_done == 0));
+      ps_done = 0;
       *fi = e->cand2_i.as<int64_t>();
       *fj = e->cand2_j.as<int64_t>();
     }
@@ -3886,11 +3945,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
         if (dev_tiles) {
           const unsigned gj = (unsigned)cdiv(nJ, 64);
           int *info = tl_info.as<int>() + 4 * b;
-          hipLaunchKernelGGL(tl_count_kernel, dim3(gj), dim3(256), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+          hipLaunchKernelGGL(tl_count_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
                              tl_cnt.as<int>());
           hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, S2, tl_cnt.as<int>(), (int)nJ, tl_h.as<int>(), info,
                              mxt[b].as<int>(), mxr[b].as<int>());
-          hipLaunchKernelGGL(tl_fill_kernel, dim3(gj), dim3(256), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+          hipLaunchKernelGGL(tl_fill_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
                              tl_cnt.as<int>(), tl_h.as<int>(), info, mxt[b].as<int>(), mxr[b].as<int>());
           GMAT_HIP(hipGetLastError());
           GMAT_TRY(pin_flags[b].reserve(16));
@@ -4210,7 +4269,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
   const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
   // tile entries per workgroup (GMAT_LR_TPW): the grid strides over the entries in multiples of 8
-  const int lr_tpw = getenv("GMAT_LR_TPW") ? std::max(1, atoi(getenv("GMAT_LR_TPW"))) : 2;
+  const int lr_tpw = getenv("GMAT_LR_TPW") ? std::max(1, atoi(getenv("GMAT_LR_TPW"))) : 1;
   auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, LrArgs lx_) {
     lx_.n_tiles = (int)g;
     unsigned grid = (unsigned)cdiv((int64_t)g, lr_tpw);
@@ -4280,6 +4339,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     for (int attempt = 0;; ++attempt) {
       sa.n_slice = S;
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
+      if (S > 0) GMAT_TRY(ensure_rho(e, S));
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
       const bool two_stage = S == 0 && use_lr && use_stage2;
       if (queued[li] && S == 0) {  // queued behind the previous launch
@@ -4379,6 +4439,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
     const bool async_s2 = S == 0 && use_stage2;  // the main counter belongs to stage 2 on S3
     if (!async_s2) pending = (int64_t)count;
+    if (use_ps && !use_stage2 && ps_chunk > 0 && pending - ps_done >= ps_chunk) {
+      // the screen of this launch has finished (its count was read): screen its candidates now
+      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, e->cand_i.as<int64_t>() + ps_done, e->cand_j.as<int64_t>() + ps_done,
+                           pending - ps_done, chi_cut, nullptr, ps_done == 0));
+      ps_done = pending;
+    }
     if (stamps_on && li == 5 && S == 0 && use_lr) {  // per-workgroup phase durations (diagnostics)
       const size_t g = mx_tiles.size() / MX_TE;
       std::vector<unsigned long long> hs(6 * g);

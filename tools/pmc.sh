@@ -16,7 +16,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   if [ "$PASSES" != "all" ] && ! echo " $PASSES " | grep -q " $i "; then continue; fi
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $RAW/p$i -o run -- python3 $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --kernel-include-regex "${KEY}" --output-format csv -d $RAW/p$i -o run -- python3 $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   mkdir -p $OUT/p$i
   for f in run_counter_collection.csv run_kernel_trace.csv; do
     src=$(find $RAW/p$i -name $f | head -1)
