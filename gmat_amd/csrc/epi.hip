@@ -1256,15 +1256,16 @@ __device__ __forceinline__ void lr_test(const ScreenArgs &a, const LrArgs &x, co
 //    whose wait (a counted vmcnt: VMEM operations retire in order) lets them land during the last
 //    stage.  Every wait is one asm statement with the barrier (vm_wait_barrier): the compiler does
 //    not know that the DMA asm writes LDS.
-template <int SK>
+// NSL LDS stage slots (a ring): stage g + NSL - 1 is loaded while stage g multiplies.
+template <int SK, int NSL>
 __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs a, LrArgs x) {
   constexpr int PB = MxShape<1>::PB, RB = MX_RB, MX_T = MxShape<1>::T, NA = MX_TILE / 16 / MX_T;
   // j side: only the S1 plane (first 64 bytes of a record: b as fp4 codes) is staged, S2 = S1 << 1
   constexpr int JB = NB_REC / 2, SI = MX_BI * NB_REC, SJ = 2 * BJ * JB;
   static_assert(PB == 2, "one slot per lane half");
-  __shared__ __attribute__((aligned(16))) uint8_t sA[2][SK * MX_TILE];
-  __shared__ __attribute__((aligned(16))) uint8_t sI[2][SK * SI];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[2][SK * SJ];
+  __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][SK * MX_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[NSL][SK * SI];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[NSL][SK * SJ];
   __shared__ __attribute__((aligned(16))) uint8_t sE[40 * 1024];    // chunk epilogue operands
   __shared__ __attribute__((aligned(16))) uint8_t sT[LR_ST_BYTES];  // test operands
   // per-lane DMA source offsets parked in LDS (registers are the loop's): [tile parity][thread] the
@@ -1443,15 +1444,42 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
   };
 
+  constexpr int LA = NSL - 1;  // stages in flight beyond the one being multiplied
+  const int P = nC * nS;        // stages per tile
   int tl = a.tiles[MX_TE * e], J0t = a.tiles[MX_TE * e + 1], J1t = a.tiles[MX_TE * e + 2];
   {
     unsigned oI, oJ;
     src_offsets(tl, J0t, J1t, oI, oJ);
     sO[0][tid] = w < 2 ? oI : oJ;
-    stamp(e, 0);
-    load(0, 0, 0, oI, oJ);
   }
-  int b = 0, par = 0;
+  stamp(e, 0);
+  // Vector-memory bookkeeping (wave-uniform): `issued` counts this wave's DMAs; at the start of stage
+  // g, mk[k] (k < LA - 1) is its value right after the loads of stage g + 1 + k (the stages in flight,
+  // oldest first); the stage appends stage g + LA's mark, and waiting for stage g + 1 is
+  // vmcnt(issued - mk[0]) (VMEM operations retire in order).
+  int issued = 0, mk[LA];
+  int g = 0;  // this workgroup's stage counter: stage g lives in slot g % NSL
+  // the stage q positions ahead of the tile start (chunk, stage of the tile, or of the next tile)
+  auto issue = [&](int q, int slot, int pr, int en_) __attribute__((always_inline)) {
+    if (q < P) {
+      const unsigned o = sO[pr][tid];
+      load(slot, q / nS, q % nS, o, o);
+      issued += NL;
+    } else if (en_ >= 0) {
+      const unsigned o = sO[pr ^ 1][tid];
+      load(slot, 0, q - P, o, o);
+      issued += NL;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < LA; ++q) {
+    issue(q, q, 0, -1);
+    mk[q] = issued;
+  }
+  vm_wait_barrier(issued - mk[0]);  // stage 0 of the first tile
+#pragma unroll
+  for (int q = 0; q + 1 < LA; ++q) mk[q] = mk[q + 1];
+  int par = 0;
   for (;;) {
     // this tile's slots (wave-uniform: slots 2w, 2w + 1) and the next entry's stage sources
     const int *trow = a.tile_rows + (int64_t)tl * MX_BI;
@@ -1471,47 +1499,40 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       const int r = trow[lane >> 2];
       sRo[par][lane] = (unsigned)((r >= 0 ? a.rows[r] : 0) * LR_REC + 2 * (lane & 3));
     }
-    vm_wait_barrier(0);  // the tile's first stage (and every wave is past the last tile's test)
+    // (the tile's first stage was waited for by the previous stage or the prologue)
     stamp(e, 1);
     double lowrank[PB] = {0.0, 0.0};
     for (int ch = 0; ch < nC; ++ch) {
-      const bool lastch = ch + 1 == nC;
-      if (ch > 0) __syncthreads();  // every wave is past the last chunk's epilogue reads of sE
-      // the DMAs after a stage's MFMAs: its successor, or the first stage of the next chunk / tile
-      auto load_after = [&](int cs2) __attribute__((always_inline)) {
-        if (cs2 + 1 < nS) {
-          const unsigned o = sO[par][tid];
-          load(b ^ 1, ch, cs2 + 1, o, o);
-        } else if (!lastch || en >= 0) {
-          const unsigned o = sO[lastch ? par ^ 1 : par][tid];
-          load(b ^ 1, lastch ? 0 : ch + 1, 0, o, o);
+      // one stage at tile position p: load the stage LA ahead (possibly of the next tile), the
+      // epilogue (and with the first chunk the test) operands after it with the chunk's first stage,
+      // multiply, then wait for the next stage (the younger DMAs stay in flight)
+      auto stage = [&](int cs2, bool first) __attribute__((always_inline)) {
+        const int p = ch * nS + cs2;
+        issue(p + LA, (g + LA) % NSL, par, en);
+        mk[LA - 1] = issued;
+        if (first) {
+          fetch_epi(ch, J0t, J1t, i0, i1);
+          issued += 5;
+          if (ch == 0) {
+            fetch_test(J0t, J1t, h ? r1 : r0, w == 0 ? sRo[par][lane] : 0u);
+            issued += SIDE_T + 4 + (w <= 4 ? 1 : 0);
+          }
         }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(g % NSL, first);
+        const bool more = p + 1 < P || en >= 0;
+        vm_wait_barrier(more ? issued - mk[0] : 0);
+#pragma unroll
+        for (int q = 0; q + 1 < LA; ++q) mk[q] = mk[q + 1];
+        ++g;
       };
-      // first stage (peeled): its load, then the epilogue (and with the first chunk the test)
-      // operands as the youngest DMAs, so its wait leaves them in flight over the next stage; the
-      // fetch code stays out of the stage loop, whose accumulators need every register
-      load_after(0);
-      fetch_epi(ch, J0t, J1t, i0, i1);
-      int nf = 5;
-      if (ch == 0) {
-        fetch_test(J0t, J1t, h ? r1 : r0, w == 0 ? sRo[par][lane] : 0u);
-        nf += SIDE_T + 4 + (w <= 4 ? 1 : 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      compute(b, true);
-      vm_wait_barrier(nS > 1 ? nf : 0);
-      b ^= 1;
+      stage(0, true);
       if (ch == 0) stamp(e, 2);
 #pragma unroll 1
-      for (int cs2 = 1; cs2 < nS; ++cs2) {
-        load_after(cs2);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(b, false);
-        vm_wait_barrier(0);
-        b ^= 1;
-      }
+      for (int cs2 = 1; cs2 < nS; ++cs2) stage(cs2, false);
       stamp(e, 3);
       epilogue(lowrank);
+      __syncthreads();  // every wave is past the epilogue's reads of sE before the next fetch
     }
     stamp(e, 4);
     // lane half h tests slot PB w + h of column c (both halves hold the sums after the exchange)
@@ -1526,6 +1547,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     }
     stamp(e, 5);
     if (en < 0) break;
+    __syncthreads();  // every wave is past the test's reads of sT before the next tile's fetch
     e = en;
     tl = tln;
     J0t = J0n;
@@ -4269,15 +4291,21 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
   const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
   // tile entries per workgroup (GMAT_LR_TPW): the grid strides over the entries in multiples of 8
+  // GMAT_LR_RING=1: a four-slot ring of 128-deep stages (three in flight) instead of the double
+  // buffer of 256-deep stages; measured 63.1 vs 58.5 ms per step (the ring's bookkeeping spills
+  // SGPRs: 6.6 instead of 2.9 SALU instructions per MFMA), so off by default
+  const bool lr_ring = e->nK >= 4 && getenv("GMAT_LR_RING") && atoi(getenv("GMAT_LR_RING")) == 1;
   const int lr_tpw = getenv("GMAT_LR_TPW") ? std::max(1, atoi(getenv("GMAT_LR_TPW"))) : 1;
   auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, LrArgs lx_) {
     lx_.n_tiles = (int)g;
     unsigned grid = (unsigned)cdiv((int64_t)g, lr_tpw);
     grid = std::min<unsigned>((unsigned)cdiv(grid, 8) * 8, g);
-    if (lr_sk == 2)
-      hipLaunchKernelGGL(lr_screen_kernel<2>, dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    if (lr_ring)
+      hipLaunchKernelGGL((lr_screen_kernel<1, 4>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    else if (lr_sk == 2)
+      hipLaunchKernelGGL((lr_screen_kernel<2, 2>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
     else
-      hipLaunchKernelGGL(lr_screen_kernel<1>, dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+      hipLaunchKernelGGL((lr_screen_kernel<1, 2>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
   };
 
   auto lr_args = [&](size_t li) {
