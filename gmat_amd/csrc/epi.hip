@@ -1414,34 +1414,40 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   };
   // sum of c~_r^2 over the chunk's rows: c~ = acc - beta G' - alpha H, two rows per v_pk_fma_f32
   const int hrow = half * BJ + c;
+  // (r, q) outer: one H chunk per (r, q) serves both slots; the reads of a row tile are issued
+  // together (no scheduling barrier: the epilogue is latency-, not register-bound)
   auto epilogue = [&](double *lowrank) __attribute__((always_inline)) {
     const float be = (float)((const double *)(sT + LR_OFF_RR))[hrow * LR_REC];
     const v2f_ nbe = {-be, -be};
+    v2f_ nal[PB], s2[PB];
 #pragma unroll
     for (int t = 0; t < PB; ++t) {
       const float al = (float)((const double *)(sT + LR_OFF_RL))[(PB * w + t) * LR_REC];
-      const v2f_ nal = {-al, -al};
-      v2f_ s2 = {0.f, 0.f};
+      nal[t] = v2f_{-al, -al};
+      s2[t] = v2f_{0.f, 0.f};
+    }
 #pragma unroll
-      for (int r = 0; r < RB; ++r) {
+    for (int r = 0; r < RB; ++r) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = 8 * r + 2 * q + h;  // logical 16-byte chunk of the chunk's 128 rows
+      for (int q = 0; q < 4; ++q) {
+        const int k = 8 * r + 2 * q + h;  // logical 16-byte chunk of the chunk's 128 rows
+        const float4 hh = *(const float4 *)&sE[8192 + hrow * 512 + 16 * (k ^ (hrow & 15))];
+#pragma unroll
+        for (int t = 0; t < PB; ++t) {
           const float4 g = *(const float4 *)&sE[(PB * w + t) * 512 + 16 * k];
-          const float4 hh = *(const float4 *)&sE[8192 + hrow * 512 + 16 * (k ^ (hrow & 15))];
 #pragma unroll
           for (int u = 0; u < 4; u += 2) {
             const v2f_ av = {acc[r][t][4 * q + u], acc[r][t][4 * q + u + 1]};
             const v2f_ gv = {u ? g.z : g.x, u ? g.w : g.y}, hv = {u ? hh.z : hh.x, u ? hh.w : hh.y};
             v2f_ cr = __builtin_elementwise_fma(nbe, gv, av);
-            cr = __builtin_elementwise_fma(nal, hv, cr);
-            s2 = __builtin_elementwise_fma(cr, cr, s2);
+            cr = __builtin_elementwise_fma(nal[t], hv, cr);
+            s2[t] = __builtin_elementwise_fma(cr, cr, s2[t]);
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
-      lowrank[t] += (double)s2[0] + (double)s2[1];
     }
+#pragma unroll
+    for (int t = 0; t < PB; ++t) lowrank[t] += (double)s2[t][0] + (double)s2[t][1];
   };
 
   constexpr int LA = NSL - 1;  // stages in flight beyond the one being multiplied
