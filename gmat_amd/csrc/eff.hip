@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 
 #include "dla.h"
 #include "geno.h"
@@ -187,6 +188,24 @@ __global__ __launch_bounds__(256, 2) void eff_screen_kernel(EffArgs x) {
   for (int p = 0; p < NR; ++p)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[p][e] = 0;
+  // per-row epilogue operands staged in LDS while the K loop runs (the candidate stores would
+  // otherwise force a reload of every operand per element): [o][r] scale, centring, c3 . py, and
+  // the row's SNP index and frequency class
+  __shared__ double eR[NO][3][ET];
+  __shared__ int64_t eI[ET];
+  __shared__ int64_t eF[ET];
+  if (tid < ET) {
+    const int r = min(r0 + tid, (int)x.n_rows - 1);
+    const int64_t i = x.rows[r];
+    eI[tid] = i;
+    eF[tid] = x.fi ? x.fi[i] : 0;
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      eR[o][0][tid] = (o ? x.sc2 : x.sc1)[r];
+      eR[o][1][tid] = (o ? x.cen2 : x.cen1)[i];
+      eR[o][2][tid] = (o ? x.u2 : x.u1)[i];
+    }
+  }
   v4i rv[NR], cv[NC];
   auto load = [&](int64_t k0) __attribute__((always_inline)) {
 #pragma unroll
@@ -226,24 +245,32 @@ __global__ __launch_bounds__(256, 2) void eff_screen_kernel(EffArgs x) {
   const int64_t j = c0 + 32 * wc + c;
   if (j >= x.m) return;
   constexpr double rem = (ES == 1 ? 0.5 : ES == 2 ? 0.5 / 128.0 : 0.5 / 16384.0) * (1.0 + 1e-9);
+  // per-column operands in registers (the lane's column is fixed)
+  double cbe[NO], cv3[NO], ccs[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    cbe[o] = (o ? x.cenc2 : x.cenc1)[j];
+    cv3[o] = (o ? x.v2 : x.v1)[j];
+    ccs[o] = (o ? x.cs2 : x.cs1)[j];
+  }
+  const int64_t fjj = x.fi ? x.fj[j] : 0;
+  const double cut0 = x.cut[0];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
     if (r >= x.n_rows) continue;
-    const int64_t i = x.rows[r];
+    const int64_t i = eI[rl];
     if (j <= i) continue;
-    const double cut = x.fi ? x.cut[x.fi[i] * 10 + x.fj[j]] : x.cut[0];
+    const double cut = x.fi ? x.cut[eF[rl] * 10 + fjj] : cut0;
 #pragma unroll
     for (int o = 0; o < NO; ++o) {
-      const double *sc = o ? x.sc2 : x.sc1;
       double t = 0.0;
 #pragma unroll
       for (int q = ES - 1; q >= 0; --q) t = t * (1.0 / 128.0) + (double)acc[o * ES + q][e];
-      const double s = sc[r], al = (o ? x.cen2 : x.cen1)[i], be = (o ? x.cenc2 : x.cenc1)[j];
-      const double T = s * t, t2 = 3.0 * be * (o ? x.u2 : x.u1)[i], t3 = 3.0 * al * (o ? x.v2 : x.v1)[j],
-                   t4 = 9.0 * al * be * x.spy;
+      const double s = eR[o][0][rl], al = eR[o][1][rl], be = cbe[o];
+      const double T = s * t, t2 = 3.0 * be * eR[o][2][rl], t3 = 3.0 * al * cv3[o], t4 = 9.0 * al * be * x.spy;
       const double eff = (T - t2 - t3 + t4) / 9.0;
-      const double bnd = (rem * s * (o ? x.cs2 : x.cs1)[j] + 1e-9 * (fabs(T) + fabs(t2) + fabs(t3) + fabs(t4))) / 9.0;
+      const double bnd = (rem * s * ccs[o] + 1e-9 * (fabs(T) + fabs(t2) + fabs(t3) + fabs(t4))) / 9.0;
       if (fabs(eff) + bnd >= cut * (1.0 - 1e-12)) {
         const unsigned long long k = atomicAdd(x.counter, 1ULL);
         if ((int64_t)k < x.cap) x.cand[k] = ((int64_t)r << 32) | ((int64_t)j << 1) | o;
@@ -268,10 +295,25 @@ __global__ void eff_exact_kernel(int kind, int64_t count, const int64_t *cand, c
   const bool right_dom = kind == GMAT_DD || (kind == GMAT_AD && o == 0);
   const int8_t *pi = (left_dom ? cd : ca) + i * n_pad, *pj = (right_dom ? cd : ca) + j * n_pad;
   const double ci = left_dom ? c_dom[i] : c_add[i], cj = right_dom ? c_dom[j] : c_add[j];
+  // x = v - centre takes one of four values per SNP (c3 = 3v in {0, 1, 3, 6}): each is the same
+  // correctly rounded __dsub_rn((double)c3 / 3.0, centre) the loop computed per individual, so the
+  // sum below is bit-identical; the codes are read 16 per load (rows are 16-byte aligned)
+  const double i0 = __dsub_rn(0.0, ci), i1 = __dsub_rn(1.0 / 3.0, ci), i3 = __dsub_rn(1.0, ci), i6 = __dsub_rn(2.0, ci);
+  const double j0 = __dsub_rn(0.0, cj), j1 = __dsub_rn(1.0 / 3.0, cj), j3 = __dsub_rn(1.0, cj), j6 = __dsub_rn(2.0, cj);
+  auto xv = [](int c3, double v0, double v1, double v3, double v6) __attribute__((always_inline)) {
+    return c3 == 0 ? v0 : c3 == 1 ? v1 : c3 == 3 ? v3 : v6;
+  };
   double e = 0.0;
-  for (int64_t k = 0; k < n; ++k) {
-    const double xi = __dsub_rn((double)pi[k] / 3.0, ci), xj = __dsub_rn((double)pj[k] / 3.0, cj);
-    e = __dadd_rn(e, __dmul_rn(__dmul_rn(xi, xj), py[k]));
+  for (int64_t k0 = 0; k0 < n; k0 += 16) {
+    const v4i a4 = *(const v4i *)(pi + k0), b4 = *(const v4i *)(pj + k0);
+    const int kn = (int)min((int64_t)16, n - k0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (q >= kn) break;
+      const int ca3 = (int)(int8_t)(a4[q >> 2] >> (8 * (q & 3))), cb3 = (int)(int8_t)(b4[q >> 2] >> (8 * (q & 3)));
+      const double xi = xv(ca3, i0, i1, i3, i6), xj = xv(cb3, j0, j1, j3, j6);
+      e = __dadd_rn(e, __dmul_rn(__dmul_rn(xi, xj), py[k0 + q]));
+    }
   }
   const double c = fi ? cut[fi[i] * 10 + fj[j]] : cut[0];
   eff[t] = e;
@@ -380,7 +422,9 @@ extern "C" int gmat_eff_scan(gmat_geno *g, int kind, const double *py, const int
   // orientation 0: (row coding, column coding) = AA (A, A), DD (D, D), AD (A, D); AD orientation 1 = (D, A)
   const bool r0dom = kind == GMAT_DD, c0dom = kind != GMAT_AA;
   const int NO = kind == GMAT_AD ? 2 : 1;
-  const int64_t RL = 512;  // listed rows per launch
+  // listed rows per launch (GMAT_EFF_RL): large launches keep the GPU full as j > i shrinks the
+  // column range of the later ones, and cost fewer host round trips
+  const int64_t RL = getenv("GMAT_EFF_RL") ? std::max<int64_t>(64, atoll(getenv("GMAT_EFF_RL"))) : 2048;
   DBuf drows, img, sc, cnt, cand, deff, dkeep;
   GMAT_TRY(drows.alloc(RL * sizeof(int64_t)));
   GMAT_TRY(img.alloc((size_t)NO * ES * RL * n_pad));
