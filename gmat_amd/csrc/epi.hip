@@ -3132,13 +3132,16 @@ int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes);
 
 // ||R^16||_F^(1/16) >= ||R||_2 (R symmetric) from a residual in r1 scaled to entries of order one:
 // four fp64 MFMA squarings (r1, r2 are overwritten)
-static int fro16_root(int64_t n_pad, DBuf &r1, DBuf &r2, DBuf &rrows, double *fro_root) {
+// the device part on stream st (row sums of squares of R^16 land in rrows)
+static int fro16_enqueue(hipStream_t st, int64_t n_pad, DBuf &r1, DBuf &r2, DBuf &rrows) {
   double *src = r1.as<double>(), *dst = r2.as<double>();
   for (int q = 0; q < 4; ++q) {
-    GMAT_TRY(dgemm(0, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad));
+    GMAT_TRY(dgemm(st, n_pad, n_pad, n_pad, 1.0, DView{src, n_pad, 0}, DView{src, n_pad, 0}, 0.0, dst, n_pad));
     std::swap(src, dst);
   }
-  GMAT_TRY(dot_rows(0, n_pad, n_pad, src, n_pad, src, n_pad, rrows.as<double>()));
+  return dot_rows(st, n_pad, n_pad, src, n_pad, src, n_pad, rrows.as<double>());
+}
+static int fro16_finish(int64_t n_pad, DBuf &rrows, double *fro_root) {
   std::vector<double> hr(n_pad);
   GMAT_HIP(hipMemcpy(hr.data(), rrows.p, n_pad * sizeof(double), hipMemcpyDeviceToHost));
   double fro2 = 0.0;
@@ -3163,7 +3166,8 @@ static int ensure_rho(gmat_epi *e, int S) {
                      e->Ps.as<double>(), unit, S, 1.0 / 64.0, r1.as<double>());  // residual in [-64, 64] units
   GMAT_HIP(hipGetLastError());
   double fr;
-  GMAT_TRY(fro16_root(n_pad, r1, r2, rrows, &fr));
+  GMAT_TRY(fro16_enqueue(0, n_pad, r1, r2, rrows));
+  GMAT_TRY(fro16_finish(n_pad, rrows, &fr));
   // 5% margin for the fp64 rounding of the squarings, plus the rounding of P*unit itself
   e->rho[S] = 1.05 * rmax * fr + 1e-15 * e->pmax * (double)e->n;
   return GMAT_OK;
@@ -3223,6 +3227,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   DBuf dp, dv;
   int rc = GMAT_OK;
   auto fail = [&](int code) {
+    (void)hipDeviceSynchronize();  // nothing in flight (the MX bound's stream) still uses the plan
     delete e;
     return code;
   };
@@ -3262,33 +3267,49 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   // accumulated with at most one rounding per product (x2 margin for the MFMA's internal
   // order), the epilogue adds 32 roundings; all are bounded by u * w'|E|w <= u * max_k
   // sum_l |E_kl| * |w|^2 (|E| symmetric non-negative).
-  {
-    DBuf qn, rabs;
-    if ((rc = e->mx_tiles.alloc((size_t)e->nK * e->nK * MX_TILE)) || (rc = qn.alloc(n_pad * n_pad * sizeof(double))) ||
-        (rc = rabs.alloc(n_pad * sizeof(double))))
-      return fail(rc);
-    hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)cdiv(n_pad * (n_pad / 32), 256)), dim3(256), 0, 0, n, n_pad,
-                       e->nK, dp.as<double>(), e->mx_tiles.as<uint32_t>(), qn.as<double>());
-    const double os = qmax > 0 ? 15.0 / qmax : 1.0;
-    hipLaunchKernelGGL(mx_residual_kernel, dim3((unsigned)n_pad), dim3(256), 0, 0, n, n_pad, dp.as<double>(),
-                       qn.as<double>(), os, r1.as<double>(), rabs.as<double>());
-    if (hipGetLastError() != hipSuccess) {
-      set_error("gmat_epi_create: MX setup kernels failed");
-      return fail(GMAT_E_HIP);
+  // The bound's four fp64 squarings run on a stream of their own beside the eigendecomposition
+  // below (rocSOLVER's dsytrd leaves most CUs idle); rho_mx is finished after it.
+  DBuf qn, rabs;
+  if ((rc = e->mx_tiles.alloc((size_t)e->nK * e->nK * MX_TILE)) || (rc = qn.alloc(n_pad * n_pad * sizeof(double))) ||
+      (rc = rabs.alloc(n_pad * sizeof(double))))
+    return fail(rc);
+  hipStream_t sx = nullptr;
+  if (hipStreamCreateWithFlags(&sx, hipStreamNonBlocking) != hipSuccess) {
+    set_error("gmat_epi_create: stream creation failed");
+    return fail(GMAT_E_HIP);
+  }
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() {
+      if (s) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+      }
     }
+  } sx_guard{sx};
+  (void)hipDeviceSynchronize();  // P, the slices and z / dg are ready for both streams
+  const double os = qmax > 0 ? 15.0 / qmax : 1.0;
+  hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)cdiv(n_pad * (n_pad / 32), 256)), dim3(256), 0, sx, n, n_pad,
+                     e->nK, dp.as<double>(), e->mx_tiles.as<uint32_t>(), qn.as<double>());
+  hipLaunchKernelGGL(mx_residual_kernel, dim3((unsigned)n_pad), dim3(256), 0, sx, n, n_pad, dp.as<double>(),
+                     qn.as<double>(), os, r1.as<double>(), rabs.as<double>());
+  if (hipGetLastError() != hipSuccess) {
+    set_error("gmat_epi_create: MX setup kernels failed");
+    return fail(GMAT_E_HIP);
+  }
+  if ((rc = fro16_enqueue(sx, n_pad, r1, r2, rrows))) return fail(rc);
+  auto finish_mx = [&]() -> int {
+    GMAT_HIP(hipStreamSynchronize(sx));
     double fr;
-    if ((rc = fro16_root(n_pad, r1, r2, rrows, &fr))) return fail(rc);
+    GMAT_TRY(fro16_finish(n_pad, rrows, &fr));
     std::vector<double> ha(n_pad);
-    if (hipMemcpy(ha.data(), rabs.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
-      set_error("gmat_epi_create: MX row sums download failed");
-      return fail(GMAT_E_HIP);
-    }
+    GMAT_HIP(hipMemcpy(ha.data(), rabs.p, n_pad * sizeof(double), hipMemcpyDeviceToHost));
     double amax = 0.0;
     for (double v : ha) amax = std::max(amax, v);
     const double u = std::ldexp(1.0, -24);
     e->rho_mx = 1.05 * fr / os + 1e-15 * pmax * (double)n + 1.01 * (2.0 * (double)n_pad + 64.0) * u * amax;
-  }
-  (void)hipDeviceSynchronize();
+    return GMAT_OK;
+  };
   e->setup[4] = now() - t_create;
   if (state) {  // the spectral state (eigenpairs, certificates, Q images) of another rank's plan
     if ((rc = import_state(e, state, state_bytes)) != GMAT_OK) return fail(rc);
@@ -3400,6 +3421,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
       rc = GMAT_OK;
     }
   }  // spectral state computed here
+  if ((rc = finish_mx()) != GMAT_OK) return fail(rc);
   std::vector<double> hz(n_pad);
   if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
     set_error("gmat_epi_create: z download failed");
