@@ -1921,7 +1921,7 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
 // the tile images stream through a double buffer in the block-upper stage order of mx_screen.
 template <int PP>
 __global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
-  constexpr int T = PP * 8, NA = MX_TILE / 16 / T;
+  constexpr int T = PP * 8, NC16 = MX_TILE / 16, NA = (NC16 + T - 1) / T;  // 16-byte chunks per tile
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
   uint8_t *sA = dyn;                        // [2][MX_TILE]
   uint8_t *wpl = dyn + 2 * MX_TILE;         // [PP][pitch]
@@ -1948,11 +1948,13 @@ __global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
   auto load = [&](int kb, int cs) __attribute__((always_inline)) {
     const int soffA = (kb * nK + cs) * MX_TILE;
 #pragma unroll
-    for (int u = 0; u < NA; ++u) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * T) * 16, soffA, 0);
+    for (int u = 0; u < NA; ++u)
+      if (NC16 % T == 0 || tid + u * T < NC16) ra[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (tid + u * T) * 16, soffA, 0);
   };
   auto store = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < NA; ++u) *(v4i *)&sA[b * MX_TILE + (tid + u * T) * 16] = ra[u];
+    for (int u = 0; u < NA; ++u)
+      if (NC16 % T == 0 || tid + u * T < NC16) *(v4i *)&sA[b * MX_TILE + (tid + u * T) * 16] = ra[u];
   };
   const uint8_t *wrow = wpl + (32 * t + c) * pitch;
   const int sw16 = 16 * ((c >> 3) & 1);
@@ -2845,7 +2847,12 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   if (n_out) *n_out = 0;
   if (np <= 0 && !n_out) return GMAT_OK;
   if (np <= 0 && reset) return GMAT_OK;
-  const int nK = e->nK, pp = nK <= 31 ? 64 : 32;
+  // pairs per workgroup: as many as the LDS holds (the P tiles streamed per workgroup are the cost;
+  // GMAT_PS_PP caps it for A/B runs)
+  const int nK = e->nK;
+  auto lds_of = [&](int q) { return 2 * (size_t)MX_TILE + (size_t)q * (nK * 64 + 16) + 4 * (size_t)q * sizeof(double); };
+  const int pp_cap = getenv("GMAT_PS_PP") ? atoi(getenv("GMAT_PS_PP")) : 96;
+  const int pp = (pp_cap >= 96 && lds_of(96) <= 160 * 1024 - 256) ? 96 : (lds_of(64) <= 160 * 1024 - 256 && pp_cap >= 64) ? 64 : 32;
   GMAT_CHECK(nK <= 63, GMAT_E_ARG, "pair screen: %d stages exceed the LDS", nK);
   GMAT_CHECK(L.U32.p && R.U32.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
                  R.qb.p && e->cand2_i.p && e->cand2_j.p && e->counter2.p &&
@@ -2892,16 +2899,20 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   if (np > 0) {
   hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, x);
   GMAT_HIP(hipGetLastError());
-  const size_t lds = 2 * MX_TILE + (size_t)pp * (nK * 64 + 16) + 4 * pp * sizeof(double);
+  const size_t lds = lds_of(pp);
   static bool attr = false;
   if (!attr) {
+    GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 256));
     GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  160 * 1024 - 256));
     GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  160 * 1024 - 256));
     attr = true;
   }
-  if (pp == 64)
+  if (pp == 96)
+    hipLaunchKernelGGL(pair_mx_kernel<96>, dim3((unsigned)cdiv(np, 96)), dim3(768), lds, st, x);
+  else if (pp == 64)
     hipLaunchKernelGGL(pair_mx_kernel<64>, dim3((unsigned)cdiv(np, 64)), dim3(512), lds, st, x);
   else
     hipLaunchKernelGGL(pair_mx_kernel<32>, dim3((unsigned)cdiv(np, 32)), dim3(256), lds, st, x);
