@@ -133,6 +133,48 @@ def parity_check(plan, rows, exp, p_cut):
     return out
 
 
+EXHAUSTIVE_HITS = os.path.join(REPO, "tests", "golden", "cfg3_exhaustive_hits_AA_2000x50000.npz")
+FULL_TRIANGLE_RECORD = "profiles/round3_full_triangle_AA_2000x50000.json"
+
+
+def full_triangle_check(g, pvp, py, hits, p_cut, live=None):
+    """The timed step's hits (merged over the ranks) against the EXHAUSTIVE scan of the same cohort:
+    every one of the 1,249,975,000 pairs refined in fp64 with no screen (gmat_epi_scan level
+    GMAT_SCREEN_NONE, the reference's computation remma_epiAA.py:71-82), recorded by
+    tools/full_triangle.py (FULL_TRIANGLE_RECORD; hit set in tests/golden) or, with
+    --full-triangle, recomputed in this run (`live`).  Identical (i, j) sets and byte-identical
+    eff / var / chi / p are required; a cohort fingerprint (per-SNP counts, P, Py) guards the record."""
+    from tools.full_triangle import cohort_fingerprint
+    out = {"source": "live exhaustive scan in this run" if live is not None else FULL_TRIANGLE_RECORD}
+    if live is not None:
+        ref = live
+    else:
+        if not os.path.exists(EXHAUSTIVE_HITS):
+            return dict(out, checked=False, reason="no recorded exhaustive hit set")
+        d = np.load(EXHAUSTIVE_HITS)
+        if bytes(d["fingerprint"]).hex() != cohort_fingerprint(g, pvp, py) or float(d["p_cut"][0]) != p_cut:
+            return dict(out, checked=False, reason="recorded hit set is for another cohort / p_cut")
+        ref = (d["i"].astype(np.int64), d["j"].astype(np.int64), d["eff"], d["var"], d["chi"], d["p"])
+    a = set(zip(hits[0].tolist(), hits[1].tolist()))
+    b = set(zip(ref[0].tolist(), ref[1].tolist()))
+    sd = len(a ^ b)
+    same = sd == 0 and all(np.array_equal(np.asarray(x).view(np.uint64), np.asarray(y).view(np.uint64))
+                           for x, y in zip(hits[2:], ref[2:]))
+    return dict(out, checked=True, exhaustive_hits=len(b), step_hits=len(a), symmetric_difference=sd,
+                values_byte_identical=bool(same), identical=bool(sd == 0 and same))
+
+
+def exhaustive_live(plan, rows, p_cut, lib):
+    """This rank's rows refined with no screen (about 113 s for the whole configs[2] triangle on one
+    MI355X); progress on stderr."""
+    from gmat_amd import _native as N
+    parts, t0 = [], time.perf_counter()
+    for k in range(0, rows.size, 2000):
+        parts.append(plan.scan("AA", rows[k:k + 2000], p_cut, n_slice=N.GMAT_SCREEN_NONE))
+        log("exhaustive: %d / %d rows, %.0f s" % (min(k + 2000, rows.size), rows.size, time.perf_counter() - t0))
+    return tuple(np.concatenate([p[t] for p in parts]) for t in range(6)), time.perf_counter() - t0
+
+
 def grm_bench(n, m_grm, seed, reps=5):
     """configs[1] GRM: agmat product on int8 MFMA, kernel time from HIP events."""
     import ctypes
@@ -315,6 +357,38 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed, geno=None, cpu_budget=10.0):
             "cpu_baseline": cpu}
 
 
+def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), reps=2):
+    """configs[3] rehearsed on one GPU: each part of the multi-GPU split (dist.rank_rows: part k of
+    the reference's folded parallel=[N,k] rows, remma_epiAA.py:125-139) timed serially on this GPU
+    -- what one rank of an N-GPU run computes between its barriers.  Reports per-part ms, the
+    max / mean imbalance and the projected N-GPU step (slowest part; the hit gather is a few
+    hundred KB), and checks that the parts' hits add up to the 1-GPU step's."""
+    from gmat_amd import dist
+    out = {}
+    for N in ways:
+        ms, hits, pairs = [], 0, []
+        for k in range(N):
+            rows = dist.rank_rows("AA", m, k, N)
+            best = None
+            for _ in range(reps):
+                lib.gmat_device_synchronize()
+                t0 = time.perf_counter()
+                res = plan.scan("AA", rows, p_cut)
+                lib.gmat_device_synchronize()
+                dt = (time.perf_counter() - t0) * 1e3
+                best = dt if best is None else min(best, dt)
+            ms.append(best)
+            hits += int(res[0].size)
+            pairs.append(float(np.sum(m - 1 - rows)))
+        mean = float(np.mean(ms))
+        out["%d" % N] = {"part_ms": [round(x, 3) for x in ms], "max_over_mean": max(ms) / mean,
+                         "pairs_max_over_mean": max(pairs) / float(np.mean(pairs)),
+                         "projected_step_ms": max(ms), "projected_speedup": step_ms / max(ms),
+                         "projected_efficiency": step_ms / max(ms) / N, "hits_sum": hits,
+                         "hits_match_step": bool(hits == hits_step)}
+    return out
+
+
 def cfg5_main(args):
     """BASELINE configs[4]: synthetic 5,000 x 100,000 cohort, 5-GRM model [A, D, AxA, AxD, DxD]:
     GRMs (agmat / dgmat_as products), weighted EM-AI REML (first --reml-iters iterations timed),
@@ -423,6 +497,9 @@ def main():
     ap.add_argument("--no-reml", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cov", action="store_true")
+    ap.add_argument("--no-split", action="store_true", help="skip the serial per-part rehearsal of the N-GPU split")
+    ap.add_argument("--full-triangle", action="store_true",
+                    help="recompute the exhaustive (unscreened) scan live for the full-triangle check (~2 min / N)")
     ap.add_argument("--config", default="cfg3", choices=["cfg3", "cfg5"],
                     help="cfg3: the headline (configs[2]/[3]); cfg5: configs[4] (5,000 x 100,000, 5 GRMs, epiDD/epiAD)")
     ap.add_argument("--reml-iters", type=int, default=5)
@@ -511,14 +588,24 @@ def main():
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
     dense_ops_step = (my_pairs * 2 * plan.lowrank_rank() * n if n_slice == -1
                       else my_pairs * max(n_slice, 1) * n * (n + 128))
-    traffic = None
+    # fabric bytes per launch of this kernel shape from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
+    # WRITE_SIZE); the record is used only when it was taken on the same kernel, screen level, rank and
+    # cohort size with an average launch time within 25 % of this run's (else traffic stays null)
+    traffic, traffic_src = None, None
+    want = {"kernel": "lr_screen_kernel", "screen_level": n_slice, "lowrank_rank": plan.lowrank_rank(),
+            "n_id": n, "n_snp": m}
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("screen_level", 1) == n_slice:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            same = all(tj.get(k) == v for k, v in want.items())
+            t_rec = tj.get("avg_launch_us", 0.0) * 1e-6
+            if same and avg_launch_s > 0 and abs(t_rec - avg_launch_s) <= 0.25 * avg_launch_s:
+                traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
+            else:
+                traffic_src = "dropped: %s recorded for %s at %.1f us per launch" % (
+                    args.traffic_json, {k: tj.get(k) for k in want}, t_rec * 1e6)
+        except Exception as exc:
+            traffic_src = "unreadable: %s" % exc
     if n_slice == -1:
         peak, kern = MX_PEAK_TFLOPS, "lr_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
         note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: R x n_pad MACs x 2 per pair (R = %d bottom "
@@ -533,11 +620,23 @@ def main():
         note = ("int8 ops (TOP/s) of the screened blocks: S slices x n_pad(n_pad+128)/2 MACs x 2 per pair; "
                 "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
     roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": traffic, "kernel": kern, "ops_note": note,
+                "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src, "kernel": kern,
+                "ops_note": note,
                 "screen_level": n_slice,
                 "issued_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
                 "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
 
+    # full-triangle check: the last step's hits merged over the ranks against the exhaustive scan
+    merged = dist.gather_hits(res)
+    live, t_live = None, None
+    if args.full_triangle:
+        ex_local, t_live = exhaustive_live(plan, rows, args.p_cut, lib)
+        live = dist.gather_hits(ex_local)
+        t_live = dist.allreduce_max(t_live)
+    full_tri = full_triangle_check(g, pvp, py, merged, args.p_cut, live) if rank == 0 else None
+    if rank == 0 and t_live is not None:
+        full_tri["exhaustive_s"] = t_live
+        full_tri["exhaustive_pairs_per_s"] = total_pairs / t_live
     cpu = parity = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         log("cpu baseline (oracle port) on stratified rows, %.0f s budget" % args.cpu_budget)
@@ -551,6 +650,10 @@ def main():
         if not args.no_reml:
             log("configs[1] REML")
             reml = reml_bench(grm_bench.last_k, args.seed)
+    split = None
+    if rank == 0 and ws == 1 and not args.no_split:
+        log("multi-GPU split rehearsed part by part")
+        split = split_emulation(plan, m, args.p_cut, t_max / args.steps * 1e3, int(round(hits_all)), lib)
     cov = None
     if rank == 0 and ws == 1 and not args.no_cov:
         log("covariate design")
@@ -564,6 +667,9 @@ def main():
         log("effect screen")
         eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed, geno=geno, cpu_budget=args.cpu_budget)
     if rank == 0:
+        if parity is None:
+            parity = {}
+        parity["full_triangle"] = full_tri
         value = total_pairs * args.steps / t_max
         out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
@@ -574,15 +680,18 @@ def main():
                           "parallelism": "rows folded over %d rank(s) (parallel=[N,k] split), backend %s"
                                          % (ws, backend or "single")},
                "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "setup": setup, "grm": grm,
-               "reml": reml, "end_to_end": e2e, "covariates": cov, "eff_screen": eff,
+               "reml": reml, "end_to_end": e2e, "covariates": cov, "eff_screen": eff, "split_rehearsal": split,
                "scan": {"hits_per_step": hits_all, "candidates_per_step": cands_all,
                         "screen_s_per_step_rank0": screen_s / args.steps, "side_s_per_step_rank0": side_s / args.steps,
                         "refine_s_per_step_rank0": ref_s / args.steps}}
         print(json.dumps(out), flush=True)
     plan.close()
     g.close()
-    if parity is not None and not parity["identical"]:
+    if parity is not None and not parity.get("identical", True):
         log("PARITY FAILURE: GPU hits differ from the oracle on the sampled rows")
+        sys.exit(3)
+    if full_tri is not None and full_tri.get("checked") and not full_tri["identical"]:
+        log("PARITY FAILURE: the step's hits differ from the exhaustive scan's")
         sys.exit(3)
 
 

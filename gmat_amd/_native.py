@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("GMAT_HIP_LIB", os.path.join(_HERE, "libgmat_hip.so"))
 
 GMAT_AA, GMAT_AD, GMAT_DD = 0, 1, 2
 GMAT_GRM_ADD, GMAT_GRM_DOM = 0, 1
+GMAT_SCREEN_NONE = -9  # gmat_epi_scan level: no screen, every pair refined exactly
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

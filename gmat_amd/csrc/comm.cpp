@@ -10,6 +10,8 @@
 // single-node runs, gmat_amd/dist.py).
 #include <rccl/rccl.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 using namespace gmat;
@@ -108,43 +110,56 @@ extern "C" int gmat_comm_allreduce_f64(gmat_comm *c, double *v, int64_t count, i
 }
 
 // Gather variable-length byte records to root: counts (size entries) is filled on every rank;
-// root's recv receives the ranks' payloads back to back in rank order (recv_cap bytes available;
-// GMAT_E_OVERFLOW with *needed set when too small).  Point-to-point sends inside one group.
+// root's recv receives the ranks' payloads back to back in rank order (recv_cap bytes available).
+// The capacity check is collective: root's verdict travels with the counts' all-reduce, so when
+// recv is too small EVERY rank returns GMAT_E_OVERFLOW (with *needed set) before any point-to-point
+// call is posted.  Point-to-point sends inside one group; the group is always closed, also on error.
 extern "C" int gmat_comm_gatherv(gmat_comm *c, const void *send, int64_t bytes, int root, int64_t *counts, void *recv,
                                  int64_t recv_cap, int64_t *needed) {
   GMAT_CHECK(c && counts && bytes >= 0 && (bytes == 0 || send) && root >= 0 && root < c->size, GMAT_E_ARG,
              "gmat_comm_gatherv: bad arguments");
-  std::vector<double> cnt(c->size, 0.0);
+  // [0, size): byte counts; [size]: root's capacity (other ranks add 0)
+  std::vector<double> cnt(c->size + 1, 0.0);
   cnt[c->rank] = (double)bytes;
-  GMAT_TRY(gmat_comm_allreduce_f64(c, cnt.data(), c->size, 0));
+  if (c->rank == root) cnt[c->size] = recv ? (double)recv_cap : 0.0;
+  GMAT_TRY(gmat_comm_allreduce_f64(c, cnt.data(), c->size + 1, 0));
   int64_t total = 0;
   for (int r = 0; r < c->size; ++r) {
     counts[r] = (int64_t)cnt[r];
     total += counts[r];
   }
   if (needed) *needed = total;
-  if (c->rank == root) GMAT_CHECK(recv_cap >= total && (total == 0 || recv), GMAT_E_OVERFLOW,
-                                  "gmat_comm_gatherv: %lld bytes needed", (long long)total);
+  GMAT_CHECK((int64_t)cnt[c->size] >= total, GMAT_E_OVERFLOW, "gmat_comm_gatherv: %lld bytes needed, root has %lld",
+             (long long)total, (long long)cnt[c->size]);
   if (total == 0) return GMAT_OK;
   GMAT_TRY(c->a.alloc((size_t)std::max<int64_t>(bytes, 1)));
   if (bytes) GMAT_HIP(hipMemcpyAsync(c->a.p, send, bytes, hipMemcpyHostToDevice, c->s));
   if (c->rank == root) GMAT_TRY(c->b.alloc((size_t)total));
+  // enqueue inside the group; the first failure is kept and the group closed before returning
+  std::string err;
   GMAT_NCCL(ncclGroupStart());
   if (c->rank == root) {
     int64_t off = 0;
-    for (int r = 0; r < c->size; ++r) {
+    for (int r = 0; r < c->size && err.empty(); ++r) {
       if (counts[r] > 0) {
-        if (r == root)
-          GMAT_HIP(hipMemcpyAsync(c->b.as<uint8_t>() + off, c->a.p, counts[r], hipMemcpyDeviceToDevice, c->s));
-        else
-          GMAT_NCCL(ncclRecv(c->b.as<uint8_t>() + off, (size_t)counts[r], ncclUint8, r, c->nc, c->s));
+        if (r == root) {
+          const hipError_t he =
+              hipMemcpyAsync(c->b.as<uint8_t>() + off, c->a.p, counts[r], hipMemcpyDeviceToDevice, c->s);
+          if (he != hipSuccess) err = std::string("hipMemcpyAsync: ") + hipGetErrorString(he);
+        } else {
+          const ncclResult_t nr = ncclRecv(c->b.as<uint8_t>() + off, (size_t)counts[r], ncclUint8, r, c->nc, c->s);
+          if (nr != ncclSuccess) err = std::string("ncclRecv: ") + ncclGetErrorString(nr);
+        }
       }
       off += counts[r];
     }
   } else if (bytes > 0) {
-    GMAT_NCCL(ncclSend(c->a.p, (size_t)bytes, ncclUint8, root, c->nc, c->s));
+    const ncclResult_t nr = ncclSend(c->a.p, (size_t)bytes, ncclUint8, root, c->nc, c->s);
+    if (nr != ncclSuccess) err = std::string("ncclSend: ") + ncclGetErrorString(nr);
   }
-  GMAT_NCCL(ncclGroupEnd());
+  const ncclResult_t ge = ncclGroupEnd();
+  GMAT_CHECK(err.empty(), GMAT_E_HIP, "gmat_comm_gatherv: %s", err.c_str());
+  GMAT_CHECK(ge == ncclSuccess, GMAT_E_HIP, "gmat_comm_gatherv: ncclGroupEnd -> %s", ncclGetErrorString(ge));
   if (c->rank == root) GMAT_HIP(hipMemcpyAsync(recv, c->b.p, total, hipMemcpyDeviceToHost, c->s));
   GMAT_HIP(hipStreamSynchronize(c->s));
   return GMAT_OK;

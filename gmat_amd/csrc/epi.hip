@@ -3475,6 +3475,13 @@ int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes) {
   GMAT_CHECK(h.p_hash == e->p_hash, GMAT_E_ARG, "plan state: computed for a different P");
   GMAT_CHECK(h.pf_ncov >= 0 && h.pf_ncov <= PF_NCOV_MAX && h.lr_R >= 0 && h.tiles_bytes >= 0, GMAT_E_ARG,
              "plan state: corrupt header");
+  // the low-rank screen's rank is whole 128-deep basis chunks below n_pad, and its tile images are
+  // exactly nC x nK tiles (the kernel derives nC = lr_R / MXK from the rank, not from the payload)
+  GMAT_CHECK(h.lr_R % MXK == 0 && h.lr_R < e->n_pad, GMAT_E_ARG, "plan state: low-rank rank %lld is not a multiple "
+             "of %d below n_pad %lld", (long long)h.lr_R, MXK, (long long)e->n_pad);
+  GMAT_CHECK(h.lr_R == 0 || h.tiles_bytes == (h.lr_R / MXK) * (int64_t)e->nK * MX_TILE, GMAT_E_ARG,
+             "plan state: %lld tile bytes for rank %lld (%lld expected)", (long long)h.tiles_bytes, (long long)h.lr_R,
+             (long long)((h.lr_R / MXK) * (int64_t)e->nK * MX_TILE));
   e->pf_mu = h.d[0];
   e->pf_tau = h.d[1];
   e->pf_eps = h.d[2];
@@ -3609,7 +3616,167 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
   return GMAT_OK;
 }
 
+// ------------------------------------------------------------------ exhaustive mode
+// Every pair of the listed rows refined exactly, no screen: the reference's computation
+// (remma_epiAA.py:71-82, remma_epiAD.py:68-80, remma_epiDD.py:68-79) on refine_kernel.  It audits
+// the certified screens (a screened scan must return the same hits, byte for byte: the refine of
+// a pair does not depend on the list it comes in) and is the fallback when no screen is wanted.
+
+// (i, j) of every pair of rows[r] (j > i for the triangular kinds, every j for AD), row r's pairs
+// starting at offs[r]
+__global__ void all_pairs_kernel(const int64_t *__restrict__ rows, const int64_t *__restrict__ offs, int64_t m, int tri,
+                                 int64_t *__restrict__ pi, int64_t *__restrict__ pj) {
+  const int r = blockIdx.y;
+  const int64_t i = rows[r], j0 = tri ? i + 1 : 0, cnt = m - j0, base = offs[r];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += (int64_t)gridDim.x * blockDim.x) {
+    pi[base + t] = i;
+    pj[base + t] = j0 + t;
+  }
+}
+
+// pairs with p < p_cut appended at *count (one atomic per wave; order restored by the host's sort)
+__global__ __launch_bounds__(256) void hit_compact_kernel(int64_t np, const int64_t *__restrict__ pi,
+                                                          const int64_t *__restrict__ pj, const double *__restrict__ eff,
+                                                          const double *__restrict__ var, const double *__restrict__ chi,
+                                                          const double *__restrict__ p, double p_cut,
+                                                          unsigned long long *count, int64_t *hi, int64_t *hj,
+                                                          double *he, double *hv, double *hc, double *hp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool hit = t < np && p[t] < p_cut;  // NaN never passes (res[res[4] < p_cut])
+  const uint64_t mask = __ballot(hit);
+  if (!mask) return;
+  const int lane = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (lane == __ffsll((unsigned long long)mask) - 1) base = atomicAdd(count, (unsigned long long)__popcll(mask));
+  base = __shfl(base, __ffsll((unsigned long long)mask) - 1);
+  if (!hit) return;
+  const int64_t o = (int64_t)base + __popcll(mask & ((1ull << lane) - 1));
+  hi[o] = pi[t];
+  hj[o] = pj[t];
+  he[o] = eff[t];
+  hv[o] = var[t];
+  hc[o] = chi[t];
+  hp[o] = p[t];
+}
+
 namespace {
+
+int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, int64_t *n_hits) {
+  const double t_start = now();
+  const int64_t m = e->m;
+  const int tri = kind != GMAT_AD;
+  int lc, rc;
+  kind_codings(kind, &lc, &rc);
+  GMAT_TRY(build_coding(e, lc));
+  GMAT_TRY(build_coding(e, rc));
+  const Coding &L = e->code[lc], &R = e->code[rc];
+  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  for (double &v : e->stats) v = 0.0;
+  e->hit_i.clear();
+  e->hit_j.clear();
+  e->hit_eff.clear();
+  e->hit_var.clear();
+  e->hit_chi.clear();
+  e->hit_p.clear();
+  // chunks of whole rows of at most `cap` pairs (one row holds at most m)
+  const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : (1 << 24));
+  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  const hipStream_t st = e->s3;
+  DBuf di, dj, de, dv, dc, dp, hi, hj, he, hv, hc, hp, cnt, drows, doffs;
+  for (DBuf *b : {&di, &dj, &de, &dv, &dc, &dp, &hi, &hj, &he, &hv, &hc, &hp}) GMAT_TRY(b->alloc((size_t)cap * 8));
+  GMAT_TRY(cnt.alloc(8));
+  GMAT_TRY(drows.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
+  GMAT_TRY(doffs.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
+  GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
+  hipEvent_t ev0, ev1;
+  GMAT_HIP(hipEventCreate(&ev0));
+  GMAT_HIP(hipEventCreate(&ev1));
+  struct EvGuard {
+    hipEvent_t a, b;
+    ~EvGuard() {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+    }
+  } evg{ev0, ev1};
+  double pairs = 0, t_ref = 0;
+  std::vector<int64_t> offs;
+  std::vector<int64_t> hbuf;
+  std::vector<double> dbuf;
+  for (int64_t r0 = 0; r0 < n_rows;) {
+    offs.clear();
+    int64_t np = 0, r1 = r0;
+    while (r1 < n_rows && r1 - r0 < 65535) {
+      const int64_t c = tri ? m - 1 - rows[r1] : m;
+      if (np + c > cap) break;
+      offs.push_back(np);
+      np += c;
+      ++r1;
+    }
+    const int64_t nr = r1 - r0;
+    pairs += (double)np;
+    if (np > 0) {
+      GMAT_HIP(hipMemcpyAsync(drows.p, rows + r0, nr * 8, hipMemcpyHostToDevice, st));
+      GMAT_HIP(hipMemcpyAsync(doffs.p, offs.data(), nr * 8, hipMemcpyHostToDevice, st));
+      const int64_t per_row = tri ? m - 1 - rows[r0] : m;  // the longest row of the chunk (rows increase)
+      hipLaunchKernelGGL(all_pairs_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(per_row, 256), 64)),
+                                                (unsigned)nr),
+                         dim3(256), 0, st, drows.as<int64_t>(), doffs.as<int64_t>(), m, tri, di.as<int64_t>(),
+                         dj.as<int64_t>());
+      GMAT_HIP(hipGetLastError());
+      GMAT_HIP(hipEventRecord(ev0, st));
+      GMAT_TRY(refine(e, st, L, R, lp, rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(), dv.as<double>(),
+                      dc.as<double>(), dp.as<double>()));
+      GMAT_HIP(hipEventRecord(ev1, st));
+      GMAT_HIP(hipMemsetAsync(cnt.p, 0, 8, st));
+      hipLaunchKernelGGL(hit_compact_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, di.as<int64_t>(),
+                         dj.as<int64_t>(), de.as<double>(), dv.as<double>(), dc.as<double>(), dp.as<double>(), p_cut,
+                         cnt.as<unsigned long long>(), hi.as<int64_t>(), hj.as<int64_t>(), he.as<double>(),
+                         hv.as<double>(), hc.as<double>(), hp.as<double>());
+      GMAT_HIP(hipGetLastError());
+      unsigned long long k = 0;
+      GMAT_HIP(hipMemcpyAsync(&k, cnt.p, 8, hipMemcpyDeviceToHost, st));
+      GMAT_HIP(hipStreamSynchronize(st));
+      float ms;
+      GMAT_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+      t_ref += ms * 1e-3;
+      if (k) {
+        const size_t o = e->hit_i.size();
+        for (auto *v : {&e->hit_i, &e->hit_j}) v->resize(o + k);
+        for (auto *v : {&e->hit_eff, &e->hit_var, &e->hit_chi, &e->hit_p}) v->resize(o + k);
+        GMAT_HIP(hipMemcpy(e->hit_i.data() + o, hi.p, k * 8, hipMemcpyDeviceToHost));
+        GMAT_HIP(hipMemcpy(e->hit_j.data() + o, hj.p, k * 8, hipMemcpyDeviceToHost));
+        GMAT_HIP(hipMemcpy(e->hit_eff.data() + o, he.p, k * 8, hipMemcpyDeviceToHost));
+        GMAT_HIP(hipMemcpy(e->hit_var.data() + o, hv.p, k * 8, hipMemcpyDeviceToHost));
+        GMAT_HIP(hipMemcpy(e->hit_chi.data() + o, hc.p, k * 8, hipMemcpyDeviceToHost));
+        GMAT_HIP(hipMemcpy(e->hit_p.data() + o, hp.p, k * 8, hipMemcpyDeviceToHost));
+      }
+    }
+    r0 = r1;
+  }
+  std::vector<int64_t> ord(e->hit_i.size());
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
+  });
+  auto apply = [&](auto &v) {
+    auto c2 = v;
+    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
+  };
+  apply(e->hit_i);
+  apply(e->hit_j);
+  apply(e->hit_eff);
+  apply(e->hit_var);
+  apply(e->hit_chi);
+  apply(e->hit_p);
+  *n_hits = (int64_t)e->hit_i.size();
+  e->stats[0] = pairs;
+  e->stats[1] = pairs;  // every pair is refined
+  e->stats[4] = t_ref;
+  e->stats[6] = now() - t_start;
+  e->stats[8] = GMAT_SCREEN_NONE;
+  return GMAT_OK;
+}
 
 }  // namespace
 
@@ -3622,6 +3789,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
     GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
   }
+  if (n_slice == GMAT_SCREEN_NONE) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
   const double t_start = now();
   int lc, rc;
   kind_codings(kind, &lc, &rc);

@@ -18,8 +18,12 @@ genotype panel, P and Py, so the scan shards with no collective on its hot path:
 Backends.  ``rccl`` (the product path on GPUs): the exchanges run in libgmat_hip on RCCL over
 xGMI (gmat_comm_* in include/gmat_hip.h); no PyTorch is imported.  The 128-byte unique id is
 created by rank 0 and shared through a file in the temp directory keyed by the launcher
-(single-node runs, as bench.py's contract).  ``gloo`` (torch.distributed on CPU) is kept only as
-the test harness of tests/test_dist_cpu.py, with the per-rank compute injected (``scan_fn``).
+(single-node runs, as bench.py's contract): the key holds the launcher's pid AND its start time,
+MASTER_PORT, the run id and the restart count, so a file left by a crashed run is never read.
+When WORLD_SIZE > 1 and a GPU is visible the backend is RCCL on every rank, and any RCCL failure
+raises (the launcher then stops the job) -- there is no silent per-rank fallback that could leave
+ranks on different backends.  ``gloo`` (torch.distributed on CPU) is the test harness of
+tests/test_dist_cpu.py, chosen only when no GPU is visible or GMAT_DIST_BACKEND=gloo says so.
 """
 import ctypes
 import os
@@ -41,8 +45,21 @@ def backend():
     return _state["backend"]
 
 
+def _proc_start(pid):
+    """Start time of a process in clock ticks since boot (/proc/<pid>/stat field 22), 0 if unknown."""
+    try:
+        with open("/proc/%d/stat" % pid) as f:
+            return int(f.read().rsplit(")", 1)[1].split()[19])
+    except (OSError, ValueError, IndexError):
+        return 0
+
+
 def _id_file():
-    key = "%s_%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "na"), os.getppid())
+    """Rendezvous file of this launch: every rank of one torchrun agent computes the same name, and
+    no earlier launch can (the agent's pid is paired with its start time)."""
+    ppid = os.getppid()
+    key = "%s_%s_%s_%d_%d" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "na"),
+                              os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"), ppid, _proc_start(ppid))
     return os.path.join(tempfile.gettempdir(), "gmat_rccl_id_" + key)
 
 
@@ -82,37 +99,43 @@ def _init_rccl(rank, ws):
             pass
 
 
+def choose_backend(explicit=None, gpu_visible=None):
+    """The backend every rank uses: GMAT_DIST_BACKEND / the argument when given, else ``rccl``
+    when a GPU is visible (the product path) and ``gloo`` otherwise (CPU test harness).  The
+    choice depends only on the launch environment, identical on all ranks of a node."""
+    if explicit is None:
+        explicit = os.environ.get("GMAT_DIST_BACKEND")
+    if explicit is not None:
+        if explicit not in ("rccl", "gloo"):
+            raise ValueError("unknown backend %r (rccl | gloo)" % explicit)
+        return explicit
+    if gpu_visible is None:
+        from . import _native as N
+        lib = N.load(required=False)
+        gpu_visible = lib is not None and N.device_count() > 0
+    return "rccl" if gpu_visible else "gloo"
+
+
 def init(backend=None):
     """Set up the process group when WORLD_SIZE > 1.  Returns the backend used (None for a
-    single process).  Default ``rccl`` when a GPU is visible, else ``gloo``; GMAT_DIST_BACKEND
-    overrides."""
+    single process).  RCCL errors are fatal (no fallback: ranks must agree on the backend)."""
     rank, ws, local = world()
     if ws <= 1:
         return None
     if _state["backend"] is not None:
         return _state["backend"]
-    if backend is None:
-        backend = os.environ.get("GMAT_DIST_BACKEND")
-    if backend is None:
-        from . import _native as N
-        lib = N.load(required=False)
-        backend = "rccl" if lib is not None and N.device_count() > 0 else "gloo"
+    backend = choose_backend(backend)
     if backend == "rccl":
         try:
             _init_rccl(rank, ws)
-        except Exception as exc:  # e.g. two ranks on one GPU (RCCL: invalid usage)
-            if os.environ.get("GMAT_DIST_BACKEND") == "rccl":
-                raise
-            import sys
-            print("gmat_amd.dist: RCCL unavailable (%s); exchanging over gloo" % exc, file=sys.stderr)
-            backend = "gloo"
+        except Exception as exc:
+            raise RuntimeError("rank %d/%d: RCCL communicator setup failed (%s); set GMAT_DIST_BACKEND=gloo to "
+                               "exchange over host TCP instead (e.g. several ranks on one GPU)" % (rank, ws, exc))
     if backend == "gloo":
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not tdist.is_initialized():
             tdist.init_process_group("gloo")
-    elif backend != "rccl":
-        raise ValueError("unknown backend %r (rccl | gloo)" % backend)
     _state["backend"] = backend
     return backend
 

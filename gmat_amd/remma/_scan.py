@@ -55,7 +55,9 @@ class EpiPlan:
 
     def scan(self, kind, rows, p_cut, n_slice=0):
         """Hits (i, j, eff, var, chi, p) with p < p_cut over first-SNP rows `rows`
-        (strictly increasing), sorted by (i, j)."""
+        (strictly increasing), sorted by (i, j).  n_slice picks the certified screen in front of
+        the exact refine (gmat_epi_scan); N.GMAT_SCREEN_NONE refines every pair (the reference's
+        computation, remma_epiAA.py:71-82) -- the audit of the screens."""
         rows = N.i64(rows)
         n_hits = ctypes.c_int64()
         chi_cut = float(chi2.isf(p_cut, 1)) if p_cut < 1 else 0.0

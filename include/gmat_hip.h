@@ -104,10 +104,14 @@ int gmat_epi_create_with(gmat_epi **out, gmat_geno *g, const double *pvp, const 
 /* Exhaustive exact scan over first-SNP rows `rows` (sorted ascending): AA/DD test pairs
  * (i, j>i) (remma_epiAA.py:71-82, remma_epiDD.py:75-86), AD tests (i, all j) including i==j
  * (remma_epiAD.py:76-87).  A pair is a hit when p < p_cut with p = chi2.sf(eff^2/var, 1);
- * chi_cut must be chi2.isf(p_cut, 1).  n_slice: slices the screen uses (0 = automatic: 1 for
- * p_cut <= 1e-4, 2 for p_cut <= 1e-2, else all kept; a launch whose candidates overflow is redone
- * with one more); the hit set does not depend on it.  *n_hits receives the number
- * of hits, retrieved with gmat_epi_hits (sorted by (i, j)). */
+ * chi_cut must be chi2.isf(p_cut, 1).  n_slice selects the certified screen in front of the exact
+ * fp64 refine: 0 = automatic (the low-rank spectral screen when the plan has one and p_cut <= 1e-4,
+ * else int8 slices of P: 2 up to p_cut 1e-2, then all kept), S > 0 = S int8 slices, -1 = the fp6
+ * quadratic form, -2 = the low-rank screen, GMAT_SCREEN_NONE = no screen (every pair refined, the
+ * reference's computation; audits the screens).  A launch whose candidates overflow is redone one
+ * level finer.  The hit set and its numbers do not depend on the level.  *n_hits receives the
+ * number of hits, retrieved with gmat_epi_hits (sorted by (i, j)). */
+#define GMAT_SCREEN_NONE (-9)
 int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
                   int n_slice, int64_t *n_hits);
 int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,
@@ -189,7 +193,8 @@ int gmat_comm_broadcast(gmat_comm *c, void *buf, int64_t bytes, int root);
 /* in place over ranks: op 0 = sum, 1 = max (fp64) */
 int gmat_comm_allreduce_f64(gmat_comm *c, double *v, int64_t count, int op);
 /* variable-length byte records to root: counts[nranks] on every rank; root's recv gets the payloads
- * back to back in rank order (GMAT_E_OVERFLOW with *needed when recv_cap is too small) */
+ * back to back in rank order.  When root's recv_cap is too small every rank returns GMAT_E_OVERFLOW
+ * (with *needed) before any send is posted (the check is collective). */
 int gmat_comm_gatherv(gmat_comm *c, const void *send, int64_t bytes, int root, int64_t *counts, void *recv,
                       int64_t recv_cap, int64_t *needed);
 int gmat_comm_barrier(gmat_comm *c);

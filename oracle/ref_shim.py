@@ -141,7 +141,15 @@ def import_reference():
     # never load the .pyc files that ship inside the reference: keep bytecode in a private prefix
     sys.pycache_prefix = "/tmp/gmat_ref_pycache"
     sys.dont_write_bytecode = True
-    if REF_ROOT not in sys.path:
-        sys.path.insert(0, REF_ROOT)
+    # the repo ships its own `gmat` alias package (resolving to gmat_amd): drop any cached gmat*
+    # modules and put the reference first, then make sure the reference's package is what loaded
+    for name in [k for k in sys.modules if k == "gmat" or k.startswith("gmat.")]:
+        del sys.modules[name]
+    while REF_ROOT in sys.path:
+        sys.path.remove(REF_ROOT)
+    sys.path.insert(0, REF_ROOT)
     import gmat  # noqa: F401
+    got = os.path.realpath(gmat.__file__)
+    if not got.startswith(os.path.realpath(REF_ROOT) + os.sep):
+        raise ImportError("import_reference: `gmat` resolved to %s, not the reference under %s" % (got, REF_ROOT))
     return gmat

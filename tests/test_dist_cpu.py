@@ -63,3 +63,43 @@ def test_rank_rows_partition():
             if kind != "AD" and ws > 1:
                 pairs = [sum(m - 1 - int(i) for i in p) for p in parts]
                 assert max(pairs) / min(pairs) < 1.1  # folded split balances pair counts
+
+
+def test_backend_choice_is_deterministic_and_fatal(monkeypatch):
+    """Every rank derives the backend from the launch environment alone (RCCL whenever a GPU is
+    visible); an RCCL setup failure raises instead of dropping that rank to gloo."""
+    from gmat_amd import dist
+    monkeypatch.delenv("GMAT_DIST_BACKEND", raising=False)
+    assert dist.choose_backend(gpu_visible=True) == "rccl"
+    assert dist.choose_backend(gpu_visible=False) == "gloo"
+    assert dist.choose_backend("gloo", gpu_visible=True) == "gloo"
+    monkeypatch.setenv("GMAT_DIST_BACKEND", "rccl")
+    assert dist.choose_backend(gpu_visible=False) == "rccl"
+    with pytest.raises(ValueError):
+        dist.choose_backend("mpi")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setattr(dist, "_state", {"backend": None, "comm": None})
+
+    def boom(rank, ws):
+        raise RuntimeError("ncclCommInitRank: invalid usage")
+
+    monkeypatch.setattr(dist, "_init_rccl", boom)
+    with pytest.raises(RuntimeError, match="RCCL communicator setup failed"):
+        dist.init("rccl")
+    assert dist.backend() is None
+
+
+def test_rendezvous_file_names_the_launch(monkeypatch):
+    """The unique-id file is keyed by the launcher's pid and start time, the port, the run id and
+    the restart count: a restarted or later launch never reads an earlier launch's id."""
+    from gmat_amd import dist
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "r1")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    a = dist._id_file()
+    assert a == dist._id_file()
+    assert str(os.getppid()) in a and dist._proc_start(os.getppid()) > 0
+    assert a.endswith("_%d_%d" % (os.getppid(), dist._proc_start(os.getppid())))
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert dist._id_file() != a

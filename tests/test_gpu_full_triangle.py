@@ -1,0 +1,108 @@
+"""Full-triangle audit of the certified screens: over EVERY pair of a cohort, the screened scan
+(prefilter -> low-rank spectral screen -> pair screen -> exact fp64 refine) returns exactly the
+hits of the exhaustive scan (level GMAT_SCREEN_NONE: every pair refined, the reference's
+computation remma_epiAA.py:71-82 / remma_epiAD.py:68-80 / remma_epiDD.py:68-79), with
+byte-identical eff / var / chi / p.  The exhaustive scan itself is checked against the oracle on
+a few rows.  tools/full_triangle.py runs the same audit on the full configs[2] cohort.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_ID = 2000
+
+
+def _cohort(m, seed):
+    from gmat_amd import _native as N, synth
+    from gmat_amd.plink import Geno
+    from gmat_amd.uvlmm.uvlmm_varcom import projection
+    from scipy.sparse import identity
+    lib = N.ensure_device()
+    geno = synth.simulate_genotypes(N_ID, m, seed=seed)
+    body = np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8)
+    g = Geno(body=body, n_id=N_ID, n_snp=m)
+    ka = np.empty((N_ID, N_ID))
+    sc = ctypes.c_double()
+    N.check(lib.gmat_grm(g.handle, 0, 0.001, N.ptr(ka), ctypes.byref(sc)), "gmat_grm")
+    kd = np.empty((N_ID, N_ID))
+    N.check(lib.gmat_grm(g.handle, 1, 0.001, N.ptr(kd), ctypes.byref(sc)), "gmat_grm")
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    y = np.ones(N_ID)
+    for k, s in ((ka, 0.4), (ka * ka, 0.2)):
+        y += np.sqrt(s) * (np.linalg.cholesky(k + 1e-4 * np.eye(N_ID)) @ rng.standard_normal(N_ID))
+    y += np.sqrt(0.4) * rng.standard_normal(N_ID)
+    gl = [ka, kd, ka * ka, ka * kd, kd * kd]
+    pvp, py = projection(y, np.ones((N_ID, 1)), identity(N_ID, format="csr"), gl, [0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
+    return geno, g, pvp, py
+
+
+def _same(a, b):
+    assert a[0].size == b[0].size, (a[0].size, b[0].size)
+    for x, y in zip(a, b):
+        assert x.dtype == y.dtype
+        np.testing.assert_array_equal(x.view(np.uint64) if x.dtype == np.float64 else x,
+                                      y.view(np.uint64) if y.dtype == np.float64 else y)
+
+
+@pytest.fixture(scope="module")
+def aa_cohort():
+    geno, g, pvp, py = _cohort(6000, 41)
+    yield geno, g, pvp, py
+    g.close()
+
+
+@pytest.fixture(scope="module")
+def small_cohort():
+    geno, g, pvp, py = _cohort(3000, 43)
+    yield geno, g, pvp, py
+    g.close()
+
+
+def _audit(g, pvp, py, kind, p_cuts):
+    from gmat_amd import _native as N
+    from gmat_amd.remma._scan import EpiPlan
+    m = g.m
+    rows = np.arange(m if kind == "AD" else m - 1, dtype=np.int64)
+    with EpiPlan(g, pvp, py) as plan:
+        assert plan.lowrank_rank() > 0
+        exh = plan.scan(kind, rows, max(p_cuts), n_slice=N.GMAT_SCREEN_NONE)
+        st = plan.stats()
+        assert st["pairs"] == (m * m if kind == "AD" else m * (m - 1) // 2)
+        assert st["n_slice"] == N.GMAT_SCREEN_NONE
+        for p_cut in p_cuts:
+            sel = exh[5] < p_cut
+            exp = tuple(a[sel] for a in exh)
+            for ns in (0, -1):  # automatic level (low-rank screen at small p_cut), fp6 quadratic form
+                got = plan.scan(kind, rows, p_cut, n_slice=ns)
+                _same(got, exp)
+    return exh
+
+
+def test_full_triangle_aa(aa_cohort):
+    geno, g, pvp, py = aa_cohort
+    exh = _audit(g, pvp, py, "AA", (1e-5, 1e-3))
+    assert np.sum(exh[5] < 1e-5) >= 1 and exh[0].size > 1000, exh[0].size
+    # the exhaustive level itself against the oracle (rows at both ends of the triangle)
+    from oracle import gmat_oracle as O
+    snp = np.ascontiguousarray(geno.T, dtype=np.float64)
+    rows = np.array([0, 2999, 5997], dtype=np.int64)
+    exp = O.epi_scan("AA", snp, pvp, py.reshape(-1, 1), snp_lst_0=rows, p_cut=1e-3)
+    sel = np.isin(exh[0], rows)
+    np.testing.assert_array_equal(np.column_stack([exh[0][sel], exh[1][sel]]), exp[:, :2].astype(np.int64))
+    np.testing.assert_allclose(np.column_stack([exh[2][sel], exh[4][sel], exh[5][sel]]), exp[:, 2:], rtol=1e-8)
+
+
+@pytest.mark.parametrize("kind", ["AD", "DD"])
+def test_full_triangle_ad_dd(small_cohort, kind):
+    geno, g, pvp, py = small_cohort
+    exh = _audit(g, pvp, py, kind, (1e-5, 1e-3))
+    assert exh[0].size > 100, exh[0].size
+    if kind == "AD":  # i == j pairs are part of the exhaustive AD scan
+        from gmat_amd import _native as N
+        from gmat_amd.remma._scan import EpiPlan
+        with EpiPlan(g, pvp, py) as plan:
+            d = plan.scan("AD", np.arange(5, dtype=np.int64), 1.0, n_slice=N.GMAT_SCREEN_NONE)
+        assert d[0].size > 0 and np.any(d[0] == d[1])
