@@ -588,22 +588,21 @@ def main():
     achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
     dense_ops_step = (my_pairs * 2 * plan.lowrank_rank() * n if n_slice == -1
                       else my_pairs * max(n_slice, 1) * n * (n + 128))
-    # fabric bytes per launch of this kernel shape from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
-    # WRITE_SIZE); the record is used only when it was taken on the same kernel, screen level, rank and
-    # cohort size with an average launch time within 25 % of this run's (else traffic stays null)
+    # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
+    # WRITE_SIZE); the record is used only when it was taken on the same kernel source (sha256 of
+    # epi.hip), screen level, rank and cohort size (else traffic stays null)
+    from tools.pmc_summary import source_sha256
     traffic, traffic_src = None, None
     want = {"kernel": "lr_screen_kernel", "screen_level": n_slice, "lowrank_rank": plan.lowrank_rank(),
-            "n_id": n, "n_snp": m}
+            "n_id": n, "n_snp": m, "source_sha256": source_sha256()}
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            same = all(tj.get(k) == v for k, v in want.items())
-            t_rec = tj.get("avg_launch_us", 0.0) * 1e-6
-            if same and avg_launch_s > 0 and abs(t_rec - avg_launch_s) <= 0.25 * avg_launch_s:
-                traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
+            if all(tj.get(k) == v for k, v in want.items()):
+                traffic, traffic_src = tj.get("hbm_bytes_per_launch"), os.path.relpath(args.traffic_json, REPO)
             else:
-                traffic_src = "dropped: %s recorded for %s at %.1f us per launch" % (
-                    args.traffic_json, {k: tj.get(k) for k in want}, t_rec * 1e6)
+                traffic_src = "dropped: %s was recorded for %s" % (os.path.relpath(args.traffic_json, REPO),
+                                                                   {k: tj.get(k) for k in want})
         except Exception as exc:
             traffic_src = "unreadable: %s" % exc
     if n_slice == -1:

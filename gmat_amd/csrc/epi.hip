@@ -3659,6 +3659,95 @@ __global__ __launch_bounds__(256) void hit_compact_kernel(int64_t np, const int6
   hp[o] = p[t];
 }
 
+// ------------------------------------------------------------------ bound audit (diagnostic)
+// The certified lower bounds of e'Pe the screens test with, evaluated exactly (fp64, no screen
+// arithmetic) for listed pairs, e = (a - alpha)(b - beta) of the screen codes over the real
+// individuals: the prefilter's mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2 and the
+// low-rank screen's lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - |Q'e|^2 (Q = the certified fp6 basis).
+// The caller compares them with the exact e'Pe (gmat_epi_pairs): every ratio must be >= 1.
+// One workgroup per pair; out[5 t + ..] = {lb_prefilter, lb_lowrank, |e|^2, 1'e, |Q'e|^2}.
+constexpr int AUD_T = 256;
+__global__ __launch_bounds__(AUD_T) void audit_kernel(int64_t n, int64_t n_pad, int R, int ncov, const int8_t *left,
+                                                      const int8_t *right, const double *alpha, const double *beta,
+                                                      const int64_t *pi, const int64_t *pj, const double *Q,
+                                                      const double *U, double pf_mu, double pf_tau, double pf_eps,
+                                                      double pf_ku, double lr_lam, double lr_tau, double lr_eps,
+                                                      double *out) {
+  __shared__ double es[AUD_T];
+  __shared__ double red[AUD_T / 64][8];
+  const int tid = threadIdx.x;
+  const int64_t t = blockIdx.x, i = pi[t], j = pj[t];
+  const int8_t *a = left + i * n_pad, *b = right + j * n_pad;
+  const double al = alpha[i], be = beta[j];
+  double ee = 0, se = 0, cr = 0, cu[4] = {0, 0, 0, 0};
+  for (int64_t s0 = 0; s0 < n_pad; s0 += AUD_T) {
+    const int64_t s = s0 + tid;
+    const int64_t nat = (s & ~31LL) + perm_nat((int)(s & 31));
+    const double e = (nat < n) ? ((double)a[s] - al) * ((double)b[s] - be) : 0.0;
+    ee += e * e;
+    se += e;
+    for (int k = 0; k < ncov; ++k) cu[k] += U[k * n_pad + s] * e;
+    es[tid] = e;
+    __syncthreads();
+    if (tid < R)
+      for (int q = 0; q < AUD_T; ++q) cr += Q[(s0 + q) * R + tid] * es[q];
+    __syncthreads();
+  }
+  double v[7] = {ee, se, tid < R ? cr * cr : 0.0, cu[0], cu[1], cu[2], cu[3]};
+  for (int q = 0; q < 7; ++q)
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o);
+  if ((tid & 63) == 0)
+    for (int q = 0; q < 7; ++q) red[tid >> 6][q] = v[q];
+  __syncthreads();
+  if (tid == 0) {
+    double s7[7];
+    for (int q = 0; q < 7; ++q) s7[q] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+    const double EE = s7[0], SE = s7[1], QQ = s7[2], dn = (double)n;
+    double uu = 0.0;
+    for (int k = 0; k < ncov; ++k) uu += s7[3 + k] * s7[3 + k];
+    out[5 * t + 0] = pf_mu > 0 ? (pf_mu - pf_eps) * EE - (pf_mu + pf_tau) * SE * SE / dn - pf_ku * uu : -INFINITY;
+    out[5 * t + 1] = R > 0 ? lr_lam * (EE - SE * SE / dn) - lr_tau * SE * SE / dn - lr_eps * EE - QQ : -INFINITY;
+    out[5 * t + 2] = EE;
+    out[5 * t + 3] = SE;
+    out[5 * t + 4] = QQ;
+  }
+}
+
+extern "C" int gmat_epi_audit(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *out5) {
+  GMAT_CHECK(e && (n_pairs == 0 || (pairs && out5)), GMAT_E_ARG, "gmat_epi_audit: bad arguments");
+  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_audit: bad kind");
+  if (n_pairs == 0) return GMAT_OK;
+  int lc, rc;
+  kind_codings(kind, &lc, &rc);
+  GMAT_TRY(build_coding(e, lc));
+  GMAT_TRY(build_coding(e, rc));
+  for (int64_t t = 0; t < n_pairs; ++t)
+    GMAT_CHECK(pairs[2 * t] >= 0 && pairs[2 * t] < e->m && pairs[2 * t + 1] >= 0 && pairs[2 * t + 1] < e->m,
+               GMAT_E_ARG, "pair %lld out of range", (long long)t);
+  std::vector<int64_t> hi(n_pairs), hj(n_pairs);
+  for (int64_t t = 0; t < n_pairs; ++t) {
+    hi[t] = pairs[2 * t];
+    hj[t] = pairs[2 * t + 1];
+  }
+  DBuf di, dj, dout;
+  GMAT_TRY(di.alloc(n_pairs * 8));
+  GMAT_TRY(dj.alloc(n_pairs * 8));
+  GMAT_TRY(dout.alloc(n_pairs * 5 * 8));
+  GMAT_HIP(hipMemcpy(di.p, hi.data(), n_pairs * 8, hipMemcpyHostToDevice));
+  GMAT_HIP(hipMemcpy(dj.p, hj.data(), n_pairs * 8, hipMemcpyHostToDevice));
+  const int R = e->lr_R > 0 && e->lr_Bs.p ? e->lr_R : 0;
+  GMAT_CHECK(R <= AUD_T, GMAT_E_ARG, "gmat_epi_audit: rank %d > %d", R, AUD_T);
+  hipLaunchKernelGGL(audit_kernel, dim3((unsigned)n_pairs), dim3(AUD_T), 0, e->s, e->n, e->n_pad, R, e->pf_ncov,
+                     screen_panel(e, lc), screen_panel(e, rc), e->code[lc].soff.as<double>(),
+                     e->code[rc].soff.as<double>(), di.as<int64_t>(), dj.as<int64_t>(), e->lr_Bs.as<double>(),
+                     e->pf_U.as<double>(), e->pf_mu, e->pf_tau, e->pf_eps, e->pf_ku, e->lr_lam, e->lr_tau, e->lr_eps,
+                     dout.as<double>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipMemcpyAsync(out5, dout.p, n_pairs * 5 * 8, hipMemcpyDeviceToHost, e->s));
+  GMAT_HIP(hipStreamSynchronize(e->s));
+  return GMAT_OK;
+}
+
 namespace {
 
 int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, int64_t *n_hits) {

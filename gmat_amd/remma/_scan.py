@@ -76,6 +76,16 @@ class EpiPlan:
                 "gmat_epi_pairs")
         return tuple(out)
 
+    def audit(self, kind, pairs):
+        """Certified lower bounds of e'Pe the screens test with, evaluated exactly for the listed
+        pairs: columns (prefilter bound, low-rank bound, |e|^2, 1'e, |Q'e|^2); compare with
+        pairs()' exact var (a ratio var / bound < 1 would be a certificate bug)."""
+        pairs = N.i64(np.asarray(pairs).reshape(-1, 2))
+        out = np.zeros((pairs.shape[0], 5))
+        N.check(self._lib.gmat_epi_audit(self._h, KINDS[kind], N.ptr(pairs), pairs.shape[0], N.ptr(out)),
+                "gmat_epi_audit")
+        return out
+
     def stats(self):
         s = np.zeros(10)
         N.check(self._lib.gmat_epi_stats(self._h, N.ptr(s)), "gmat_epi_stats")

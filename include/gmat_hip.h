@@ -124,6 +124,11 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
  * [6] total seconds, [7] screen kernel launches, [8] screen level (-1 low-rank, 0 MX, k int8 slices),
  * [9] bound coefficient */
 int gmat_epi_stats(const gmat_epi *e, double *out10);
+/* Diagnostic: the certified lower bounds of e'Pe that the screens test with, evaluated exactly in
+ * fp64 for listed pairs (i, j) (e = the screen codes' centred product over the real individuals):
+ * out5[5 t ..] = {prefilter bound, low-rank bound, |e|^2, 1'e, |Q'e|^2} (-inf where the plan has no
+ * such screen).  Compared with the exact e'Pe of gmat_epi_pairs, every ratio must be >= 1. */
+int gmat_epi_audit(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *out5);
 /* screen certificates of the plan: [0] rank of the low-rank spectral screen (padded to 128; 0 =
  * none, scans use the fp6 quadratic form), [1] its lam, [2] the prefilter's mu, [3] n_pad.  In
  * gmat_epi_stats, [8] = -1 marks a scan screened by the low-rank bound. */

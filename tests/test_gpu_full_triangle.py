@@ -81,9 +81,30 @@ def _audit(g, pvp, py, kind, p_cuts):
     return exh
 
 
+def _certificates(g, pvp, py, kind, pairs):
+    """exact var >= each screen's certified lower bound (gmat_epi_audit) on every listed pair"""
+    from gmat_amd.remma._scan import EpiPlan
+    with EpiPlan(g, pvp, py) as plan:
+        _, var, _, _ = plan.pairs(kind, pairs)
+        lb = plan.audit(kind, pairs)
+    worst = {}
+    for col, name in ((0, "prefilter"), (1, "lowrank")):
+        pos = lb[:, col] > 0
+        assert pos.sum() > 0.1 * pairs.shape[0], (name, pos.sum())
+        r = var[pos] / lb[pos, col]
+        assert r.min() >= 1.0, (name, float(r.min()))
+        worst[name] = float(r.min())
+    print("min exact var / certified bound:", worst)
+
+
 def test_full_triangle_aa(aa_cohort):
     geno, g, pvp, py = aa_cohort
     exh = _audit(g, pvp, py, "AA", (1e-5, 1e-3))
+    rng = np.random.default_rng(5)
+    i = rng.integers(0, g.m - 1, 8000)
+    j = rng.integers(0, g.m, 8000)
+    near = np.column_stack([exh[0], exh[1]])[exh[5] >= 1e-5]
+    _certificates(g, pvp, py, "AA", np.vstack([np.column_stack([i, j])[i < j], near]))
     assert np.sum(exh[5] < 1e-5) >= 1 and exh[0].size > 1000, exh[0].size
     # the exhaustive level itself against the oracle (rows at both ends of the triangle)
     from oracle import gmat_oracle as O
@@ -100,6 +121,11 @@ def test_full_triangle_ad_dd(small_cohort, kind):
     geno, g, pvp, py = small_cohort
     exh = _audit(g, pvp, py, kind, (1e-5, 1e-3))
     assert exh[0].size > 100, exh[0].size
+    rng = np.random.default_rng(6)
+    i = rng.integers(0, g.m, 4000)
+    j = rng.integers(0, g.m, 4000)
+    sel = (i < j) if kind == "DD" else np.ones(i.size, bool)
+    _certificates(g, pvp, py, kind, np.vstack([np.column_stack([i, j])[sel], np.column_stack([exh[0], exh[1]])]))
     if kind == "AD":  # i == j pairs are part of the exhaustive AD scan
         from gmat_amd import _native as N
         from gmat_amd.remma._scan import EpiPlan

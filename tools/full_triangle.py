@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--p-cuts", default="1e-5,1e-4,1e-3")
     ap.add_argument("--pairs-per-call", type=float, default=6e7, help="exhaustive rows per call (progress lines)")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "full_triangle"))
+    ap.add_argument("--audit-pairs", type=int, default=200000)
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     import bench
@@ -139,6 +140,31 @@ def main():
             rec["diff"]["%g/%s" % (pc, name)] = d
             ok = ok and d["symmetric_difference"] == 0 and d["values_byte_identical"]
             log("p_cut %g %s: %s" % (pc, name, json.dumps(d)))
+    rec["identical"] = bool(ok)
+    # certificate audit: exact var / certified lower bound over random pairs of the triangle and the
+    # pairs just above the smallest threshold (the ones the screens must reject with least room)
+    rng = np.random.default_rng(7)
+    ri = rng.integers(0, m - 1, 600000)
+    rj = rng.integers(0, m, 600000)
+    keep = (ri < rj) if kind != "AD" else np.ones(ri.size, bool)
+    samp = np.column_stack([ri[keep], rj[keep]])[:args.audit_pairs]
+    near_pairs = np.column_stack([exh[0], exh[1]])[(exh[5] >= p_cuts[0]) & (exh[5] < 2 * p_cuts[0])]
+    rec["audit"] = {}
+    for name, pr in (("random", samp), ("near_threshold", near_pairs)):
+        if not pr.shape[0]:
+            continue
+        t1 = time.perf_counter()
+        _, var, _, _ = plan.pairs(kind, pr)
+        lb = plan.audit(kind, pr)
+        a = {"pairs": int(pr.shape[0]), "s": time.perf_counter() - t1}
+        for col, scr in ((0, "prefilter"), (1, "lowrank")):
+            pos = lb[:, col] > 0
+            r = var[pos] / lb[pos, col]
+            a[scr] = {"bound_positive": int(pos.sum()), "min_ratio_var_over_bound": float(r.min()) if r.size else None,
+                      "median_ratio": float(np.median(r)) if r.size else None}
+            ok = ok and (not r.size or float(r.min()) >= 1.0)
+        rec["audit"][name] = a
+        log("audit %s: %s" % (name, json.dumps(a)))
     rec["identical"] = bool(ok)
     p0 = p_cuts[0]
     sel = exh[5] < p0
