@@ -181,7 +181,9 @@ def grm_bench(n, m_grm, seed, reps=5):
     from gmat_amd import _native as N, synth
     from gmat_amd.plink import Geno
     lib = N.ensure_device()
-    geno = synth.simulate_genotypes(n, m_grm, seed=seed + 11)
+    # full-sib families of five in the last generation: A and A x A distinct from the identity, so the
+    # configs[1] REML below is identifiable and converges
+    geno = synth.simulate_genotypes(n, m_grm, seed=seed + 11, family_size=5)
     body = np.frombuffer(synth.pack_bed(geno)[3:], dtype=np.uint8)
     g = Geno(body=body, n_id=n, n_snp=m_grm)
     k = np.empty((n, n))
@@ -228,7 +230,8 @@ def reml_bench(k, seed):
     st = np.zeros(4)
     N.check(lib.gmat_reml_stats(N.ptr(st)), "gmat_reml_stats")
     flop = st[3]
-    return {"config": "configs[1]: 2-GRM REML [A, AxA] n=%d" % n, "iters": int(st[1]),
+    return {"config": "configs[1]: 2-GRM REML [A, AxA] n=%d, full-sib families of 5, simulated (0.4, 0.2, 0.4)" % n,
+            "iters": int(st[1]), "converged": bool(int(st[1]) < 200),
             "ms_per_iter": st[2] * 1e3, "wall_s": wall, "var": [float(v) for v in var],
             "fp64_tflops": flop / st[2] / 1e12 if st[2] > 0 else None,
             "frac": flop / st[2] / 1e12 / FP64_PEAK_TFLOPS if st[2] > 0 else None,
@@ -389,37 +392,35 @@ def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), rep
     return out
 
 
-def cfg5_main(args):
-    """BASELINE configs[4]: synthetic 5,000 x 100,000 cohort, 5-GRM model [A, D, AxA, AxD, DxD]:
-    GRMs (agmat / dgmat_as products), weighted EM-AI REML (first --reml-iters iterations timed),
-    P / Py, then the exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included)
-    scans at p_cut, rows sharded over the ranks like configs[3].  One JSON line."""
+def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
+    """BASELINE configs[4]: synthetic 5,000 x 100,000 cohort (full-sib families of five in the last
+    generation), 5-GRM model [A, D, AxA, AxD, DxD]: GRMs (agmat / dgmat_as products), weighted EM-AI
+    REML (uvlmm_varcom.py:41-99, up to reml_iters iterations or convergence), P / Py, then the
+    exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included) scans at p_cut, rows
+    sharded over the ranks like configs[3] (GRM and REML on rank 0).  Returns the record on rank 0."""
     import ctypes
     from gmat_amd import dist, synth
     from gmat_amd import _native as N
     from gmat_amd.plink import Geno
-    from gmat_amd.remma._scan import EpiPlan
     from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat, projection
     from scipy.sparse import identity
-    backend = dist.init()
-    rank, ws, _ = dist.world()
     lib = N.ensure_device()
-    n, m = args.n_id, args.n_snp
     nb = (n + 3) // 4
     t0 = time.time()
     lo, hi = dist.snp_shard(m, rank, ws)
-    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=args.seed)
+    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed, family_size=5)
     if dist.allreduce_sum(n_bad) > 0:
-        shard = synth.simulate_genotypes(n, m, seed=args.seed)[lo:hi]
+        shard = synth.simulate_genotypes(n, m, seed=seed, family_size=5)[lo:hi]
     local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
+    del shard
     g = Geno(body=dist.allgather_packed(local, m, nb), n_id=n, n_snp=m)
-    log("cfg5 cohort %d x %d in %.1f s" % (n, m, time.time() - t0))
+    t_cohort = time.time() - t0
+    log("cfg5 cohort %d x %d in %.1f s" % (n, m, t_cohort))
     var = np.array([0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
-    out = {"metric": "SNP-pairs tested/sec (whole node), configs[4]", "unit": "SNP-pairs/s", "n_gpus": ws,
-           "higher_is_better": True, "data": "synthetic", "dtype": "fp6xfp4/fp64",
-           "config": {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP, p_cut=%g"
-                                  % (n, m, args.p_cut), "n_id": n, "n_snp": m, "p_cut": args.p_cut,
-                      "parallelism": "rows folded over %d rank(s), backend %s" % (ws, backend or "single")}}
+    out = {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP (full-sib families of "
+                       "5), p_cut=%g" % (n, m, p_cut), "n_gpus": ws,
+           "parallelism": "scan rows folded over %d rank(s), backend %s; GRM and REML on rank 0" % (ws, backend or "single"),
+           "cohort_s": t_cohort}
     pvp = py = None
     if rank == 0:
         mats, grm = [], {}
@@ -431,21 +432,25 @@ def cfg5_main(args):
             st = np.zeros(4)
             N.check(lib.gmat_grm_stats(N.ptr(st)), "gmat_grm_stats")
             grm[name] = {"kernel_ms": st[0] * 1e3, "wall_ms": (time.perf_counter() - t1) * 1e3,
-                         "gflops_kernel": 2.0 * n * n * m / st[0] / 1e9}
+                         "gflops_kernel": 2.0 * n * n * m / st[0] / 1e9,
+                         "int8_frac_of_peak": st[1] / st[0] / 1e12 / INT8_PEAK_TOPS}
             mats.append(k)
         a, d = mats
         gl = [a, d, a * a, a * d, d * d]
-        rng = np.random.Generator(np.random.PCG64(args.seed + 1))
+        rng = np.random.Generator(np.random.PCG64(seed + 1))
         y = np.ones(n)
         for k, s_ in zip(gl, var[:5]):
             y += np.sqrt(s_) * (np.linalg.cholesky(k + 1e-3 * np.eye(n)) @ rng.standard_normal(n))
         y += np.sqrt(var[5]) * rng.standard_normal(n)
         t1 = time.perf_counter()
-        est = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), gl, maxiter=args.reml_iters)
+        est = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), gl, maxiter=reml_iters)
         st = np.zeros(4)
         N.check(lib.gmat_reml_stats(N.ptr(st)), "gmat_reml_stats")
-        out["reml"] = {"iters_run": int(st[1]), "ms_per_iter": st[2] * 1e3, "wall_s": time.perf_counter() - t1,
-                       "fp64_tflops": st[3] / st[2] / 1e12 if st[2] else None, "var_after": [float(v) for v in est]}
+        out["reml"] = {"iters": int(st[1]), "maxiter": reml_iters, "converged": bool(int(st[1]) < reml_iters),
+                       "ms_per_iter": st[2] * 1e3, "wall_s": time.perf_counter() - t1,
+                       "fp64_tflops": st[3] / st[2] / 1e12 if st[2] else None,
+                       "frac": st[3] / st[2] / 1e12 / FP64_PEAK_TFLOPS if st[2] else None,
+                       "var": [float(v) for v in est], "simulated": var.tolist()}
         out["grm"] = grm
         pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), gl, var)
     pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
@@ -455,15 +460,14 @@ def cfg5_main(args):
     out["plan_create_s"] = time.perf_counter() - t1
     out["setup"] = plan.setup_stats()
     out["lowrank_rank"] = plan.lowrank_rank()
-    total = 0.0
-    t_all = 0.0
+    total = t_all = 0.0
     for kind in ("DD", "AD"):
         rows = dist.rank_rows(kind, m, rank, ws)
-        plan.scan(kind, rows[:8], args.p_cut)  # builds the coding (side vectors) outside the timing
+        plan.scan(kind, rows[:8], p_cut)  # builds the coding (side vectors) outside the timing
         lib.gmat_device_synchronize()
         dist.barrier()
         t1 = time.perf_counter()
-        res = plan.scan(kind, rows, args.p_cut)
+        res = plan.scan(kind, rows, p_cut)
         lib.gmat_device_synchronize()
         dist.barrier()
         dt = dist.allreduce_max(time.perf_counter() - t1)
@@ -474,10 +478,25 @@ def cfg5_main(args):
                              "candidates": int(dist.allreduce_sum(st["candidates"])), "screen_level": int(st["n_slice"])}
         total += pairs
         t_all += dt
-    out["value"] = total / t_all
+    out["pairs_per_s"] = total / t_all
     plan.close()
     g.close()
+    return out if rank == 0 else None
+
+
+def cfg5_main(args):
+    """bench.py --config cfg5: the configs[4] leg alone, as its own JSON line."""
+    from gmat_amd import dist
+    backend = dist.init()
+    rank, ws, _ = dist.world()
+    rec = cfg5_leg(args.n_id, args.n_snp, args.p_cut, args.seed, args.reml_iters, rank, ws, backend)
     if rank == 0:
+        out = {"metric": "SNP-pairs tested/sec (whole node), configs[4]", "value": rec["pairs_per_s"],
+               "unit": "SNP-pairs/s", "n_gpus": ws, "higher_is_better": True, "data": "synthetic",
+               "dtype": "fp6xfp4/fp64", "config": {"workload": rec["workload"], "n_id": args.n_id,
+                                                   "n_snp": args.n_snp, "p_cut": args.p_cut,
+                                                   "parallelism": rec["parallelism"]}}
+        out.update({k: v for k, v in rec.items() if k not in ("workload", "parallelism")})
         print(json.dumps(out), flush=True)
 
 
@@ -502,7 +521,8 @@ def main():
                     help="recompute the exhaustive (unscreened) scan live for the full-triangle check (~2 min / N)")
     ap.add_argument("--config", default="cfg3", choices=["cfg3", "cfg5"],
                     help="cfg3: the headline (configs[2]/[3]); cfg5: configs[4] (5,000 x 100,000, 5 GRMs, epiDD/epiAD)")
-    ap.add_argument("--reml-iters", type=int, default=5)
+    ap.add_argument("--reml-iters", type=int, default=200, help="configs[4] REML: maxiter (the reference's default)")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the configs[4] leg of the default line")
     ap.add_argument("--covariates", action="store_true",
                     help="profiling: the timed step uses the covariate design of the covariates leg")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
@@ -665,6 +685,12 @@ def main():
     if rank == 0 and ws == 1 and not args.no_eff:
         log("effect screen")
         eff = eff_bench(g, pvp, py, plan, n, m, args.p_cut, args.seed, geno=geno, cpu_budget=args.cpu_budget)
+    plan.close()
+    g.close()
+    cfg5 = None
+    if not args.no_cfg5:  # every rank: the configs[4] scans are sharded like configs[3]
+        log("configs[4] leg")
+        cfg5 = cfg5_leg(5000, 100000, args.p_cut, args.seed, args.reml_iters, rank, ws, backend)
     if rank == 0:
         if parity is None:
             parity = {}
@@ -680,12 +706,11 @@ def main():
                                          % (ws, backend or "single")},
                "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "setup": setup, "grm": grm,
                "reml": reml, "end_to_end": e2e, "covariates": cov, "eff_screen": eff, "split_rehearsal": split,
+               "cfg5": cfg5,
                "scan": {"hits_per_step": hits_all, "candidates_per_step": cands_all,
                         "screen_s_per_step_rank0": screen_s / args.steps, "side_s_per_step_rank0": side_s / args.steps,
                         "refine_s_per_step_rank0": ref_s / args.steps}}
         print(json.dumps(out), flush=True)
-    plan.close()
-    g.close()
     if parity is not None and not parity.get("identical", True):
         log("PARITY FAILURE: GPU hits differ from the oracle on the sampled rows")
         sys.exit(3)

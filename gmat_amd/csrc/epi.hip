@@ -111,6 +111,7 @@ struct ScreenArgs {
   double pf_su[4];
   double pf_ku;
   int pf_ncov;
+  unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -428,83 +429,98 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   }
   // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
   // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
-  // per-row: i (as double; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
-  __shared__ double rowv[7][PF_T];
-  const double n = a.n_id;
+  // The test runs in fp32 with a certified slack (fp64 costs twice the issue slots and two registers
+  // per value): every quantity below is a signed sum of the monomials of (a - alpha)^2 (b - beta)^2 or
+  // (a - alpha)(b - beta) over the individuals, whose absolute values add up to at most
+  //   M = sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2   (|1'e| <= sqrt(n M)),
+  // so the fp32 evaluation (about a dozen roundings of 2^-24 each, inputs rounded from fp64 included)
+  // is off by at most 2^-20 M for |e|^2 and 2^-21 sqrt(n M) for 1'e, and vlo = (mu - eps)|e|^2 -
+  // (mu + tau)(1'e)^2/n by at most 2^-19 (2 mu + tau) M: vlo is lowered by 2^-17 (2 mu + tau) M.  eff
+  // = sL3 c3 - beta sa + alpha (beta spy - sb) is off by at most 2^-20 times the sum of the three
+  // terms' magnitudes, which is added to eff_hi with the int8 slicing bound.  The final comparison's
+  // three roundings are covered by the factor 1 + 2^-18.
+  // per-row: i (-1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
+  __shared__ int rowi[PF_T];
+  __shared__ float rowv[6][PF_T];
+  const float n = (float)a.n_id;
   if (tid < PF_T) {
     const int r = min(r0 + tid, a.n_rows - 1);
     const int64_t i = a.rows[r];
     const double al = a.alpha[i], ca = a.csum_l[i];
-    rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
-    rowv[1][tid] = al;
-    rowv[2][tid] = ca;
-    rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
-    rowv[4][tid] = a.sL3[i];
-    rowv[5][tid] = a.sa[i];
-    rowv[6][tid] = (2.0 + al) * (2.0 + al);
+    rowi[tid] = a.mono_l[i] ? -1 : (int)i;
+    rowv[0][tid] = (float)al;
+    rowv[1][tid] = (float)ca;
+    rowv[2][tid] = (float)(a.csq_l[i] - 2.0 * al * ca);
+    rowv[3][tid] = (float)a.sL3[i];
+    rowv[4][tid] = (float)a.sa[i];
+    rowv[5][tid] = (float)((2.0 + al) * (2.0 + al));
   }
   __syncthreads();
-  // vlo = (mu - eps)|e|^2 - (mu + tau)(1'e)^2/n - 1e-12 mu (|expansion terms| + (1'e)^2/n), the
-  // absolute terms bounded by sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2
-  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
+  const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id);
+  const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
+  const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
+  constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int64_t j = c0 + 64 * wc + 32 * q + c;
     const int J = (int)(j / 32);
     const bool jok = j < a.m && j >= a.j_lo;
     // per-column: beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum, beta spy - sb,
-    // sum_k (b + beta)^2
-    double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
+    // sum_k (b + beta)^2 (fp64 sums rounded once)
+    float cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
     bool cmono = true;
     if (jok) {
-      cbe = a.beta[j];
-      ccb = a.csum_r[j];
-      const double cb2 = a.csq_r[j];
-      cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
-      cnb = n * cbe - ccb;
-      cbsb = cbe * a.spy - a.sb[j];
-      cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+      const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j], dn = a.n_id;
+      cbe = (float)be;
+      ccb = (float)cb;
+      cC1n = (float)(cb2 - 2.0 * be * cb + dn * be * be);
+      cnb = (float)(dn * be - cb);
+      cbsb = (float)(be * a.spy - a.sb[j]);
+      cmag = (float)(cb2 + 2.0 * be * cb + dn * be * be);
       cmono = a.mono_r[j];
+    }
+    bool live[16];
+    unsigned n_live = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+      const int iv = rowi[rl];
+      bool lv = false;
+      if (r < a.n_rows && jok && iv >= 0 && !cmono && !(a.tri && j <= (int64_t)iv)) {
+        const float al = rowv[0][rl], sL3 = rowv[3][rl], be = cbe;
+        float c3 = 0.0f;
+#pragma unroll
+        for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
+        const float t1 = sL3 * c3, t2 = be * rowv[4][rl], t3 = al * cbsb;
+        const float eff = t1 - t2 + t3;
+        const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
+        const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
+        // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
+        const float ee = sa2b2 + be * (be * rowv[2][rl] - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n);
+        const float se = sab - be * rowv[1][rl] + al * cnb;
+        const float vlo = mu_e * ee - k1 * se * se - k2 * rowv[5][rl] * cmag;
+        lv = !(vlo > 0.0f) || eff_hi * eff_hi * CMP >= chi_cut * vlo;
+      }
+      live[e] = lv;
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
       const bool rok = r < a.n_rows;
-      const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
-      bool live = false;
-      const double iv = rowv[0][rl];
-      if (rok && jok && iv >= 0.0 && !cmono) {
-        const int64_t i = (int64_t)iv;
-        if (!(a.tri && j <= i)) {
-          const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
-          double c3 = 0.0;
-#pragma unroll
-          for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[q][t][e];
-          const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
-          const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
-          const double sab = (double)acc4[q][0][e], sa2b = (double)acc4[q][1][e], sab2 = (double)acc4[q][2][e],
-                       sa2b2 = (double)acc4[q][3][e];
-          // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
-          const double ee =
-              sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
-          const double se = sab - be * rowv[2][rl] + al * cnb;
-          const double vlo = mu_e * ee - k1 * se * se - k2 * rowv[6][rl] * cmag;
-          live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
-        }
-      }
-      const unsigned long long bal = __ballot(live);
+      const unsigned long long bal = __ballot(live[e]);
+      n_live += (unsigned)__popcll(bal);
       const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
       if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
       if (blk && rok && jok) {
-        const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+        const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
         for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
         if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
 #pragma unroll
           for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
       }
-      __builtin_amdgcn_sched_barrier(0);  // one element's prefilter at a time
     }
+    if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
   }
 }
 
@@ -1855,65 +1871,75 @@ struct PairArgs {
   int64_t *oi, *oj;  // surviving pairs
 };
 
-// one wave per pair, 8 individuals per lane and step
+// One wave per pair, PS_PPW pairs per wave; z, diag(P) and Py staged once per workgroup in LDS as
+// fp32.  The sums run in fp32 with a certified slack: each lane adds its n_pad / 64 terms per
+// quantity and the wave reduces the lane partials in fp64; the inputs' fp32 rounding (U = P x
+// codes, z, diag(P), Py: 2^-24 relative each) adds a few 2^-24 per term (the bound is below; it is
+// carried to the pair screen's variance bound, side[np + p], and to its eff bound, side[3 np + p]).
+constexpr int PS_PPW = 8;
 __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
-  const int lane = threadIdx.x & 63;
-  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (p >= x.np) return;
-  const int64_t i = x.ci[p], j = x.cj[p], n_pad = x.n_pad;
-  const double al = x.alpha[i], be = x.beta[j], ab = al * be;
-  const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
-  const float *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
-  double s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
-  for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
-    const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
-    const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
+  extern __shared__ __attribute__((aligned(16))) float zdp[];  // [3][n_pad]: z, diag(P), Py
+  const int64_t n_pad = x.n_pad;
+  for (int64_t q = threadIdx.x; q < n_pad; q += blockDim.x) {
+    zdp[q] = (float)x.z[q];
+    zdp[n_pad + q] = (float)x.dg[q];
+    zdp[2 * n_pad + q] = (float)x.py[q];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = 0; k < PS_PPW; ++k) {
+    const int64_t p = ((int64_t)blockIdx.x * 4 + wv) * PS_PPW + k;
+    if (p >= x.np) return;
+    const int64_t i = x.ci[p], j = x.cj[p];
+    const double dal = x.alpha[i], dbe = x.beta[j], dab = dal * dbe;
+    const float al = (float)dal, be = (float)dbe, ab = (float)dab;
+    const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
+    const float *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
+    float s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
+    for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
+      const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
+      const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
+      const float4 u0 = *(const float4 *)(ua + q0), u1 = *(const float4 *)(ua + q0 + 4);
+      const float4 v0 = *(const float4 *)(ub + q0), v1 = *(const float4 *)(ub + q0 + 4);
+      const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-    for (int k = 0; k < 8; k += 2) {
-      const v2f_ u2 = *(const v2f_ *)(ua + q0 + k), v2 = *(const v2f_ *)(ub + q0 + k);
-      const v2d_ z2 = *(const v2d_ *)(x.z + q0 + k), d2 = *(const v2d_ *)(x.dg + q0 + k),
-                 y2 = *(const v2d_ *)(x.py + q0 + k);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double av = (double)ca[k + h], bv = (double)cb[k + h], w = av * bv;
-        const double tu = be * (double)u2[h], tv = al * (double)v2[h], tz = ab * z2[h];
+      for (int h = 0; h < 8; ++h) {
+        const float av = (float)ca[h], bv = (float)cb[h], w = av * bv;  // exact small integers
+        const float z = zdp[q0 + h], d = zdp[n_pad + q0 + h], y = zdp[2 * n_pad + q0 + h];
+        const float tu = be * uu[h], tv = al * vv[h], tz = ab * z;
         s1 += w * ((tz - tu) - tv);
-        s1a += w * ((fabs(tu) + fabs(tv)) + fabs(tz));
-        s2 += av * (double)v2[h];
-        s2a += fabs(av * (double)v2[h]);
-        s3 += d2[h] * (w * w);
-        s3a += fabs(d2[h]) * (w * w);
-        const double e = (av - al) * (bv - be), ey = e * y2[h];
+        s1a += w * ((fabsf(tu) + fabsf(tv)) + fabsf(tz));
+        s2 += av * vv[h];
+        s2a += av * fabsf(vv[h]);
+        s3 += d * (w * w);
+        s3a += fabsf(d) * (w * w);
+        const float ey = ((av - al) * (bv - be)) * y;
         ef += ey;
-        efa += fabs(ey);
+        efa += fabsf(ey);
         sw += w * w;
       }
     }
-  }
+    double r[9] = {s1, s1a, s2, s2a, s3, s3a, ef, efa, sw};
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off);
-    s1a += __shfl_xor(s1a, off);
-    s2 += __shfl_xor(s2, off);
-    s2a += __shfl_xor(s2a, off);
-    s3 += __shfl_xor(s3, off);
-    s3a += __shfl_xor(s3a, off);
-    ef += __shfl_xor(ef, off);
-    efa += __shfl_xor(efa, off);
-    sw += __shfl_xor(sw, off);
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) r[t] += __shfl_xor(r[t], off);
+    if (lane != 0) continue;
+    const double t3 = dbe * dbe * x.qa[i], t5 = dal * dal * x.qb[j], t7 = dab * dab * x.zz, t8 = 2.0 * dab * r[2],
+                 t4 = -2.0 * dab * dbe * x.ra[i], t6 = -2.0 * dab * dal * x.rb[j];
+    x.side[p] = r[4] + 2.0 * r[0] + t3 + t5 + t7 + t8 + t4 + t6;
+    // fp32 sums: a lane adds n_pad / 64 terms of at most 4 roundings each, so a sum is within
+    // (n_pad / 64 + 4) 2^-24 of its absolute sum (the lane reduction is fp64); fsl doubles that.  Plus
+    // U itself in fp32 and the fp64 rounding of U = P x codes and of the host terms (far inside 1e-10
+    // of the magnitudes).  side[3 np + p] is the eff bound's slack.
+    const double fsl = 2.0 * (double)(n_pad / 64 + 8) * 0x1p-24;
+    const double su = 2.0 * r[1] + 2.0 * fabs(dab) * r[3];
+    x.side[x.np + p] = fsl * (su + r[5]) + 1e-10 * (r[5] + su + fabs(t3) + fabs(t5) + fabs(t7) + fabs(t4) + fabs(t6));
+    x.side[2 * x.np + p] = r[6];
+    x.side[3 * x.np + p] = (fsl + 1e-10) * r[7];
+    x.side[4 * x.np + p] = r[8];
   }
-  if (lane != 0) return;
-  const double t3 = be * be * x.qa[i], t5 = al * al * x.qb[j], t7 = ab * ab * x.zz, t8 = 2.0 * ab * s2,
-               t4 = -2.0 * ab * be * x.ra[i], t6 = -2.0 * ab * al * x.rb[j];
-  x.side[p] = s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
-  // U in fp32: |U32 - U| <= 2^-24 |U| per entry, i.e. 2^-24 (1 + 2^-23) of the s1 / s2 magnitudes;
-  // the fp64 rounding of the dots and of U = P x codes itself (n u |P||a| per entry): far inside
-  // 1e-10 of the magnitudes summed
-  const double su = 2.0 * s1a + 2.0 * fabs(ab) * s2a;
-  x.side[x.np + p] = 6.0e-8 * su + 1e-10 * (s3a + su + fabs(t3) + fabs(t5) + fabs(t7) + fabs(t4) + fabs(t6));
-  x.side[2 * x.np + p] = ef;
-  x.side[3 * x.np + p] = efa;
-  x.side[4 * x.np + p] = sw;
 }
 
 // PP pairs per workgroup (PP / 32 column tiles x four 32-row tiles, one wave each); the pairs' w
@@ -2012,7 +2038,7 @@ __global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
   const double M = (red[tid] + red[PP + tid]) + (red[2 * PP + tid] + red[3 * PP + tid]);
   const double var = M + x.side[p], sw = x.side[4 * x.np + p];
   const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
-  const double eff_hi = fabs(x.side[2 * x.np + p]) + 1e-10 * x.side[3 * x.np + p];
+  const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
   if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
     const unsigned long long k = atomicAdd(x.counter, 1ULL);
     x.oi[k] = x.ci[p];
@@ -2897,8 +2923,6 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   x.oj = e->cand2_j.as<int64_t>();
   if (reset) GMAT_HIP(hipMemsetAsync(e->counter2.p, 0, 8, st));
   if (np > 0) {
-  hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, x);
-  GMAT_HIP(hipGetLastError());
   const size_t lds = lds_of(pp);
   static bool attr = false;
   if (!attr) {
@@ -2908,8 +2932,13 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
                                  160 * 1024 - 256));
     GMAT_HIP(hipFuncSetAttribute((const void *)pair_mx_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  160 * 1024 - 256));
+    GMAT_HIP(hipFuncSetAttribute((const void *)pair_side_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - 256));
     attr = true;
   }
+  hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4 * PS_PPW)), dim3(256),
+                     (size_t)3 * e->n_pad * sizeof(float), st, x);
+  GMAT_HIP(hipGetLastError());
   if (pp == 96)
     hipLaunchKernelGGL(pair_mx_kernel<96>, dim3((unsigned)cdiv(np, 96)), dim3(768), lds, st, x);
   else if (pp == 64)
@@ -3946,6 +3975,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // host waits only for the tile count, not for the flags and a host-side build
   const bool dev_tiles = use_lr && !use_stage2 && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
   DBuf tl_cnt, tl_h, tl_info;
+  DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
+  if (getenv("GMAT_LIVE_COUNT")) {
+    GMAT_TRY(live_cnt.alloc(8));
+    GMAT_HIP(hipMemset(live_cnt.p, 0, 8));
+  }
   if (dev_tiles) {
     GMAT_TRY(tl_cnt.alloc((size_t)TL_G * nJ * sizeof(int)));
     GMAT_TRY(tl_h.alloc((size_t)nJ * sizeof(int)));
@@ -4163,6 +4197,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.tile_rows = mxr[b].as<int>();
     sa.tile_side = nullptr;
     sa.pf_store = use_lr && S == 0;
+    sa.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
     sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
     sa.pfc_stride = (int64_t)Rn * m;
     sa.pf_mu = e->pf_mu;
@@ -4859,6 +4894,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
             ncand_total, t_stage2);
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
+  if (live_cnt.p) {
+    unsigned long long lc = 0;
+    GMAT_HIP(hipMemcpy(&lc, live_cnt.p, 8, hipMemcpyDeviceToHost));
+    fprintf(stderr, "gmat_epi_scan: %.0f pairs, prefilter keeps %llu pairs (%.4f%%), %.0f low-rank candidates\n",
+            pairs_tested, lc, 100.0 * (double)lc / std::max(pairs_tested, 1.0), ncand_total);
+  }
   const bool lr_only = use_lr && S_max_used == 0;
   e->stats[8] = lr_only ? -1 : S_max_used;
   e->stats[9] = lr_only ? e->lr_lam : (S_max_used == 0 ? e->rho_mx : e->rho[S_max_used]);

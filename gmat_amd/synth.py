@@ -16,8 +16,10 @@ _DOSE_TO_CODE = np.array([0b00, 0b10, 0b11], dtype=np.uint8)
 MISSING_CODE = 0b01
 
 
-def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01):
-    """Return an (n_snp, n_id) uint8 dosage matrix in {0,1,2} (SNP-major)."""
+def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01, family_size=None):
+    """Return an (n_snp, n_id) uint8 dosage matrix in {0,1,2} (SNP-major).  With family_size f the
+    last generation comes in full-sib families of f (both parents shared), which makes A and A x A
+    clearly distinct from the identity (the configs[1] REML cohort)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     freq = rng.uniform(0.1, 0.9, size=n_snp)
     n_blk = (n_snp + block - 1) // block
@@ -27,8 +29,11 @@ def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, ma
     for g in range(n_gen):
         n_next = n_id if g == n_gen - 1 else max(n_id, n_pop)
         new = np.empty((2 * n_next, n_snp), dtype=bool)
+        fam = None
+        if family_size and g == n_gen - 1:
+            fam = rng.integers(0, n_pop, size=(2, (n_next + family_size - 1) // family_size))
         for side in range(2):
-            par = rng.integers(0, n_pop, size=n_next)
+            par = rng.integers(0, n_pop, size=n_next) if fam is None else np.repeat(fam[side], family_size)[:n_next]
             pick = rng.integers(0, 2, size=(n_next, n_blk), dtype=np.uint8)
             pick = np.repeat(pick, block, axis=1)[:, :n_snp].astype(bool)
             h0 = pop[2 * par]
@@ -44,7 +49,8 @@ def simulate_genotypes(n_id, n_snp, seed=1, n_founder=60, n_gen=6, block=250, ma
     return geno
 
 
-def simulate_genotype_shard(n_id, n_snp, lo, hi, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01):
+def simulate_genotype_shard(n_id, n_snp, lo, hi, seed=1, n_founder=60, n_gen=6, block=250, maf_min=0.01,
+                            family_size=None):
     """SNPs [lo, hi) of ``simulate_genotypes(n_id, n_snp, seed)`` -- the same cohort, bit for bit --
     with only the shard's columns propagated through the pedigree (the expensive part); every
     random draw is made in the same order and size as the full generator (they are cheap), so
@@ -61,8 +67,11 @@ def simulate_genotype_shard(n_id, n_snp, lo, hi, seed=1, n_founder=60, n_gen=6, 
     for g in range(n_gen):
         n_next = n_id if g == n_gen - 1 else max(n_id, n_pop)
         new = np.empty((2 * n_next, hi - lo), dtype=bool)
+        fam = None
+        if family_size and g == n_gen - 1:
+            fam = rng.integers(0, n_pop, size=(2, (n_next + family_size - 1) // family_size))
         for side in range(2):
-            par = rng.integers(0, n_pop, size=n_next)
+            par = rng.integers(0, n_pop, size=n_next) if fam is None else np.repeat(fam[side], family_size)[:n_next]
             pick = rng.integers(0, 2, size=(n_next, n_blk), dtype=np.uint8)
             pick = np.repeat(pick[:, b_lo:b_hi], block, axis=1)[:, lo - b_lo * block:hi - b_lo * block].astype(bool)
             new[side::2] = np.where(pick, pop[2 * par + 1], pop[2 * par])

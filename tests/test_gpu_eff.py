@@ -221,7 +221,7 @@ def _oracle_setup(prefix, gmats_kind):
     return O, snp, dec, pvp, py
 
 
-@pytest.mark.parametrize("kind,maf", [("AA", False), ("AD", False), ("DD", True), ("AD", True)])
+@pytest.mark.parametrize("kind,maf", [("AA", False), ("AD", False), ("DD", False), ("AA", True), ("DD", True), ("AD", True)])
 def test_mouse_approx_pipeline(mouse, kind, maf, tmp_path):
     """remma_epiXX_approx / _maf_approx with seeded random pairs, end to end vs the oracle:
     variance estimate from the same random pairs, screen survivors, exact re-test, merge."""
