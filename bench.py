@@ -393,8 +393,8 @@ def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), rep
 
 
 def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
-    """BASELINE configs[4]: synthetic 5,000 x 100,000 cohort (full-sib families of five in the last
-    generation), 5-GRM model [A, D, AxA, AxD, DxD]: GRMs (agmat / dgmat_as products), weighted EM-AI
+    """BASELINE configs[4]: synthetic related 5,000 x 100,000 cohort, 5-GRM model [A, D, AxA, AxD, DxD]:
+    GRMs (agmat / dgmat_as products), weighted EM-AI
     REML (uvlmm_varcom.py:41-99, up to reml_iters iterations or convergence), P / Py, then the
     exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included) scans at p_cut, rows
     sharded over the ranks like configs[3] (GRM and REML on rank 0).  Returns the record on rank 0."""
@@ -408,17 +408,17 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
     nb = (n + 3) // 4
     t0 = time.time()
     lo, hi = dist.snp_shard(m, rank, ws)
-    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed, family_size=5)
+    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed)
     if dist.allreduce_sum(n_bad) > 0:
-        shard = synth.simulate_genotypes(n, m, seed=seed, family_size=5)[lo:hi]
+        shard = synth.simulate_genotypes(n, m, seed=seed)[lo:hi]
     local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
     del shard
     g = Geno(body=dist.allgather_packed(local, m, nb), n_id=n, n_snp=m)
     t_cohort = time.time() - t0
     log("cfg5 cohort %d x %d in %.1f s" % (n, m, t_cohort))
     var = np.array([0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
-    out = {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP (full-sib families of "
-                       "5), p_cut=%g" % (n, m, p_cut), "n_gpus": ws,
+    out = {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP, p_cut=%g" % (n, m, p_cut),
+           "n_gpus": ws,
            "parallelism": "scan rows folded over %d rank(s), backend %s; GRM and REML on rank 0" % (ws, backend or "single"),
            "cohort_s": t_cohort}
     pvp = py = None

@@ -112,6 +112,8 @@ struct ScreenArgs {
   double pf_ku;
   int pf_ncov;
   unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
+  uint32_t *lmask;  // compacted low-rank path: per (band row, 32-column block) the prefilter's live
+                    // pairs as a bit mask (bit c = column 32 J + c), or null
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -510,7 +512,10 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const unsigned long long bal = __ballot(live[e]);
       n_live += (unsigned)__popcll(bal);
       const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
-      if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+      if (rok && c == 0 && J < a.nJ) {
+        if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
+        if (a.lmask) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
+      }
       if (blk && rok && jok) {
         const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
@@ -726,7 +731,10 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     }
     const unsigned long long bal = __ballot(live);
     const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
-    if (rok && c == 0 && J < a.nJ) a.flags[(int64_t)r * a.nJ + J] = blk;
+    if (rok && c == 0 && J < a.nJ) {
+      if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
+      if (a.lmask) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
+    }
     if (blk && rok && jok) {
       const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
@@ -1576,6 +1584,208 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     J1t = J1n;
     par ^= 1;
   }
+}
+
+// ------------------------------------------------------------------ compacted low-rank screen
+// The low-rank screen of lr_screen_kernel on the prefilter's live PAIRS instead of its flagged
+// (band row, 32-column block) slots: at configs[2] 0.40 % of the pairs survive the prefilter but
+// 8.5 % of the 32-pair blocks hold one, so testing whole blocks multiplies ~21x the necessary work.
+// A slot is (band row r, 32 live second SNPs of r in ascending order: slot lists, lc_* kernels); a
+// tile is 16 slots (8 waves x 2 slots, the MX shape), one tile per workgroup.  Per 128-individual
+// stage the A tile image (Q' fp6, shared by every slot) and the slots' i-side nibble records come
+// through LDS-DMA as in lr_screen_kernel, and so do the 512 columns' j-side S1 planes (each column
+// its own SNP: 32 KB per stage), in an NSL-slot ring.  The chunk epilogue reads G' of the slot
+// rows and H of the columns from memory, the test reads the prefilter's stored operands (E3
+// slices, code products) and the per-SNP records; the bound and the test are lr_screen_kernel's.
+struct LrcArgs {
+  const uint8_t *tiles;  // [nC][nK] Q' tile images
+  const uint8_t *nib_i, *nib_j;
+  int nK, nC, R;
+  const int *slot_row, *slot_j;  // slot lists of the launch
+  const float *G, *H;            // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
+  const double *recL, *recR;     // per-SNP test records (LR_REC doubles each)
+  double lam, tau, eps, E;
+};
+constexpr int LRC_NSL = 3, LRC_JB = 64;          // ring slots; j-side bytes per column and stage (S1 plane)
+constexpr int LRC_SJ = MX_BI * 32 * LRC_JB;      // j-side bytes per stage (32 KB)
+
+__device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, int ri, int64_t i, int64_t j,
+                                         double lowrank) {
+  const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+  double c3 = 0.0;
+#pragma unroll
+  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (t < a.e3_t ? (double)a.c13[t * a.c13_stride + o3] : 0.0);
+  const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
+               sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+  const double *rl = x.recL + i * LR_REC, *rr = x.recR + j * LR_REC;
+  const double al = rl[0], ca = rl[1], ca2 = rl[2], sl3 = rl[3], sai = rl[4];
+  const double be = rr[0], cb = rr[1], cb2 = rr[2], sbj = rr[3];
+  const double n = a.n_id;
+  const double eff = sl3 * c3 - be * sai - al * sbj + al * be * a.spy;
+  const double eff_hi = fabs(eff) + a.e3_eps * sl3 * cb;
+  const double t_ee[9] = {sa2b2, -2.0 * be * sa2b, be * be * ca2, -2.0 * al * sab2, 4.0 * al * be * sab,
+                          -2.0 * al * be * be * ca, al * al * cb2, -2.0 * al * al * be * cb, n * al * al * be * be};
+  double ee = 0.0, mag = 0.0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    ee += t_ee[q];
+    mag += fabs(t_ee[q]);
+  }
+  const double se = sab - be * ca - al * cb + n * al * be;
+  // |Q'e|^2 <= (|c~| + |eta|)^2; fp32 sums of squares: relative error < 1e-4
+  const double qb = sqrt(lowrank * (1.0 + 1e-4)) + sqrt(x.E);
+  const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - qb * qb -
+                     1e-12 * (x.lam + x.tau) * (mag + se * se / n);
+  if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) {
+    const unsigned long long k = atomicAdd(a.counter, 1ULL);
+    if ((int64_t)k < a.cap) {
+      a.cand_i[k] = i;
+      a.cand_j[k] = j;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArgs x) {
+  constexpr int NSL = LRC_NSL, T = 512, RB = MX_RB, PB = 2, NA = MX_TILE / 16 / T, LA = NSL - 1;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][MX_TILE];
+  __shared__ __attribute__((aligned(16))) uint8_t sI[NSL][MX_BI * NB_REC];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[NSL][LRC_SJ];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nK = x.nK, nC = x.nC;
+  const int64_t R = x.R;
+  const int sbase = (int)blockIdx.x * MX_BI;  // the tile's first slot
+  // this wave's two slots (wave-uniform)
+  const int rr0 = x.slot_row[sbase + PB * w], rr1 = x.slot_row[sbase + PB * w + 1];
+  if (__builtin_amdgcn_readfirstlane(x.slot_row[sbase]) < 0) return;  // empty tile (never queued)
+  const int64_t i0 = rr0 >= 0 ? a.rows[rr0] : -1, i1 = rr1 >= 0 ? a.rows[rr1] : -1;
+  // DMA sources.  j side: instruction u of wave w moves its slots' (t, column, chunk) = item 64 u +
+  // lane (t = item / 128, column = item / 4 % 32, physical chunk = item % 4 holding logical chunk
+  // (item % 4) ^ ((column >> 2) & 3): the 16 lanes of a ds_read_b128 group hit 16 distinct slots).
+  unsigned oJ[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int item = 64 * u + lane, t = item >> 7, col = (item >> 2) & 31, pc = item & 3;
+    const int rr = t ? rr1 : rr0;
+    const int jj = rr >= 0 ? x.slot_j[(sbase + PB * w + t) * 32 + col] : -1;
+    oJ[u] = (unsigned)((jj >= 0 ? jj : 0) * nK * NB_REC + (pc ^ ((col >> 2) & 3)) * 16);
+  }
+  unsigned oI = 0;  // i side (waves 0, 1): slot tid / 8 of the tile, 16-byte chunk tid % 8 of its record
+  if (w < 2) {
+    const int r = x.slot_row[sbase + (tid >> 3)];
+    oI = (unsigned)((r >= 0 ? a.rows[r] : 0) * nK * NB_REC + (tid & 7) * 16);
+  }
+  auto load = [&](int nb, int q) __attribute__((always_inline)) {  // stage q = (chunk q / nK, stage q % nK)
+    const int ch = q / nK, kc = q % nK;
+    const uint8_t *src = x.tiles + (int64_t)(ch * nK + kc) * MX_TILE;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) lds_dma16(src + (tid + u * T) * 16, &sA[nb][(w * 64 + u * T) * 16]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) lds_dma16(x.nib_j + oJ[u] + kc * NB_REC, &sJ[nb][w * 4096 + u * 1024]);
+    if (w < 2) lds_dma16(x.nib_i + oI + kc * NB_REC, &sI[nb][w * 1024]);
+  };
+  const int NL = NA + 4 + (w < 2 ? 1 : 0);  // this wave's DMAs per stage
+  v16f_ acc[RB][PB];
+  const int sw16 = 16 * ((c >> 3) & 1), jf = (c >> 2) & 3;
+  auto afrag = [&](int b, int kk, int r) __attribute__((always_inline)) {
+    const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
+    const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+    return v8i_{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto compute = [&](int b, bool first) __attribute__((always_inline)) {
+    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    v8i_ fa = afrag(b, 0, 0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8i_ fb[PB];
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        const v4i j1 = *(const v4i *)&sJ[b][(PB * w + t) * 2048 + c * LRC_JB + 16 * ((2 * kk + h) ^ jf)];
+        const v4i j2 = j1 << 1;
+        const v4i m1 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
+        const v4i m2 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fb[t][q] = (m1[q] & j1[q]) | (m2[q] & j2[q]);
+#pragma unroll
+        for (int q = 4; q < 8; ++q) fb[t][q] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const bool last = kk == 1 && r == RB - 1;
+        const v8i_ fn = last ? fa : afrag(b, r < RB - 1 ? kk : 1, (r + 1) % RB);
+#pragma unroll
+        for (int t = 0; t < PB; ++t)  // x2 (scale 128): the fp4 codes hold w/2
+          acc[r][t] = mfma_mx(fa, fb[t], (first && kk == 0) ? z : acc[r][t], fa[6], 128);
+        fa = fn;
+      }
+    }
+  };
+  // chunk epilogue: sum_r (c~_r)^2, c~ = acc - beta_j G'(i) - alpha_i H(j), G' / H read from memory
+  // (accumulator element e of lane (c, h) in row tile r is row 32 r + 8 (e / 4) + 4 h + e % 4)
+  int64_t jc[PB];
+  float nbe[PB], nal[PB];
+#pragma unroll
+  for (int t = 0; t < PB; ++t) {
+    const int rr = t ? rr1 : rr0;
+    const int jj = rr >= 0 ? x.slot_j[(sbase + PB * w + t) * 32 + c] : -1;
+    jc[t] = jj;
+    nbe[t] = jj >= 0 ? -(float)x.recR[(int64_t)jj * LR_REC] : 0.f;
+    const int64_t ii = t ? i1 : i0;
+    nal[t] = ii >= 0 ? -(float)x.recL[ii * LR_REC] : 0.f;
+  }
+  double lowrank[PB] = {0.0, 0.0};
+  auto epilogue = [&](int ch) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      float4 g[PB][4], hv[PB][4];
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        const int64_t ii = t ? i1 : i0;
+        const float *gp = x.G + (ii >= 0 ? ii : 0) * R + ch * MXK + 32 * r + 4 * h;
+        const float *hp = x.H + (jc[t] >= 0 ? jc[t] : 0) * R + ch * MXK + 32 * r + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          g[t][q] = *(const float4 *)(gp + 8 * q);
+          hv[t][q] = *(const float4 *)(hp + 8 * q);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < PB; ++t) {
+        v2f_ s2 = {0.f, 0.f};
+        const v2f_ nb2 = {nbe[t], nbe[t]}, na2 = {nal[t], nal[t]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; u += 2) {
+            const v2f_ av = {acc[r][t][4 * q + u], acc[r][t][4 * q + u + 1]};
+            const v2f_ gv = {u ? g[t][q].z : g[t][q].x, u ? g[t][q].w : g[t][q].y};
+            const v2f_ hh = {u ? hv[t][q].z : hv[t][q].x, u ? hv[t][q].w : hv[t][q].y};
+            v2f_ cr = __builtin_elementwise_fma(nb2, gv, av);
+            cr = __builtin_elementwise_fma(na2, hh, cr);
+            s2 = __builtin_elementwise_fma(cr, cr, s2);
+          }
+        lowrank[t] += (double)s2[0] + (double)s2[1];
+      }
+    }
+  };
+  // stage pipeline: LA stages in flight; slot of stage q is q % NSL; the wait before stage q + 1
+  // leaves the younger stages' DMAs in flight (VMEM operations retire in order)
+  const int P = nC * nK;
+  for (int q = 0; q < LA && q < P; ++q) load(q % NSL, q);
+  vm_wait_barrier(NL * (min(LA, P) - 1));
+  for (int q = 0; q < P; ++q) {
+    if (q + LA < P) load((q + LA) % NSL, q + LA);  // its slot was read in stage q - 1 (barrier passed)
+    const int kc = q % nK;
+    compute(q % NSL, kc == 0);
+    if (kc == nK - 1) epilogue(q / nK);
+    const int ahead = min(q + LA, P - 1) - (q + 1);  // stages issued beyond q + 1
+    vm_wait_barrier(q + 1 < P ? NL * ahead : 0);
+  }
+  // lane half h tests slot PB w + h, column c (the other half-wave's rows of the same column added)
+  const double tot = (h ? lowrank[1] : lowrank[0]) + __shfl_xor(h ? lowrank[0] : lowrank[1], 32);
+  const int ri = h ? rr1 : rr0;
+  const int64_t i = h ? i1 : i0, j = h ? jc[1] : jc[0];
+  if (ri >= 0 && j >= 0) lrc_test(a, x, ri, i, j, tot);
 }
 
 // Left / right test records of a coding (lr_screen_kernel's per-SNP test operands in one 64-byte
@@ -2589,6 +2799,84 @@ __global__ __launch_bounds__(1024) void tl_fill_kernel(const uint8_t *__restrict
   }
 }
 
+// ---- slot lists of the compacted low-rank screen (lrc_screen_kernel), built on the device from the
+// prefilter's live-pair masks: band row r's live pairs, in ascending j, are cut into slots of 32
+// (the last one padded with -1); slot s = (slot_row[s], slot_j[32 s .. 32 s + 31]).  Slots are
+// numbered row by row and grouped 16 to a tile; the padding slots of the last tile have row -1.
+// lc_count: live pairs per band row (one workgroup per row).
+constexpr int LC_T = 256, LC_SLOTS = MX_BI;  // threads per row; slots per tile
+__global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint32_t *__restrict__ lmask, int nJ,
+                                                        int *__restrict__ cnt) {
+  __shared__ int part[LC_T / 64];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  int c = 0;
+  for (int J = tid; J < nJ; J += LC_T) c += __popc(lmask[(int64_t)r * nJ + J]);
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((tid & 63) == 0) part[tid >> 6] = c;
+  __syncthreads();
+  if (tid == 0) cnt[r] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+// one workgroup: exclusive scan of the rows' slot counts (soff), info = {slots, tiles}, the padding
+// slots of the last tile
+__global__ __launch_bounds__(1024) void lc_scan_kernel(const int *__restrict__ cnt, int Rn, int *__restrict__ soff,
+                                                       int *__restrict__ info, int *__restrict__ slot_row) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, per = (Rn + 1023) / 1024, r0 = t * per, r1 = min(Rn, r0 + per);
+  int sum = 0;
+  for (int r = r0; r < r1; ++r) sum += (cnt[r] + 31) / 32;
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int r = r0; r < r1; ++r) {
+    soff[r] = run;
+    run += (cnt[r] + 31) / 32;
+  }
+  if (t == 0) {
+    const int slots = part[1023], tiles = (slots + LC_SLOTS - 1) / LC_SLOTS;
+    info[0] = slots;
+    info[1] = tiles;
+    for (int q = slots; q < tiles * LC_SLOTS; ++q) slot_row[q] = -1;
+  }
+}
+// lc_fill: band row r's live second SNPs in ascending order into its slots (one workgroup per row;
+// each thread takes a contiguous range of column blocks, a block-wide scan places its pairs)
+__global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restrict__ lmask, int nJ,
+                                                       const int *__restrict__ cnt, const int *__restrict__ soff,
+                                                       int *__restrict__ slot_row, int *__restrict__ slot_j) {
+  __shared__ int part[LC_T];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int per = (nJ + LC_T - 1) / LC_T, J0 = min(nJ, tid * per), J1 = min(nJ, J0 + per);
+  const uint32_t *mk = lmask + (int64_t)r * nJ;
+  int c = 0;
+  for (int J = J0; J < J1; ++J) c += __popc(mk[J]);
+  part[tid] = c;
+  __syncthreads();
+  for (int off = 1; off < LC_T; off <<= 1) {
+    const int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  const int base = soff[r] * 32, n_live = cnt[r], n_slots = (n_live + 31) / 32;
+  int k = part[tid] - c;
+  for (int J = J0; J < J1; ++J) {
+    uint32_t w = mk[J];
+    while (w) {
+      const int b = __ffs(w) - 1;
+      w &= w - 1;
+      slot_j[base + k++] = 32 * J + b;
+    }
+  }
+  for (int q = n_live + tid; q < n_slots * 32; q += LC_T) slot_j[base + q] = -1;
+  for (int q = tid; q < n_slots; q += LC_T) slot_row[soff[r] + q] = r;
+}
+
 struct Coding {
   bool ready = false;
   DBuf U;                         // P * screen code panel  [m][n_pad] (fp64, while the coding is built)
@@ -2684,6 +2972,9 @@ struct gmat_epi {
     Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2], count2;
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
+  struct LrcBuffers {
+    DBuf drows[2], lmask[2], e13[2], pfc[2], slot_row[2], slot_j[2], cnt[2], soff[2], info[2];
+  } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
     if (s2) (void)hipStreamDestroy(s2);
@@ -2884,7 +3175,9 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
                  R.qb.p && e->cand2_i.p && e->cand2_j.p && e->counter2.p &&
                  e->cand2_i.bytes >= (size_t)np * 8 && L.U32.bytes >= (size_t)e->m * e->n_pad * 4 &&
                  R.U32.bytes >= (size_t)e->m * e->n_pad * 4 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
-             GMAT_E_ARG, "pair screen: plan buffers missing");
+             GMAT_E_ARG, "pair screen: plan buffers missing (U32 %d %d nib %d %d mx %zu z %d cand2 %zu / %lld counter2 %d)",
+             L.U32.p != nullptr, R.U32.p != nullptr, L.nibI.p != nullptr, R.nibJ.p != nullptr, e->mx_tiles.bytes,
+             e->z.p != nullptr, e->cand2_i.bytes, (long long)np, e->counter2.p != nullptr);
   // the side-term buffer is sized for the largest call once (calls queued on one stream share it)
   if (e->ps_side.bytes < (size_t)5 * np * sizeof(double)) {
     GMAT_HIP(hipStreamSynchronize(st));
@@ -3896,6 +4189,402 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   return GMAT_OK;
 }
 
+// ---- the compacted low-rank scan (default level for p_cut <= 1e-4 when the plan has the low-rank
+// certificate): per launch of 512 first SNPs (two folded 256-row chunks, equal work)
+//   S2: prefilter (live-pair masks, E3 slices and code products of live blocks) -> slot lists (lc_*)
+//   sm: compacted low-rank screen of the launch's slots (candidates appended to cand)
+//   S3: pair screen of the candidates in chunks beside the later launches, the exact refine at flush
+// Launch L + 1's prefilter runs beside launch L's screen (two buffer sets); the host reads a
+// launch's slot count (pinned) to reserve candidate room before queueing its screen, so the
+// candidate buffer can never overflow (a screen adds at most 32 per slot).
+int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+                 int64_t *n_hits) {
+  const double t_start = now();
+  const int64_t m = e->m, n_pad = e->n_pad;
+  int lc, rc;
+  kind_codings(kind, &lc, &rc);
+  GMAT_TRY(build_coding(e, lc));
+  GMAT_TRY(build_coding(e, rc));
+  const Coding &L = e->code[lc], &R = e->code[rc];
+  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();  // reference codes (refine)
+  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc);
+  const int tri = kind != GMAT_AD;
+  for (double &v : e->stats) v = 0.0;
+  e->hit_i.clear();
+  e->hit_j.clear();
+  e->hit_eff.clear();
+  e->hit_var.clear();
+  e->hit_chi.clear();
+  e->hit_p.clear();
+  // launches: chunks of 256 rows, folded (chunk k with chunk NC-1-k) for equal work per launch
+  struct Launch {
+    std::vector<int64_t> rows;
+    int64_t j_lo = 0;
+  };
+  std::vector<Launch> plan;
+  double pairs_tested = 0;
+  {
+    const int64_t half = ROWS_PER_LAUNCH / 2, nc = cdiv(n_rows, half);
+    for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
+      Launch ln;
+      for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) ln.rows.push_back(rows[t]);
+      if (l != k)
+        for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) ln.rows.push_back(rows[t]);
+      if (ln.rows.empty()) continue;
+      ln.j_lo = tri ? ln.rows[0] + 1 : 0;
+      if (tri && ln.j_lo >= m) continue;
+      for (int64_t r : ln.rows) pairs_tested += tri ? (double)(m - 1 - r) : (double)m;
+      plan.push_back(std::move(ln));
+    }
+  }
+  const int64_t nJ = cdiv(m, BJ), RL = ROWS_PER_LAUNCH;
+  const int64_t max_slots = RL * cdiv(m, 32) + LC_SLOTS;
+  auto &B = e->lrc;
+  for (int b = 0; b < 2; ++b) {
+    GMAT_TRY(B.drows[b].alloc(RL * 8));
+    GMAT_TRY(B.lmask[b].alloc((size_t)RL * nJ * 4));
+    GMAT_TRY(B.e13[b].alloc((size_t)E3_PF * 2 * RL * m * sizeof(int)));
+    GMAT_TRY(B.pfc[b].alloc((size_t)4 * RL * m * sizeof(int)));
+    GMAT_TRY(B.slot_row[b].alloc((size_t)max_slots * sizeof(int)));
+    GMAT_TRY(B.slot_j[b].alloc((size_t)max_slots * 32 * sizeof(int)));
+    GMAT_TRY(B.cnt[b].alloc(RL * sizeof(int)));
+    GMAT_TRY(B.soff[b].alloc(RL * sizeof(int)));
+    GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
+    GMAT_TRY(e->pins.rows[b].reserve(RL * 8));
+    GMAT_TRY(e->pins.cnt[b].reserve(8));
+    GMAT_TRY(e->pins.t2[b].reserve(16));
+  }
+  if (e->cand_cap == 0 || e->cand_i.bytes < (size_t)e->cand_cap * 8) {
+    const char *cenv = getenv("GMAT_CAND_CAP");
+    e->cand_cap = cenv ? std::max<int64_t>(1024, atoll(cenv)) : std::max<int64_t>(e->cand_cap, 1 << 24);
+    for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp})
+      GMAT_TRY(d->alloc(e->cand_cap * 8));
+  }
+  if (!e->counter.p) GMAT_TRY(e->counter.alloc(8));
+  const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
+  if (use_ps && e->cand2_i.bytes < (size_t)e->cand_cap * 8) {
+    GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->counter2.alloc(8));
+  }
+  DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
+  if (getenv("GMAT_LIVE_COUNT")) {
+    GMAT_TRY(live_cnt.alloc(8));
+    GMAT_HIP(hipMemset(live_cnt.p, 0, 8));
+  }
+  if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
+  if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
+  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
+  GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
+  struct Events {
+    std::vector<hipEvent_t> v;
+    ~Events() {
+      for (auto x : v) (void)hipEventDestroy(x);
+    }
+    int make(hipEvent_t *x) {
+      GMAT_HIP(hipEventCreate(x));
+      v.push_back(*x);
+      return GMAT_OK;
+    }
+  } evs;
+  hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], ref_beg, ref_end;
+  for (int b = 0; b < 2; ++b) {
+    GMAT_TRY(evs.make(&side_beg[b]));
+    GMAT_TRY(evs.make(&side_end[b]));
+    GMAT_TRY(evs.make(&scr_beg[b]));
+    GMAT_TRY(evs.make(&scr_end[b]));
+    GMAT_HIP(hipEventRecord(scr_end[b], sm));  // buffer sets free at the start
+  }
+  GMAT_TRY(evs.make(&ref_beg));
+  GMAT_TRY(evs.make(&ref_end));
+  GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
+  double t_screen = 0, t_side = 0, t_ref = 0, ncand_total = 0, n_refined = 0, ops = 0;
+  const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 65536;
+  int64_t ps_done = 0;  // candidates [0, ps_done) already pair-screened (queued on S3)
+  // candidate room: known_count (exact, after the last screen whose count was read) + inflight (32 per
+  // slot of the screen queued since) bounds the buffer's fill
+  int64_t known_count = 0, inflight = 0;
+  // the prefilter pass and the slot lists of launch li into buffer set b (stream S2)
+  auto enqueue_side = [&](size_t li, int b) -> int {
+    const Launch &ln = plan[li];
+    const int Rn = (int)ln.rows.size();
+    GMAT_HIP(hipStreamWaitEvent(S2, scr_end[b], 0));  // buffer set b free (screen two launches back)
+    std::memcpy(e->pins.rows[b].p, ln.rows.data(), Rn * 8);
+    GMAT_HIP(hipMemcpyAsync(B.drows[b].p, e->pins.rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
+    GMAT_HIP(hipEventRecord(side_beg[b], S2));
+    GMAT_HIP(hipMemsetAsync(B.lmask[b].p, 0, (size_t)Rn * nJ * 4, S2));
+    SideArgs x;
+    ScreenArgs &a = x.a;
+    std::memset(&a, 0, sizeof(a));
+    a.n_pad = n_pad;
+    a.left = slp;
+    a.right = srp;
+    a.m = m;
+    a.rows = B.drows[b].as<int64_t>();
+    a.n_rows = Rn;
+    a.tri = tri;
+    a.c13 = B.e13[b].as<int>();
+    a.c13_stride = (int64_t)2 * Rn * m;
+    a.sL3 = L.sL3.as<double>();
+    a.csum_l = L.csum.as<double>();
+    a.csum_r = R.csum.as<double>();
+    a.csq_l = L.csq.as<double>();
+    a.csq_r = R.csq.as<double>();
+    a.pf_store = 1;
+    a.pfc = B.pfc[b].as<int>();
+    a.pfc_stride = (int64_t)Rn * m;
+    a.pf_mu = e->pf_mu;
+    a.pf_eps = e->pf_eps;
+    a.pf_tau = e->pf_tau;
+    a.pf_ncov = e->pf_ncov;
+    a.pf_ku = e->pf_ku;
+    for (int k = 0; k < 4; ++k) a.pf_su[k] = e->pf_su[k];
+    a.pf_sU = e->pf_ncov ? L.sU.as<double>() : nullptr;
+    a.pf_ua = e->pf_ncov ? L.uc.as<double>() : nullptr;
+    a.pf_ub = e->pf_ncov ? R.uc.as<double>() : nullptr;
+    a.n_id = (double)e->n;
+    a.flags = nullptr;
+    a.lmask = B.lmask[b].as<uint32_t>();
+    a.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
+    a.nJ = (int)nJ;
+    a.e3_t = E3_PF;
+    a.e3_eps = 0.5 * std::pow(128.0, -(E3_PF - 1)) + 1e-12;
+    a.ld_e = m;
+    a.j_lo = ln.j_lo;
+    a.alpha = L.soff.as<double>();
+    a.sa = L.sa.as<double>();
+    a.beta = R.soff.as<double>();
+    a.sb = R.sb.as<double>();
+    a.mono_l = L.mono.as<uint8_t>();
+    a.mono_r = R.mono.as<uint8_t>();
+    a.spy = e->spy;
+    a.chi_cut = chi_cut;
+    x.n_pad = n_pad;
+    const int64_t ss = m * n_pad;
+    const int64_t ncols = m - (ln.j_lo / 32) * 32;
+    for (int t = 0; t < E3_PF; ++t) x.rs[t] = L.L3q.as<int8_t>() + t * ss;
+    x.cs[0] = srp;
+    x.rs4 = L.p4.as<uint8_t>();
+    x.cs4 = R.p4.as<uint8_t>();
+    if (e->pf_ncov == 0) {
+      x.n_rt = (int)cdiv(Rn, PF_T);
+      hipLaunchKernelGGL(prefilter_pass_kernel, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_T))), dim3(512), 0, S2, x);
+    } else {
+      for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
+      x.n_rt = (int)cdiv(Rn, PC_TR);
+      const dim3 gp((unsigned)(x.n_rt * cdiv(ncols, PC_TC)));
+      switch (e->pf_ncov) {
+        case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, gp, dim3(512), 0, S2, x); break;
+        case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, gp, dim3(512), 0, S2, x); break;
+        case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, gp, dim3(512), 0, S2, x); break;
+        default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, gp, dim3(512), 0, S2, x); break;
+      }
+    }
+    GMAT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
+                       B.cnt[b].as<int>());
+    hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, S2, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
+                       B.info[b].as<int>(), B.slot_row[b].as<int>());
+    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
+                       B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].p, B.info[b].p, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
+    GMAT_HIP(hipEventRecord(side_end[b], S2));
+    return GMAT_OK;
+  };
+  // refine (after the pair screen of what is left) of candidates [0, count), hits collected
+  Pinned &pin_res = e->pins.res;
+  auto flush = [&](int64_t count) -> int {
+    if (count <= 0) return GMAT_OK;
+    const int64_t *fi = e->cand_i.as<int64_t>(), *fj = e->cand_j.as<int64_t>();
+    int64_t nf = count;
+    GMAT_HIP(hipEventRecord(ref_beg, S3));
+    if (use_ps) {
+      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, fi + ps_done, fj + ps_done, count - ps_done, chi_cut, &nf,
+                           ps_done == 0));
+      fi = e->cand2_i.as<int64_t>();
+      fj = e->cand2_j.as<int64_t>();
+    }
+    ps_done = 0;
+    ncand_total += (double)count;
+    n_refined += (double)nf;
+    if (nf > 0) {
+      GMAT_TRY(refine(e, S3, L, R, lp, rp, fi, fj, nf, e->ceff.as<double>(), e->cvar.as<double>(),
+                      e->cchi.as<double>(), e->cp.as<double>()));
+      GMAT_TRY(pin_res.reserve((size_t)nf * 48));
+      int64_t *ci = pin_res.as<int64_t>(), *cj = ci + nf;
+      double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cq = cc + nf;
+      GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipMemcpyAsync(cq, e->cp.p, nf * 8, hipMemcpyDeviceToHost, S3));
+      GMAT_HIP(hipEventRecord(ref_end, S3));
+      GMAT_HIP(hipStreamSynchronize(S3));
+      for (int64_t k = 0; k < nf; ++k)
+        if (cq[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
+          e->hit_i.push_back(ci[k]);
+          e->hit_j.push_back(cj[k]);
+          e->hit_eff.push_back(ce[k]);
+          e->hit_var.push_back(cv[k]);
+          e->hit_chi.push_back(cc[k]);
+          e->hit_p.push_back(cq[k]);
+        }
+    } else {
+      GMAT_HIP(hipEventRecord(ref_end, S3));
+      GMAT_HIP(hipStreamSynchronize(S3));
+    }
+    float ms;
+    GMAT_HIP(hipEventElapsedTime(&ms, ref_beg, ref_end));
+    t_ref += ms * 1e-3;
+    return GMAT_OK;
+  };
+  auto read_count = [&](int b) -> int64_t { return (int64_t)*e->pins.cnt[b].as<unsigned long long>(); };
+  ScreenArgs sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.m = m;
+  sa.tri = tri;
+  sa.n_id = (double)e->n;
+  sa.e3_t = E3_PF;
+  sa.e3_eps = 0.5 * std::pow(128.0, -(E3_PF - 1)) + 1e-12;
+  sa.ld_e = m;
+  sa.spy = e->spy;
+  sa.chi_cut = chi_cut;
+  sa.counter = e->counter.as<unsigned long long>();
+  LrcArgs lx;
+  lx.tiles = e->lr_tiles.as<uint8_t>();
+  lx.nib_i = L.nibI.as<uint8_t>();
+  lx.nib_j = R.nibJ.as<uint8_t>();
+  lx.nK = e->nK;
+  lx.nC = e->lr_R / MXK;
+  lx.R = e->lr_R;
+  lx.G = L.lrGa.as<float>();
+  lx.H = R.lrG.as<float>();
+  lx.recL = L.lrRecL.as<double>();
+  lx.recR = R.lrRecR.as<double>();
+  lx.lam = e->lr_lam;
+  lx.tau = e->lr_tau;
+  lx.eps = e->lr_eps;
+  lx.E = e->lr_E;
+  int64_t prev_count = 0;  // candidates after the previous launch's screen (known once it completed)
+  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
+  for (size_t li = 0; li < plan.size(); ++li) {
+    const int b = (int)(li & 1);
+    const Launch &ln = plan[li];
+    if (li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1));
+    GMAT_HIP(hipEventSynchronize(side_end[b]));
+    const int *info = e->pins.t2[b].as<int>();
+    const int64_t slots = info[0], tiles = info[1];
+    float ms_side;
+    GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
+    t_side += ms_side * 1e-3;
+    // candidate room: a screen adds at most 32 per slot
+    bool flushed = false;  // the candidates of the earlier launches were refined just now
+    if (known_count + inflight + 32 * slots > e->cand_cap) {
+      flushed = true;
+      GMAT_HIP(hipStreamSynchronize(sm));
+      GMAT_HIP(hipMemcpy(e->pins.cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost));
+      GMAT_TRY(flush(read_count(b)));
+      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
+      known_count = inflight = 0;
+      prev_count = 0;
+      if (32 * slots > e->cand_cap) {  // grow the candidate buffers (nothing pending)
+        e->cand_cap = 2 * 32 * slots;
+        for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp}) GMAT_TRY(d->alloc(e->cand_cap * 8));
+        if (use_ps) {
+          GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
+          GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
+        }
+        if (getenv("GMAT_DEBUG")) fprintf(stderr, "candidate buffer grown to %lld\n", (long long)e->cand_cap);
+      }
+    }
+    sa.rows = B.drows[b].as<int64_t>();
+    sa.n_rows = (int)ln.rows.size();
+    sa.j_lo = ln.j_lo;
+    sa.c13 = B.e13[b].as<int>();
+    sa.c13_stride = (int64_t)2 * sa.n_rows * m;
+    sa.pfc = B.pfc[b].as<int>();
+    sa.pfc_stride = (int64_t)sa.n_rows * m;
+    sa.cap = e->cand_cap;
+    sa.cand_i = e->cand_i.as<int64_t>();
+    sa.cand_j = e->cand_j.as<int64_t>();
+    lx.slot_row = B.slot_row[b].as<int>();
+    lx.slot_j = B.slot_j[b].as<int>();
+    GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
+    GMAT_HIP(hipEventRecord(scr_beg[b], sm));
+    if (tiles > 0) hipLaunchKernelGGL(lrc_screen_kernel, dim3((unsigned)tiles), dim3(512), 0, sm, sa, lx);
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipMemcpyAsync(e->pins.cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
+    GMAT_HIP(hipEventRecord(scr_end[b], sm));
+    ops += (double)tiles * 2.0 * (double)e->lr_R * (double)n_pad * LC_SLOTS * 32;  // incl. empty slots
+    inflight = 32 * slots;
+    // the previous launch's screen has completed (or is about to): pair-screen its candidates on S3
+    if (li > 0) {
+      const int pb = b ^ 1;
+      GMAT_HIP(hipEventSynchronize(scr_end[pb]));
+      float ms;
+      GMAT_HIP(hipEventElapsedTime(&ms, scr_beg[pb], scr_end[pb]));
+      t_screen += ms * 1e-3;
+      prev_count = flushed ? 0 : read_count(pb);
+      known_count = prev_count;  // exact after screen li - 1
+      if (use_ps && !flushed && prev_count - ps_done >= ps_chunk) {
+        GMAT_HIP(hipStreamWaitEvent(S3, scr_end[pb], 0));
+        GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, e->cand_i.as<int64_t>() + ps_done, e->cand_j.as<int64_t>() + ps_done,
+                             prev_count - ps_done, chi_cut, nullptr, ps_done == 0));
+        ps_done = prev_count;
+      }
+    }
+  }
+  GMAT_HIP(hipStreamSynchronize(sm));
+  if (!plan.empty()) {
+    const int lb = (int)((plan.size() - 1) & 1);
+    float ms;
+    GMAT_HIP(hipEventElapsedTime(&ms, scr_beg[lb], scr_end[lb]));
+    t_screen += ms * 1e-3;
+    GMAT_TRY(flush(read_count(lb)));
+  }
+  std::vector<int64_t> ord(e->hit_i.size());
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
+  });
+  auto apply = [&](auto &v) {
+    auto c2 = v;
+    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
+  };
+  apply(e->hit_i);
+  apply(e->hit_j);
+  apply(e->hit_eff);
+  apply(e->hit_var);
+  apply(e->hit_chi);
+  apply(e->hit_p);
+  *n_hits = (int64_t)e->hit_i.size();
+  e->stats[0] = pairs_tested;
+  e->stats[1] = ncand_total;
+  e->stats[2] = ops;
+  e->stats[3] = t_screen;
+  e->stats[4] = t_ref;
+  e->stats[5] = t_side;
+  e->stats[6] = now() - t_start;
+  e->stats[7] = (double)plan.size();
+  e->stats[8] = -1;
+  e->stats[9] = e->lr_lam;
+  if (live_cnt.p) {
+    unsigned long long lcnt = 0;
+    GMAT_HIP(hipMemcpy(&lcnt, live_cnt.p, 8, hipMemcpyDeviceToHost));
+    fprintf(stderr, "gmat_epi_scan (compacted): %.0f pairs, prefilter keeps %llu pairs (%.4f%%), %.0f low-rank candidates, "
+            "%.0f refined\n", pairs_tested, lcnt, 100.0 * (double)lcnt / std::max(pairs_tested, 1.0), ncand_total,
+            n_refined);
+  }
+  if (getenv("GMAT_DEBUG"))
+    fprintf(stderr, "gmat_epi_scan (compacted): %zu launches, %.0f candidates, %.0f refined, screen %.3f s, side %.3f s\n",
+            plan.size(), ncand_total, n_refined, t_screen, t_side);
+  return GMAT_OK;
+}
+
 }  // namespace
 
 extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
@@ -3908,6 +4597,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
   }
   if (n_slice == GMAT_SCREEN_NONE) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
+  // the compacted low-rank scan serves the low-rank level (automatic at p_cut <= 1e-4, or forced by
+  // n_slice -2); GMAT_LR_BLOCKS=1 keeps the block-granular path below (A/B runs)
+  const bool lr_level = e->lr_R > 0 && e->pf_mu > 0.0 && (n_slice == -2 || (n_slice == 0 && p_cut <= 1e-4));
+  if (lr_level && pair_screen_fits(e) && !getenv("GMAT_LR_BLOCKS") && !getenv("GMAT_NO_PREFILTER"))
+    return scan_lowrank(e, kind, rows, n_rows, p_cut, chi_cut, n_hits);
   const double t_start = now();
   int lc, rc;
   kind_codings(kind, &lc, &rc);
@@ -4197,6 +4891,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.tile_rows = mxr[b].as<int>();
     sa.tile_side = nullptr;
     sa.pf_store = use_lr && S == 0;
+    sa.lmask = nullptr;
     sa.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
     sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
     sa.pfc_stride = (int64_t)Rn * m;

@@ -121,3 +121,23 @@ def test_cfg5_reml_first_iterations_vs_oracle(cfg5):
     O.wemai_multi_gmat(y.reshape(-1, 1), np.ones((N5, 1)), np.arange(N5), N5, gl, maxiter=2, history=oh)
     np.testing.assert_allclose(hist, np.array(oh), rtol=1e-7)
     assert var.size == 6
+
+
+def test_cfg5_reml_to_the_end_vs_oracle(cfg5):
+    """The 5-GRM REML at n = 5,000 run to convergence or the reference's maxiter (200): the oracle,
+    started from the GPU's iterate k - 2 (uvlmm_varcom.py:107 `init`), reproduces the last two
+    iterates -- the whole trajectory is the reference's, not only its first steps."""
+    from oracle import gmat_oracle as O
+    from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat
+    from scipy.sparse import identity
+    g, geno, gl, y, pvp, py = cfg5
+    var = _wemai_multi_gmat(y, np.ones((N5, 1)), identity(N5, format="csr"), gl, maxiter=200)
+    hist = _wemai_multi_gmat.last_history
+    k = hist.shape[0]
+    assert k >= 3
+    print("REML iterations %d (converged: %s), var %s" % (k, k < 200, np.array2string(var, precision=5)))
+    oh = []
+    O.wemai_multi_gmat(y.reshape(-1, 1), np.ones((N5, 1)), np.arange(N5), N5, gl, init=hist[k - 3], maxiter=2,
+                       history=oh)
+    np.testing.assert_allclose(np.array(oh), hist[k - 2:], rtol=1e-6)
+    np.testing.assert_allclose(var, hist[-1], rtol=0, atol=0)

@@ -8,7 +8,7 @@ tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && cd - > /dev/null
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split > $OUT/prof.out 2>&1 || { tail -20 $OUT/prof.out; exit 1; }
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/prof.out 2>&1 || { tail -20 $OUT/prof.out; exit 1; }
 find $OUT/prof -name "*kernel_stats.csv" -exec head -12 {} \;
 bash tools/pmc.sh r3b_pmc || exit 1
 for k in lr_screen_kernel prefilter_pass_kernel; do

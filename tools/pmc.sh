@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 RAW=gpurun_out/$TAG/raw  # inside gpurun_out so a long pass shows progress; deleted after filtering
 mkdir -p $OUT $RAW
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS=${ARGS:-"bench.py --steps 1 --warmup 0 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split"}
+ARGS=${ARGS:-"bench.py --steps 1 --warmup 0 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5"}
 i=0
 PASSES=${PASSES:-all}
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
