@@ -525,7 +525,6 @@ def main():
     ap.add_argument("--no-cfg5", action="store_true", help="skip the configs[4] leg of the default line")
     ap.add_argument("--covariates", action="store_true",
                     help="profiling: the timed step uses the covariate design of the covariates leg")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "screen_traffic.json"))
     args = ap.parse_args()
     if args.config == "cfg5":
         if args.n_id == 2000:
@@ -578,6 +577,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     screen_s = launches = ops = cands = hits = side_s = ref_s = 0.0
+    ks = {}
     n_slice = 0
     for _ in range(args.steps):
         res = step()
@@ -590,6 +590,8 @@ def main():
         ref_s += st["refine_s"]
         n_slice = int(st["n_slice"])
         hits += res[0].size
+        for k, v in plan.kernel_stats().items():
+            ks[k] = ks.get(k, 0.0) + v
     sync()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -597,53 +599,59 @@ def main():
     hits_all = dist.allreduce_sum(hits) / args.steps
     cands_all = dist.allreduce_sum(cands) / args.steps
 
-    # roofline of the dominant kernel (the quadratic-form screen): its ops per launch / average
-    # launch time.  The spectral prefilter clears most 32-pair blocks before the
-    # screen, so the screen's work is counted over the blocks it actually multiplies: per
-    # processed block of BI x 32 pairs, n_pad (n_pad + 128) / 2 MACs x 2 per pair and pass
-    # (gmat_epi_stats[2]); the per-pair dense figure would exceed the peak and mean nothing.
-    my_pairs = float(sum(m - 1 - int(i) for i in rows))
-    avg_launch_s = screen_s / max(launches, 1)
-    alg_ops_launch = ops / max(launches, 1)
-    achieved = alg_ops_launch / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
-    dense_ops_step = (my_pairs * 2 * plan.lowrank_rank() * n if n_slice == -1
-                      else my_pairs * max(n_slice, 1) * n * (n + 128))
-    # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
-    # WRITE_SIZE); the record is used only when it was taken on the same kernel source (sha256 of
-    # epi.hip), screen level, rank and cohort size (else traffic stays null)
+    # roofline of the dominant kernel (by kernel time per step): its MFMA ops per launch / its average
+    # launch time, both from the library's own accounting (HIP events recorded on the kernel's own
+    # stream, gmat_epi_kernel_stats).  prefilter_pass_kernel: 4 fp4 code products + 2 int8 E3 slices
+    # over n_pad individuals per pair of every tile that runs = 16 n_pad fp4-equivalent ops per pair
+    # (an int8 op counted twice: half the fp4 rate); lrc_screen_kernel: R x n_pad MACs x 2 per slot pair.
     from tools.pmc_summary import source_sha256
-    traffic, traffic_src = None, None
-    want = {"kernel": "lr_screen_kernel", "screen_level": n_slice, "lowrank_rank": plan.lowrank_rank(),
-            "n_id": n, "n_snp": m, "source_sha256": source_sha256()}
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if all(tj.get(k) == v for k, v in want.items()):
-                traffic, traffic_src = tj.get("hbm_bytes_per_launch"), os.path.relpath(args.traffic_json, REPO)
-            else:
-                traffic_src = "dropped: %s was recorded for %s" % (os.path.relpath(args.traffic_json, REPO),
-                                                                   {k: tj.get(k) for k in want})
-        except Exception as exc:
-            traffic_src = "unreadable: %s" % exc
-    if n_slice == -1:
-        peak, kern = MX_PEAK_TFLOPS, "lr_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
-        note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: R x n_pad MACs x 2 per pair (R = %d bottom "
-                "eigen-directions of P); screened share of the dense work %.4f"
-                % (plan.lowrank_rank(), ops / args.steps / max(dense_ops_step, 1.0)))
-    elif n_slice == 0:
-        peak, kern = MX_PEAK_TFLOPS, "mx_screen_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, fp6 x fp4)"
-        note = ("fp6 x fp4 ops (TFLOP/s) of the screened blocks: n_pad(n_pad+128)/2 MACs x 2 per pair, one pass; "
-                "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
-    else:
-        peak, kern = INT8_PEAK_TOPS, "screen_kernel (v_mfma_i32_32x32x32_i8)"
-        note = ("int8 ops (TOP/s) of the screened blocks: S slices x n_pad(n_pad+128)/2 MACs x 2 per pair; "
-                "screened share of the dense work %.4f" % (ops / args.steps / max(dense_ops_step, 1.0)))
-    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src, "kernel": kern,
-                "ops_note": note,
-                "screen_level": n_slice,
-                "issued_ops_per_launch": ops / max(launches, 1), "avg_launch_ms": avg_launch_s * 1e3,
-                "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
+    kern_rec = {}
+    for name, t_key, n_key, o_key, what in (
+            ("prefilter_pass_kernel", "prefilter_s", "prefilter_launches", "prefilter_ops",
+             "fp4-equivalent MFMA ops (fp4 + 2 x int8) of the tiles that run: 16 n_pad per pair "
+             "(4 fp4 code products, 2 int8 E3 slices)"),
+            ("lrc_screen_kernel", "screen_s", "screen_launches", "screen_ops",
+             "fp6 x fp4 ops: R x n_pad MACs x 2 per slot pair (R = %d bottom eigen-directions of P, empty slot "
+             "columns included)" % plan.lowrank_rank())):
+        if ks.get(n_key, 0) > 0 and ks.get(t_key, 0) > 0:
+            t_launch = ks[t_key] / ks[n_key]
+            kern_rec[name] = {"kernel_s_per_step": ks[t_key] / args.steps, "avg_launch_ms": t_launch * 1e3,
+                              "ops_per_launch": ks[o_key] / ks[n_key],
+                              "achieved": ks[o_key] / ks[n_key] / t_launch / 1e12, "ops_note": what}
+    if kern_rec:
+        dom = max(kern_rec, key=lambda k: kern_rec[k]["kernel_s_per_step"])
+        kr = kern_rec[dom]
+        # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
+        # WRITE_SIZE); used only when recorded on the same kernel source (sha256 of epi.hip), kernel,
+        # rank and cohort size (else traffic stays null)
+        traffic, traffic_src = None, None
+        tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % dom)
+        want = {"kernel": dom, "lowrank_rank": plan.lowrank_rank(), "n_id": n, "n_snp": m,
+                "source_sha256": source_sha256()}
+        if os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                if all(tj.get(k) == v for k, v in want.items()):
+                    traffic, traffic_src = tj.get("hbm_bytes_per_launch"), os.path.relpath(tpath, REPO)
+                else:
+                    traffic_src = "dropped: %s was recorded for %s" % (os.path.relpath(tpath, REPO),
+                                                                       {k: tj.get(k) for k in want})
+            except Exception as exc:
+                traffic_src = "unreadable: %s" % exc
+        else:
+            traffic_src = "no PMC record %s" % os.path.relpath(tpath, REPO)
+        roofline = {"bound": "mfma", "achieved": kr["achieved"], "peak": MX_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": kr["achieved"] / MX_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": dom, "ops_note": kr["ops_note"], "avg_launch_ms": kr["avg_launch_ms"],
+                    "issued_ops_per_launch": kr["ops_per_launch"], "kernels": kern_rec,
+                    "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
+    else:  # a level without per-kernel accounting (int8 / MX screens): the screen kernel's own stats
+        avg_launch_s = screen_s / max(launches, 1)
+        achieved = ops / max(launches, 1) / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
+        peak = MX_PEAK_TFLOPS if n_slice <= 0 else INT8_PEAK_TOPS
+        roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                    "traffic": None, "kernel": "screen level %d" % n_slice, "avg_launch_ms": avg_launch_s * 1e3,
+                    "issued_ops_per_launch": ops / max(launches, 1)}
 
     # full-triangle check: the last step's hits merged over the ranks against the exhaustive scan
     merged = dist.gather_hits(res)

@@ -112,6 +112,7 @@ struct ScreenArgs {
   double pf_ku;
   int pf_ncov;
   unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
+  unsigned long long *pf_stamp;    // diagnostics (GMAT_PF_STAMPS): 4 s_memrealtime stamps per workgroup, or null
   uint32_t *lmask;  // compacted low-rank path: per (band row, 32-column block) the prefilter's live
                     // pairs as a bit mask (bit c = column 32 J + c), or null
 };
@@ -190,6 +191,8 @@ struct SideArgs {
   const uint8_t *rs4, *cs4;  // prefilter: fp4 code panels (a | b) [m][n_pad / 2]
   int64_t n_pad;
   int n_rt;             // row tiles
+  int blocked;          // prefilter_pass_kernel: rs[0..E3_PF), rs4, cs4 are stage-blocked panels
+                        // ([n_pad / 64][m][64 B] int8, [n_pad / 64][m][32 B] fp4; block_panel_kernel)
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
@@ -325,24 +328,32 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PF_T;
   if (r0 >= a.n_rows || c0 >= a.m) return;
   if (a.tri && c0 + PF_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
+  auto pstamp = [&](int k) __attribute__((always_inline)) {
+    if (a.pf_stamp && threadIdx.x == 0) a.pf_stamp[4 * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  pstamp(0);
   // 8 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
   constexpr int O_R8 = 0, O_R4 = 16384, O_C4 = 20480;
   __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
   const uint8_t *src[PF_Q];
-  int stp[PF_Q];
+  int64_t stp[PF_Q];
+  // stage-blocked panels (x.blocked): a stage's 64-byte / 32-byte pieces of consecutive SNPs are
+  // contiguous, so an instruction's 1 KB comes from 8 whole 128-byte lines (row-major panels: from
+  // 16 - 32 lines, 32 - 64 bytes used of each)
+  const int64_t rstride = x.blocked ? SG_K : x.n_pad, fstride = x.blocked ? SG_K / 2 : x.n_pad / 2;
 #pragma unroll
   for (int u = 0; u < PF_Q; ++u) {
     const int q = w + 8 * u;
     if (q < 16) {  // int8 L3 slices: 16 rows x 4 chunks per instruction
       const int row = (q & 7) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-      src[u] = (const uint8_t *)x.rs[q >> 3] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
-      stp[u] = SG_K;
+      src[u] = (const uint8_t *)x.rs[q >> 3] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
+      stp[u] = x.blocked ? a.m * SG_K : SG_K;
     } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 16..19 rows, 20..23 columns)
       const int qq = q & 3, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
       const int64_t idx = q < 20 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (q < 20 ? x.rs4 : x.cs4) + idx * (x.n_pad / 2) + 16 * lg;
-      stp[u] = SG_K / 2;
+      src[u] = (q < 20 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
+      stp[u] = x.blocked ? a.m * (SG_K / 2) : SG_K / 2;
     }
   }
   auto issue = [&](int st) __attribute__((always_inline)) {
@@ -384,6 +395,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int pre = min(S, PF_NS - 1);
   for (int st = 0; st < pre; ++st) issue(st);
   wait_for(0, pre - 1);
+  pstamp(1);
   const int rrow = 32 * wr + c;
   for (int st = 0; st < S; ++st) {
     const uint8_t *bf = ring[st % PF_NS];
@@ -429,6 +441,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
     wait_for(st + 1, min(st + PF_NS - 1, S - 1));
   }
+  pstamp(2);
   // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
   // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
   // The test runs in fp32 with a certified slack (fp64 costs twice the issue slots and two registers
@@ -527,6 +540,8 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
     if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
   }
+  __syncthreads();
+  pstamp(3);
 }
 
 // ------------------------------------------------------------------ prefilter pass, covariate designs
@@ -2666,6 +2681,15 @@ __global__ __launch_bounds__(256) void cov_image_kernel(int64_t n_pad, const int
     dot[j] = rsum[0];
   }
 }
+// stage-blocked copy of an SNP-major panel: dst[(st m + snp) w + b] = src[snp W + st w + b] for
+// stages st of w bytes (W bytes per SNP); 16 bytes per thread
+__global__ void block_panel_kernel(int64_t m, int64_t W, int64_t w, const uint8_t *__restrict__ src,
+                                   uint8_t *__restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = W / 16;
+  if (t >= m * per) return;
+  const int64_t snp = t / per, o = (t % per) * 16, st = o / w, b = o % w;
+  *(v4i *)(dst + (st * m + snp) * w + b) = *(const v4i *)(src + snp * W + o);
+}
 __global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= m * (n_pad / 2)) return;
@@ -2890,6 +2914,8 @@ struct Coding {
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
   DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
+  DBuf p4b, L3b;                  // stage-blocked copies for the prefilter pass: p4 [n_pad/64][m][32 B],
+                                  // L3q slices 0 .. E3_PF-1 [E3_PF][n_pad/64][m][64 B]
   DBuf Lu, sU, uc;                // covariate directions: int8 images of (screen code o u_k) [ncov][m][n_pad],
                                   // their per-row scales and u_k . code [ncov][m]
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
@@ -2955,6 +2981,12 @@ struct gmat_epi {
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
   double stats[10] = {0};
+  // per-kernel accounting of the last compacted low-rank scan (gmat_epi_kernel_stats): [0] prefilter
+  // kernel seconds (HIP events on its stream), [1] its launches, [2] its MFMA ops (fp4-equivalent:
+  // fp4 ops + 2 x int8 ops, the rate ratio), [3] low-rank screen seconds, [4] its launches,
+  // [5] its fp6 x fp4 ops (R n_pad MACs x 2 per slot pair, empty slots included), [6] pair screen +
+  // refine seconds at flush, [7] live pairs (GMAT_LIVE_COUNT) or -1
+  double kstats[8] = {0};
   // plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition,
   // [3] low-rank certificate, [4] slices + residual bounds, [5] coding builds (side vectors, lazily
   // in the first scan of a kind), [6] Cholesky factorisations run by the certificates
@@ -3075,6 +3107,15 @@ int build_coding_impl(gmat_epi *e, int which) {
   GMAT_TRY(cd.p4.alloc((size_t)m * n_pad / 2));
   hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
                      cd.p4.as<uint8_t>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_TRY(cd.p4b.alloc((size_t)m * n_pad / 2));
+  hipLaunchKernelGGL(block_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 32), 256)), dim3(256), 0, e->s, m, n_pad / 2,
+                     (int64_t)SG_K / 2, cd.p4.as<uint8_t>(), cd.p4b.as<uint8_t>());
+  GMAT_TRY(cd.L3b.alloc((size_t)E3_PF * m * n_pad));
+  for (int t = 0; t < E3_PF; ++t)
+    hipLaunchKernelGGL(block_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad,
+                       (int64_t)SG_K, (const uint8_t *)cd.L3q.as<int8_t>() + (int64_t)t * m * n_pad,
+                       cd.L3b.as<uint8_t>() + (int64_t)t * m * n_pad);
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.nibI.alloc((size_t)m * n_pad));
   GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
@@ -4211,6 +4252,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc);
   const int tri = kind != GMAT_AD;
   for (double &v : e->stats) v = 0.0;
+  for (double &v : e->kstats) v = 0.0;
   e->hit_i.clear();
   e->hit_j.clear();
   e->hit_eff.clear();
@@ -4273,6 +4315,13 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_TRY(live_cnt.alloc(8));
     GMAT_HIP(hipMemset(live_cnt.p, 0, 8));
   }
+  DBuf pf_st;  // GMAT_PF_STAMPS: per-workgroup phase stamps of the prefilter of launch 5
+  const size_t stamp_launch = 5;
+  int64_t stamp_grid = 0;
+  if (getenv("GMAT_PF_STAMPS")) {
+    GMAT_TRY(pf_st.alloc((size_t)4 * 8 * 1 << 20));
+    GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)4 * 8 * 1 << 20));
+  }
   if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
   if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
   if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
@@ -4289,8 +4338,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       return GMAT_OK;
     }
   } evs;
-  hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], ref_beg, ref_end;
+  hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], pf_beg[2], pf_end[2], ref_beg, ref_end;
+  double t_pf = 0, pf_ops = 0;
+  std::vector<double> pf_ops_of(plan.size(), 0.0);
   for (int b = 0; b < 2; ++b) {
+    GMAT_TRY(evs.make(&pf_beg[b]));
+    GMAT_TRY(evs.make(&pf_end[b]));
     GMAT_TRY(evs.make(&side_beg[b]));
     GMAT_TRY(evs.make(&side_end[b]));
     GMAT_TRY(evs.make(&scr_beg[b]));
@@ -4348,6 +4401,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     a.flags = nullptr;
     a.lmask = B.lmask[b].as<uint32_t>();
     a.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
+    a.pf_stamp = (pf_st.p && li == stamp_launch) ? pf_st.as<unsigned long long>() : nullptr;
     a.nJ = (int)nJ;
     a.e3_t = E3_PF;
     a.e3_eps = 0.5 * std::pow(128.0, -(E3_PF - 1)) + 1e-12;
@@ -4368,9 +4422,28 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     x.cs[0] = srp;
     x.rs4 = L.p4.as<uint8_t>();
     x.cs4 = R.p4.as<uint8_t>();
+    x.blocked = 0;
     if (e->pf_ncov == 0) {
+      if (!getenv("GMAT_PF_ROWMAJOR")) {  // stage-blocked operands (A/B: GMAT_PF_ROWMAJOR=1)
+        x.blocked = 1;
+        for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
+        x.rs4 = L.p4b.as<uint8_t>();
+        x.cs4 = R.p4b.as<uint8_t>();
+      }
       x.n_rt = (int)cdiv(Rn, PF_T);
+      // MFMA work of the tiles that run (a tile entirely left of the diagonal exits at once): per pair
+      // 4 fp4 code products + 2 int8 E3 slices over n_pad individuals = 16 n_pad fp4-equivalent ops
+      int64_t run = 0;
+      for (int rt = 0; rt < x.n_rt; ++rt)
+        for (int64_t ct = 0; ct < cdiv(ncols, PF_T); ++ct) {
+          const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_T;
+          if (c0 < m && !(tri && c0 + PF_T - 1 <= ln.rows[rt * PF_T])) ++run;
+        }
+      pf_ops_of[li] = (double)run * PF_T * PF_T * 16.0 * (double)n_pad;
+      GMAT_HIP(hipEventRecord(pf_beg[b], S2));
+      if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_T);
       hipLaunchKernelGGL(prefilter_pass_kernel, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_T))), dim3(512), 0, S2, x);
+      GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
       for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
       x.n_rt = (int)cdiv(Rn, PC_TR);
@@ -4481,6 +4554,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     float ms_side;
     GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
     t_side += ms_side * 1e-3;
+    if (pf_ops_of[li] > 0) {
+      float ms_pf;
+      GMAT_HIP(hipEventElapsedTime(&ms_pf, pf_beg[b], pf_end[b]));
+      t_pf += ms_pf * 1e-3;
+      pf_ops += pf_ops_of[li];
+    }
     // candidate room: a screen adds at most 32 per slot
     bool flushed = false;  // the candidates of the earlier launches were refined just now
     if (known_count + inflight + 32 * slots > e->cand_cap) {
@@ -4572,9 +4651,36 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   e->stats[7] = (double)plan.size();
   e->stats[8] = -1;
   e->stats[9] = e->lr_lam;
+  e->kstats[0] = t_pf;
+  e->kstats[1] = pf_ops > 0 ? (double)plan.size() : 0.0;
+  e->kstats[2] = pf_ops;
+  e->kstats[3] = t_screen;
+  e->kstats[4] = (double)plan.size();
+  e->kstats[5] = ops;
+  e->kstats[6] = t_ref;
+  e->kstats[7] = -1;
+  if (pf_st.p && stamp_grid > 0 && stamp_grid <= (1 << 20)) {  // phase times of the stamped launch
+    std::vector<unsigned long long> hs((size_t)4 * stamp_grid);
+    GMAT_HIP(hipMemcpy(hs.data(), pf_st.p, hs.size() * 8, hipMemcpyDeviceToHost));
+    double d[3] = {0, 0, 0};
+    unsigned long long t_min = ~0ull, t_max = 0;
+    int64_t nw = 0;
+    for (int64_t g = 0; g < stamp_grid; ++g) {
+      const unsigned long long *q = &hs[4 * g];
+      if (!q[0] || !q[3]) continue;  // tiles that exit at once
+      ++nw;
+      for (int k = 0; k < 3; ++k) d[k] += (double)(q[k + 1] - q[k]) * 0.01;  // 100 MHz ticks -> us
+      t_min = std::min(t_min, q[0]);
+      t_max = std::max(t_max, q[3]);
+    }
+    fprintf(stderr, "prefilter launch %zu: %lld tiles run, per tile: prologue %.2f us, main loop %.2f us, epilogue "
+            "%.2f us; launch span %.1f us\n", stamp_launch, (long long)nw, d[0] / std::max<int64_t>(nw, 1),
+            d[1] / std::max<int64_t>(nw, 1), d[2] / std::max<int64_t>(nw, 1), (double)(t_max - t_min) * 0.01);
+  }
   if (live_cnt.p) {
     unsigned long long lcnt = 0;
     GMAT_HIP(hipMemcpy(&lcnt, live_cnt.p, 8, hipMemcpyDeviceToHost));
+    e->kstats[7] = (double)lcnt;
     fprintf(stderr, "gmat_epi_scan (compacted): %.0f pairs, prefilter keeps %llu pairs (%.4f%%), %.0f low-rank candidates, "
             "%.0f refined\n", pairs_tested, lcnt, 100.0 * (double)lcnt / std::max(pairs_tested, 1.0), ncand_total,
             n_refined);
@@ -4892,6 +4998,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.tile_side = nullptr;
     sa.pf_store = use_lr && S == 0;
     sa.lmask = nullptr;
+    sa.pf_stamp = nullptr;
     sa.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
     sa.pfc = use_pf ? pfc[b].as<int>() : nullptr;
     sa.pfc_stride = (int64_t)Rn * m;
@@ -4963,6 +5070,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       SideArgs x;
       x.a = make_args(li, b);
       x.n_pad = n_pad;
+      x.blocked = 0;
       x.n_rt = (int)cdiv(Rn, SG_T);
       const int64_t ss = m * n_pad;
       const int64_t ncols = m - (ln.j_lo / 32) * 32;
@@ -5614,6 +5722,12 @@ extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, d
     if (chi) chi[k] = e->hit_chi[k];
     if (p) p[k] = e->hit_p[k];
   }
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_kernel_stats(const gmat_epi *e, double *out8) {
+  GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_kernel_stats: bad arguments");
+  for (int k = 0; k < 8; ++k) out8[k] = e->kstats[k];
   return GMAT_OK;
 }
 

@@ -93,6 +93,14 @@ class EpiPlan:
                 "n_slice", "bound_coef")
         return dict(zip(keys, s.tolist()))
 
+    def kernel_stats(self):
+        """Per-kernel accounting of the last low-rank-level scan (gmat_epi_kernel_stats)."""
+        s = np.zeros(8)
+        N.check(self._lib.gmat_epi_kernel_stats(self._h, N.ptr(s)), "gmat_epi_kernel_stats")
+        keys = ("prefilter_s", "prefilter_launches", "prefilter_ops", "screen_s", "screen_launches", "screen_ops",
+                "flush_s", "live_pairs")
+        return dict(zip(keys, s.tolist()))
+
     def setup_stats(self):
         """Plan setup seconds (gmat_epi_setup_stats): create total, prefilter certificate,
         eigendecomposition, low-rank certificate, slices/residual bounds, coding builds, and

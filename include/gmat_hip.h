@@ -124,6 +124,11 @@ int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs,
  * [6] total seconds, [7] screen kernel launches, [8] screen level (-1 low-rank, 0 MX, k int8 slices),
  * [9] bound coefficient */
 int gmat_epi_stats(const gmat_epi *e, double *out10);
+/* per-kernel accounting of the last scan at the low-rank level (compacted path): [0] prefilter kernel
+ * seconds (HIP events on its stream), [1] its launches, [2] its MFMA ops in fp4-equivalents (fp4 ops +
+ * 2 x int8 ops), [3] low-rank screen seconds, [4] its launches, [5] its fp6 x fp4 ops, [6] pair screen
+ * + refine seconds at flush, [7] pairs kept by the prefilter (GMAT_LIVE_COUNT set) or -1 */
+int gmat_epi_kernel_stats(const gmat_epi *e, double *out8);
 /* Diagnostic: the certified lower bounds of e'Pe that the screens test with, evaluated exactly in
  * fp64 for listed pairs (i, j) (e = the screen codes' centred product over the real individuals):
  * out5[5 t ..] = {prefilter bound, low-rank bound, |e|^2, 1'e, |Q'e|^2} (-inf where the plan has no
