@@ -193,6 +193,7 @@ struct SideArgs {
   int n_rt;             // row tiles
   int blocked;          // prefilter_pass_kernel: rs[0..E3_PF), rs4, cs4 are stage-blocked panels
                         // ([n_pad / 64][m][64 B] int8, [n_pad / 64][m][32 B] fp4; block_panel_kernel)
+  const float *recL, *recR;  // prefilter_pass_kernel: test records, row / column role (pf_rec_kernel)
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
@@ -301,6 +302,7 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 // chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA instruction q (1 KB) at
 // q KB, wave w issuing q = w + 8u (u < 3).
 constexpr int PF_T = 128, PF_ST = 24 * 1024, PF_NS = 5, PF_Q = 3;
+constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
   v8i_ r = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -393,6 +395,16 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   }
   const int S = (int)(x.n_pad / SG_K);
   const int pre = min(S, PF_NS - 1);
+  // the epilogue's test records (32 B per row / column) by one LDS-DMA per wave ahead of the stages:
+  // waves 0-3 the 128 rows, 4-7 the 128 columns, lane l half l & 1 of record 32 (w & 3) + l / 2.  It
+  // retires before stage 0 (in-order vmcnt), so the stage waits cover it.
+  __shared__ __attribute__((aligned(16))) float rec[2 * PF_T][PF_REC];
+  {
+    const int k = 32 * (w & 3) + (lane >> 1);
+    const float *s = w < 4 ? x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC
+                           : x.recR + min(c0 + k, a.m - 1) * PF_REC;
+    lds_dma16(s + 4 * (lane & 1), &rec[32 * w][0]);
+  }
   for (int st = 0; st < pre; ++st) issue(st);
   wait_for(0, pre - 1);
   pstamp(1);
@@ -454,92 +466,84 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // = sL3 c3 - beta sa + alpha (beta spy - sb) is off by at most 2^-20 times the sum of the three
   // terms' magnitudes, which is added to eff_hi with the int8 slicing bound.  The final comparison's
   // three roundings are covered by the factor 1 + 2^-18.
-  // per-row: i (-1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa, (2 + alpha)^2
-  __shared__ int rowi[PF_T];
-  __shared__ float rowv[6][PF_T];
-  const float n = (float)a.n_id;
-  if (tid < PF_T) {
-    const int r = min(r0 + tid, a.n_rows - 1);
-    const int64_t i = a.rows[r];
-    const double al = a.alpha[i], ca = a.csum_l[i];
-    rowi[tid] = a.mono_l[i] ? -1 : (int)i;
-    rowv[0][tid] = (float)al;
-    rowv[1][tid] = (float)ca;
-    rowv[2][tid] = (float)(a.csq_l[i] - 2.0 * al * ca);
-    rowv[3][tid] = (float)a.sL3[i];
-    rowv[4][tid] = (float)a.sa[i];
-    rowv[5][tid] = (float)((2.0 + al) * (2.0 + al));
-  }
-  __syncthreads();
+  // per-row / per-column values: the records in rec[] (pf_rec_kernel).  Straight-line evaluation
+  // (no branches: with two waves per SIMD the LDS latency of a record read behind a branch is not
+  // hidden), row records read once for both column blocks, live bits collected per column block.
   const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id);
   const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
   const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
   constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f;
+  const float4 *rv = (const float4 *)&rec[0][0];
+  int64_t jq[2];
+  bool cok[2];
+  float cbe[2], ccb[2], cC1n[2], cnb[2], cbsb[2], cmag[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int64_t j = c0 + 64 * wc + 32 * q + c;
-    const int J = (int)(j / 32);
-    const bool jok = j < a.m && j >= a.j_lo;
-    // per-column: beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum, beta spy - sb,
-    // sum_k (b + beta)^2 (fp64 sums rounded once)
-    float cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0;
-    bool cmono = true;
-    if (jok) {
-      const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j], dn = a.n_id;
-      cbe = (float)be;
-      ccb = (float)cb;
-      cC1n = (float)(cb2 - 2.0 * be * cb + dn * be * be);
-      cnb = (float)(dn * be - cb);
-      cbsb = (float)(be * a.spy - a.sb[j]);
-      cmag = (float)(cb2 + 2.0 * be * cb + dn * be * be);
-      cmono = a.mono_r[j];
-    }
-    bool live[16];
-    unsigned n_live = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
-      const int iv = rowi[rl];
-      bool lv = false;
-      if (r < a.n_rows && jok && iv >= 0 && !cmono && !(a.tri && j <= (int64_t)iv)) {
-        const float al = rowv[0][rl], sL3 = rowv[3][rl], be = cbe;
-        float c3 = 0.0f;
-#pragma unroll
-        for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
-        const float t1 = sL3 * c3, t2 = be * rowv[4][rl], t3 = al * cbsb;
-        const float eff = t1 - t2 + t3;
-        const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
-        const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
-        // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
-        const float ee = sa2b2 + be * (be * rowv[2][rl] - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n);
-        const float se = sab - be * rowv[1][rl] + al * cnb;
-        const float vlo = mu_e * ee - k1 * se * se - k2 * rowv[5][rl] * cmag;
-        lv = !(vlo > 0.0f) || eff_hi * eff_hi * CMP >= chi_cut * vlo;
-      }
-      live[e] = lv;
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
-      const bool rok = r < a.n_rows;
-      const unsigned long long bal = __ballot(live[e]);
-      n_live += (unsigned)__popcll(bal);
-      const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
-      if (rok && c == 0 && J < a.nJ) {
-        if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
-        if (a.lmask) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
-      }
-      if (blk && rok && jok) {
-        const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-#pragma unroll
-        for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
-        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
-#pragma unroll
-          for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
-      }
-    }
-    if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
+    const int cl = 64 * wc + 32 * q + c;
+    jq[q] = c0 + cl;
+    // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
+    const float4 cv0 = rv[2 * (PF_T + cl)], cv1 = rv[2 * (PF_T + cl) + 1];
+    cbe[q] = cv0.x;
+    ccb[q] = cv0.y;
+    cC1n[q] = cv0.z;
+    cnb[q] = cv0.w;
+    cbsb[q] = cv1.x;
+    cmag[q] = cv1.y;
+    cok[q] = (jq[q] < a.m) & (jq[q] >= a.j_lo) & (cv1.z == 0.0f);
   }
+  // masks: lane t < 32 of the wave writes the word of (e = t / 2, half t % 2) of each column block
+  const int te = (lane >> 1) & 15, th = lane & 1;
+  unsigned mine[2] = {0u, 0u}, n_live = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+    const float4 r0v = rv[2 * rl], r1v = rv[2 * rl + 1];  // i, alpha, csum, R1 | sL3, sa, (2 + alpha)^2
+    const int iv = __float_as_int(r0v.x);
+    const float al = r0v.y, sL3 = r1v.x;
+    const bool rok = (r < a.n_rows) & (iv >= 0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const bool ok = rok & cok[q] & !(a.tri & (jq[q] <= (int64_t)iv));
+      const float be = cbe[q];
+      float c3 = 0.0f;
+#pragma unroll
+      for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
+      const float t1 = sL3 * c3, t2 = be * r1v.y, t3 = al * cbsb[q];
+      const float eff = t1 - t2 + t3;
+      const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb[q] + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
+      const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
+      // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
+      const float ee = sa2b2 + be * (be * r0v.w - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n[q]);
+      const float se = sab - be * r0v.z + al * cnb[q];
+      const float vlo = mu_e * ee - k1 * se * se - k2 * r1v.z * cmag[q];
+      const bool lv = ok & (!(vlo > 0.0f) | (eff_hi * eff_hi * CMP >= chi_cut * vlo));
+      const unsigned long long bal = __ballot(lv);
+      n_live += (unsigned)__popcll(bal);
+      const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
+      mine[q] = te == e ? (th ? w1 : w0) : mine[q];
+      if (h ? w1 : w0) {  // a live block: its E3 (and code products) for the low-rank / pair screens
+        const int64_t j = jq[q];
+        if ((r < a.n_rows) & (j < a.m) & (j >= a.j_lo)) {
+          const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+#pragma unroll
+          for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
+          if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+#pragma unroll
+            for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
+        }
+      }
+    }
+  }
+  const int tr = r0 + 32 * wr + (te & 3) + 8 * (te >> 2) + 4 * th;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
+    if (lane < 32 && tr < a.n_rows && J < a.nJ) {
+      if (a.flags) a.flags[(int64_t)tr * a.nJ + J] = mine[q] != 0;
+      if (a.lmask) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
+    }
+  }
+  if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
   __syncthreads();
   pstamp(3);
 }
@@ -2690,6 +2694,37 @@ __global__ void block_panel_kernel(int64_t m, int64_t W, int64_t w, const uint8_
   const int64_t snp = t / per, o = (t % per) * 16, st = o / w, b = o % w;
   *(v4i *)(dst + (st * m + snp) * w + b) = *(const v4i *)(src + snp * W + o);
 }
+// prefilter test records (prefilter_pass_kernel's epilogue, 32 bytes per SNP, fetched by LDS-DMA with
+// the first stage): fp64 per-SNP sums rounded once to fp32, exactly the values the test used to derive
+// itself.  Row role: [i (int bits; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa,
+// (2 + alpha)^2, 0]; column role: [beta, csum, C1n = csq - 2 beta csum + n beta^2, n beta - csum,
+// beta spy - sb, sum_k (b + beta)^2, monomorphic, 0]
+__global__ void pf_rec_kernel(int64_t m, double n, double spy, const double *__restrict__ soff,
+                              const double *__restrict__ csum, const double *__restrict__ csq,
+                              const double *__restrict__ sL3, const double *__restrict__ sa,
+                              const double *__restrict__ sb, const uint8_t *__restrict__ mono, float *recL,
+                              float *recR) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const double al = soff[j], c = csum[j], c2 = csq[j];
+  float *l = recL + j * PF_REC, *r = recR + j * PF_REC;
+  l[0] = __int_as_float(mono[j] ? -1 : (int)j);
+  l[1] = (float)al;
+  l[2] = (float)c;
+  l[3] = (float)(c2 - 2.0 * al * c);
+  l[4] = (float)sL3[j];
+  l[5] = (float)sa[j];
+  l[6] = (float)((2.0 + al) * (2.0 + al));
+  l[7] = 0.0f;
+  r[0] = (float)al;
+  r[1] = (float)c;
+  r[2] = (float)(c2 - 2.0 * al * c + n * al * al);
+  r[3] = (float)(n * al - c);
+  r[4] = (float)(al * spy - sb[j]);
+  r[5] = (float)(c2 + 2.0 * al * c + n * al * al);
+  r[6] = mono[j] ? 1.0f : 0.0f;
+  r[7] = 0.0f;
+}
 __global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint8_t *p4) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= m * (n_pad / 2)) return;
@@ -2916,6 +2951,7 @@ struct Coding {
   DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
   DBuf p4b, L3b;                  // stage-blocked copies for the prefilter pass: p4 [n_pad/64][m][32 B],
                                   // L3q slices 0 .. E3_PF-1 [E3_PF][n_pad/64][m][64 B]
+  DBuf pfRecL, pfRecR;            // prefilter test records, row / column role [m][PF_REC] fp32
   DBuf Lu, sU, uc;                // covariate directions: int8 images of (screen code o u_k) [ncov][m][n_pad],
                                   // their per-row scales and u_k . code [ncov][m]
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
@@ -3116,6 +3152,13 @@ int build_coding_impl(gmat_epi *e, int which) {
     hipLaunchKernelGGL(block_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad,
                        (int64_t)SG_K, (const uint8_t *)cd.L3q.as<int8_t>() + (int64_t)t * m * n_pad,
                        cd.L3b.as<uint8_t>() + (int64_t)t * m * n_pad);
+  GMAT_HIP(hipGetLastError());
+  GMAT_TRY(cd.pfRecL.alloc((size_t)m * PF_REC * sizeof(float)));
+  GMAT_TRY(cd.pfRecR.alloc((size_t)m * PF_REC * sizeof(float)));
+  hipLaunchKernelGGL(pf_rec_kernel, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, e->s, m, (double)n, e->spy,
+                     cd.soff.as<double>(), cd.csum.as<double>(), cd.csq.as<double>(), cd.sL3.as<double>(),
+                     cd.sa.as<double>(), cd.sb.as<double>(), cd.mono.as<uint8_t>(), cd.pfRecL.as<float>(),
+                     cd.pfRecR.as<float>());
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.nibI.alloc((size_t)m * n_pad));
   GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
@@ -4423,6 +4466,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     x.rs4 = L.p4.as<uint8_t>();
     x.cs4 = R.p4.as<uint8_t>();
     x.blocked = 0;
+    x.recL = L.pfRecL.as<float>();
+    x.recR = R.pfRecR.as<float>();
     if (e->pf_ncov == 0) {
       if (!getenv("GMAT_PF_ROWMAJOR")) {  // stage-blocked operands (A/B: GMAT_PF_ROWMAJOR=1)
         x.blocked = 1;
@@ -5071,6 +5116,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.a = make_args(li, b);
       x.n_pad = n_pad;
       x.blocked = 0;
+      x.recL = L.pfRecL.as<float>();
+      x.recR = R.pfRecR.as<float>();
       x.n_rt = (int)cdiv(Rn, SG_T);
       const int64_t ss = m * n_pad;
       const int64_t ncols = m - (ln.j_lo / 32) * 32;

@@ -15,3 +15,7 @@ if [ -n "$LIVE" ]; then
   GMAT_LIVE_COUNT=1 timeout -k 10 200 python bench.py --steps 1 --warmup 0 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/live.json 2> $OUT/live.err || { tail -5 $OUT/live.err; exit 1; }
   grep "prefilter keeps" $OUT/live.err | tail -3
 fi
+if [ -n "$STAMPS" ]; then
+  GMAT_PF_STAMPS=1 timeout -k 10 200 python bench.py --steps 1 --warmup 0 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/stamps.json 2> $OUT/stamps.err || { tail -5 $OUT/stamps.err; exit 1; }
+  grep "prefilter launch" $OUT/stamps.err | tail -3
+fi
