@@ -193,13 +193,11 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
   return GMAT_OK;
 }
 
-int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *work,
-                          double *ainv) {
-  // X = L^-1 by right-looking block forward substitution (work: n*n, lower): block row i of X is
+int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *linv) {
+  // X = L^-1 by right-looking block forward substitution (linv: n*n, lower): block row i of X is
   // inv(L_ii) times the accumulated right-hand side, then every later block row j subtracts
   // L_ji X_i in one wide product ((n - i0) x (i0 + 64) x 64) -- the large GEMMs carry the n^3/3
   // flops instead of 64-row strips.
-  double *linv = work;
   hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s, linv, n * n);
   GMAT_HIP(hipGetLastError());
   for (int64_t i0 = 0; i0 < n; i0 += NB) {
@@ -214,6 +212,13 @@ int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl
       GMAT_TRY(dgemm(s, rem, i0 + kb, kb, -1.0, DView{l + (i0 + kb) * ldl + i0, ldl, 0}, DView{xi, n, 0}, 1.0,
                      linv + (i0 + kb) * n, n));
   }
+  return GMAT_OK;
+}
+
+int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *work,
+                          double *ainv) {
+  double *linv = work;
+  GMAT_TRY(chol_lower_inverse(s, n, l, ldl, dinv, linv));
   // ainv = Linv' Linv (lower tiles, then mirror)
   GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{linv, n, 1}, DView{linv, n, 0}, 0.0, ainv, n, 2));
   GMAT_TRY(fill_sym_upper(s, n, ainv, n));

@@ -35,6 +35,9 @@ int dgemm_i8b(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DVie
 // the diagonal blocks are written to dinv (n x 64 doubles).  *logdet_dev (device double)
 // receives sum(log(diag(L)))*2; *info_dev (device int) > 0 marks a non-positive pivot.
 int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev);
+// linv = L^-1 (n x n, lower triangle; the upper triangle is zeroed) from the factor and its
+// diagonal-block inverses.
+int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *linv);
 // ainv = (L L')^-1 from the factor (lower triangle of l) and its diagonal-block inverses;
 // work is n*n doubles of scratch.  ainv is fully populated (symmetric).
 int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv,

@@ -494,9 +494,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // masks: lane t < 32 of the wave writes the word of (e = t / 2, half t % 2) of each column block
   const int te = (lane >> 1) & 15, th = lane & 1;
   unsigned mine[2] = {0u, 0u}, n_live = 0;
+  const int rw = r0 + 32 * wr;
+  const int64_t cw = c0 + 64 * wc - a.j_lo;
+  const uint32_t voff = (uint32_t)(4 * h * a.ld_e + c);
+  int *const b13 = (int *)a.c13 + ((int64_t)a.n_rows + rw) * a.ld_e + cw;
+  int *const bpf = (int *)a.pfc + (int64_t)rw * a.ld_e + cw;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+    const int kr = (e & 3) + 8 * (e >> 2);
+    const int rl = 32 * wr + kr + 4 * h, r = r0 + rl;
     const float4 r0v = rv[2 * rl], r1v = rv[2 * rl + 1];  // i, alpha, csum, R1 | sL3, sa, (2 + alpha)^2
     const int iv = __float_as_int(r0v.x);
     const float al = r0v.y, sL3 = r1v.x;
@@ -521,16 +527,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       n_live += (unsigned)__popcll(bal);
       const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
       mine[q] = te == e ? (th ? w1 : w0) : mine[q];
-      if (h ? w1 : w0) {  // a live block: its E3 (and code products) for the low-rank / pair screens
-        const int64_t j = jq[q];
-        if ((r < a.n_rows) & (j < a.m) & (j >= a.j_lo)) {
-          const int64_t o1 = (int64_t)r * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
+      if ((h ? w1 : w0) != 0 && (r < a.n_rows) && cok[q]) {
+        // a live block: its E3 (and code products) for the low-rank / pair screens (cok: j in range;
+        // a monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+        const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
 #pragma unroll
-          for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[q][t][e];
-          if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+        for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e];
+        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
 #pragma unroll
-            for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[q][p][e];
-        }
+          for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
       }
     }
   }
@@ -544,7 +549,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
   }
   if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
-  __syncthreads();
+  if (a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
   pstamp(3);
 }
 
