@@ -57,7 +57,7 @@ _PROTOS = {
     "gmat_float_repr": (_INT, [_D, ctypes.c_char_p, _INT]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
     "gmat_probe_mx_accum": (_INT, [_INT, _P, _P, _P]),
-    "gmat_probe_eig_bottom": (_INT, [_I64, _P, _INT, _P, _P]),
+    "gmat_probe_eig_bottom": (_INT, [_I64, _P, _INT, _D, _INT, _P, _P, _P, _P]),
     "gmat_comm_unique_id": (_INT, [_P]),
     "gmat_comm_init": (_INT, [_P, _INT, _INT, _P]),
     "gmat_comm_destroy": (_INT, [_P]),

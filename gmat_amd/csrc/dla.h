@@ -43,10 +43,13 @@ int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, c
 int spd_inverse_from_chol(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv,
                           double *work, double *ainv);
 
-// The ne smallest eigenpairs of the symmetric n x n matrix a (device, lower triangle read,
-// destroyed): eigenvalues ascending to w_host, eigenvector r to z[r*n .. r*n+n) (device).
-// Synchronous (eig.hip).
-int sym_eig_bottom(int64_t n, double *a, int ne, double *w_host, double *z);
+// The ne smallest eigenpairs of the symmetric n x n matrix a (device, both triangles, row-major,
+// not modified), by Chebyshev-filtered subspace iteration (eig.hip): Ritz values ascending to
+// w_host, Ritz vector r to z[r*n .. r*n+n) (device, orthonormal); iterates until every pair's
+// residual |a z_r - w_r z_r| is <= tol * (Gershgorin bound of |a|) or maxit block iterations.
+// res_host (ne residual norms) and iters may be null.  Synchronous.
+int sym_eig_bottom(int64_t n, const double *a, int ne, double tol, int maxit, double *w_host, double *z,
+                   double *res_host, int *iters);
 
 // Small device helpers.
 int fill_sym_upper(hipStream_t s, int64_t n, double *a, int64_t lda);           // upper := lower'

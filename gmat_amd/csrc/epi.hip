@@ -1829,69 +1829,6 @@ __global__ void lr_rec_kernel(int64_t m, const double *soff, const double *csum,
 }
 
 
-// ------------------------------------------------------------------ stage-2 side terms
-// E1 / Ed / E2 slice products (E1_t = L'q_t[i].b_j, Ed_t = Ldq_t[i].b_j^2, E2_t = a_i.R'q_t[j]) of the
-// stage-2 MX tiles' slots only, written into the launch's band arrays where cand_test reads them.
-// Nine int8 dot products over n_pad per (slot, column) on v_dot4_i32_i8 (the slots are a few per
-// cent of the flagged blocks; E3 and the code products are already there from the prefilter pass).
-struct SlotSideArgs {
-  const int8_t *Lq, *Ldq, *a, *b, *b2, *Rq;  // slices at stride ss
-  int64_t ss;
-};
-// Eight lanes per (slot, column) pair, each over an eighth of the individuals (a short dependent
-// load chain), reduced with shuffles; a workgroup covers 2 slots x 32 columns, 8 per tile.
-__global__ __launch_bounds__(512) void slot_side_kernel(ScreenArgs a, SlotSideArgs x) {
-  const int tile = blockIdx.x >> 3;
-  const int tl = a.tiles[MX_TE * tile];
-  if (tl < 0) return;
-  const int part = threadIdx.x & 7, pr = threadIdx.x >> 3;  // K part, pair of this workgroup
-  const int s = 2 * (blockIdx.x & 7) + (pr >> 5), c = pr & 31;
-  const int J = a.tiles[MX_TE * tile + 1 + s / (MX_BI / 2)];
-  const int r = a.tile_rows[(int64_t)tl * MX_BI + s];
-  const int64_t i = a.rows[r < 0 ? 0 : r], j = min((int64_t)(J < 0 ? 0 : J) * BJ + c, a.m - 1);
-  const int64_t n4 = a.n_pad / 16, q0 = part * (n4 / 8), q1 = part == 7 ? n4 : q0 + n4 / 8;
-  const v4i *li[SIDE_T], *ld[SIDE_T], *rq[SIDE_T];
-#pragma unroll
-  for (int t = 0; t < SIDE_T; ++t) {
-    li[t] = (const v4i *)(x.Lq + t * x.ss + i * a.n_pad);
-    ld[t] = (const v4i *)(x.Ldq + t * x.ss + i * a.n_pad);
-    rq[t] = (const v4i *)(x.Rq + t * x.ss + j * a.n_pad);
-  }
-  const v4i *pa = (const v4i *)(x.a + i * a.n_pad), *pb = (const v4i *)(x.b + j * a.n_pad),
-            *pb2 = (const v4i *)(x.b2 + j * a.n_pad);
-  int e1[SIDE_T] = {0, 0, 0}, ed[SIDE_T] = {0, 0, 0}, e2[SIDE_T] = {0, 0, 0};
-#pragma unroll 2
-  for (int64_t q = q0; q < q1; ++q) {
-    const v4i va = pa[q], vb = pb[q], vb2 = pb2[q];
-#pragma unroll
-    for (int t = 0; t < SIDE_T; ++t) {
-      const v4i l = li[t][q], d = ld[t][q], rr = rq[t][q];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        e1[t] = __builtin_amdgcn_sdot4(l[u], vb[u], e1[t], false);
-        ed[t] = __builtin_amdgcn_sdot4(d[u], vb2[u], ed[t], false);
-        e2[t] = __builtin_amdgcn_sdot4(va[u], rr[u], e2[t], false);
-      }
-    }
-  }
-#pragma unroll
-  for (int off = 1; off < 8; off <<= 1)
-#pragma unroll
-    for (int t = 0; t < SIDE_T; ++t) {
-      e1[t] += __shfl_xor(e1[t], off);
-      ed[t] += __shfl_xor(ed[t], off);
-      e2[t] += __shfl_xor(e2[t], off);
-    }
-  const int64_t jj = (int64_t)J * BJ + c;
-  if (part != 0 || r < 0 || J < 0 || jj >= a.m || jj < a.j_lo) return;
-  const int64_t o1 = (int64_t)r * a.ld_e + (jj - a.j_lo), od = o1 + 2 * (int64_t)a.n_rows * a.ld_e;
-#pragma unroll
-  for (int t = 0; t < SIDE_T; ++t) {
-    ((int *)a.c13)[t * a.c13_stride + o1] = e1[t];
-    ((int *)a.c13)[t * a.c13_stride + od] = ed[t];
-    ((int *)a.c2)[t * a.c2_stride + o1] = e2[t];
-  }
-}
 
 // ------------------------------------------------------------------ exact fp64 refine
 // For pairs (pi[t], pj[t]): e = (a - alpha)(b - beta) in fp64 (storage order), var = e'Pe,
@@ -3016,7 +2953,6 @@ struct gmat_epi {
   Coding code[2];  // 0 = additive (dosage), 1 = dominance (het)
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
-  DBuf cand1_i, cand1_j, counter1;  // low-rank screen's candidates (stage 1; the MX screen re-tests them)
   DBuf cand2_i, cand2_j, counter2, ps_side;  // pair screen survivors; its per-pair side terms
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
@@ -3038,7 +2974,6 @@ struct gmat_epi {
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
   struct ScanBufs {
     DBuf drows[2], dtiles[2], bl[2], ba[2], e13[2], e2[2], pfc[2], flags[2], mxt[2], mxr[2];
-    DBuf mxt2[2], mxr2[2];  // stage-2 MX tiles of a launch
   } sb;
   // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
   struct ScanPins {
@@ -3342,7 +3277,7 @@ void kind_codings(int kind, int *lc, int *rc) {
 }
 
 
-// Low-rank screen setup: bottom eigenpairs of P (rocSOLVER syevd, the intercept direction lifted
+// Low-rank screen setup: bottom eigenpairs of P (eig.hip, the intercept direction lifted
 // out of the bottom by s 11'/n), fp6 quantisation of B (the exact values the MFMA multiplies),
 // and the certificate: the largest lam (bisection) for which an fp64 Cholesky of
 //   A = P - lam I + (lam + tau) 11'/n + B D(lam) B',  d_r = (lam - lam_r)_+ (1 + kappa)
@@ -3351,11 +3286,11 @@ void kind_codings(int kind, int *lc, int *rc) {
 // cmax) adds n (R + 4) u (...) in the spectral norm.  Returns GMAT_OK with lr_R = 0 when the
 // screen is disabled (GMAT_LR_RANK=0 / GMAT_NO_LR) or not applicable.
 // Bottom eigenpairs of P with the intercept direction lifted out of the bottom (P + 4 tr(P)/n
-// 11'/n): rocSOLVER syevd (ascending); lam[r], r < ne, and eigenvector r as row r of Z (natural
+// 11'/n): Ritz pairs of eig.hip's filtered subspace iteration (ascending); lam[r], r < ne, and eigenvector r as row r of Z (natural
 // order).  The screens only need SOME basis and bounds -- every certificate below is checked by its
 // own Cholesky -- so the eigenvectors' accuracy affects tightness, never correctness.
 struct Eigen {
-  int ne = 0;
+  int ne = 0, iters = 0;
   std::vector<double> lam, Z;
   DBuf dZ;  // Z on the device (ne x n)
 };
@@ -3371,7 +3306,11 @@ int eigen_bottom(gmat_epi *e, const double *dP, double trP, int ne, Eigen *eg) {
   eg->ne = ne;
   eg->lam.resize(ne);
   eg->Z.resize((size_t)n * ne);
-  GMAT_TRY(sym_eig_bottom(n, A.as<double>(), ne, eg->lam.data(), Z.as<double>()));
+  // residual tolerance 2e-4 of the Gershgorin bound: the certificates then reach within ~0.1 % of
+  // those of exact eigenpairs on the bench cohort (tighter costs block iterations, not hits)
+  const char *tenv = getenv("GMAT_EIG_TOL");
+  GMAT_TRY(sym_eig_bottom(n, A.as<double>(), ne, tenv ? atof(tenv) : 2e-4, 12, eg->lam.data(), Z.as<double>(), nullptr,
+                          &eg->iters));
   GMAT_HIP(hipMemcpy(eg->Z.data(), Z.p, eg->Z.size() * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }
@@ -3690,7 +3629,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   // order), the epilogue adds 32 roundings; all are bounded by u * w'|E|w <= u * max_k
   // sum_l |E_kl| * |w|^2 (|E| symmetric non-negative).
   // The bound's four fp64 squarings run on a stream of their own beside the eigendecomposition
-  // below (rocSOLVER's dsytrd leaves most CUs idle); rho_mx is finished after it.
+  // below (whose small Rayleigh-Ritz steps leave most CUs idle); rho_mx is finished after it.
   DBuf qn, rabs;
   if ((rc = e->mx_tiles.alloc((size_t)e->nK * e->nK * MX_TILE)) || (rc = qn.alloc(n_pad * n_pad * sizeof(double))) ||
       (rc = rabs.alloc(n_pad * sizeof(double))))
@@ -4769,8 +4708,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc), *srq = screen_sq(e, rc);  // screen codes
   const int8_t *slq = screen_sq(e, lc);
   const int tri = (kind != GMAT_AD);
-  const char *venv = getenv("GMAT_SCREEN_VARIANT");
-  // tile shape of the screen (Shape<SH>); GMAT_SCREEN_VARIANT overrides for A/B runs
+  // tile shape of the int8 screen: Shape<SCREEN_SHAPE>
   // screen level S: 0 = MX (fp6 x fp4, one pass, tighter than one int8 slice), 1..n_slice = int8
   // slices.  Automatic: MX when the candidate band stays thin (p_cut <= 1e-4), 2 slices up to
   // p_cut 1e-2, else all; n_slice > 0 forces S slices, n_slice < 0 forces MX.  A launch whose
@@ -4783,8 +4721,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
                       : (n_slice < 0 ? 0 : (p_cut <= 1e-4 ? 0 : std::min(e->n_slice, p_cut <= 1e-2 ? 2 : 4)));
   GMAT_CHECK(S >= 0 && S <= e->n_slice, GMAT_E_ARG, "n_slice %d not in [1, %d]", S, e->n_slice);
   int S_max_used = S;
-  const int shape = venv ? (atoi(venv) ? 1 : 0) : SCREEN_SHAPE;
-  const int BI = shape ? Shape<1>::BI : Shape<0>::BI, MT = shape ? Shape<1>::MT : Shape<0>::MT;
+  constexpr int BI = Shape<SCREEN_SHAPE>::BI, MT = Shape<SCREEN_SHAPE>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   for (double &v : e->stats) v = 0.0;
   e->hit_i.clear();
@@ -4817,13 +4754,9 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const int64_t nJ = cdiv(m, BJ), max_mx = (ROWS_PER_LAUNCH / MX_BI) * nJ + 16;
   const bool use_pf = e->pf_mu > 0.0 && !getenv("GMAT_NO_PREFILTER");
   const bool use_lr = use_pf && e->lr_R > 0 && n_slice != -1;  // level 0 = low-rank screen
-  // GMAT_STAGE2=1: re-screen the low-rank candidates with the MX quadratic form before the refine
-  // (7x fewer refined pairs, but the sparse (row, block) slots fill MX tiles poorly: slower end to
-  // end at the bench configuration, kept for study)
-  const bool use_stage2 = use_lr && getenv("GMAT_STAGE2") != nullptr;
   // low-rank screen tile lists built on the device right behind the prefilter (tl_*_kernel): the
   // host waits only for the tile count, not for the flags and a host-side build
-  const bool dev_tiles = use_lr && !use_stage2 && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
+  const bool dev_tiles = use_lr && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
   DBuf tl_cnt, tl_h, tl_info;
   DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
   if (getenv("GMAT_LIVE_COUNT")) {
@@ -4859,11 +4792,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e->cchi.alloc(e->cand_cap * 8));
     GMAT_TRY(e->cp.alloc(e->cand_cap * 8));
     GMAT_TRY(e->counter.alloc(8));
-  }
-  if (e->cand1_i.bytes < (size_t)e->cand_cap * 8) {
-    GMAT_TRY(e->cand1_i.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cand1_j.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->counter1.alloc(8));
   }
   // pair screen between the screens and the refine (GMAT_NO_PAIR_SCREEN: off, for A/B runs)
   const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
@@ -4970,16 +4898,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
     return GMAT_OK;
   };
-
-  // stage-2 (low-rank level) events per buffer set, on S3
-  hipEvent_t s2beg[2], s2end[2];
-  for (int q = 0; q < 2; ++q) {
-    GMAT_HIP(hipEventCreate(&s2beg[q]));
-    GMAT_HIP(hipEventCreate(&s2end[q]));
-    GMAT_HIP(hipEventRecord(s2beg[q], S3));
-    GMAT_HIP(hipEventRecord(s2end[q], S3));
-  }
-  EvPair s2beg_guard{s2beg}, s2end_guard{s2end};
 
   // per-launch host plan (rows, tile list); empty launches dropped
   struct Launch {
@@ -5111,7 +5029,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       const Launch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
       GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-      GMAT_HIP(hipStreamWaitEvent(S2, s2end[b], 0));       // ... and its stage-2 re-screen
       if (side_serial) GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b ^ 1], 0));  // A/B: no overlap with the screen
       GMAT_TRY(stage_rows(ln, b));
       GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
@@ -5188,7 +5105,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-    GMAT_HIP(hipStreamWaitEvent(S2, s2end[b], 0));
     GMAT_TRY(stage_rows(ln, b));
     GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipMemcpyAsync(dtiles[b].p, ln.tiles.data(), ln.tiles.size() * sizeof(int), hipMemcpyHostToDevice,
@@ -5341,129 +5257,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
   if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0, S != 0));
-  // Stage 2 of the low-rank level: the low-rank screen's candidates (launch li, in cand1) are
-  // grouped into (band row, 32-column block) slots, packed into MX tiles (half-tiles per block,
-  // dealt to the XCDs like build_mx), their E1 / Ed / E2 computed (slot_side_kernel) and the MX
-  // quadratic form re-screens them into the main candidate buffer.  Returns the stage-2 tiles.
-  Pinned &pin_count1 = e->pins.count1, &pin_c1 = e->pins.c1;
-  auto &pin_t2 = e->pins.t2, &pin_r2 = e->pins.r2;
-  GMAT_TRY(pin_count1.reserve(8));
-  GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
-  double t_stage2 = 0.0, n_stage1 = 0.0;
-  bool s2_timed[2] = {false, false};
-  int64_t pend_bound = 0;  // upper bound of the main candidate count while stage 2 runs on S3
-  auto s2_retire = [&](int b) -> int {  // stage 2 of buffer set b has completed: account its time
-    GMAT_HIP(hipEventSynchronize(s2end[b]));
-    if (s2_timed[b]) {
-      float ms2;
-      GMAT_HIP(hipEventElapsedTime(&ms2, s2beg[b], s2end[b]));
-      t_stage2 += ms2 * 1e-3;
-      s2_timed[b] = false;
-    }
-    return GMAT_OK;
-  };
-  auto main_count = [&](int64_t *out) -> int {  // drain stage 2 and read the main counter
-    GMAT_HIP(hipStreamSynchronize(sm));
-    GMAT_HIP(hipStreamSynchronize(S3));
-    GMAT_HIP(hipMemcpyAsync(pin_count.p, e->counter.p, 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipStreamSynchronize(S3));
-    *out = (int64_t)*pin_count.as<unsigned long long>();
-    return GMAT_OK;
-  };
-  const hipStream_t S2s = getenv("GMAT_STAGE2_SERIAL") ? sm : S3;  // A/B: stage 2 in line with the screens
-  auto stage2 = [&](size_t li, int b, const ScreenArgs &sa, const MxArgs &mx, int64_t n1) -> int {
-    const Launch &ln = plan[li];
-    GMAT_TRY(pin_c1.reserve((size_t)n1 * 16));
-    int64_t *ci = pin_c1.as<int64_t>(), *cj = ci + n1;
-    GMAT_HIP(hipMemcpyAsync(ci, e->cand1_i.p, n1 * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemcpyAsync(cj, e->cand1_j.p, n1 * 8, hipMemcpyDeviceToHost, sm));
-    GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
-    GMAT_HIP(hipStreamSynchronize(sm));  // cand1 is free for the next low-rank screen
-    std::vector<std::pair<int64_t, int>> rix(ln.rows.size());  // SNP -> band row
-    for (size_t r = 0; r < ln.rows.size(); ++r) rix[r] = {ln.rows[r], (int)r};
-    std::sort(rix.begin(), rix.end());
-    std::vector<std::pair<int, int>> sl(n1);  // (J, band row)
-    for (int64_t k = 0; k < n1; ++k) {
-      const auto it = std::lower_bound(rix.begin(), rix.end(), std::make_pair(ci[k], 0));
-      sl[k] = {(int)(cj[k] / BJ), it->second};
-    }
-    std::sort(sl.begin(), sl.end());
-    sl.erase(std::unique(sl.begin(), sl.end()), sl.end());
-    std::vector<int> lst, rl;
-    int halves = 0;
-    for (size_t q = 0; q < sl.size();) {
-      const int J = sl[q].first;
-      int cnt = 0;
-      for (; q < sl.size() && sl[q].first == J; ++q, ++cnt) {
-        if (cnt % (MX_BI / 2) == 0) {
-          if (halves % 2 == 0) {
-            lst.push_back((int)(rl.size() / MX_BI));
-            lst.push_back(J);
-            lst.push_back(-1);
-            rl.insert(rl.end(), MX_BI, -1);
-          } else {
-            lst.back() = J;
-          }
-          ++halves;
-        }
-        rl[rl.size() - MX_BI + ((halves - 1) % 2) * (MX_BI / 2) + cnt % (MX_BI / 2)] = sl[q].second;
-      }
-    }
-    const int64_t n2 = (int64_t)lst.size() / MX_TE, C = cdiv(n2, 8);
-    std::vector<int> t2((size_t)MX_TE * 8 * C, -1);
-    for (int64_t q = 0; q < n2; ++q) {
-      const int64_t bb = 8 * (q % C) + q / C;
-      for (int k = 0; k < MX_TE; ++k) t2[MX_TE * bb + k] = lst[MX_TE * q + k];
-    }
-    // at most 32 candidates per slot: keep the main buffer from overflowing by construction
-    const int64_t add = 32 * (int64_t)sl.size();
-    if (pend_bound + add > e->cand_cap) {
-      int64_t c = 0;
-      GMAT_TRY(main_count(&c));
-      GMAT_TRY(flush(c));
-      GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, S3));
-      GMAT_HIP(hipStreamSynchronize(S3));
-      pend_bound = 0;
-    }
-    pend_bound += add;
-    GMAT_TRY(s2_retire(b));  // stage 2 two launches back no longer reads this buffer set
-    GMAT_TRY(e->sb.mxt2[b].alloc(t2.size() * sizeof(int)));
-    GMAT_TRY(e->sb.mxr2[b].alloc(rl.size() * sizeof(int)));
-    GMAT_TRY(pin_t2[b].reserve(t2.size() * sizeof(int)));
-    GMAT_TRY(pin_r2[b].reserve(rl.size() * sizeof(int)));
-    std::memcpy(pin_t2[b].p, t2.data(), t2.size() * sizeof(int));
-    std::memcpy(pin_r2[b].p, rl.data(), rl.size() * sizeof(int));
-    GMAT_HIP(hipEventRecord(s2beg[b], S2s));
-    GMAT_HIP(hipMemcpyAsync(e->sb.mxt2[b].p, pin_t2[b].p, t2.size() * sizeof(int), hipMemcpyHostToDevice, S2s));
-    GMAT_HIP(hipMemcpyAsync(e->sb.mxr2[b].p, pin_r2[b].p, rl.size() * sizeof(int), hipMemcpyHostToDevice, S2s));
-    ScreenArgs s2 = sa;
-    s2.tiles = e->sb.mxt2[b].as<int>();
-    s2.tile_rows = e->sb.mxr2[b].as<int>();
-    s2.n_slice = 0;
-    s2.delta = e->rho_mx;
-    SlotSideArgs sx;
-    sx.Lq = L.Lq.as<int8_t>();
-    sx.Ldq = L.Ldq.as<int8_t>();
-    sx.a = slp;
-    sx.b = srp;
-    sx.b2 = srq;
-    sx.Rq = R.Rq.as<int8_t>();
-    sx.ss = m * n_pad;
-    const unsigned g = (unsigned)(t2.size() / MX_TE);
-    hipLaunchKernelGGL(slot_side_kernel, dim3(8 * g), dim3(512), 0, S2s, s2, sx);
-    hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, S2s, s2, mx);
-    GMAT_HIP(hipGetLastError());
-    GMAT_HIP(hipEventRecord(s2end[b], S2s));
-    s2_timed[b] = true;
-    return GMAT_OK;
-  };
   const bool stamps_on = getenv("GMAT_LR_STAMPS") != nullptr;
   DBuf dstamp;
   if (stamps_on) GMAT_TRY(dstamp.alloc((size_t)max_mx * 8 * 6 * 8));
   // The next launch's low-rank screen is queued on sm right behind the current one (its side
   // pass and tile list are ready by then), so the host's per-launch bookkeeping no longer leaves
   // the GPU idle; a launch that overflows the candidate buffer discards the queued one.
-  const bool pipe_next = use_lr && !use_stage2 && !stamps_on;
+  const bool pipe_next = use_lr && !stamps_on;
   std::vector<char> queued(plan.size(), 0);
   hipEvent_t evs7[2], evs2[2];
   for (int q = 0; q < 2; ++q) {
@@ -5474,24 +5274,14 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   auto &pin_cnt = e->pins.cnt;
   GMAT_TRY(pin_cnt[0].reserve(8));
   GMAT_TRY(pin_cnt[1].reserve(8));
-  // GMAT_LR_SK=1: 128-deep stages (A/B); default 256-deep when the K extent allows
-  const int lr_sk = (getenv("GMAT_LR_SK") && atoi(getenv("GMAT_LR_SK")) == 1) || (e->nK % 2) ? 1 : 2;
-  // tile entries per workgroup (GMAT_LR_TPW): the grid strides over the entries in multiples of 8
-  // GMAT_LR_RING=1: a four-slot ring of 128-deep stages (three in flight) instead of the double
-  // buffer of 256-deep stages; measured 63.1 vs 58.5 ms per step (the ring's bookkeeping spills
-  // SGPRs: 6.6 instead of 2.9 SALU instructions per MFMA), so off by default
-  const bool lr_ring = e->nK >= 4 && getenv("GMAT_LR_RING") && atoi(getenv("GMAT_LR_RING")) == 1;
-  const int lr_tpw = getenv("GMAT_LR_TPW") ? std::max(1, atoi(getenv("GMAT_LR_TPW"))) : 1;
+  // 256-deep stages when the K extent allows (an even number of 128-deep MX K blocks), else 128
+  const int lr_sk = (e->nK % 2) ? 1 : 2;
   auto launch_lr_kernel = [&](unsigned g, const ScreenArgs &sa_, LrArgs lx_) {
-    lx_.n_tiles = (int)g;
-    unsigned grid = (unsigned)cdiv((int64_t)g, lr_tpw);
-    grid = std::min<unsigned>((unsigned)cdiv(grid, 8) * 8, g);
-    if (lr_ring)
-      hipLaunchKernelGGL((lr_screen_kernel<1, 4>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
-    else if (lr_sk == 2)
-      hipLaunchKernelGGL((lr_screen_kernel<2, 2>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+    lx_.n_tiles = (int)g;  // one tile entry per workgroup
+    if (lr_sk == 2)
+      hipLaunchKernelGGL((lr_screen_kernel<2, 2>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
     else
-      hipLaunchKernelGGL((lr_screen_kernel<1, 2>), dim3(grid), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
+      hipLaunchKernelGGL((lr_screen_kernel<1, 2>), dim3(g), dim3(MxShape<1>::T), 0, sm, sa_, lx_);
   };
 
   auto lr_args = [&](size_t li) {
@@ -5555,7 +5345,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       sa.scale_main = e->qmax / 127.0 * std::pow(128.0, -(S - 1));
       if (S > 0) GMAT_TRY(ensure_rho(e, S));
       sa.delta = S == 0 ? e->rho_mx : e->rho[S];
-      const bool two_stage = S == 0 && use_lr && use_stage2;
       if (queued[li] && S == 0) {  // queued behind the previous launch
         queued[li] = 0;
       } else {
@@ -5572,27 +5361,16 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       ntiles = (int64_t)plan[li].tiles.size() / 2;
       if (S == 0 && use_lr && gT[b] > 0) {
-        const unsigned g = (unsigned)gT[b];
-        ScreenArgs s1 = sa;  // with stage 2 the low-rank candidates go to cand1
-        if (two_stage) {
-          s1.counter = e->counter1.as<unsigned long long>();
-          s1.cand_i = e->cand1_i.as<int64_t>();
-          s1.cand_j = e->cand1_j.as<int64_t>();
-        }
-        launch_lr_kernel(g, s1, lx);
+        launch_lr_kernel((unsigned)gT[b], sa, lx);
       } else if (S == 0 && !mx_tiles.empty()) {
         const unsigned g = (unsigned)(mx_tiles.size() / MX_TE);
         hipLaunchKernelGGL(mx_screen_kernel<1>, dim3(g), dim3(MxShape<1>::T), 0, sm, sa, mx);
       }
-      else if (S == 0) {
-      } else if (shape)
-        hipLaunchKernelGGL(screen_kernel<1>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
-      else
-        hipLaunchKernelGGL(screen_kernel<0>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
+      else if (S != 0)
+        hipLaunchKernelGGL(screen_kernel<SCREEN_SHAPE>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(evs2[b], sm));
       GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
-      if (two_stage) GMAT_HIP(hipMemcpyAsync(pin_count1.p, e->counter1.p, 8, hipMemcpyDeviceToHost, sm));
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
       }
       // next launch's side terms overlap this screen; its tile list is built on the host
@@ -5607,23 +5385,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       GMAT_HIP(hipEventSynchronize(screen_end[b]));
       count = *pin_cnt[b].as<unsigned long long>();
-      if (two_stage) {
-        // stage 2 (MX re-screen of the low-rank candidates) runs on S3 beside the next launches;
-        // the main counter is read when the buffer is flushed
-        const int64_t n1 = (int64_t)*pin_count1.as<unsigned long long>();
-        if (n1 > e->cand_cap) {  // the low-rank band overflowed: escalate like an MX overflow
-          GMAT_HIP(hipMemsetAsync(e->counter1.p, 0, 8, sm));
-          GMAT_TRY(main_count(&pending));
-          pend_bound = 0;
-          count = (unsigned long long)n1;
-        } else {
-          if (n1 > 0) {
-            n_stage1 += (double)n1;
-            GMAT_TRY(stage2(li, b, sa, mx, n1));
-          }
-          count = 0;
-        }
-      }
       if ((int64_t)count <= e->cand_cap) break;
       // overflow in this launch: refine what earlier launches left and redo this one; if it
       // overflowed on its own, redo it with one more slice (thinner candidate band).  A queued
@@ -5636,7 +5397,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
           S_max_used = std::max(S_max_used, S);
         } else {  // the finest screen still overflows on one launch (large p_cut): grow the buffer
           const int64_t cap = std::max<int64_t>(2 * e->cand_cap, (int64_t)(1.25 * (double)count) + 1024);
-          for (DBuf *bf : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp, &e->cand1_i, &e->cand1_j})
+          for (DBuf *bf : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp})
             GMAT_TRY(bf->alloc((size_t)cap * 8));
           if (use_ps)
             for (DBuf *bf : {&e->cand2_i, &e->cand2_j}) GMAT_TRY(bf->alloc((size_t)cap * 8));
@@ -5651,9 +5412,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       pending = 0;
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
     }
-    const bool async_s2 = S == 0 && use_stage2;  // the main counter belongs to stage 2 on S3
-    if (!async_s2) pending = (int64_t)count;
-    if (use_ps && !use_stage2 && ps_chunk > 0 && pending - ps_done >= ps_chunk) {
+    pending = (int64_t)count;
+    if (use_ps && ps_chunk > 0 && pending - ps_done >= ps_chunk) {
       // the screen of this launch has finished (its count was read): screen its candidates now
       GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, e->cand_i.as<int64_t>() + ps_done, e->cand_j.as<int64_t>() + ps_done,
                            pending - ps_done, chi_cut, nullptr, ps_done == 0));
@@ -5701,7 +5461,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     else
       ops += (double)ntiles * S * (double)n_pad * (double)(n_pad + MT) * BI * BJ;
     ++launches_done;
-    if (!async_s2 && pending > e->cand_cap / 2) {
+    if (pending > e->cand_cap / 2) {
       GMAT_HIP(hipStreamSynchronize(sm));  // a queued next launch is discarded: the counter restarts
       if (li + 1 < plan.size()) queued[li + 1] = 0;
       GMAT_TRY(flush(pending));
@@ -5710,10 +5470,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     }
   }
   GMAT_HIP(hipStreamSynchronize(S2));
-  if (use_stage2 && S == 0) {
-    GMAT_TRY(main_count(&pending));
-    for (int q = 0; q < 2; ++q) GMAT_TRY(s2_retire(q));
-  }
   GMAT_TRY(flush(pending));
   // sort hits by (i, j)
   std::vector<int64_t> ord(e->hit_i.size());
@@ -5737,16 +5493,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   e->stats[2] = ops;
   e->stats[3] = t_screen;
   e->stats[4] = t_ref;
-  e->stats[5] = t_side + t_stage2;  // side terms + the low-rank level's stage-2 MX re-screen
+  e->stats[5] = t_side;
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "gmat_epi_scan: %lld launches, tile-list building %.3f s on the host, total %.3f s\n",
             (long long)launches_done, t_build, e->stats[6]);
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "gmat_epi_scan: %.0f screen candidates, %.0f refined%s\n", ncand_total, n_refined,
             use_ps ? " (pair screen)" : "");
-  if (getenv("GMAT_DEBUG") && use_stage2)
-    fprintf(stderr, "gmat_epi_scan: low-rank screen candidates %.0f -> MX re-screen %.0f (%.3f s)\n", n_stage1,
-            ncand_total, t_stage2);
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
   if (live_cnt.p) {

@@ -57,18 +57,20 @@ extern "C" int gmat_probe_mx_accum(int n_steps, const uint8_t *codes, const uint
   return GMAT_OK;
 }
 
-// gmat_probe_eig_bottom: the plan's partial symmetric eigensolver (eig.hip: tridiagonalisation,
-// Sturm multisection, inverse iteration, cluster Gram-Schmidt, back-transformation) on a host
-// matrix, so tests can compare it with a dense reference decomposition.
+// gmat_probe_eig_bottom: the plan's partial symmetric eigensolver (eig.hip: Chebyshev-filtered
+// subspace iteration with a device Rayleigh-Ritz) on a host matrix, so tests can compare it with a
+// dense reference decomposition.  res_out (ne residual norms) and iters_out may be null.
 #include "dla.h"
-extern "C" int gmat_probe_eig_bottom(int64_t n, const double *a_host, int ne, double *w_out, double *z_out) {
+extern "C" int gmat_probe_eig_bottom(int64_t n, const double *a_host, int ne, double tol, int maxit, double *w_out,
+                                     double *z_out, double *res_out, int *iters_out) {
   using namespace gmat;
-  GMAT_CHECK(n >= 2 && a_host && w_out && z_out && ne >= 1 && ne <= n, GMAT_E_ARG, "gmat_probe_eig_bottom: bad arguments");
+  GMAT_CHECK(n >= 2 && a_host && w_out && z_out && ne >= 1 && ne <= n && maxit >= 1, GMAT_E_ARG,
+             "gmat_probe_eig_bottom: bad arguments");
   DBuf a, z;
   GMAT_TRY(a.alloc((size_t)n * n * sizeof(double)));
   GMAT_TRY(z.alloc((size_t)n * ne * sizeof(double)));
   GMAT_HIP(hipMemcpy(a.p, a_host, (size_t)n * n * sizeof(double), hipMemcpyHostToDevice));
-  GMAT_TRY(sym_eig_bottom(n, a.as<double>(), ne, w_out, z.as<double>()));
+  GMAT_TRY(sym_eig_bottom(n, a.as<double>(), ne, tol, maxit, w_out, z.as<double>(), res_out, iters_out));
   GMAT_HIP(hipMemcpy(z_out, z.p, (size_t)n * ne * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }

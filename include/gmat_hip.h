@@ -217,8 +217,11 @@ int gmat_comm_barrier(gmat_comm *c);
  * screen's fp32 accumulation bound (eta_r) on the hardware. */
 int gmat_probe_mx_accum(int n_steps, const uint8_t *codes, const uint8_t *scales, float *out);
 /* The scan plan's partial symmetric eigensolver on a host matrix (n x n, symmetric): the ne
- * smallest eigenvalues ascending to w_out, eigenvector r to z_out[r*n .. r*n+n).  Test support. */
-int gmat_probe_eig_bottom(int64_t n, const double *a_host, int ne, double *w_out, double *z_out);
+ * smallest Ritz values ascending to w_out, Ritz vector r to z_out[r*n .. r*n+n), iterating until
+ * every residual is <= tol x the Gershgorin bound of |a| or maxit block iterations; res_out (ne
+ * residual norms) and iters_out may be NULL.  Test support. */
+int gmat_probe_eig_bottom(int64_t n, const double *a_host, int ne, double tol, int maxit, double *w_out,
+                          double *z_out, double *res_out, int *iters_out);
 
 #ifdef __cplusplus
 }

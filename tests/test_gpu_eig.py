@@ -1,5 +1,5 @@
-"""The scan plan's partial symmetric eigensolver (gmat_amd/csrc/eig.hip) against numpy's dense
-decomposition, on projection matrices P of the kind the plan decomposes (uvlmm_varcom.py:
+"""The scan plan's partial symmetric eigensolver (gmat_amd/csrc/eig.hip: Chebyshev-filtered subspace
+iteration, device Rayleigh-Ritz) against numpy's dense decomposition, on projection matrices P of the kind the plan decomposes (uvlmm_varcom.py:
 P = V^-1 - V^-1 X (X'V^-1 X)^-1 X'V^-1, intercept direction lifted as epi.hip eigen_bottom does),
 with and without covariates (P's exact null directions: a repeated eigenvalue 0)."""
 import numpy as np
@@ -27,20 +27,48 @@ def _p_matrix(n, m, ncov, seed):
     return p + 4.0 * trp / n * np.ones((n, n)) / n
 
 
-@pytest.mark.parametrize("n,ncov,ne", [(600, 0, 200), (2000, 0, 385), (2000, 3, 385), (1237, 2, 64)])
-def test_eig_bottom_vs_numpy(n, ncov, ne):
+def _eig(a, ne, tol, maxit):
     from gmat_amd import _native as N
+    import ctypes
     lib = N.ensure_device()
-    a = np.ascontiguousarray(_p_matrix(n, 3 * n, ncov, seed=n + ncov))
+    n = a.shape[0]
     w = np.zeros(ne)
     z = np.zeros((ne, n))
-    N.check(lib.gmat_probe_eig_bottom(n, N.ptr(a), ne, N.ptr(w), N.ptr(z)), "gmat_probe_eig_bottom")
-    wr = np.linalg.eigvalsh(a)[:ne]
-    anorm = np.abs(np.linalg.eigvalsh(a)).max()
-    np.testing.assert_allclose(w, wr, rtol=0, atol=1e-11 * anorm)
+    res = np.zeros(ne)
+    it = ctypes.c_int(0)
+    N.check(lib.gmat_probe_eig_bottom(n, N.ptr(a), ne, tol, maxit, N.ptr(w), N.ptr(z), N.ptr(res), ctypes.byref(it)),
+            "gmat_probe_eig_bottom")
+    return w, z, res, it.value
+
+
+# (n, ncov, ne): the LDS-resident Rayleigh-Ritz (block k <= 192: ne 64, 129) and the global one
+@pytest.mark.parametrize("n,ncov,ne", [(600, 0, 200), (2000, 0, 129), (2000, 3, 385), (1237, 2, 64)])
+def test_eig_bottom_vs_numpy(n, ncov, ne):
+    a = np.ascontiguousarray(_p_matrix(n, 3 * n, ncov, seed=n + ncov))
+    w, z, res, iters = _eig(a, ne, 1e-13, 80)
+    wall = np.linalg.eigvalsh(a)
+    wr = wall[:ne]
+    anorm = np.abs(wall).max()
+    np.testing.assert_allclose(w, wr, rtol=0, atol=1e-10 * anorm)
     if ncov:
         assert np.all(np.abs(w[:ncov]) < 1e-10 * anorm)  # the covariates' null directions
     resid = np.abs(z @ a - w[:, None] * z).max()
     assert resid < 1e-9 * anorm, resid
+    np.testing.assert_allclose(np.linalg.norm(z @ a - w[:, None] * z, axis=1), res, rtol=1e-6, atol=1e-12 * anorm)
     orth = np.abs(z @ z.T - np.eye(ne)).max()
     assert orth < 1e-8, orth
+    assert iters < 80
+
+
+def test_eig_bottom_plan_tolerance():
+    """At the plan's tolerance (2e-4 of the Gershgorin bound, <= 12 block iterations) the Ritz values
+    bound the true eigenvalues from above and lie within the residual of them (Weyl / Kato)."""
+    n, ne = 2000, 129
+    a = np.ascontiguousarray(_p_matrix(n, 3 * n, 0, seed=7))
+    w, z, res, iters = _eig(a, ne, 2e-4, 12)
+    wr = np.linalg.eigvalsh(a)[:ne]
+    assert iters <= 12
+    assert np.all(w >= wr - 1e-12)
+    assert np.all(w - wr <= res.max() + 1e-12)
+    orth = np.abs(z @ z.T - np.eye(ne)).max()
+    assert orth < 1e-10, orth

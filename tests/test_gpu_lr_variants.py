@@ -1,7 +1,7 @@
-"""Scan-schedule variants of the low-rank screen path give byte-identical results: several tile
-entries per workgroup (GMAT_LR_TPW), the four-slot stage ring (GMAT_LR_RING=1), 128-deep stages
-(GMAT_LR_SK=1), and the pair screen run in chunks beside the later launches (GMAT_PS_CHUNK small,
-or 0: all at flush time).  The default is checked against the oracle (remma_epiAA.py:71-82 and the
+"""Scan-schedule variants of the low-rank screen path give byte-identical results: the compacted
+screen (default) against the block-granular one (GMAT_LR_BLOCKS=1: lr_screen_kernel over every
+flagged 32-pair block), and the pair screen run in chunks beside the later launches (GMAT_PS_CHUNK
+small, or 0: all at flush time).  The default is checked against the oracle (remma_epiAA.py:71-82 and the
 epiAD sibling) on sampled rows, every variant against the default on the whole scan (several
 launches, so the next-tile prefetch and the chunked pair screen both run)."""
 import os
@@ -11,8 +11,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [{"GMAT_LR_TPW": "3"}, {"GMAT_LR_TPW": "16"}, {"GMAT_LR_RING": "1"}, {"GMAT_LR_SK": "1"},
-            {"GMAT_PS_CHUNK": "700"}, {"GMAT_PS_CHUNK": "0"}, {"GMAT_LR_TPW": "5", "GMAT_PS_CHUNK": "300"}]
+VARIANTS = [{"GMAT_LR_BLOCKS": "1"}, {"GMAT_PS_CHUNK": "700"}, {"GMAT_PS_CHUNK": "0"},
+            {"GMAT_LR_BLOCKS": "1", "GMAT_PS_CHUNK": "300"}]
 
 
 @pytest.fixture(scope="module")
