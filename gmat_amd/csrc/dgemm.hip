@@ -5,6 +5,12 @@
 // f64 MFMA lane maps (gfx950, verified by tools/probe_mfma.hip): A: lane l holds
 // A[l&15][k = l>>4]; B: B[k = l>>4][l&15]; C/D: 4 doubles per lane, element i at
 // row (l>>4) + 4*i, col l&15.
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "dla.h"
 
 namespace gmat {
@@ -26,88 +32,102 @@ struct Ld {
   }
 };
 
-// Each thread fetches 4 elements of the 64 x 16 (x, k) tile.
-template <class L>
-__device__ __forceinline__ void fetch(const L &l, int64_t x0, int64_t k0, int tid, double r[4]) {
+// Each thread fetches X / 16 elements of the X x 16 (x, k) tile (X = 64 or 32 rows of A, 64 of B).
+template <int X, class L>
+__device__ __forceinline__ void fetch(const L &l, int64_t x0, int64_t k0, int tid, double r[X / 16]) {
   if (l.contig_k) {
     int k = tid & 15, x = tid >> 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = l.at(x0 + x + 16 * q, k0 + k);
+    for (int q = 0; q < X / 16; ++q) r[q] = l.at(x0 + x + 16 * q, k0 + k);
   } else {
-    int x = tid & 63, k = tid >> 6;
+    int x = tid % X, k = tid / X;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = l.at(x0 + x, k0 + k + 4 * q);
+    for (int q = 0; q < X / 16; ++q) r[q] = l.at(x0 + x, k0 + k + (256 / X) * q);
   }
 }
-template <class L>
-__device__ __forceinline__ void store(const L &l, double (*s)[TM + 1], int tid, const double r[4]) {
+template <int X, class L>
+__device__ __forceinline__ void store(const L &l, double (*s)[TM + 1], int tid, const double r[X / 16]) {
   if (l.contig_k) {
     int k = tid & 15, x = tid >> 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s[k][x + 16 * q] = r[q];
+    for (int q = 0; q < X / 16; ++q) s[k][x + 16 * q] = r[q];
   } else {
-    int x = tid & 63, k = tid >> 6;
+    int x = tid % X, k = tid / X;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s[k + 4 * q][x] = r[q];
+    for (int q = 0; q < X / 16; ++q) s[k + (256 / X) * q][x] = r[q];
   }
 }
 
-template <class LA, class LB>
+// TMv = 64: 64 x 64 tiles, 4 waves of 32 x 32 (2 x 2 MFMA tiles); TMv = 32: 32 x 64 tiles, 4 waves of
+// 16 x 32 -- twice the workgroups for shapes whose 64 x 64 grid leaves most CUs idle (the tall-skinny
+// products of the eigensolver, n x n x k with k ~ 192: 96 tiles on 256 CUs).
+template <int TMv, class LA, class LB>
 __global__ __launch_bounds__(256) void dgemm_kernel(int64_t M, int64_t N, int64_t K, double alpha, LA la,
                                                     LB lb, double beta, double *__restrict__ C, int64_t ldc,
                                                     int mask) {
-  const int64_t bm = (int64_t)blockIdx.y * TM, bn = (int64_t)blockIdx.x * TN;
-  if (mask >= 1 && blockIdx.y < blockIdx.x) return;
+  constexpr int MI = TMv / 32;  // 16-row MFMA blocks per wave
+  const int64_t bm = (int64_t)blockIdx.y * TMv, bn = (int64_t)blockIdx.x * TN;
+  if (mask >= 1 && bm + TMv - 1 < bn) return;
+  // mask < 0: split-K part blockIdx.z over k in [z * kq, (z + 1) * kq), kq = -mask, written to the
+  // z-th M x N partial product (C + z M ldc)
+  int64_t kbeg = 0, kend = K;
+  if (mask < 0) {
+    kbeg = (int64_t)blockIdx.z * (int64_t)(-mask);
+    kend = kbeg - mask < K ? kbeg - mask : K;
+    C += (int64_t)blockIdx.z * M * ldc;
+  }
   __shared__ double As[2][TK][TM + 1];
   __shared__ double Bs[2][TK][TN + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  v4d acc[2][2];
+  v4d acc[MI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v4d{0, 0, 0, 0};
 
   // mask 2: both operands vanish for k < row (A' A with A lower triangular): start at the tile row
-  const int kt0 = mask == 2 ? (int)(bm / TK) : 0;
-  double ra[4], rb[4];
-  fetch(la, bm, (int64_t)kt0 * TK, tid, ra);
-  fetch(lb, bn, (int64_t)kt0 * TK, tid, rb);
-  store(la, As[0], tid, ra);
-  store(lb, Bs[0], tid, rb);
+  const int kt0 = mask == 2 ? (int)(bm / TK) : (int)(kbeg / TK);
+  double ra[TMv / 16], rb[4];
+  fetch<TMv>(la, bm, (int64_t)kt0 * TK, tid, ra);
+  fetch<64>(lb, bn, (int64_t)kt0 * TK, tid, rb);
+  store<TMv>(la, As[0], tid, ra);
+  store<64>(lb, Bs[0], tid, rb);
   __syncthreads();
-  const int nk = (int)((K + TK - 1) / TK);
+  const int nk = (int)((kend + TK - 1) / TK);
   for (int kt = kt0; kt < nk; ++kt) {
     const int cur = (kt - kt0) & 1;
     if (kt + 1 < nk) {
-      fetch(la, bm, (int64_t)(kt + 1) * TK, tid, ra);
-      fetch(lb, bn, (int64_t)(kt + 1) * TK, tid, rb);
+      fetch<TMv>(la, bm, (int64_t)(kt + 1) * TK, tid, ra);
+      fetch<64>(lb, bn, (int64_t)(kt + 1) * TK, tid, rb);
     }
 #pragma unroll
     for (int ks = 0; ks < TK / 4; ++ks) {
       const int kk = ks * 4 + (lane >> 4);
-      double a0 = As[cur][kk][wm * 32 + (lane & 15)];
-      double a1 = As[cur][kk][wm * 32 + 16 + (lane & 15)];
+      double av[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) av[i] = As[cur][kk][wm * (TMv / 2) + 16 * i + (lane & 15)];
       double b0 = Bs[cur][kk][wn * 32 + (lane & 15)];
       double b1 = Bs[cur][kk][wn * 32 + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], b0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], b1, acc[i][1], 0, 0, 0);
+      }
     }
     if (kt + 1 < nk) {
-      store(la, As[cur ^ 1], tid, ra);
-      store(lb, Bs[cur ^ 1], tid, rb);
+      store<TMv>(la, As[cur ^ 1], tid, ra);
+      store<64>(lb, Bs[cur ^ 1], tid, rb);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int64_t row = bm + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        int64_t row = bm + wm * (TMv / 2) + i * 16 + (lane >> 4) + 4 * r;
         int64_t col = bn + wn * 32 + j * 16 + (lane & 15);
         if (row < M && col < N) {
           double v = alpha * acc[i][j][r];
@@ -187,6 +207,45 @@ __global__ __launch_bounds__(256) void dot_kernel(int64_t M, int64_t N, int64_t 
   }
 }
 
+// C = alpha sum_z P_z + beta C over the split-K partial products (fixed order: deterministic).
+__global__ void splitk_sum_kernel(int64_t M, int64_t N, int splits, const double *__restrict__ ws, double alpha,
+                                  double beta, double *__restrict__ C, int64_t ldc) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int64_t r = idx / N, c = idx % N;
+  double acc = 0.0;
+  for (int z = 0; z < splits; ++z) acc += ws[(int64_t)z * M * N + idx];
+  double v = alpha * acc;
+  if (beta != 0.0) v += beta * C[r * ldc + c];
+  C[r * ldc + c] = v;
+}
+
+// Split-K scratch: one grow-only buffer per (device, stream), so the partial products of successive
+// products on a stream reuse it in stream order and concurrent streams never share one.  (A
+// stream-ordered hipMallocAsync / hipFreeAsync pair per product on the null stream handed out
+// memory that a later product's partial kernel overwrote while it was still being summed.)
+int splitk_workspace(hipStream_t s, size_t bytes, double **out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> bufs;
+  int dev = 0;
+  GMAT_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  auto &b = bufs[{dev, s}];
+  if (b.second < bytes) {
+    if (b.first) {
+      GMAT_HIP(hipStreamSynchronize(s));  // the old buffer may still be read by queued work
+      GMAT_HIP(hipFree(b.first));
+      b.first = nullptr;
+      b.second = 0;
+    }
+    const size_t want = std::max(bytes, (size_t)64 << 20);
+    GMAT_HIP(hipMalloc(&b.first, want));
+    b.second = want;
+  }
+  *out = static_cast<double *>(b.first);
+  return GMAT_OK;
+}
+
 template <class LA, class LB>
 int launch(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, LA la, LB lb, double beta, double *C,
            int64_t ldc, int mask) {
@@ -207,8 +266,28 @@ int launch(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, LA la, 
     GMAT_HIP(hipGetLastError());
     return GMAT_OK;
   }
-  dim3 grid((unsigned)cdiv(N, TN), (unsigned)cdiv(M, TM));
-  hipLaunchKernelGGL((dgemm_kernel<LA, LB>), grid, dim3(256), 0, s, M, N, K, alpha, la, lb, beta, C, ldc, mask);
+  const int64_t tiles = cdiv(N, TN) * cdiv(M, TM);
+  static const bool nosplit = getenv("GMAT_DGEMM_NOSPLIT") != nullptr;  // A/B diagnostics
+  if (mask == 0 && tiles < 256 && K >= 1024 && !nosplit) {
+    // split-K: a 64 x 64 grid that leaves most CUs idle is latency bound (one K-step of loads in
+    // flight per workgroup); `splits` workgroups per tile each take a contiguous K range into their
+    // own partial product (stream-ordered scratch), summed in a fixed order (deterministic)
+    const int splits = (int)std::min<int64_t>(8, std::max<int64_t>(2, 768 / tiles));
+    const int64_t kq = round_up(cdiv(K, splits), TK);
+    const int64_t per = M * N;
+    double *ws = nullptr;
+    GMAT_TRY(splitk_workspace(s, (size_t)per * splits * sizeof(double), &ws));
+    dim3 grid((unsigned)cdiv(N, TN), (unsigned)cdiv(M, TM), (unsigned)splits);
+    hipLaunchKernelGGL((dgemm_kernel<64, LA, LB>), grid, dim3(256), 0, s, M, N, K, 1.0, la, lb, 0.0, ws, N, -(int)kq);
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)cdiv(per, 256)), dim3(256), 0, s, M, N, splits, ws, alpha, beta,
+                       C, ldc);
+    GMAT_HIP(hipGetLastError());
+    return GMAT_OK;
+  }
+  {
+    dim3 grid((unsigned)cdiv(N, TN), (unsigned)cdiv(M, TM));
+    hipLaunchKernelGGL((dgemm_kernel<64, LA, LB>), grid, dim3(256), 0, s, M, N, K, alpha, la, lb, beta, C, ldc, mask);
+  }
   GMAT_HIP(hipGetLastError());
   return GMAT_OK;
 }

@@ -187,6 +187,172 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_small_kernel(int k, const
   }
 }
 
+// The same reduction for k <= 192 with the whole (zero-padded) 192 x 192 matrix in registers: wave w
+// holds columns c = w + 8 cc (cc < 24), lane l rows r = l + 64 rr (rr < 3), 72 doubles per lane, so a
+// step costs straight-line FMAs and three barriers instead of packed-triangle LDS traffic.  Step j:
+// the owner wave of column j (j mod 8) builds v and tau from its registers (wave reduction) and
+// publishes v; every wave forms its columns' share of A v for its rows and publishes it; every lane
+// then sums the eight shares of its three rows (all waves redundantly: p, K = tau/2 p'v and w = p - K v
+// need no further barrier), wave 0 publishes w, and every lane applies A -= v w' + w v' to its 72
+// entries.  Rows / columns <= j pick up garbage from the full-matrix update; they are never read again
+// (step j + 1 reads column j + 1 below the diagonal and the diagonal entry).  v and w are double
+// buffered by step parity (a wave may still be reading step j's while the owner of j + 1 writes).
+constexpr int TRR_K = 192, TRR_CC = TRR_K / 8, TRR_RR = TRR_K / 64;
+__global__ __launch_bounds__(512) void tridiag_reg_kernel(int k, const double *__restrict__ H, double *__restrict__ d,
+                                                          double *__restrict__ e, double *__restrict__ V,
+                                                          double *__restrict__ tv) {
+  __shared__ double sv[2][TRR_K], sw[2][TRR_K], pp[8][TRR_K];
+  __shared__ double stau[2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double a[TRR_CC][TRR_RR];
+#pragma unroll
+  for (int cc = 0; cc < TRR_CC; ++cc)
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) {
+      const int r = lane + 64 * rr, c = wv + 8 * cc;
+      a[cc][rr] = (r < k && c < k) ? 0.5 * (H[(int64_t)r * k + c] + H[(int64_t)c * k + r]) : 0.0;
+    }
+  for (int j = 0; j + 2 < k; ++j) {
+    const int par = j & 1, cj = j >> 3;
+    double *v = sv[par], *wq = sw[par];
+    if (wv == (j & 7)) {  // owner of column j: x = A[j+1:, j], v = x - alpha e_{j+1}
+      double x[TRR_RR];
+#pragma unroll
+      for (int rr = 0; rr < TRR_RR; ++rr) x[rr] = 0.0;
+#pragma unroll
+      for (int cc = 0; cc < TRR_CC; ++cc)
+        if (cc == cj)
+#pragma unroll
+          for (int rr = 0; rr < TRR_RR; ++rr) x[rr] = a[cc][rr];
+      double djj = 0.0, x0 = 0.0, s = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < TRR_RR; ++rr) {
+        const int r = lane + 64 * rr;
+        if (r == j) djj = x[rr];
+        if (r == j + 1) x0 = x[rr];
+        if (r <= j) x[rr] = 0.0;
+        s += x[rr] * x[rr];
+      }
+      s = wave_sum(s);
+      x0 = wave_sum(x0);
+      djj = wave_sum(djj);
+      const double sigma = s - x0 * x0;
+      double tau = 0.0, alpha = x0, v0 = x0;
+      if (sigma > 0.0) {
+        alpha = x0 >= 0.0 ? -sqrt(s) : sqrt(s);
+        v0 = x0 - alpha;
+        tau = 2.0 / (sigma + v0 * v0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < TRR_RR; ++rr) {
+        const int r = lane + 64 * rr;
+        const double vr = tau != 0.0 ? (r == j + 1 ? v0 : x[rr]) : 0.0;
+        v[r] = vr;
+        if (r > j && r < k) V[(int64_t)j * k + (r - j - 1)] = vr;
+      }
+      if (lane == 0) {
+        stau[par] = tau;
+        d[j] = djj;
+        e[j] = alpha;
+        tv[j] = tau;
+      }
+    }
+    __syncthreads();
+    const double tau = stau[par];
+    if (tau == 0.0) continue;  // uniform: nothing to reflect
+    // this wave's columns' share of A v for my three rows
+    double part[TRR_RR];
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) part[rr] = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < TRR_CC; ++cc) {
+      if (wv + 8 * cc <= j) continue;  // v_c = 0 (uniform)
+      const double vc = v[wv + 8 * cc];
+#pragma unroll
+      for (int rr = 0; rr < TRR_RR; ++rr)
+        if (64 * rr + 63 > j) part[rr] = fma(a[cc][rr], vc, part[rr]);
+    }
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) pp[wv][lane + 64 * rr] = part[rr];
+    __syncthreads();
+    double pr[TRR_RR], vr[TRR_RR], pv = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) {
+      const int r = lane + 64 * rr;
+      double q = 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q += pp[u][r];
+      pr[rr] = tau * q;
+      vr[rr] = v[r];
+      pv = fma(pr[rr], vr[rr], pv);
+    }
+    const double K = 0.5 * tau * wave_sum(pv);
+    double wr[TRR_RR];
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) {
+      wr[rr] = fma(-K, vr[rr], pr[rr]);
+      if (wv == 0) wq[lane + 64 * rr] = wr[rr];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < TRR_CC; ++cc) {
+      const int c = wv + 8 * cc;
+      if (c <= j) continue;  // columns already reduced (uniform)
+      const double vc = v[c], wc = wq[c];
+#pragma unroll
+      for (int rr = 0; rr < TRR_RR; ++rr)
+        if (64 * rr + 63 > j) a[cc][rr] -= fma(vr[rr], wc, wr[rr] * vc);
+    }
+  }
+  // the trailing 2 x 2 block: d[k-2], d[k-1], e[k-2] from their owners
+#pragma unroll
+  for (int cc = 0; cc < TRR_CC; ++cc)
+#pragma unroll
+    for (int rr = 0; rr < TRR_RR; ++rr) {
+      const int r = lane + 64 * rr, c = wv + 8 * cc;
+      if (k >= 2 && c == k - 2 && r == k - 2) {
+        d[k - 2] = a[cc][rr];
+        tv[k - 2] = 0.0;
+      }
+      if (k >= 2 && c == k - 2 && r == k - 1) e[k - 2] = a[cc][rr];
+      if (c == k - 1 && r == k - 1) {
+        d[k - 1] = a[cc][rr];
+        tv[k - 1] = 0.0;
+      }
+    }
+}
+
+// Back-transformation for k <= 192, one wave per column: the next reflector is fetched into
+// registers (3 entries per lane) while the current one is applied, and the column lives in LDS
+// (a single wave: program order, no barrier).
+__global__ __launch_bounds__(64) void tri_back_reg_kernel(int k, const double *__restrict__ V, const double *__restrict__ tv,
+                                                          double *__restrict__ S) {
+  __shared__ double col[2 * TRR_K];  // reads run up to j + 1 + 191 (masked by v = 0 past the column)
+  const int lane = threadIdx.x;
+  double *s = S + (int64_t)blockIdx.x * k;
+  for (int i = lane; i < 2 * TRR_K; i += 64) col[i] = i < k ? s[i] : 0.0;
+  double vn[TRR_RR];
+  int j = k - 3;
+#pragma unroll
+  for (int u = 0; u < TRR_RR; ++u) vn[u] = (j >= 0 && lane + 64 * u < k - j - 1) ? V[(int64_t)j * k + lane + 64 * u] : 0.0;
+  for (; j >= 0; --j) {
+    double vc[TRR_RR];
+#pragma unroll
+    for (int u = 0; u < TRR_RR; ++u) {
+      vc[u] = vn[u];
+      vn[u] = (j >= 1 && lane + 64 * u < k - j) ? V[(int64_t)(j - 1) * k + lane + 64 * u] : 0.0;
+    }
+    const double tau = tv[j];
+    double dt = 0.0;
+#pragma unroll
+    for (int u = 0; u < TRR_RR; ++u) dt = fma(vc[u], col[j + 1 + lane + 64 * u], dt);
+    dt = tau * wave_sum(dt);
+#pragma unroll
+    for (int u = 0; u < TRR_RR; ++u) col[j + 1 + lane + 64 * u] -= dt * vc[u];
+  }
+  for (int i = lane; i < k; i += 64) s[i] = col[i];
+}
+
 // Back-transformation S := Q S for the first ncol columns (column r at S[r k ..]): reflectors
 // applied last to first, one wave per column, the column in LDS.
 __global__ __launch_bounds__(64) void tri_back_kernel(int k, const double *__restrict__ V, const double *__restrict__ tv,
@@ -439,7 +605,9 @@ int chol_qr(EigWork &w, int64_t n, int k, const double *Y, double *Yout) {
 // th_host, eigenvector r to S[r k .. r k + k).
 int small_eig(EigWork &w, int k, const double *H, double *th_host) {
   const size_t tri_lds = (size_t)k * (k + 1) / 2 * sizeof(double) + 2 * (size_t)k * sizeof(double);
-  if (k <= TRI_LDS_K) {
+  if (k <= TRR_K) {
+    hipLaunchKernelGGL(tridiag_reg_kernel, dim3(1), dim3(512), 0, 0, k, H, w.dd, w.de, w.V, w.tv);
+  } else if (k <= TRI_LDS_K) {
     GMAT_HIP(hipFuncSetAttribute((const void *)tridiag_small_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)LDS_MAX));
     hipLaunchKernelGGL(tridiag_small_kernel<true>, dim3(1), dim3(TRI_THREADS), tri_lds, 0, k, H, nullptr, w.dd, w.de,
@@ -498,7 +666,10 @@ int small_eig(EigWork &w, int k, const double *H, double *th_host) {
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipDeviceSynchronize());
   }
-  hipLaunchKernelGGL(tri_back_kernel, dim3(k), dim3(64), (size_t)k * sizeof(double), 0, k, w.V, w.tv, w.S);
+  if (k <= TRR_K)
+    hipLaunchKernelGGL(tri_back_reg_kernel, dim3(k), dim3(64), 0, 0, k, w.V, w.tv, w.S);
+  else
+    hipLaunchKernelGGL(tri_back_kernel, dim3(k), dim3(64), (size_t)k * sizeof(double), 0, k, w.V, w.tv, w.S);
   GMAT_HIP(hipGetLastError());
   return GMAT_OK;
 }
@@ -537,9 +708,27 @@ int sym_eig_bottom(int64_t n, const double *a, int ne, double tol, int maxit, do
   hipLaunchKernelGGL(init_block_kernel, dim3(gb), dim3(256), 0, 0, nk, w.X);
   GMAT_HIP(hipGetLastError());
   std::vector<double> th(k), res(ne);
+  // Schedule: a Rayleigh-Ritz step after the first filter pass (it sets the cut at the block's
+  // largest Ritz value), then groups of RR_EVERY passes of which only the last ends in a
+  // Rayleigh-Ritz step and the convergence test; the other passes only re-orthonormalise (one
+  // Cholesky QR: the next filter pass and its QR absorb the loss of orthogonality).
+  constexpr int RR_EVERY = 5;
   int it = 0;
   double rmax = INFINITY;
+  double tm[4] = {0, 0, 0, 0};  // GMAT_DEBUG: filter, QR, Rayleigh-Ritz, residual seconds
+  auto mark = [&](int ph, double t_ph) {
+    if (dbg) {
+      (void)hipDeviceSynchronize();
+      tm[ph] += std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - t_ph;
+    }
+  };
+  auto clock_now = [&]() {
+    if (dbg) (void)hipDeviceSynchronize();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
   for (it = 0; it < maxit;) {
+    const bool rr = it == 0 || (it % RR_EVERY) == 0 || it + 1 == maxit || k == n;
+    double t_ph = clock_now();
     const double *Yf = w.X;
     if (k < n && cut < b) {  // Chebyshev filter of degree deg on [cut, b]: Y_1 = (A - c) X / e, ...
       const double c = 0.5 * (b + cut), e = 0.5 * (b - cut);
@@ -557,24 +746,37 @@ int sym_eig_bottom(int64_t n, const double *a, int ne, double tol, int maxit, do
       GMAT_HIP(hipGetLastError());
       Yf = buf[1];
     }
+    mark(0, t_ph);
+    t_ph = clock_now();
+    ++it;
+    if (!rr) {  // orthonormal basis for the next pass, back in X
+      GMAT_TRY(chol_qr(w, n, k, Yf, w.W));
+      GMAT_HIP(hipMemcpyAsync(w.X, w.W, (size_t)nk * sizeof(double), hipMemcpyDeviceToDevice, 0));
+      mark(1, t_ph);
+      continue;
+    }
     // orthonormal basis Yo = Y2 (Cholesky QR twice, through W), Rayleigh-Ritz
     double *Yo = w.Y2;
     GMAT_TRY(chol_qr(w, n, k, Yf, w.W));
     GMAT_TRY(chol_qr(w, n, k, w.W, Yo));
+    mark(1, t_ph);
+    t_ph = clock_now();
     GMAT_TRY(dgemm(0, n, k, n, 1.0, DView{a, n, 0}, DView{Yo, k, 0}, 0.0, w.W, k));
     GMAT_TRY(dgemm(0, k, k, n, 1.0, DView{Yo, k, 1}, DView{w.W, k, 0}, 0.0, w.H, k));
     GMAT_TRY(small_eig(w, k, w.H, th.data()));
     GMAT_TRY(dgemm(0, n, k, k, 1.0, DView{Yo, k, 0}, DView{w.S, k, 1}, 0.0, w.X, k));
+    mark(2, t_ph);
+    t_ph = clock_now();
     GMAT_TRY(dgemm(0, n, ne, k, 1.0, DView{w.W, k, 0}, DView{w.S, k, 1}, 0.0, w.WS, ne));
     hipLaunchKernelGGL(ritz_res_kernel, dim3(ne), dim3(256), 0, 0, n, k, ne, w.WS, w.X, w.th, w.res);
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipMemcpy(res.data(), w.res, ne * sizeof(double), hipMemcpyDeviceToHost));
+    mark(3, t_ph);
     rmax = 0.0;
     for (int r = 0; r < ne; ++r) rmax = std::max(rmax, res[r]);
     if (dbg)
       fprintf(stderr, "sym_eig_bottom n %lld ne %d k %d: iteration %d cut %.6g b %.6g theta[ne-1] %.6g max res %.3g\n",
               (long long)n, ne, k, it, cut, b, th[ne - 1], rmax);
-    ++it;
     if (rmax <= tol * b || k == n) break;
     cut = th[k - 1];
   }
@@ -586,8 +788,10 @@ int sym_eig_bottom(int64_t n, const double *a, int ne, double tol, int maxit, do
   if (iters) *iters = it;
   GMAT_HIP(hipDeviceSynchronize());
   if (dbg)
-    fprintf(stderr, "sym_eig_bottom n %lld ne %d k %d: %d iterations, max res %.3g, %.1f ms\n", (long long)n, ne, k, it,
-            rmax, 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    fprintf(stderr, "sym_eig_bottom n %lld ne %d k %d: %d iterations, max res %.3g, %.1f ms (filter %.1f, QR %.1f, "
+                    "Rayleigh-Ritz %.1f, residuals %.1f)\n", (long long)n, ne, k, it, rmax,
+            1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), 1e3 * tm[0], 1e3 * tm[1],
+            1e3 * tm[2], 1e3 * tm[3]);
   return GMAT_OK;
 }
 

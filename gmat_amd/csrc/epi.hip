@@ -292,16 +292,18 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 }
 
 // ------------------------------------------------------------------ prefilter pass
-// The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 128 x 128
-// (band row, column) tiles, 8 waves of 32 x 64: the pass streams its operands at ~20 bytes per
-// 64 x 64 x 64 MFMA block, so it is bound by each CU's load rate; a 128-wide tile halves the bytes
-// per pair.  Stage image (24 KB, 64 individuals), five-slot LDS-DMA ring (120 KB), four stages in
-// flight: int8 L3 slices 0, 1 (128 rows x 64 B each), fp4 codes a (128 rows x 32 B) and b (128
-// columns x 32 B).  The squares' fp4 codes (sq4) and the int8 b of the E3 products (i8_of_fp4) come
-// from the codes in registers.  16-byte chunks XOR-swizzled through the DMA source address (int8:
-// chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA instruction q (1 KB) at
-// q KB, wave w issuing q = w + 8u (u < 3).
-constexpr int PF_T = 128, PF_ST = 24 * 1024, PF_NS = 5, PF_Q = 3;
+// The prefilter of the low-rank / MX screens (the PASS 1 products of side_gemm_kernel) on 64 x 256
+// (band row, column) tiles, 8 waves of 32 x 64 (2 row x 4 column waves).  The pass is bound by the
+// chip's L2 -> LDS fabric (~6.4 TB/s of LDS-DMA with every CU streaming), so the tile shape minimises
+// the bytes per pair at the register file's limit of 16,384 pairs (six accumulators each): a row
+// brings 160 B per stage (two int8 L3 slices + fp4 codes), a column 32 B, so 64 x 256 streams 18 KB
+// per stage where 128 x 128 streamed 24 KB.  Stage image (64 individuals), five-slot LDS-DMA ring
+// (90 KB), four stages in flight: int8 L3 slices 0, 1 (64 rows x 64 B each), fp4 codes a (64 rows x
+// 32 B) and b (256 columns x 32 B).  The squares' fp4 codes (sq4) and the int8 b of the E3 products
+// (i8_of_fp4) come from the codes in registers.  16-byte chunks XOR-swizzled through the DMA source
+// address (int8: chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA
+// instruction q (1 KB) at q KB, wave w < 6 issuing q = w + 6u (u < 3), waves 6 and 7 none.
+constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 18 * 1024, PF_NS = 5, PF_Q = 3, PF_QW = 6;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
@@ -326,17 +328,19 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
   const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
   const int rt = tile % x.n_rt, ct = tile / x.n_rt;
-  const int r0 = rt * PF_T;
-  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PF_T;
+  const int r0 = rt * PF_TR;
+  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PF_TC;
   if (r0 >= a.n_rows || c0 >= a.m) return;
-  if (a.tri && c0 + PF_T - 1 <= a.rows[r0]) return;  // rows ascend within a launch
+  if (a.tri && c0 + PF_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
   auto pstamp = [&](int k) __attribute__((always_inline)) {
     if (a.pf_stamp && threadIdx.x == 0) a.pf_stamp[4 * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
   };
   pstamp(0);
-  // 8 waves: wave w = rows 32 (w >> 1) .. +32 x columns 64 (w & 1) .. +64 (two 32-column blocks)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1, h = lane >> 5, c = lane & 31;
-  constexpr int O_R8 = 0, O_R4 = 16384, O_C4 = 20480;
+  // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, h = lane >> 5, c = lane & 31;
+  constexpr int O_R8 = 0, O_R8S = 4096, O_R4 = 8192, O_C4 = 10240;
+  static_assert(O_C4 + PF_TC * 32 == PF_ST && PF_ST == 1024 * PF_Q * PF_QW, "prefilter stage image");
+  const bool dma_wave = w < PF_QW;  // waves 0..5 issue the stage DMAs
   __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
   const uint8_t *src[PF_Q];
   int64_t stp[PF_Q];
@@ -346,31 +350,33 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const int64_t rstride = x.blocked ? SG_K : x.n_pad, fstride = x.blocked ? SG_K / 2 : x.n_pad / 2;
 #pragma unroll
   for (int u = 0; u < PF_Q; ++u) {
-    const int q = w + 8 * u;
-    if (q < 16) {  // int8 L3 slices: 16 rows x 4 chunks per instruction
-      const int row = (q & 7) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-      src[u] = (const uint8_t *)x.rs[q >> 3] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
+    const int q = min(w, PF_QW - 1) + PF_QW * u;
+    if (q < 8) {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
+      const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+      src[u] = (const uint8_t *)x.rs[q >> 2] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
       stp[u] = x.blocked ? a.m * SG_K : SG_K;
-    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 16..19 rows, 20..23 columns)
-      const int qq = q & 3, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-      const int64_t idx = q < 20 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (q < 20 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
+    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 8, 9 rows, 10..17 columns)
+      const int qq = q < 10 ? q - 8 : q - 10, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
+      const int64_t idx = q < 10 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+      src[u] = (q < 10 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
       stp[u] = x.blocked ? a.m * (SG_K / 2) : SG_K / 2;
     }
   }
   auto issue = [&](int st) __attribute__((always_inline)) {
+    if (dma_wave)
 #pragma unroll
-    for (int u = 0; u < PF_Q; ++u)
-      lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PF_NS][(w + 8 * u) * 1024]);
+      for (int u = 0; u < PF_Q; ++u)
+        lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PF_NS][(w + PF_QW * u) * 1024]);
   };
   // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage),
   // then the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm
   // writes LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist
   // the next stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations
-  // retire in order (they do on gfx9 for loads).
+  // retire in order (they do on gfx9 for loads).  Waves 6 and 7 issue no stage DMA: they wait for
+  // nothing of their own (their record DMA is older than any stage) and meet the others at the barrier.
   static_assert(PF_Q == 3 && PF_NS == 5, "wait_for's vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
-    const int ahead = last - st;
+    const int ahead = dma_wave ? last - st : 0;
     if (ahead >= 3)
       asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if (ahead == 2)
@@ -395,15 +401,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   }
   const int S = (int)(x.n_pad / SG_K);
   const int pre = min(S, PF_NS - 1);
-  // the epilogue's test records (32 B per row / column) by one LDS-DMA per wave ahead of the stages:
-  // waves 0-3 the 128 rows, 4-7 the 128 columns, lane l half l & 1 of record 32 (w & 3) + l / 2.  It
-  // retires before stage 0 (in-order vmcnt), so the stage waits cover it.
-  __shared__ __attribute__((aligned(16))) float rec[2 * PF_T][PF_REC];
+  // the epilogue's test records (32 B per row / column) by LDS-DMA ahead of the stages: wave w the
+  // 32 columns 32 w .., waves 0 and 1 also the 32 rows 32 w ..; lane l half l & 1 of record l / 2.
+  // They retire before stage 0 (in-order vmcnt), so the stage waits cover them.
+  __shared__ __attribute__((aligned(16))) float rec[PF_TR + PF_TC][PF_REC];
   {
-    const int k = 32 * (w & 3) + (lane >> 1);
-    const float *s = w < 4 ? x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC
-                           : x.recR + min(c0 + k, a.m - 1) * PF_REC;
-    lds_dma16(s + 4 * (lane & 1), &rec[32 * w][0]);
+    const int k = 32 * w + (lane >> 1);
+    if (w < PF_TR / 32)
+      lds_dma16(x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC + 4 * (lane & 1), &rec[32 * w][0]);
+    lds_dma16(x.recR + min(c0 + k, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[PF_TR + 32 * w][0]);
   }
   for (int st = 0; st < pre; ++st) issue(st);
   wait_for(0, pre - 1);
@@ -425,7 +431,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     for (int kk = 0; kk < 2; ++kk) {
       const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
       const v4i f0 = *(const v4i *)&bf[O_R8 + rrow * 64 + 16 * lr];
-      const v4i f1 = *(const v4i *)&bf[O_R8 + 8192 + rrow * 64 + 16 * lr];
+      const v4i f1 = *(const v4i *)&bf[O_R8S + rrow * 64 + 16 * lr];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const v4i fc = i8_of_fp4((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
@@ -482,7 +488,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     const int cl = 64 * wc + 32 * q + c;
     jq[q] = c0 + cl;
     // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
-    const float4 cv0 = rv[2 * (PF_T + cl)], cv1 = rv[2 * (PF_T + cl) + 1];
+    const float4 cv0 = rv[2 * (PF_TR + cl)], cv1 = rv[2 * (PF_TR + cl) + 1];
     cbe[q] = cv0.x;
     ccb[q] = cv0.y;
     cC1n[q] = cv0.z;
@@ -2980,6 +2986,7 @@ struct gmat_epi {
     Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2], count2;
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
+  hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
   struct LrcBuffers {
     DBuf drows[2], lmask[2], e13[2], pfc[2], slot_row[2], slot_j[2], cnt[2], soff[2], info[2];
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
@@ -2987,6 +2994,7 @@ struct gmat_epi {
     if (s1) (void)hipStreamDestroy(s1);
     if (s2) (void)hipStreamDestroy(s2);
     if (s3) (void)hipStreamDestroy(s3);
+    if (s4) (void)hipStreamDestroy(s4);
   }
 };
 
@@ -3306,11 +3314,15 @@ int eigen_bottom(gmat_epi *e, const double *dP, double trP, int ne, Eigen *eg) {
   eg->ne = ne;
   eg->lam.resize(ne);
   eg->Z.resize((size_t)n * ne);
-  // residual tolerance 2e-4 of the Gershgorin bound: the certificates then reach within ~0.1 % of
-  // those of exact eigenpairs on the bench cohort (tighter costs block iterations, not hits)
+  // residual tolerance 3e-4 of the Gershgorin bound (two Rayleigh-Ritz steps on the bench cohort);
+  // lam_r = theta_r - |residual_r| (a Ritz value lies within its residual of an eigenvalue): with
+  // these the certificates reach within ~0.3 % of those of exact eigenpairs (tighter costs block
+  // iterations, not hits)
   const char *tenv = getenv("GMAT_EIG_TOL");
-  GMAT_TRY(sym_eig_bottom(n, A.as<double>(), ne, tenv ? atof(tenv) : 2e-4, 12, eg->lam.data(), Z.as<double>(), nullptr,
-                          &eg->iters));
+  std::vector<double> res(ne);
+  GMAT_TRY(sym_eig_bottom(n, A.as<double>(), ne, tenv ? atof(tenv) : 3e-4, 16, eg->lam.data(), Z.as<double>(),
+                          res.data(), &eg->iters));
+  for (int r = 0; r < ne; ++r) eg->lam[r] -= res[r];
   GMAT_HIP(hipMemcpy(eg->Z.data(), Z.p, eg->Z.size() * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }
@@ -4312,7 +4324,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
   if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
   if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
-  const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
+  if (!e->s4) GMAT_HIP(hipStreamCreateWithFlags(&e->s4, hipStreamNonBlocking));
+  // the prefilter passes of even / odd launches on two streams: launch L + 1 (other buffer set) can
+  // start on the CUs that the tail of launch L leaves idle (a launch's ~800 equal tiles fill its last
+  // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
+  const hipStream_t sm = e->s1, S3 = e->s3;
+  const hipStream_t S2b[2] = {e->s2, getenv("GMAT_PF_ONE_STREAM") ? e->s2 : e->s4};
   GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
   struct Events {
     std::vector<hipEvent_t> v;
@@ -4348,6 +4365,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   int64_t known_count = 0, inflight = 0;
   // the prefilter pass and the slot lists of launch li into buffer set b (stream S2)
   auto enqueue_side = [&](size_t li, int b) -> int {
+    const hipStream_t S2 = S2b[b];
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, scr_end[b], 0));  // buffer set b free (screen two launches back)
@@ -4419,19 +4437,19 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         x.rs4 = L.p4b.as<uint8_t>();
         x.cs4 = R.p4b.as<uint8_t>();
       }
-      x.n_rt = (int)cdiv(Rn, PF_T);
+      x.n_rt = (int)cdiv(Rn, PF_TR);
       // MFMA work of the tiles that run (a tile entirely left of the diagonal exits at once): per pair
       // 4 fp4 code products + 2 int8 E3 slices over n_pad individuals = 16 n_pad fp4-equivalent ops
       int64_t run = 0;
       for (int rt = 0; rt < x.n_rt; ++rt)
-        for (int64_t ct = 0; ct < cdiv(ncols, PF_T); ++ct) {
-          const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_T;
-          if (c0 < m && !(tri && c0 + PF_T - 1 <= ln.rows[rt * PF_T])) ++run;
+        for (int64_t ct = 0; ct < cdiv(ncols, PF_TC); ++ct) {
+          const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_TC;
+          if (c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR])) ++run;
         }
-      pf_ops_of[li] = (double)run * PF_T * PF_T * 16.0 * (double)n_pad;
+      pf_ops_of[li] = (double)run * PF_TR * PF_TC * 16.0 * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
-      if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_T);
-      hipLaunchKernelGGL(prefilter_pass_kernel, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_T))), dim3(512), 0, S2, x);
+      if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
+      hipLaunchKernelGGL(prefilter_pass_kernel, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512), 0, S2, x);
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
       for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
@@ -5050,8 +5068,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.cs4 = R.p4.as<uint8_t>();
       if (e->pf_ncov == 0) {  // prefilter pass: 128 x 128 tiles
         SideArgs xp = x;
-        xp.n_rt = (int)cdiv(Rn, PF_T);
-        const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_T));
+        xp.n_rt = (int)cdiv(Rn, PF_TR);
+        const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
         hipLaunchKernelGGL(prefilter_pass_kernel, dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
