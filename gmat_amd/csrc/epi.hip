@@ -323,6 +323,23 @@ __device__ __forceinline__ v4i i8_of_fp4(unsigned x0, unsigned x1) {
   r[3] = (int)__builtin_amdgcn_perm(h1, l1, 0x07030602u);
   return r;
 }
+// int8 values of 16 fp4 codes WITHOUT the interleave: even individuals of the first dword, odd ones,
+// then the same for the second (K slot order 0 2 4 6 1 3 5 7 per 8 individuals).  The prefilter's
+// stage-blocked int8 L3 panels are stored in that order (block_panel_perm8_kernel), so A and B agree
+// slot by slot and the two v_perm per dword are gone.
+__device__ __forceinline__ v4i i8_of_fp4_eo(unsigned x0, unsigned x1) {
+  v4i r;
+  r[0] = (int)((x0 >> 1) & 0x07070707u);
+  r[1] = (int)((x0 >> 5) & 0x07070707u);
+  r[2] = (int)((x1 >> 1) & 0x07070707u);
+  r[3] = (int)((x1 >> 5) & 0x07070707u);
+  return r;
+}
+// LDS-DMA with the LDS destination given as a wave-uniform byte address (m0), no per-call
+// generic -> LDS address conversion
+__device__ __forceinline__ void lds_dma16_m0(const void *g, unsigned m0) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(m0) : "memory");
+}
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const ScreenArgs &a = x.a;
   const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
@@ -337,36 +354,40 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   };
   pstamp(0);
   // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, h = lane >> 5, c = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wr = w >> 2, wc = w & 3;  // wave-uniform (SGPR)
   constexpr int O_R8 = 0, O_R8S = 4096, O_R4 = 8192, O_C4 = 10240;
   static_assert(O_C4 + PF_TC * 32 == PF_ST && PF_ST == 1024 * PF_Q * PF_QW, "prefilter stage image");
   const bool dma_wave = w < PF_QW;  // waves 0..5 issue the stage DMAs
   __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
   const uint8_t *src[PF_Q];
   int64_t stp[PF_Q];
-  // stage-blocked panels (x.blocked): a stage's 64-byte / 32-byte pieces of consecutive SNPs are
-  // contiguous, so an instruction's 1 KB comes from 8 whole 128-byte lines (row-major panels: from
-  // 16 - 32 lines, 32 - 64 bytes used of each)
-  const int64_t rstride = x.blocked ? SG_K : x.n_pad, fstride = x.blocked ? SG_K / 2 : x.n_pad / 2;
+  // stage-blocked panels: a stage's 64-byte / 32-byte pieces of consecutive SNPs are contiguous, so
+  // an instruction's 1 KB comes from 8 whole 128-byte lines (int8 pieces in the even / odd
+  // individual order of i8_of_fp4_eo)
+  constexpr int64_t rstride = SG_K, fstride = SG_K / 2;
 #pragma unroll
   for (int u = 0; u < PF_Q; ++u) {
     const int q = min(w, PF_QW - 1) + PF_QW * u;
     if (q < 8) {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
       const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
       src[u] = (const uint8_t *)x.rs[q >> 2] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
-      stp[u] = x.blocked ? a.m * SG_K : SG_K;
+      stp[u] = a.m * SG_K;
     } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 8, 9 rows, 10..17 columns)
       const int qq = q < 10 ? q - 8 : q - 10, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
       const int64_t idx = q < 10 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
       src[u] = (q < 10 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
-      stp[u] = x.blocked ? a.m * (SG_K / 2) : SG_K / 2;
+      stp[u] = a.m * (SG_K / 2);
     }
   }
-  auto issue = [&](int st) __attribute__((always_inline)) {
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
+  // stage st into ring slot `slot` (= st % PF_NS, kept by the caller)
+  auto issue = [&](int st, int slot) __attribute__((always_inline)) {
     if (dma_wave)
 #pragma unroll
       for (int u = 0; u < PF_Q; ++u)
-        lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PF_NS][(w + PF_QW * u) * 1024]);
+        lds_dma16_m0(src[u] + (int64_t)st * stp[u], ring_m0 + slot * PF_ST + PF_QW * u * 1024);
   };
   // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage),
   // then the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm
@@ -411,14 +432,17 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       lds_dma16(x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC + 4 * (lane & 1), &rec[32 * w][0]);
     lds_dma16(x.recR + min(c0 + k, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[PF_TR + 32 * w][0]);
   }
-  for (int st = 0; st < pre; ++st) issue(st);
+  for (int st = 0; st < pre; ++st) issue(st, st);
   wait_for(0, pre - 1);
   pstamp(1);
   const int rrow = 32 * wr + c;
+  int slot = 0, slot_ahead = PF_NS - 1;  // ring slots of stage st and of stage st + 4
   for (int st = 0; st < S; ++st) {
-    const uint8_t *bf = ring[st % PF_NS];
+    const uint8_t *bf = ring[slot];
     // slot (st + 4) % 5 was read in stage st - 1, which every wave has left (barrier)
-    if (st + PF_NS - 1 < S) issue(st + PF_NS - 1);
+    if (st + PF_NS - 1 < S) issue(st + PF_NS - 1, slot_ahead);
+    slot = slot == PF_NS - 1 ? 0 : slot + 1;
+    slot_ahead = slot_ahead == PF_NS - 1 ? 0 : slot_ahead + 1;
     // lane (c, h) holds the fp4 codes of individuals 32h .. 32h + 31 of the stage; the int8 E3
     // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
     v4i rb4[2];
@@ -434,7 +458,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const v4i f1 = *(const v4i *)&bf[O_R8S + rrow * 64 + 16 * lr];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const v4i fc = i8_of_fp4((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
+        const v4i fc = i8_of_fp4_eo((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
         acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
         acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
       }
@@ -2642,6 +2666,22 @@ __global__ void block_panel_kernel(int64_t m, int64_t W, int64_t w, const uint8_
   const int64_t snp = t / per, o = (t % per) * 16, st = o / w, b = o % w;
   *(v4i *)(dst + (st * m + snp) * w + b) = *(const v4i *)(src + snp * W + o);
 }
+// The same for int8 rows with each 8 bytes reordered to individuals 0 2 4 6 1 3 5 7 (the K slot
+// order of i8_of_fp4_eo)
+__global__ void block_panel_perm8_kernel(int64_t m, int64_t W, int64_t w, const uint8_t *__restrict__ src,
+                                         uint8_t *__restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = W / 16;
+  if (t >= m * per) return;
+  const int64_t snp = t / per, o = (t % per) * 16, st = o / w, b = o % w;
+  v4i v = *(const v4i *)(src + snp * W + o);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // bytes 0..7 of dwords (2h, 2h + 1): even ones first, then odd
+    const unsigned lo = (unsigned)v[2 * h], hi = (unsigned)v[2 * h + 1];
+    v[2 * h] = (int)__builtin_amdgcn_perm(hi, lo, 0x06040200u);
+    v[2 * h + 1] = (int)__builtin_amdgcn_perm(hi, lo, 0x07050301u);
+  }
+  *(v4i *)(dst + (st * m + snp) * w + b) = v;
+}
 // prefilter test records (prefilter_pass_kernel's epilogue, 32 bytes per SNP, fetched by LDS-DMA with
 // the first stage): fp64 per-SNP sums rounded once to fp32, exactly the values the test used to derive
 // itself.  Row role: [i (int bits; -1 = monomorphic), alpha, csum, R1 = csq - 2 alpha csum, sL3, sa,
@@ -3097,8 +3137,8 @@ int build_coding_impl(gmat_epi *e, int which) {
                      (int64_t)SG_K / 2, cd.p4.as<uint8_t>(), cd.p4b.as<uint8_t>());
   GMAT_TRY(cd.L3b.alloc((size_t)E3_PF * m * n_pad));
   for (int t = 0; t < E3_PF; ++t)
-    hipLaunchKernelGGL(block_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad,
-                       (int64_t)SG_K, (const uint8_t *)cd.L3q.as<int8_t>() + (int64_t)t * m * n_pad,
+    hipLaunchKernelGGL(block_panel_perm8_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m,
+                       n_pad, (int64_t)SG_K, (const uint8_t *)cd.L3q.as<int8_t>() + (int64_t)t * m * n_pad,
                        cd.L3b.as<uint8_t>() + (int64_t)t * m * n_pad);
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.pfRecL.alloc((size_t)m * PF_REC * sizeof(float)));
@@ -4430,13 +4470,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     x.blocked = 0;
     x.recL = L.pfRecL.as<float>();
     x.recR = R.pfRecR.as<float>();
-    if (e->pf_ncov == 0) {
-      if (!getenv("GMAT_PF_ROWMAJOR")) {  // stage-blocked operands (A/B: GMAT_PF_ROWMAJOR=1)
-        x.blocked = 1;
-        for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
-        x.rs4 = L.p4b.as<uint8_t>();
-        x.cs4 = R.p4b.as<uint8_t>();
-      }
+    if (e->pf_ncov == 0) {  // prefilter_pass_kernel reads stage-blocked operands
+      x.blocked = 1;
+      for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
+      x.rs4 = L.p4b.as<uint8_t>();
+      x.cs4 = R.p4b.as<uint8_t>();
       x.n_rt = (int)cdiv(Rn, PF_TR);
       // MFMA work of the tiles that run (a tile entirely left of the diagonal exits at once): per pair
       // 4 fp4 code products + 2 int8 E3 slices over n_pad individuals = 16 n_pad fp4-equivalent ops
@@ -5066,8 +5104,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       x.cs[0] = srp;
       x.rs4 = L.p4.as<uint8_t>();
       x.cs4 = R.p4.as<uint8_t>();
-      if (e->pf_ncov == 0) {  // prefilter pass: 128 x 128 tiles
+      if (e->pf_ncov == 0) {  // prefilter pass (stage-blocked operands)
         SideArgs xp = x;
+        xp.blocked = 1;
+        for (int t = 0; t < E3_PF; ++t) xp.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
+        xp.rs4 = L.p4b.as<uint8_t>();
+        xp.cs4 = R.p4b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
         hipLaunchKernelGGL(prefilter_pass_kernel, dim3(gp), dim3(512), 0, S2, xp);
