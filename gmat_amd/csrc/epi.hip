@@ -305,6 +305,7 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 // instruction q (1 KB) at q KB, wave w < 6 issuing q = w + 6u (u < 3), waves 6 and 7 none.
 constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 18 * 1024, PF_NS = 5, PF_Q = 3, PF_QW = 6;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
+constexpr int PF_NSTAMP = 7;  // GMAT_PF_STAMPS: start, prologue, main loop, column records, tests, stores, end
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
   v8i_ r = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -323,16 +324,17 @@ __device__ __forceinline__ v4i i8_of_fp4(unsigned x0, unsigned x1) {
   r[3] = (int)__builtin_amdgcn_perm(h1, l1, 0x07030602u);
   return r;
 }
-// int8 values of 16 fp4 codes WITHOUT the interleave: even individuals of the first dword, odd ones,
-// then the same for the second (K slot order 0 2 4 6 1 3 5 7 per 8 individuals).  The prefilter's
-// stage-blocked int8 L3 panels are stored in that order (block_panel_perm8_kernel), so A and B agree
-// slot by slot and the two v_perm per dword are gone.
-__device__ __forceinline__ v4i i8_of_fp4_eo(unsigned x0, unsigned x1) {
+// int8 values 2b of 16 fp4 codes (code = 2b for b in {0, 1, 2}) WITHOUT the interleave: even
+// individuals of the first dword, odd ones, then the same for the second (K slot order 0 2 4 6 1 3 5 7
+// per 8 individuals).  The prefilter's stage-blocked int8 L3 panels are stored in that order
+// (block_panel_perm8_kernel), so A and B agree slot by slot: three VALU per dword, no v_perm.  The
+// products come out doubled (exactly: every term is even) and are halved where they are used.
+__device__ __forceinline__ v4i i8x2_of_fp4_eo(unsigned x0, unsigned x1) {
   v4i r;
-  r[0] = (int)((x0 >> 1) & 0x07070707u);
-  r[1] = (int)((x0 >> 5) & 0x07070707u);
-  r[2] = (int)((x1 >> 1) & 0x07070707u);
-  r[3] = (int)((x1 >> 5) & 0x07070707u);
+  r[0] = (int)(x0 & 0x0f0f0f0fu);
+  r[1] = (int)((x0 >> 4) & 0x0f0f0f0fu);
+  r[2] = (int)(x1 & 0x0f0f0f0fu);
+  r[3] = (int)((x1 >> 4) & 0x0f0f0f0fu);
   return r;
 }
 // LDS-DMA with the LDS destination given as a wave-uniform byte address (m0), no per-call
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   if (r0 >= a.n_rows || c0 >= a.m) return;
   if (a.tri && c0 + PF_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
   auto pstamp = [&](int k) __attribute__((always_inline)) {
-    if (a.pf_stamp && threadIdx.x == 0) a.pf_stamp[4 * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+    if (a.pf_stamp && threadIdx.x == 0) a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
   };
   pstamp(0);
   // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   int64_t stp[PF_Q];
   // stage-blocked panels: a stage's 64-byte / 32-byte pieces of consecutive SNPs are contiguous, so
   // an instruction's 1 KB comes from 8 whole 128-byte lines (int8 pieces in the even / odd
-  // individual order of i8_of_fp4_eo)
+  // individual order of i8x2_of_fp4_eo)
   constexpr int64_t rstride = SG_K, fstride = SG_K / 2;
 #pragma unroll
   for (int u = 0; u < PF_Q; ++u) {
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const v4i f1 = *(const v4i *)&bf[O_R8S + rrow * 64 + 16 * lr];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const v4i fc = i8_of_fp4_eo((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
+        const v4i fc = i8x2_of_fp4_eo((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
         acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
         acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
       }
@@ -496,21 +498,22 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // = sL3 c3 - beta sa + alpha (beta spy - sb) is off by at most 2^-20 times the sum of the three
   // terms' magnitudes, which is added to eff_hi with the int8 slicing bound.  The final comparison's
   // three roundings are covered by the factor 1 + 2^-18.
-  // per-row / per-column values: the records in rec[] (pf_rec_kernel).  Straight-line evaluation
-  // (no branches: with two waves per SIMD the LDS latency of a record read behind a branch is not
-  // hidden), row records read once for both column blocks, live bits collected per column block.
+  // per-row / per-column values: the records in rec[] (pf_rec_kernel).  Two passes: the tests of all
+  // 32 (row, column block) elements of a lane as straight-line code (no branch between them, so the
+  // row records' LDS reads are scheduled ahead of their use), collecting the live masks and a per-lane
+  // bit per element for the stores; then the stores of the live blocks' products (a few per cent).
   const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id);
   const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
   const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
   constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f;
   const float4 *rv = (const float4 *)&rec[0][0];
-  int64_t jq[2];
+  int jq[2];  // SNP indices < 2^31
   bool cok[2];
   float cbe[2], ccb[2], cC1n[2], cnb[2], cbsb[2], cmag[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int cl = 64 * wc + 32 * q + c;
-    jq[q] = c0 + cl;
+    jq[q] = (int)(c0 + cl);
     // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
     const float4 cv0 = rv[2 * (PF_TR + cl)], cv1 = rv[2 * (PF_TR + cl) + 1];
     cbe[q] = cv0.x;
@@ -523,7 +526,8 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   }
   // masks: lane t < 32 of the wave writes the word of (e = t / 2, half t % 2) of each column block
   const int te = (lane >> 1) & 15, th = lane & 1;
-  unsigned mine[2] = {0u, 0u}, n_live = 0;
+  unsigned mine[2] = {0u, 0u}, n_live = 0, st_bits = 0u;
+  pstamp(3);
   const int rw = r0 + 32 * wr;
   const int64_t cw = c0 + 64 * wc - a.j_lo;
   const uint32_t voff = (uint32_t)(4 * h * a.ld_e + c);
@@ -535,16 +539,16 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     const int rl = 32 * wr + kr + 4 * h, r = r0 + rl;
     const float4 r0v = rv[2 * rl], r1v = rv[2 * rl + 1];  // i, alpha, csum, R1 | sL3, sa, (2 + alpha)^2
     const int iv = __float_as_int(r0v.x);
-    const float al = r0v.y, sL3 = r1v.x;
+    const float al = r0v.y, sL3 = r1v.x, sL3h = 0.5f * sL3;
     const bool rok = (r < a.n_rows) & (iv >= 0);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const bool ok = rok & cok[q] & !(a.tri & (jq[q] <= (int64_t)iv));
+      const bool ok = rok & cok[q] & !(a.tri & (jq[q] <= iv));
       const float be = cbe[q];
-      float c3 = 0.0f;
+      float c3 = 0.0f;  // twice the E3 slice sum (the doubled int8 b), halved through sL3h
 #pragma unroll
       for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
-      const float t1 = sL3 * c3, t2 = be * r1v.y, t3 = al * cbsb[q];
+      const float t1 = sL3h * c3, t2 = be * r1v.y, t3 = al * cbsb[q];
       const float eff = t1 - t2 + t3;
       const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb[q] + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
       const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
@@ -557,18 +561,28 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       n_live += (unsigned)__popcll(bal);
       const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
       mine[q] = te == e ? (th ? w1 : w0) : mine[q];
-      if ((h ? w1 : w0) != 0 && (r < a.n_rows) && cok[q]) {
-        // a live block: its E3 (and code products) for the low-rank / pair screens (cok: j in range;
-        // a monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+      // a live block (its row r < n_rows: some lane of the half passed rok) whose column this lane holds
+      st_bits |= (((h ? w1 : w0) != 0u) & cok[q] ? 1u : 0u) << (2 * e + q);
+    }
+  }
+  pstamp(4);
+  // a live block's E3 (and code products) for the low-rank / pair screens (cok: j in range; a
+  // monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int kr = (e & 3) + 8 * (e >> 2);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if ((st_bits >> (2 * e + q)) & 1u) {
         const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
 #pragma unroll
-        for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e];
+        for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e] >> 1;  // exact
         if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
 #pragma unroll
           for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
       }
-    }
   }
+  pstamp(5);
   const int tr = r0 + 32 * wr + (te & 3) + 8 * (te >> 2) + 4 * th;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -580,7 +594,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   }
   if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
   if (a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
-  pstamp(3);
+  pstamp(6);
 }
 
 // ------------------------------------------------------------------ prefilter pass, covariate designs
@@ -2667,7 +2681,7 @@ __global__ void block_panel_kernel(int64_t m, int64_t W, int64_t w, const uint8_
   *(v4i *)(dst + (st * m + snp) * w + b) = *(const v4i *)(src + snp * W + o);
 }
 // The same for int8 rows with each 8 bytes reordered to individuals 0 2 4 6 1 3 5 7 (the K slot
-// order of i8_of_fp4_eo)
+// order of i8x2_of_fp4_eo)
 __global__ void block_panel_perm8_kernel(int64_t m, int64_t W, int64_t w, const uint8_t *__restrict__ src,
                                          uint8_t *__restrict__ dst) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = W / 16;
@@ -4358,8 +4372,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const size_t stamp_launch = 5;
   int64_t stamp_grid = 0;
   if (getenv("GMAT_PF_STAMPS")) {
-    GMAT_TRY(pf_st.alloc((size_t)4 * 8 * 1 << 20));
-    GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)4 * 8 * 1 << 20));
+    GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
+    GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
   }
   if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
   if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
@@ -4705,22 +4719,24 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   e->kstats[6] = t_ref;
   e->kstats[7] = -1;
   if (pf_st.p && stamp_grid > 0 && stamp_grid <= (1 << 20)) {  // phase times of the stamped launch
-    std::vector<unsigned long long> hs((size_t)4 * stamp_grid);
+    std::vector<unsigned long long> hs((size_t)PF_NSTAMP * stamp_grid);
     GMAT_HIP(hipMemcpy(hs.data(), pf_st.p, hs.size() * 8, hipMemcpyDeviceToHost));
-    double d[3] = {0, 0, 0};
+    double d[PF_NSTAMP - 1] = {0, 0, 0, 0, 0, 0};
     unsigned long long t_min = ~0ull, t_max = 0;
     int64_t nw = 0;
     for (int64_t g = 0; g < stamp_grid; ++g) {
-      const unsigned long long *q = &hs[4 * g];
-      if (!q[0] || !q[3]) continue;  // tiles that exit at once
+      const unsigned long long *q = &hs[PF_NSTAMP * g];
+      if (!q[0] || !q[PF_NSTAMP - 1]) continue;  // tiles that exit at once
       ++nw;
-      for (int k = 0; k < 3; ++k) d[k] += (double)(q[k + 1] - q[k]) * 0.01;  // 100 MHz ticks -> us
+      for (int k = 0; k + 1 < PF_NSTAMP; ++k) d[k] += (double)(q[k + 1] - q[k]) * 0.01;  // 100 MHz ticks -> us
       t_min = std::min(t_min, q[0]);
-      t_max = std::max(t_max, q[3]);
+      t_max = std::max(t_max, q[PF_NSTAMP - 1]);
     }
+    const double nn = (double)std::max<int64_t>(nw, 1);
     fprintf(stderr, "prefilter launch %zu: %lld tiles run, per tile: prologue %.2f us, main loop %.2f us, epilogue "
-            "%.2f us; launch span %.1f us\n", stamp_launch, (long long)nw, d[0] / std::max<int64_t>(nw, 1),
-            d[1] / std::max<int64_t>(nw, 1), d[2] / std::max<int64_t>(nw, 1), (double)(t_max - t_min) * 0.01);
+            "%.2f us (column records %.2f, tests %.2f, stores %.2f, masks %.2f); launch span %.1f us\n", stamp_launch,
+            (long long)nw, d[0] / nn, d[1] / nn, (d[2] + d[3] + d[4] + d[5]) / nn, d[2] / nn, d[3] / nn, d[4] / nn,
+            d[5] / nn, (double)(t_max - t_min) * 0.01);
   }
   if (live_cnt.p) {
     unsigned long long lcnt = 0;
