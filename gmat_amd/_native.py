@@ -55,6 +55,7 @@ _PROTOS = {
     "gmat_blup": (_INT, [_I64, _I64, _I64, _INT, _P, _P, _P, _P, _P, _P]),
     "gmat_write_grm_text": (_INT, [ctypes.c_char_p, _P, _I64, _INT, ctypes.c_char_p, _INT]),
     "gmat_float_repr": (_INT, [_D, ctypes.c_char_p, _INT]),
+    "gmat_append_hit_rows": (_INT, [ctypes.c_char_p, _I64, _P, _P, _INT, _P, _P, _P, _P]),
     "gmat_snp_test": (_INT, [_P, _INT, _P, _P, _P, _P]),
     "gmat_probe_mx_accum": (_INT, [_INT, _P, _P, _P]),
     "gmat_probe_eig_bottom": (_INT, [_I64, _P, _INT, _D, _INT, _P, _P, _P, _P]),

@@ -6,6 +6,9 @@
 // Right-looking, 64-wide panels: a one-workgroup kernel factors the diagonal block (16-wide
 // sub-panels in registers) and inverts its factor; the panel solve and the trailing update are
 // MFMA dgemm calls.
+#include <mutex>
+#include <vector>
+
 #include "dla.h"
 
 namespace gmat {
@@ -190,6 +193,65 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
     double *a22 = a + (k0 + kb) * lda + (k0 + kb);
     GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
   }
+  return GMAT_OK;
+}
+
+// cholesky() and chol_lower_inverse() overlapped: block row i of L^-1 needs only panel i of L (its
+// diagonal block's inverse and the panel below it, final once the panel solve of step i is done), so
+// the inverse's step i runs on a second stream as soon as that panel is out, beside the factorisation's
+// trailing update and later panels.  Both chains are dozens of small dependent launches that leave most
+// CUs idle; side by side they take about the time of the longer one.  The inverse is computed even if
+// a pivot fails (the caller checks *info_dev).
+int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
+                     double *linv) {
+  static std::mutex mu;
+  static hipStream_t side[64] = {nullptr};
+  static std::vector<hipEvent_t> evs[64];
+  int dev = 0;
+  GMAT_HIP(hipGetDevice(&dev));
+  GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_ARG, "cholesky_inverse: device %d", dev);
+  std::lock_guard<std::mutex> lock(mu);
+  if (!side[dev]) GMAT_HIP(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
+  const hipStream_t s2 = side[dev];
+  const int64_t nb = cdiv(n, NB);
+  while ((int64_t)evs[dev].size() < nb + 2) {
+    hipEvent_t e;
+    GMAT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    evs[dev].push_back(e);
+  }
+  hipEvent_t *ev = evs[dev].data();  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done
+  GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
+  GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
+  GMAT_HIP(hipEventRecord(ev[0], s));
+  GMAT_HIP(hipStreamWaitEvent(s2, ev[0], 0));  // after the caller's earlier work on s
+  hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s2, linv, n * n);
+  GMAT_HIP(hipGetLastError());
+  for (int64_t k0 = 0, i = 0; k0 < n; k0 += NB, ++i) {
+    const int kb = (int)std::min<int64_t>(NB, n - k0);
+    double *akk = a + k0 * lda + k0;
+    hipLaunchKernelGGL(potf2_kernel, dim3(1), dim3(256), 0, s, kb, akk, lda, dinv + k0 * NB, logdet_dev, info_dev, k0);
+    GMAT_HIP(hipGetLastError());
+    const int64_t rem = n - k0 - kb;
+    double *panel = a + (k0 + kb) * lda + k0;
+    if (rem > 0)  // L21 = A21 * inv(L11)'
+      GMAT_TRY(dgemm(s, rem, kb, kb, 1.0, DView{panel, lda, 0}, DView{dinv + k0 * NB, NB, 1}, 0.0, panel, lda));
+    GMAT_HIP(hipEventRecord(ev[1 + i], s));
+    // inverse step i on the side stream (chol_lower_inverse's loop body)
+    GMAT_HIP(hipStreamWaitEvent(s2, ev[1 + i], 0));
+    double *xi = linv + k0 * n;
+    if (k0 > 0) GMAT_TRY(dgemm(s2, kb, k0, kb, 1.0, DView{dinv + k0 * NB, NB, 0}, DView{xi, n, 0}, 0.0, xi, n));
+    hipLaunchKernelGGL(copy_block_kernel, dim3(kb), dim3(NB), 0, s2, kb, dinv + k0 * NB, xi + k0, n);
+    GMAT_HIP(hipGetLastError());
+    if (rem > 0) {
+      GMAT_TRY(dgemm(s2, rem, k0 + kb, kb, -1.0, DView{a + (k0 + kb) * lda + k0, lda, 0}, DView{xi, n, 0}, 1.0,
+                     linv + (k0 + kb) * n, n));
+      // A22 -= L21 L21'  (lower tiles)
+      double *a22 = a + (k0 + kb) * lda + (k0 + kb);
+      GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
+    }
+  }
+  GMAT_HIP(hipEventRecord(ev[nb + 1], s2));
+  GMAT_HIP(hipStreamWaitEvent(s, ev[nb + 1], 0));
   return GMAT_OK;
 }
 

@@ -35,6 +35,11 @@ int dgemm_i8b(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DVie
 // the diagonal blocks are written to dinv (n x 64 doubles).  *logdet_dev (device double)
 // receives sum(log(diag(L)))*2; *info_dev (device int) > 0 marks a non-positive pivot.
 int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev);
+// cholesky() followed by chol_lower_inverse(l = a) into linv, the inverse's block steps overlapped
+// with the factorisation on a second stream (ordered after the caller's earlier work on s; s waits
+// for both on return).
+int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
+                     double *linv);
 // linv = L^-1 (n x n, lower triangle; the upper triangle is zeroed) from the factor and its
 // diagonal-block inverses.
 int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *linv);

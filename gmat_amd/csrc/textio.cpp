@@ -1,4 +1,5 @@
-// Multi-threaded writers of the relationship-matrix text formats (gmatrix.py:10-31).
+// Multi-threaded writers of the relationship-matrix text formats (gmatrix.py:10-31), and the scans'
+// hit rows (DataFrame.to_csv of remma_epiAA.py:84-86 / remma_epiAA_pair.py: ints, then float reprs).
 //
 // 'mat' is np.savetxt's default ("%.18e", ' ' between values, '\n' per row): glibc's
 // printf and CPython's '%' formatting both round correctly, so the bytes are identical.
@@ -6,6 +7,7 @@
 // shortest round-trip repr of each value (CPython float_repr_style 'short'): digits from
 // std::to_chars (shortest round trip), laid out with CPython's rules -- fixed notation for
 // decimal exponents -4 <= e < 16, otherwise d[.ddd]e(+|-)XX.
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -110,6 +112,39 @@ extern "C" int gmat_float_repr(double v, char *out, int cap) {
   const int l = py_repr(v, out);
   out[l] = 0;
   return l;
+}
+
+// Append n hit rows "i j v_0 .. v_{nf-1}\n" (values as CPython repr) to path: the scans' result
+// files, byte-identical to the reference's DataFrame.to_csv(sep=' ', header=False, index=False)
+// rows (remma_epiAA.py:84-86) and to gmat_amd.remma._scan.format_rows.
+extern "C" int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *i, const int64_t *j, int nf,
+                                    const double *f0, const double *f1, const double *f2, const double *f3) {
+  const double *fv[4] = {f0, f1, f2, f3};
+  GMAT_CHECK(path && n >= 0 && nf >= 1 && nf <= 4 && (n == 0 || (i && j)), GMAT_E_ARG,
+             "gmat_append_hit_rows: bad arguments");
+  for (int k = 0; k < nf; ++k) GMAT_CHECK(n == 0 || fv[k], GMAT_E_ARG, "gmat_append_hit_rows: column %d missing", k);
+  FILE *f = fopen(path, "ab");
+  GMAT_CHECK(f, GMAT_E_ARG, "gmat_append_hit_rows: cannot open %s", path);
+  std::string buf;
+  buf.reserve((size_t)std::min<int64_t>(n, 1 << 20) * (16 + 25 * nf));
+  char tmp[96];
+  int rc = GMAT_OK;
+  for (int64_t r = 0; r < n; ++r) {
+    const int l = snprintf(tmp, sizeof(tmp), "%lld %lld", (long long)i[r], (long long)j[r]);
+    buf.append(tmp, l);
+    for (int k = 0; k < nf; ++k) {
+      buf.push_back(' ');
+      buf.append(tmp, py_repr(fv[k][r], tmp));
+    }
+    buf.push_back('\n');
+    if (buf.size() > (8u << 20) || r + 1 == n) {
+      if (fwrite(buf.data(), 1, buf.size(), f) != buf.size()) rc = GMAT_E_ARG;
+      buf.clear();
+    }
+  }
+  if (fclose(f) != 0) rc = GMAT_E_ARG;
+  GMAT_CHECK(rc == GMAT_OK, rc, "gmat_append_hit_rows: write to %s failed", path);
+  return GMAT_OK;
 }
 
 extern "C" int gmat_write_grm_text(const char *path, const double *mat, int64_t n, int fmt, const char *ids_blob,

@@ -6,6 +6,7 @@ hits; this module keeps the reference's argument handling, defaults, error condi
 output files and row order.
 """
 import ctypes
+import os
 import logging
 import time
 
@@ -146,11 +147,22 @@ def open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file):
 
 
 def format_rows(cols, n_float):
-    """Rows as pandas DataFrame.to_csv writes them: ints, then float64 reprs."""
+    """Rows as pandas DataFrame.to_csv writes them: ints, then float64 reprs (the Python statement
+    of what append_rows writes natively)."""
     i, j = cols[0], cols[1]
     fl = cols[2:2 + n_float]
     return "".join("%d %d %s\n" % (a, b, " ".join(repr(float(v[t])) for v in fl)) for t, (a, b) in
                    enumerate(zip(i.tolist(), j.tolist())))
+
+
+def append_rows(path, cols, n_float):
+    """Append format_rows(cols, n_float) to the file at path through the library's C++ writer
+    (gmat_append_hit_rows: same bytes, ~30x faster than the Python formatting)."""
+    lib = N.load()
+    i, j = N.i64(cols[0]), N.i64(cols[1])
+    fl = [N.f64(v) for v in cols[2:2 + n_float]] + [None] * (4 - n_float)
+    N.check(lib.gmat_append_hit_rows(os.fsencode(path), i.size, N.ptr(i), N.ptr(j), n_float, *[N.ptr(v) for v in fl]),
+            "gmat_append_hit_rows")
 
 
 def resolve_rows(kind, num_snp, snp_lst_0):
@@ -189,8 +201,7 @@ def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut,
         ends = np.searchsorted(hi, uniq, side="right")
         pos = np.searchsorted(uniq, rows)
         order = np.concatenate([np.arange(starts[k], ends[k]) for k in pos]) if rows.size else np.zeros(0, int)
-    with open(out_file, "a") as f:
-        f.write(format_rows([hi[order], hj[order], eff[order], chi[order], p[order]], 3))
+    append_rows(out_file, [hi[order], hj[order], eff[order], chi[order], p[order]], 3)
     return 0
 
 
@@ -242,8 +253,7 @@ def run_pairs(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_pair_file, m
                 raise ValueError("snp_pair is out of range!")
             eff, var, chi, p = plan.pairs(kind, chunk)
             keep = p < p_cut
-            with open(out_file, "a") as f:
-                f.write(format_rows([chunk[keep, 0], chunk[keep, 1], eff[keep], var[keep], chi[keep], p[keep]], 4))
+            append_rows(out_file, [chunk[keep, 0], chunk[keep, 1], eff[keep], var[keep], chi[keep], p[keep]], 4)
     finally:
         plan.close()
         plan.geno.close()

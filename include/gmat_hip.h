@@ -174,6 +174,10 @@ int gmat_eff_stats(double *out4);
 int gmat_write_grm_text(const char *path, const double *mat, int64_t n, int fmt, const char *ids_blob, int n_threads);
 /* CPython repr(float) of v (the value text of fmt 1/2); returns its length (cap >= 32). */
 int gmat_float_repr(double v, char *out, int cap);
+/* Append n scan result rows "i j v_0 .. v_{nf-1}\n" (1 <= nf <= 4 value columns f0..f3, CPython
+ * float repr) to the file at path: the reference's DataFrame.to_csv rows (remma_epiAA.py:84-86). */
+int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *i, const int64_t *j, int nf, const double *f0,
+                         const double *f1, const double *f2, const double *f3);
 
 /* ---- single-SNP tests (remma_add / remma_dom) ----
  * For every SNP j of the (imputed) panel: x_j = g_j - 2p_j (kind GMAT_GRM_ADD) or

@@ -89,3 +89,29 @@ def test_text_writers_match_numpy_and_pandas(tmp_path):
         e = str(tmp_path / ("e%d" % fmt))
         pd.DataFrame({"a": a, "b": b, "v": mat[ind]}).to_csv(e, sep=" ", index=False, header=False)
         assert open(p, "rb").read() == open(e, "rb").read()
+
+
+def test_hit_row_writer_matches_python_rows(tmp_path):
+    """gmat_append_hit_rows (the scans' result files, remma_epiAA.py:84-86 DataFrame.to_csv rows) is
+    byte-identical to the Python statement _scan.format_rows, for 3 and 4 value columns, appended
+    after existing content, and for zero rows."""
+    if not os.path.exists(LIB):
+        pytest.skip("libgmat_hip.so not built")
+    import numpy as np
+    from gmat_amd.remma._scan import append_rows, format_rows
+    rng = np.random.default_rng(7)
+    n = 3000
+    i = np.sort(rng.integers(0, 100000, n)).astype(np.int64)
+    j = rng.integers(0, 100000, n).astype(np.int64)
+    cols = [rng.standard_normal(n) * 10.0 ** rng.integers(-12, 12, n), rng.random(n) * 40.0,
+            rng.random(n) * 10.0 ** rng.integers(-20, -4, n), rng.random(n)]
+    cols[0][:6] = [0.0, -0.0, 1e-4, 1e-5, 1e16, 2.0]
+    for nf in (3, 4):
+        path = str(tmp_path / ("hits%d" % nf))
+        with open(path, "w") as f:
+            f.write("snp_0 snp_1 eff chi_val p_val\n")
+        append_rows(path, [i, j] + cols[:nf], nf)
+        append_rows(path, [i[:0], j[:0]] + [c[:0] for c in cols[:nf]], nf)
+        with open(path) as f:
+            got = f.read()
+        assert got == "snp_0 snp_1 eff chi_val p_val\n" + format_rows([i, j] + cols[:nf], nf)
