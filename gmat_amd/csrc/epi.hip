@@ -3037,12 +3037,12 @@ struct gmat_epi {
   } sb;
   // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
   struct ScanPins {
-    Pinned res, count, rows[2], flags[2], mxt[2], mxr[2], count1, c1, t2[2], r2[2], cnt[2], count2;
+    Pinned res, count, rows[3], flags[3], mxt[3], mxr[3], count1, c1, t2[3], r2[3], cnt[3], count2;
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
-  struct LrcBuffers {
-    DBuf drows[2], lmask[2], e13[2], pfc[2], slot_row[2], slot_j[2], cnt[2], soff[2], info[2];
+  struct LrcBuffers {  // three sets: the prefilters of launches L + 1 and L + 2 are queued while L screens
+    DBuf drows[3], lmask[3], e13[3], pfc[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3];
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
@@ -4339,7 +4339,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const int64_t nJ = cdiv(m, BJ), RL = ROWS_PER_LAUNCH;
   const int64_t max_slots = RL * cdiv(m, 32) + LC_SLOTS;
   auto &B = e->lrc;
-  for (int b = 0; b < 2; ++b) {
+  constexpr int NBUF = 3;  // buffer sets: launch L uses set L % 3
+  for (int b = 0; b < NBUF; ++b) {
     GMAT_TRY(B.drows[b].alloc(RL * 8));
     GMAT_TRY(B.lmask[b].alloc((size_t)RL * nJ * 4));
     GMAT_TRY(B.e13[b].alloc((size_t)E3_PF * 2 * RL * m * sizeof(int)));
@@ -4399,10 +4400,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       return GMAT_OK;
     }
   } evs;
-  hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], pf_beg[2], pf_end[2], ref_beg, ref_end;
+  hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
   double t_pf = 0, pf_ops = 0;
   std::vector<double> pf_ops_of(plan.size(), 0.0);
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < NBUF; ++b) {
     GMAT_TRY(evs.make(&pf_beg[b]));
     GMAT_TRY(evs.make(&pf_end[b]));
     GMAT_TRY(evs.make(&side_beg[b]));
@@ -4422,10 +4423,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   int64_t known_count = 0, inflight = 0;
   // the prefilter pass and the slot lists of launch li into buffer set b (stream S2)
   auto enqueue_side = [&](size_t li, int b) -> int {
-    const hipStream_t S2 = S2b[b];
+    const hipStream_t S2 = S2b[li & 1];
     const Launch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
-    GMAT_HIP(hipStreamWaitEvent(S2, scr_end[b], 0));  // buffer set b free (screen two launches back)
+    GMAT_HIP(hipStreamWaitEvent(S2, scr_end[b], 0));  // buffer set b free (screen three launches back)
     std::memcpy(e->pins.rows[b].p, ln.rows.data(), Rn * 8);
     GMAT_HIP(hipMemcpyAsync(B.drows[b].p, e->pins.rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
@@ -4608,11 +4609,15 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   lx.eps = e->lr_eps;
   lx.E = e->lr_E;
   int64_t prev_count = 0;  // candidates after the previous launch's screen (known once it completed)
-  if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0));
+  // two launches' prefilters queued ahead of the screen being launched (the prefilter streams never
+  // wait for a host round trip between launches)
+  // (same-box A/B: 28.0 ms per configs[2] step two launches ahead against 28.6 one ahead)
+  constexpr size_t ahead = 2;
+  for (size_t li = 0; li < std::min<size_t>(ahead, plan.size()); ++li) GMAT_TRY(enqueue_side(li, (int)li));
   for (size_t li = 0; li < plan.size(); ++li) {
-    const int b = (int)(li & 1);
+    const int b = (int)(li % NBUF);
     const Launch &ln = plan[li];
-    if (li + 1 < plan.size()) GMAT_TRY(enqueue_side(li + 1, b ^ 1));
+    if (li + ahead < plan.size()) GMAT_TRY(enqueue_side(li + ahead, (int)((li + ahead) % NBUF)));
     GMAT_HIP(hipEventSynchronize(side_end[b]));
     const int *info = e->pins.t2[b].as<int>();
     const int64_t slots = info[0], tiles = info[1];
@@ -4667,7 +4672,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     inflight = 32 * slots;
     // the previous launch's screen has completed (or is about to): pair-screen its candidates on S3
     if (li > 0) {
-      const int pb = b ^ 1;
+      const int pb = (int)((li - 1) % NBUF);
       GMAT_HIP(hipEventSynchronize(scr_end[pb]));
       float ms;
       GMAT_HIP(hipEventElapsedTime(&ms, scr_beg[pb], scr_end[pb]));
@@ -4684,7 +4689,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   }
   GMAT_HIP(hipStreamSynchronize(sm));
   if (!plan.empty()) {
-    const int lb = (int)((plan.size() - 1) & 1);
+    const int lb = (int)((plan.size() - 1) % NBUF);
     float ms;
     GMAT_HIP(hipEventElapsedTime(&ms, scr_beg[lb], scr_end[lb]));
     t_screen += ms * 1e-3;
