@@ -28,6 +28,7 @@ sys.path.insert(0, REPO)
 METRIC = "SNP-pairs tested/sec (whole node) + GRM GFLOP/s, mouse-sized cohort"
 INT8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA (2x the 2.5 PF dense bf16), MI355X_MICROARCH.md
 MX_PEAK_TFLOPS = 10000.0  # dense block-scaled fp6/fp4 MFMA (4x bf16 per clock), MI355X_MICROARCH.md
+LDS_DMA_PEAK_TBPS = 6.4  # chip-wide L2/MALL -> LDS rate of LDS-DMA with every CU streaming, MI355X_MICROARCH.md
 FP64_PEAK_TFLOPS = 78.6  # dense fp64 MFMA, MI355X_MICROARCH.md
 
 
@@ -645,6 +646,16 @@ def main():
                     "kernel": dom, "ops_note": kr["ops_note"], "avg_launch_ms": kr["avg_launch_ms"],
                     "issued_ops_per_launch": kr["ops_per_launch"], "kernels": kern_rec,
                     "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
+        if dom == "prefilter_pass_kernel":
+            # the prefilter's other roof: every tile streams 18 KB per 64-individual stage (+ 10 KB of
+            # test records) from L2 / MALL into LDS by LDS-DMA, and the chip moves ~6.4 TB/s of
+            # LDS-DMA with every CU streaming (MI355X_MICROARCH.md, ldsdma-fill)
+            n_pad_ = -(-n // 256) * 256  # the panel padding (geno.hip: round_up(n_id, 256))
+            tiles_per_launch = kr["ops_per_launch"] / (16.0 * n_pad_) / (64 * 256)
+            dma_bytes = tiles_per_launch * (n_pad_ / 64 * 18432 + 10240)
+            dma_tbps = dma_bytes / (kr["avg_launch_ms"] * 1e-3) / 1e12
+            roofline["lds_dma"] = {"bytes_per_launch": dma_bytes, "achieved_TBps": dma_tbps, "peak_TBps": LDS_DMA_PEAK_TBPS,
+                                   "frac": dma_tbps / LDS_DMA_PEAK_TBPS, "tiles_per_launch": tiles_per_launch}
     else:  # a level without per-kernel accounting (int8 / MX screens): the screen kernel's own stats
         avg_launch_s = screen_s / max(launches, 1)
         achieved = ops / max(launches, 1) / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
