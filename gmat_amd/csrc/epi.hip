@@ -1277,7 +1277,6 @@ struct LrArgs {
   const float *G, *H;      // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
   const double *recL, *recR;  // per-SNP test records (LR_REC doubles each, lr_rec_kernel)
   double lam, tau, eps, E;  // E = sum_r eta_r^2
-  unsigned long long *stamp;  // diagnostics (GMAT_LR_STAMPS): s_memrealtime stamps 0 .. 5 per tile entry
 };
 // Test records: left {alpha, csum, csq, sL3, sa, mono}, right {beta, csum, csq, sb, mono}, padded to
 // 64 bytes (four 16-byte DMA chunks)
@@ -1375,9 +1374,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
   };
   int e = next_entry((int)blockIdx.x);
   if (e < 0) return;
-  auto stamp = [&](int ent, int k) __attribute__((always_inline)) {
-    if (x.stamp && tid == 0) x.stamp[6 * ent + k] = __builtin_amdgcn_s_memrealtime();
-  };
+
   // Stage operands by LDS-DMA (global_load_lds_dwordx4: lane i's 16 bytes land at M0 + 16 i): the A
   // tile image (NA wave-instructions per image), the j-side S1 planes (waves 4..7: 16 columns x 4
   // chunks each, physical chunk p of column js holding logical chunk p ^ ((js >> 2) & 3): the 16
@@ -1550,7 +1547,6 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
     src_offsets(tl, J0t, J1t, oI, oJ);
     sO[0][tid] = w < 2 ? oI : oJ;
   }
-  stamp(e, 0);
   // Vector-memory bookkeeping (wave-uniform): `issued` counts this wave's DMAs; at the start of stage
   // g, mk[k] (k < LA - 1) is its value right after the loads of stage g + 1 + k (the stages in flight,
   // oldest first); the stage appends stage g + LA's mark, and waiting for stage g + 1 is
@@ -1598,7 +1594,6 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       sRo[par][lane] = (unsigned)((r >= 0 ? a.rows[r] : 0) * LR_REC + 2 * (lane & 3));
     }
     // (the tile's first stage was waited for by the previous stage or the prologue)
-    stamp(e, 1);
     double lowrank[PB] = {0.0, 0.0};
     for (int ch = 0; ch < nC; ++ch) {
       // one stage at tile position p: load the stage LA ahead (possibly of the next tile), the
@@ -1625,14 +1620,11 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
         ++g;
       };
       stage(0, true);
-      if (ch == 0) stamp(e, 2);
 #pragma unroll 1
       for (int cs2 = 1; cs2 < nS; ++cs2) stage(cs2, false);
-      stamp(e, 3);
       epilogue(lowrank);
       __syncthreads();  // every wave is past the epilogue's reads of sE before the next fetch
     }
-    stamp(e, 4);
     // lane half h tests slot PB w + h of column c (both halves hold the sums after the exchange)
     {
       const double tot = (h ? lowrank[1] : lowrank[0]) + __shfl_xor(h ? lowrank[0] : lowrank[1], 32);
@@ -1643,7 +1635,6 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
       const bool ok = i >= 0 && ri >= 0 && Jh >= 0 && j >= a.j_lo && j < a.m && !(a.tri && j <= i);
       lr_test(a, x, sT, PB * w + h, c, half, ok, i, j, tot);
     }
-    stamp(e, 5);
     if (en < 0) break;
     __syncthreads();  // every wave is past the test's reads of sT before the next tile's fetch
     e = en;
@@ -3037,7 +3028,7 @@ struct gmat_epi {
   } sb;
   // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
   struct ScanPins {
-    Pinned res, count, rows[3], flags[3], mxt[3], mxr[3], count1, c1, t2[3], r2[3], cnt[3], count2;
+    Pinned res, rows[3], flags[3], mxt[3], mxr[3], t2[3], cnt[3], count2;
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
@@ -4169,24 +4160,187 @@ extern "C" int gmat_epi_audit(gmat_epi *e, int kind, const int64_t *pairs, int64
 
 namespace {
 
+// ---- pieces shared by the three scan paths (scan_exhaustive, scan_lowrank, scan_blocks)
+
+// the codings of one scan kind: reference codes (refine) and screen codes of both sides
+struct ScanSide {
+  int lc = 0, rc = 0, tri = 1;
+  const Coding *L = nullptr, *R = nullptr;
+  const int8_t *lp = nullptr, *rp = nullptr;    // reference codes (refine)
+  const int8_t *slp = nullptr, *srp = nullptr;  // screen codes
+};
+
+// builds the codings `kind` needs and clears the previous scan's hits and counters
+int scan_begin(gmat_epi *e, int kind, ScanSide *c) {
+  kind_codings(kind, &c->lc, &c->rc);
+  GMAT_TRY(build_coding(e, c->lc));
+  GMAT_TRY(build_coding(e, c->rc));
+  c->L = &e->code[c->lc];
+  c->R = &e->code[c->rc];
+  c->lp = c->lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  c->rp = c->rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
+  c->slp = screen_panel(e, c->lc);
+  c->srp = screen_panel(e, c->rc);
+  c->tri = kind != GMAT_AD;
+  for (double &v : e->stats) v = 0.0;
+  for (double &v : e->kstats) v = 0.0;
+  for (auto *v : {&e->hit_i, &e->hit_j}) v->clear();
+  for (auto *v : {&e->hit_eff, &e->hit_var, &e->hit_chi, &e->hit_p}) v->clear();
+  return GMAT_OK;
+}
+
+// one launch of the screened scans: its first SNPs, the first column a pair of it can reach and
+// (block-granular int8 screen only) its (row offset, J) tile list, built when a level needs it
+struct ScanLaunch {
+  std::vector<int64_t> rows;
+  std::vector<int> tiles;
+  int64_t j_lo = 0;
+};
+
+// launches of ROWS_PER_LAUNCH rows: chunk k of half that size folded with chunk NC-1-k (equal work
+// per launch, as the triangle's rows shrink); launches without a pair are dropped.  *pairs = the
+// pairs the launches test.
+std::vector<ScanLaunch> fold_launches(const int64_t *rows, int64_t n_rows, int64_t m, int tri, double *pairs) {
+  std::vector<ScanLaunch> plan;
+  *pairs = 0;
+  const int64_t half = ROWS_PER_LAUNCH / 2, nc = cdiv(n_rows, half);
+  for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
+    ScanLaunch ln;
+    for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) ln.rows.push_back(rows[t]);
+    if (l != k)
+      for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) ln.rows.push_back(rows[t]);
+    if (ln.rows.empty()) continue;
+    ln.j_lo = tri ? ln.rows[0] + 1 : 0;
+    if (tri && ln.j_lo >= m) continue;
+    for (int64_t r : ln.rows) *pairs += tri ? (double)(m - 1 - r) : (double)m;
+    plan.push_back(std::move(ln));
+  }
+  return plan;
+}
+
+// candidate buffers of the screened scans (kept by the plan): `dflt` candidates unless a previous
+// scan left larger ones (GMAT_CAND_CAP: tests give a small buffer to exercise the overflow paths);
+// the pair screen's survivor buffers beside them
+int ensure_candidates(gmat_epi *e, int64_t dflt, bool use_ps) {
+  if (e->cand_cap == 0 || e->cand_i.bytes < (size_t)e->cand_cap * 8) {
+    const char *cenv = getenv("GMAT_CAND_CAP");
+    e->cand_cap = cenv ? std::max<int64_t>(1024, atoll(cenv)) : std::max<int64_t>(e->cand_cap, dflt);
+    for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp}) GMAT_TRY(d->alloc(e->cand_cap * 8));
+  }
+  if (!e->counter.p) GMAT_TRY(e->counter.alloc(8));
+  if (use_ps && e->cand2_i.bytes < (size_t)e->cand_cap * 8) {
+    GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
+    GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
+  }
+  if (use_ps && !e->counter2.p) GMAT_TRY(e->counter2.alloc(8));
+  return GMAT_OK;
+}
+
+// grows the (empty) candidate buffers to `cap`
+int grow_candidates(gmat_epi *e, int64_t cap, bool use_ps) {
+  for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp}) GMAT_TRY(d->alloc((size_t)cap * 8));
+  if (use_ps)
+    for (DBuf *d : {&e->cand2_i, &e->cand2_j}) GMAT_TRY(d->alloc((size_t)cap * 8));
+  e->cand_cap = cap;
+  if (getenv("GMAT_DEBUG")) fprintf(stderr, "candidate buffer grown to %lld\n", (long long)cap);
+  return GMAT_OK;
+}
+
+struct RefineTally {
+  double t_ref = 0, n_cand = 0, n_refined = 0;  // seconds on the refine stream, candidates, refined pairs
+};
+
+// The flush of a screened scan, on stream st: the pair screen (use_ps) of candidates [ps_done, count)
+// (those below ps_done were pair-screened beside the launches), the exact fp64 refine of the
+// survivors, and the hits p < p_cut appended to the plan's lists.  The candidate buffer is free
+// afterwards.
+int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, int64_t count, int64_t ps_done,
+                   double chi_cut, double p_cut, hipEvent_t beg, hipEvent_t end, RefineTally *tl) {
+  if (count <= 0) return GMAT_OK;
+  const int64_t *fi = e->cand_i.as<int64_t>(), *fj = e->cand_j.as<int64_t>();
+  int64_t nf = count;
+  GMAT_HIP(hipEventRecord(beg, st));
+  if (use_ps) {
+    GMAT_TRY(pair_screen(e, st, *c.L, *c.R, c.slp, c.srp, fi + ps_done, fj + ps_done, count - ps_done, chi_cut, &nf,
+                         ps_done == 0));
+    fi = e->cand2_i.as<int64_t>();
+    fj = e->cand2_j.as<int64_t>();
+  }
+  tl->n_cand += (double)count;
+  tl->n_refined += (double)nf;
+  Pinned &pin = e->pins.res;
+  if (nf > 0) {
+    GMAT_TRY(refine(e, st, *c.L, *c.R, c.lp, c.rp, fi, fj, nf, e->ceff.as<double>(), e->cvar.as<double>(),
+                    e->cchi.as<double>(), e->cp.as<double>()));
+    GMAT_TRY(pin.reserve((size_t)nf * 48));
+    int64_t *ci = pin.as<int64_t>(), *cj = ci + nf;
+    double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cq = cc + nf;
+    GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(cq, e->cp.p, nf * 8, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipEventRecord(end, st));
+    GMAT_HIP(hipStreamSynchronize(st));
+    for (int64_t k = 0; k < nf; ++k)
+      if (cq[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
+        e->hit_i.push_back(ci[k]);
+        e->hit_j.push_back(cj[k]);
+        e->hit_eff.push_back(ce[k]);
+        e->hit_var.push_back(cv[k]);
+        e->hit_chi.push_back(cc[k]);
+        e->hit_p.push_back(cq[k]);
+      }
+  } else {
+    GMAT_HIP(hipEventRecord(end, st));
+    GMAT_HIP(hipStreamSynchronize(st));
+  }
+  float ms;
+  GMAT_HIP(hipEventElapsedTime(&ms, beg, end));
+  tl->t_ref += ms * 1e-3;
+  return GMAT_OK;
+}
+
+// hits in (i, j) order, as the reference's row loop emits them
+int64_t sort_hits(gmat_epi *e) {
+  std::vector<int64_t> ord(e->hit_i.size());
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
+  });
+  auto apply = [&](auto &v) {
+    auto c2 = v;
+    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
+  };
+  apply(e->hit_i);
+  apply(e->hit_j);
+  apply(e->hit_eff);
+  apply(e->hit_var);
+  apply(e->hit_chi);
+  apply(e->hit_p);
+  return (int64_t)e->hit_i.size();
+}
+
+// owner of the events a scan creates
+struct ScanEvents {
+  std::vector<hipEvent_t> v;
+  ~ScanEvents() {
+    for (auto x : v) (void)hipEventDestroy(x);
+  }
+  int make(hipEvent_t *x) {
+    GMAT_HIP(hipEventCreate(x));
+    v.push_back(*x);
+    return GMAT_OK;
+  }
+};
+
 int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, int64_t *n_hits) {
   const double t_start = now();
   const int64_t m = e->m;
-  const int tri = kind != GMAT_AD;
-  int lc, rc;
-  kind_codings(kind, &lc, &rc);
-  GMAT_TRY(build_coding(e, lc));
-  GMAT_TRY(build_coding(e, rc));
-  const Coding &L = e->code[lc], &R = e->code[rc];
-  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
-  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
-  for (double &v : e->stats) v = 0.0;
-  e->hit_i.clear();
-  e->hit_j.clear();
-  e->hit_eff.clear();
-  e->hit_var.clear();
-  e->hit_chi.clear();
-  e->hit_p.clear();
+  ScanSide c;
+  GMAT_TRY(scan_begin(e, kind, &c));
+  const int tri = c.tri;
   // chunks of whole rows of at most `cap` pairs (one row holds at most m)
   const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : (1 << 24));
   if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
@@ -4197,16 +4351,10 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   GMAT_TRY(drows.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
   GMAT_TRY(doffs.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
   GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
+  ScanEvents evs;
   hipEvent_t ev0, ev1;
-  GMAT_HIP(hipEventCreate(&ev0));
-  GMAT_HIP(hipEventCreate(&ev1));
-  struct EvGuard {
-    hipEvent_t a, b;
-    ~EvGuard() {
-      (void)hipEventDestroy(a);
-      (void)hipEventDestroy(b);
-    }
-  } evg{ev0, ev1};
+  GMAT_TRY(evs.make(&ev0));
+  GMAT_TRY(evs.make(&ev1));
   double pairs = 0, t_ref = 0;
   std::vector<int64_t> offs;
   std::vector<int64_t> hbuf;
@@ -4233,8 +4381,8 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
                          dj.as<int64_t>());
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ev0, st));
-      GMAT_TRY(refine(e, st, L, R, lp, rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(), dv.as<double>(),
-                      dc.as<double>(), dp.as<double>()));
+      GMAT_TRY(refine(e, st, *c.L, *c.R, c.lp, c.rp, di.as<int64_t>(), dj.as<int64_t>(), np, de.as<double>(),
+                      dv.as<double>(), dc.as<double>(), dp.as<double>()));
       GMAT_HIP(hipEventRecord(ev1, st));
       GMAT_HIP(hipMemsetAsync(cnt.p, 0, 8, st));
       hipLaunchKernelGGL(hit_compact_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, di.as<int64_t>(),
@@ -4262,22 +4410,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
     }
     r0 = r1;
   }
-  std::vector<int64_t> ord(e->hit_i.size());
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
-  });
-  auto apply = [&](auto &v) {
-    auto c2 = v;
-    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
-  };
-  apply(e->hit_i);
-  apply(e->hit_j);
-  apply(e->hit_eff);
-  apply(e->hit_var);
-  apply(e->hit_chi);
-  apply(e->hit_p);
-  *n_hits = (int64_t)e->hit_i.size();
+  *n_hits = sort_hits(e);
   e->stats[0] = pairs;
   e->stats[1] = pairs;  // every pair is refined
   e->stats[4] = t_ref;
@@ -4298,44 +4431,13 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
                  int64_t *n_hits) {
   const double t_start = now();
   const int64_t m = e->m, n_pad = e->n_pad;
-  int lc, rc;
-  kind_codings(kind, &lc, &rc);
-  GMAT_TRY(build_coding(e, lc));
-  GMAT_TRY(build_coding(e, rc));
-  const Coding &L = e->code[lc], &R = e->code[rc];
-  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();  // reference codes (refine)
-  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
-  const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc);
-  const int tri = kind != GMAT_AD;
-  for (double &v : e->stats) v = 0.0;
-  for (double &v : e->kstats) v = 0.0;
-  e->hit_i.clear();
-  e->hit_j.clear();
-  e->hit_eff.clear();
-  e->hit_var.clear();
-  e->hit_chi.clear();
-  e->hit_p.clear();
-  // launches: chunks of 256 rows, folded (chunk k with chunk NC-1-k) for equal work per launch
-  struct Launch {
-    std::vector<int64_t> rows;
-    int64_t j_lo = 0;
-  };
-  std::vector<Launch> plan;
+  ScanSide c;
+  GMAT_TRY(scan_begin(e, kind, &c));
+  const Coding &L = *c.L, &R = *c.R;
+  const int8_t *slp = c.slp, *srp = c.srp;
+  const int tri = c.tri;
   double pairs_tested = 0;
-  {
-    const int64_t half = ROWS_PER_LAUNCH / 2, nc = cdiv(n_rows, half);
-    for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
-      Launch ln;
-      for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) ln.rows.push_back(rows[t]);
-      if (l != k)
-        for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) ln.rows.push_back(rows[t]);
-      if (ln.rows.empty()) continue;
-      ln.j_lo = tri ? ln.rows[0] + 1 : 0;
-      if (tri && ln.j_lo >= m) continue;
-      for (int64_t r : ln.rows) pairs_tested += tri ? (double)(m - 1 - r) : (double)m;
-      plan.push_back(std::move(ln));
-    }
-  }
+  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested);
   const int64_t nJ = cdiv(m, BJ), RL = ROWS_PER_LAUNCH;
   const int64_t max_slots = RL * cdiv(m, 32) + LC_SLOTS;
   auto &B = e->lrc;
@@ -4354,19 +4456,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_TRY(e->pins.cnt[b].reserve(8));
     GMAT_TRY(e->pins.t2[b].reserve(16));
   }
-  if (e->cand_cap == 0 || e->cand_i.bytes < (size_t)e->cand_cap * 8) {
-    const char *cenv = getenv("GMAT_CAND_CAP");
-    e->cand_cap = cenv ? std::max<int64_t>(1024, atoll(cenv)) : std::max<int64_t>(e->cand_cap, 1 << 24);
-    for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp})
-      GMAT_TRY(d->alloc(e->cand_cap * 8));
-  }
-  if (!e->counter.p) GMAT_TRY(e->counter.alloc(8));
   const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
-  if (use_ps && e->cand2_i.bytes < (size_t)e->cand_cap * 8) {
-    GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->counter2.alloc(8));
-  }
+  GMAT_TRY(ensure_candidates(e, 1 << 24, use_ps));
   DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
   if (getenv("GMAT_LIVE_COUNT")) {
     GMAT_TRY(live_cnt.alloc(8));
@@ -4389,17 +4480,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, getenv("GMAT_PF_ONE_STREAM") ? e->s2 : e->s4};
   GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
-  struct Events {
-    std::vector<hipEvent_t> v;
-    ~Events() {
-      for (auto x : v) (void)hipEventDestroy(x);
-    }
-    int make(hipEvent_t *x) {
-      GMAT_HIP(hipEventCreate(x));
-      v.push_back(*x);
-      return GMAT_OK;
-    }
-  } evs;
+  ScanEvents evs;
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
   double t_pf = 0, pf_ops = 0;
   std::vector<double> pf_ops_of(plan.size(), 0.0);
@@ -4415,7 +4496,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   GMAT_TRY(evs.make(&ref_beg));
   GMAT_TRY(evs.make(&ref_end));
   GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
-  double t_screen = 0, t_side = 0, t_ref = 0, ncand_total = 0, n_refined = 0, ops = 0;
+  double t_screen = 0, t_side = 0, ops = 0;
+  RefineTally tally;
   const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 65536;
   int64_t ps_done = 0;  // candidates [0, ps_done) already pair-screened (queued on S3)
   // candidate room: known_count (exact, after the last screen whose count was read) + inflight (32 per
@@ -4424,7 +4506,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // the prefilter pass and the slot lists of launch li into buffer set b (stream S2)
   auto enqueue_side = [&](size_t li, int b) -> int {
     const hipStream_t S2 = S2b[li & 1];
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, scr_end[b], 0));  // buffer set b free (screen three launches back)
     std::memcpy(e->pins.rows[b].p, ln.rows.data(), Rn * 8);
@@ -4533,53 +4615,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // (Refining each pair-screen chunk's survivors beside the later launches instead of all of them at
   // flush time was measured slower: 32.7 vs 28.4 ms per configs[2] step -- refine workgroups hold
   // CUs that the whole-CU prefilter workgroups then wait for.)
-  // refine (after the pair screen of what is left) of candidates [0, count), hits collected
-  Pinned &pin_res = e->pins.res;
+  // pair screen of what is left, refine of candidates [0, count), hits collected
   auto flush = [&](int64_t count) -> int {
-    if (count <= 0) return GMAT_OK;
-    const int64_t *fi = e->cand_i.as<int64_t>(), *fj = e->cand_j.as<int64_t>();
-    int64_t nf = count;
-    GMAT_HIP(hipEventRecord(ref_beg, S3));
-    if (use_ps) {
-      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, fi + ps_done, fj + ps_done, count - ps_done, chi_cut, &nf,
-                           ps_done == 0));
-      fi = e->cand2_i.as<int64_t>();
-      fj = e->cand2_j.as<int64_t>();
-    }
+    const int64_t done = ps_done;
     ps_done = 0;
-    ncand_total += (double)count;
-    n_refined += (double)nf;
-    if (nf > 0) {
-      GMAT_TRY(refine(e, S3, L, R, lp, rp, fi, fj, nf, e->ceff.as<double>(), e->cvar.as<double>(),
-                      e->cchi.as<double>(), e->cp.as<double>()));
-      GMAT_TRY(pin_res.reserve((size_t)nf * 48));
-      int64_t *ci = pin_res.as<int64_t>(), *cj = ci + nf;
-      double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cq = cc + nf;
-      GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipMemcpyAsync(cq, e->cp.p, nf * 8, hipMemcpyDeviceToHost, S3));
-      GMAT_HIP(hipEventRecord(ref_end, S3));
-      GMAT_HIP(hipStreamSynchronize(S3));
-      for (int64_t k = 0; k < nf; ++k)
-        if (cq[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
-          e->hit_i.push_back(ci[k]);
-          e->hit_j.push_back(cj[k]);
-          e->hit_eff.push_back(ce[k]);
-          e->hit_var.push_back(cv[k]);
-          e->hit_chi.push_back(cc[k]);
-          e->hit_p.push_back(cq[k]);
-        }
-    } else {
-      GMAT_HIP(hipEventRecord(ref_end, S3));
-      GMAT_HIP(hipStreamSynchronize(S3));
-    }
-    float ms;
-    GMAT_HIP(hipEventElapsedTime(&ms, ref_beg, ref_end));
-    t_ref += ms * 1e-3;
-    return GMAT_OK;
+    return refine_collect(e, c, S3, use_ps, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
   };
   auto read_count = [&](int b) -> int64_t { return (int64_t)*e->pins.cnt[b].as<unsigned long long>(); };
   ScreenArgs sa;
@@ -4616,7 +4656,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   for (size_t li = 0; li < std::min<size_t>(ahead, plan.size()); ++li) GMAT_TRY(enqueue_side(li, (int)li));
   for (size_t li = 0; li < plan.size(); ++li) {
     const int b = (int)(li % NBUF);
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     if (li + ahead < plan.size()) GMAT_TRY(enqueue_side(li + ahead, (int)((li + ahead) % NBUF)));
     GMAT_HIP(hipEventSynchronize(side_end[b]));
     const int *info = e->pins.t2[b].as<int>();
@@ -4640,15 +4680,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
       known_count = inflight = 0;
       prev_count = 0;
-      if (32 * slots > e->cand_cap) {  // grow the candidate buffers (nothing pending)
-        e->cand_cap = 2 * 32 * slots;
-        for (DBuf *d : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp}) GMAT_TRY(d->alloc(e->cand_cap * 8));
-        if (use_ps) {
-          GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
-          GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
-        }
-        if (getenv("GMAT_DEBUG")) fprintf(stderr, "candidate buffer grown to %lld\n", (long long)e->cand_cap);
-      }
+      if (32 * slots > e->cand_cap) GMAT_TRY(grow_candidates(e, 2 * 32 * slots, use_ps));  // nothing pending
     }
     sa.rows = B.drows[b].as<int64_t>();
     sa.n_rows = (int)ln.rows.size();
@@ -4695,27 +4727,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     t_screen += ms * 1e-3;
     GMAT_TRY(flush(read_count(lb)));
   }
-  std::vector<int64_t> ord(e->hit_i.size());
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
-  });
-  auto apply = [&](auto &v) {
-    auto c2 = v;
-    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
-  };
-  apply(e->hit_i);
-  apply(e->hit_j);
-  apply(e->hit_eff);
-  apply(e->hit_var);
-  apply(e->hit_chi);
-  apply(e->hit_p);
-  *n_hits = (int64_t)e->hit_i.size();
+  *n_hits = sort_hits(e);
   e->stats[0] = pairs_tested;
-  e->stats[1] = ncand_total;
+  e->stats[1] = tally.n_cand;
   e->stats[2] = ops;
   e->stats[3] = t_screen;
-  e->stats[4] = t_ref;
+  e->stats[4] = tally.t_ref;
   e->stats[5] = t_side;
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)plan.size();
@@ -4727,7 +4744,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   e->kstats[3] = t_screen;
   e->kstats[4] = (double)plan.size();
   e->kstats[5] = ops;
-  e->kstats[6] = t_ref;
+  e->kstats[6] = tally.t_ref;
   e->kstats[7] = -1;
   if (pf_st.p && stamp_grid > 0 && stamp_grid <= (1 << 20)) {  // phase times of the stamped launch
     std::vector<unsigned long long> hs((size_t)PF_NSTAMP * stamp_grid);
@@ -4754,43 +4771,32 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_HIP(hipMemcpy(&lcnt, live_cnt.p, 8, hipMemcpyDeviceToHost));
     e->kstats[7] = (double)lcnt;
     fprintf(stderr, "gmat_epi_scan (compacted): %.0f pairs, prefilter keeps %llu pairs (%.4f%%), %.0f low-rank candidates, "
-            "%.0f refined\n", pairs_tested, lcnt, 100.0 * (double)lcnt / std::max(pairs_tested, 1.0), ncand_total,
-            n_refined);
+            "%.0f refined\n", pairs_tested, lcnt, 100.0 * (double)lcnt / std::max(pairs_tested, 1.0), tally.n_cand,
+            tally.n_refined);
   }
   if (getenv("GMAT_DEBUG"))
     fprintf(stderr, "gmat_epi_scan (compacted): %zu launches, %.0f candidates, %.0f refined, screen %.3f s, side %.3f s\n",
-            plan.size(), ncand_total, n_refined, t_screen, t_side);
+            plan.size(), tally.n_cand, tally.n_refined, t_screen, t_side);
   return GMAT_OK;
 }
 
-}  // namespace
 
-extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
-                             int n_slice, int64_t *n_hits) {
-  GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
-  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
-  const int64_t m = e->m, n_pad = e->n_pad;
-  for (int64_t t = 0; t < n_rows; ++t) {
-    GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
-    GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
-  }
-  if (n_slice == GMAT_SCREEN_NONE) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
-  // the compacted low-rank scan serves the low-rank level (automatic at p_cut <= 1e-4, or forced by
-  // n_slice -2); GMAT_LR_BLOCKS=1 keeps the block-granular path below (A/B runs)
-  const bool lr_level = e->lr_R > 0 && e->pf_mu > 0.0 && (n_slice == -2 || (n_slice == 0 && p_cut <= 1e-4));
-  if (lr_level && pair_screen_fits(e) && !getenv("GMAT_LR_BLOCKS") && !getenv("GMAT_NO_PREFILTER"))
-    return scan_lowrank(e, kind, rows, n_rows, p_cut, chi_cut, n_hits);
+// ---- the block-granular scan: the int8 slice screens (p_cut > 1e-4), the MX quadratic form
+// (n_slice -1) and the low-rank screen when the compacted scan cannot serve it (n_pad > 8064: the pair
+// screen does not fit in LDS; GMAT_LR_BLOCKS=1 for A/B runs).  Per launch of 512 first SNPs:
+//   S2: side terms (prefilter flags + E3, or the int8 side GEMMs E1 / Ed / E2) into buffer set L % 2
+//   sm: the screen over the launch's tile list (candidates appended to cand)
+//   S3: pair screen + exact refine when the candidate buffer is flushed
+int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut, int n_slice,
+                int64_t *n_hits) {
   const double t_start = now();
-  int lc, rc;
-  kind_codings(kind, &lc, &rc);
-  GMAT_TRY(build_coding(e, lc));
-  GMAT_TRY(build_coding(e, rc));
-  const Coding &L = e->code[lc], &R = e->code[rc];
-  const int8_t *lp = lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();  // reference codes (refine)
-  const int8_t *rp = rc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
-  const int8_t *slp = screen_panel(e, lc), *srp = screen_panel(e, rc), *srq = screen_sq(e, rc);  // screen codes
-  const int8_t *slq = screen_sq(e, lc);
-  const int tri = (kind != GMAT_AD);
+  const int64_t m = e->m, n_pad = e->n_pad;
+  ScanSide c;
+  GMAT_TRY(scan_begin(e, kind, &c));
+  const int lc = c.lc, rc = c.rc;
+  const Coding &L = *c.L, &R = *c.R;
+  const int8_t *slp = c.slp, *srp = c.srp, *srq = screen_sq(e, rc), *slq = screen_sq(e, lc);  // screen codes
+  const int tri = c.tri;
   // tile shape of the int8 screen: Shape<SCREEN_SHAPE>
   // screen level S: 0 = MX (fp6 x fp4, one pass, tighter than one int8 slice), 1..n_slice = int8
   // slices.  Automatic: MX when the candidate band stays thin (p_cut <= 1e-4), 2 slices up to
@@ -4806,25 +4812,8 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   int S_max_used = S;
   constexpr int BI = Shape<SCREEN_SHAPE>::BI, MT = Shape<SCREEN_SHAPE>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
-  for (double &v : e->stats) v = 0.0;
-  e->hit_i.clear();
-  e->hit_j.clear();
-  e->hit_eff.clear();
-  e->hit_var.clear();
-  e->hit_chi.clear();
-  e->hit_p.clear();
-
-  // launches: chunks of 64 rows, folded (chunk k with chunk NC-1-k) for equal work per launch
-  const int64_t half = ROWS_PER_LAUNCH / 2;
-  const int64_t nc = cdiv(n_rows, half);
-  std::vector<std::vector<int64_t>> launches;
-  for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
-    std::vector<int64_t> rws;
-    for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) rws.push_back(rows[t]);
-    if (l != k)
-      for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) rws.push_back(rows[t]);
-    launches.push_back(rws);
-  }
+  double pairs_tested = 0;
+  std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested);
 
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
@@ -4839,14 +4828,13 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   const bool use_lr = use_pf && e->lr_R > 0 && n_slice != -1;  // level 0 = low-rank screen
   // low-rank screen tile lists built on the device right behind the prefilter (tl_*_kernel): the
   // host waits only for the tile count, not for the flags and a host-side build
-  const bool dev_tiles = use_lr && !getenv("GMAT_LR_STAMPS") && !getenv("GMAT_HOST_TILES");
   DBuf tl_cnt, tl_h, tl_info;
   DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
   if (getenv("GMAT_LIVE_COUNT")) {
     GMAT_TRY(live_cnt.alloc(8));
     GMAT_HIP(hipMemset(live_cnt.p, 0, 8));
   }
-  if (dev_tiles) {
+  if (use_lr) {
     GMAT_TRY(tl_cnt.alloc((size_t)TL_G * nJ * sizeof(int)));
     GMAT_TRY(tl_h.alloc((size_t)nJ * sizeof(int)));
     GMAT_TRY(tl_info.alloc(2 * 4 * sizeof(int)));
@@ -4865,145 +4853,43 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     GMAT_TRY(e13[b].alloc((size_t)SIDE_T * SIDE_P * ROWS_PER_LAUNCH * m * sizeof(int)));
     GMAT_TRY(e2[b].alloc((size_t)SIDE_T * ROWS_PER_LAUNCH * m * sizeof(int)));
   }
-  if (e->cand_cap == 0) {
-    const char *cenv = getenv("GMAT_CAND_CAP");  // tests: a small buffer exercises the overflow paths
-    e->cand_cap = cenv ? std::max<int64_t>(1024, atoll(cenv)) : (1 << 22);
-    GMAT_TRY(e->cand_i.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cand_j.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->ceff.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cvar.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cchi.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cp.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->counter.alloc(8));
-  }
   // pair screen between the screens and the refine (GMAT_NO_PAIR_SCREEN: off, for A/B runs)
   const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
-  if (use_ps && e->cand2_i.bytes < (size_t)e->cand_cap * 8) {
-    GMAT_TRY(e->cand2_i.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->cand2_j.alloc(e->cand_cap * 8));
-    GMAT_TRY(e->counter2.alloc(8));
-  }
-  // scan-private streams (the null stream would serialise them): screen + refine on sm,
-  // side terms on S2; ordered after the coding setup by a device synchronisation
+  GMAT_TRY(ensure_candidates(e, 1 << 22, use_ps));
+  // scan-private streams (the null stream would serialise them): screen on sm, side terms on S2,
+  // pair screen + refine on S3; ordered after the coding setup by a device synchronisation
+  // (Refining launch by launch beside the screens was measured 2.7x slower overall: refine waves
+  // occupy CUs that a screen workgroup, which needs a whole CU, then waits for.)
   if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
   if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
-  const hipStream_t sm = e->s1, S2 = e->s2;
+  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
   GMAT_HIP(hipDeviceSynchronize());
-  struct Ev {
-    hipEvent_t e[8];
-    Ev() {
-      for (auto &x : e) x = nullptr;
-    }
-    ~Ev() {
-      for (auto &x : e)
-        if (x) (void)hipEventDestroy(x);
-    }
-  } evs;
-  for (auto &x : evs.e) GMAT_HIP(hipEventCreate(&x));
-  hipEvent_t *ev = evs.e;  // 0/1 side start/done (per buffer: 0,1 = buf 0; 5,6 = buf 1), 2 screen done,
-                           // 3/4 refine, 7 screen start
-  hipEvent_t side_beg[2] = {ev[0], ev[5]}, side_end[2] = {ev[1], ev[6]};
-  hipEvent_t screen_end[2];
-  GMAT_HIP(hipEventCreate(&screen_end[0]));
-  GMAT_HIP(hipEventCreate(&screen_end[1]));
-  struct EvPair {
-    hipEvent_t *p;
-    ~EvPair() {
-      (void)hipEventDestroy(p[0]);
-      (void)hipEventDestroy(p[1]);
-    }
-  } screen_end_guard{screen_end};
-  double t_screen = 0, t_side = 0, t_ref = 0, pairs_tested = 0, ncand_total = 0, ops = 0;
+  ScanEvents evs;
+  // per buffer set: side pass begin / end, screen begin / end (+ its count copy); refine begin / end
+  hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], screen_end[2], ref_beg, ref_end;
+  for (int b = 0; b < 2; ++b)
+    for (hipEvent_t *x : {&side_beg[b], &side_end[b], &scr_beg[b], &scr_end[b], &screen_end[b]}) GMAT_TRY(evs.make(x));
+  GMAT_TRY(evs.make(&ref_beg));
+  GMAT_TRY(evs.make(&ref_end));
+  double t_screen = 0, t_side = 0, ops = 0;
+  RefineTally tally;
   int64_t launches_done = 0;
   int64_t pending = 0;  // candidates waiting in the device buffer
   GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
-  // exact refine of candidates [0, count) and collection of the hits
-  // The exact refine runs on its own stream (s3) when the candidate buffer is flushed.  (Refining
-  // launch by launch beside the screens was measured 2.7x slower overall: refine waves occupy
-  // CUs that a screen workgroup, which needs a whole CU, then waits for.)
-  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
-  const hipStream_t S3 = e->s3;
-  double n_refined = 0;
-  // pair screen (use_ps) and exact refine of candidates [0, count) on S3
-  // pair screen of the candidates [ps_done, ...) already queued on S3 beside the screens (chunks of
-  // GMAT_PS_CHUNK, default 65,536 candidates); the flush screens the rest and reads the survivors
+  // pair screen of the candidates [0, ps_done) already queued on S3 beside the screens (chunks of
+  // GMAT_PS_CHUNK, default 65,536 candidates); the flush screens the rest and refines the survivors
   int64_t ps_done = 0;
   const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 65536;
-  auto enqueue_refine = [&](int64_t count, const int64_t **fi, const int64_t **fj, int64_t *nf) -> int {
-    *fi = e->cand_i.as<int64_t>();
-    *fj = e->cand_j.as<int64_t>();
-    *nf = count;
-    GMAT_HIP(hipEventRecord(ev[3], S3));
-    if (use_ps) {
-      GMAT_TRY(pair_screen(e, S3, L, R, slp, srp, *fi + ps_done, *fj + ps_done, count - ps_done, chi_cut, nf,
-                           ps_done == 0));
-      ps_done = 0;
-      *fi = e->cand2_i.as<int64_t>();
-      *fj = e->cand2_j.as<int64_t>();
-    }
-    GMAT_TRY(refine(e, S3, L, R, lp, rp, *fi, *fj, *nf, e->ceff.as<double>(), e->cvar.as<double>(),
-                    e->cchi.as<double>(), e->cp.as<double>()));
-    GMAT_HIP(hipEventRecord(ev[4], S3));
-    return GMAT_OK;
-  };
-  Pinned &pin_res = e->pins.res;
-  // refine what is left of [0, count), collect the hits; the buffer is free afterwards
   auto flush = [&](int64_t count) -> int {
-    if (count <= 0) return GMAT_OK;
-    const int64_t *fi, *fj;
-    int64_t nf;
-    GMAT_TRY(enqueue_refine(count, &fi, &fj, &nf));
-    ncand_total += (double)count;
-    n_refined += (double)nf;
-    if (nf <= 0) return GMAT_OK;
-    GMAT_TRY(pin_res.reserve((size_t)nf * 48));
-    int64_t *ci = pin_res.as<int64_t>(), *cj = ci + nf;
-    double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cp = cc + nf;
-    GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipMemcpyAsync(cp, e->cp.p, nf * 8, hipMemcpyDeviceToHost, S3));
-    GMAT_HIP(hipStreamSynchronize(S3));
-    float ms34;
-    GMAT_HIP(hipEventElapsedTime(&ms34, ev[3], ev[4]));
-    t_ref += ms34 * 1e-3;  // span of the refine stream's work (it shares the GPU with the screens)
-    for (int64_t k = 0; k < nf; ++k) {
-      if (cp[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
-        e->hit_i.push_back(ci[k]);
-        e->hit_j.push_back(cj[k]);
-        e->hit_eff.push_back(ce[k]);
-        e->hit_var.push_back(cv[k]);
-        e->hit_chi.push_back(cc[k]);
-        e->hit_p.push_back(cp[k]);
-      }
-    }
-    return GMAT_OK;
+    const int64_t done = ps_done;
+    ps_done = 0;
+    return refine_collect(e, c, S3, use_ps, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
   };
-
-  // per-launch host plan (rows, tile list); empty launches dropped
-  struct Launch {
-    std::vector<int64_t> rows;
-    std::vector<int> tiles;  // (row offset, J) per workgroup of the int8 screen
-    int64_t j_lo = 0;
-  };
-  std::vector<Launch> plan;
-  for (auto &rws : launches) {
-    const int Rn = (int)rws.size();
-    if (Rn == 0) continue;
-    const int64_t j_lo = tri ? rws[0] + 1 : 0;
-    if (tri && j_lo >= m) continue;
-    Launch ln;
-    ln.rows = rws;
-    ln.j_lo = j_lo;
-    for (int t = 0; t < Rn; ++t) pairs_tested += tri ? (double)(m - 1 - rws[t]) : (double)m;
-    plan.push_back(std::move(ln));
-  }
 
   // the int8 screen's (row offset, J) tile list of a launch, built when a level >= 1 needs it
   auto ensure_tiles = [&](size_t li) {
-    Launch &ln = plan[li];
+    ScanLaunch &ln = plan[li];
     if (!ln.tiles.empty()) return;
     const int Rn = (int)ln.rows.size();
     for (int r0 = 0; r0 < Rn; r0 += BI) {
@@ -5017,7 +4903,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // kernel arguments of launch li on buffer set b
   auto make_args = [&](size_t li, int b) -> ScreenArgs {
     ScreenArgs sa;
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     sa.slices = e->slices.as<int8_t>();
     sa.slices_bytes = (int64_t)e->n_slice * n_pad * n_pad;
@@ -5096,23 +4982,19 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   // side terms of launch `li` into buffer set b (stream s2)
   // pinned host staging: asynchronous copies from / to pageable memory block the host until the
   // stream drains, which would serialise the side passes of launch li+1 behind screen li
-  Pinned &pin_count = e->pins.count;
   auto &pin_rows = e->pins.rows, &pin_flags = e->pins.flags, &pin_mxt = e->pins.mxt, &pin_mxr = e->pins.mxr;
-  GMAT_TRY(pin_count.reserve(8));
-  auto stage_rows = [&](const Launch &ln, int b) -> int {
+  auto stage_rows = [&](const ScanLaunch &ln, int b) -> int {
     GMAT_TRY(pin_rows[b].reserve(ln.rows.size() * 8));
     std::memcpy(pin_rows[b].p, ln.rows.data(), ln.rows.size() * 8);
     return GMAT_OK;
   };
-  const bool side_serial = getenv("GMAT_SIDE_SERIAL") != nullptr;
   auto enqueue_side = [&](size_t li, int b, bool full) -> int {
     side_full[b] = full;
     e3_slices[b] = (!full && use_pf) ? E3_PF : SIDE_T;
     if (!full && use_pf) {  // fused passes: prefilter flags + E3, then E1 / Ed / E2 for flagged blocks
-      const Launch &ln = plan[li];
+      const ScanLaunch &ln = plan[li];
       const int Rn = (int)ln.rows.size();
       GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
-      if (side_serial) GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b ^ 1], 0));  // A/B: no overlap with the screen
       GMAT_TRY(stage_rows(ln, b));
       GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
       GMAT_HIP(hipEventRecord(side_beg[b], S2));
@@ -5154,22 +5036,17 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       }
       GMAT_HIP(hipGetLastError());
       if (x.a.pf_store) {  // the low-rank screen needs nothing else
-        if (dev_tiles) {
-          const unsigned gj = (unsigned)cdiv(nJ, 64);
-          int *info = tl_info.as<int>() + 4 * b;
-          hipLaunchKernelGGL(tl_count_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
-                             tl_cnt.as<int>());
-          hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, S2, tl_cnt.as<int>(), (int)nJ, tl_h.as<int>(), info,
-                             mxt[b].as<int>(), mxr[b].as<int>());
-          hipLaunchKernelGGL(tl_fill_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
-                             tl_cnt.as<int>(), tl_h.as<int>(), info, mxt[b].as<int>(), mxr[b].as<int>());
-          GMAT_HIP(hipGetLastError());
-          GMAT_TRY(pin_flags[b].reserve(16));
-          GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, info, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
-        } else {
-          GMAT_TRY(pin_flags[b].reserve((size_t)Rn * nJ));
-          GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, flags[b].p, (size_t)Rn * nJ, hipMemcpyDeviceToHost, S2));
-        }
+        const unsigned gj = (unsigned)cdiv(nJ, 64);
+        int *info = tl_info.as<int>() + 4 * b;
+        hipLaunchKernelGGL(tl_count_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+                           tl_cnt.as<int>());
+        hipLaunchKernelGGL(tl_scan_kernel, dim3(1), dim3(1024), 0, S2, tl_cnt.as<int>(), (int)nJ, tl_h.as<int>(), info,
+                           mxt[b].as<int>(), mxr[b].as<int>());
+        hipLaunchKernelGGL(tl_fill_kernel, dim3(gj), dim3(1024), 0, S2, flags[b].as<uint8_t>(), Rn, (int)nJ,
+                           tl_cnt.as<int>(), tl_h.as<int>(), info, mxt[b].as<int>(), mxr[b].as<int>());
+        GMAT_HIP(hipGetLastError());
+        GMAT_TRY(pin_flags[b].reserve(16));
+        GMAT_HIP(hipMemcpyAsync(pin_flags[b].p, info, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
         GMAT_HIP(hipEventRecord(side_end[b], S2));
         return GMAT_OK;
       }
@@ -5189,7 +5066,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       return GMAT_OK;
     }
     ensure_tiles(li);
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     GMAT_HIP(hipStreamWaitEvent(S2, screen_end[b], 0));  // buffer b free (screen two launches back)
     GMAT_TRY(stage_rows(ln, b));
@@ -5238,12 +5115,12 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       double t0;
       ~Acc() { t += now() - t0; }
     } acc_guard{t_build, tb0};
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     std::vector<int> &mx_tiles = mxT[b], &mx_rows = mxR[b];
     int64_t &n_mx = nMX[b];
     built_for[b] = li;
-    if (dev_tiles) {  // the lists are on the device already: the tile count is all the host needs
+    if (use_lr) {  // the lists are on the device already: the tile count is all the host needs
       GMAT_HIP(hipEventSynchronize(side_end[b]));
       const int *info = pin_flags[b].as<int>();
       n_mx = info[1];
@@ -5344,20 +5221,11 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   GMAT_HIP(hipEventRecord(screen_end[0], sm));
   GMAT_HIP(hipEventRecord(screen_end[1], sm));
   if (!plan.empty()) GMAT_TRY(enqueue_side(0, 0, S != 0));
-  const bool stamps_on = getenv("GMAT_LR_STAMPS") != nullptr;
-  DBuf dstamp;
-  if (stamps_on) GMAT_TRY(dstamp.alloc((size_t)max_mx * 8 * 6 * 8));
   // The next launch's low-rank screen is queued on sm right behind the current one (its side
   // pass and tile list are ready by then), so the host's per-launch bookkeeping no longer leaves
   // the GPU idle; a launch that overflows the candidate buffer discards the queued one.
-  const bool pipe_next = use_lr && !stamps_on;
+  const bool pipe_next = use_lr;
   std::vector<char> queued(plan.size(), 0);
-  hipEvent_t evs7[2], evs2[2];
-  for (int q = 0; q < 2; ++q) {
-    GMAT_HIP(hipEventCreate(&evs7[q]));
-    GMAT_HIP(hipEventCreate(&evs2[q]));
-  }
-  EvPair evs7_guard{evs7}, evs2_guard{evs2};
   auto &pin_cnt = e->pins.cnt;
   GMAT_TRY(pin_cnt[0].reserve(8));
   GMAT_TRY(pin_cnt[1].reserve(8));
@@ -5387,7 +5255,6 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     lx.lam = e->lr_lam;
     lx.tau = e->lr_tau;
     lx.eps = e->lr_eps;
-    lx.stamp = (stamps_on && li == 5) ? dstamp.as<unsigned long long>() : nullptr;
     lx.recL = L.lrRecL.as<double>();
     lx.recR = R.lrRecR.as<double>();
     lx.n_tiles = 0;
@@ -5401,16 +5268,16 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
     sa.tiles = mxt[b].as<int>();
     const LrArgs lx = lr_args(li);
     GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
-    GMAT_HIP(hipEventRecord(evs7[b], sm));
+    GMAT_HIP(hipEventRecord(scr_beg[b], sm));
     if (gT[b] > 0) launch_lr_kernel((unsigned)gT[b], sa, lx);
     GMAT_HIP(hipGetLastError());
-    GMAT_HIP(hipEventRecord(evs2[b], sm));
+    GMAT_HIP(hipEventRecord(scr_end[b], sm));
     GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
     GMAT_HIP(hipEventRecord(screen_end[b], sm));
     return GMAT_OK;
   };
   for (size_t li = 0; li < plan.size(); ++li) {
-    const Launch &ln = plan[li];
+    const ScanLaunch &ln = plan[li];
     const int b = (int)(li & 1);
     const int Rn = (int)ln.rows.size();
     int64_t ntiles = 0;  // int8 screen workgroups (tile lists are built lazily)
@@ -5437,7 +5304,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       } else {
       queued[li] = 0;
       GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
-      GMAT_HIP(hipEventRecord(evs7[b], sm));
+      GMAT_HIP(hipEventRecord(scr_beg[b], sm));
       sa.tiles = S == 0 ? mxt[b].as<int>() : dtiles[b].as<int>();
       if (S != 0 && !side_full[b]) {  // escalated from the MX screen: the int8 screen needs E1 / Ed / E2
         GMAT_HIP(hipStreamSynchronize(S2));
@@ -5456,7 +5323,7 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
       else if (S != 0)
         hipLaunchKernelGGL(screen_kernel<SCREEN_SHAPE>, dim3((unsigned)ntiles), dim3(256), 0, sm, sa);
       GMAT_HIP(hipGetLastError());
-      GMAT_HIP(hipEventRecord(evs2[b], sm));
+      GMAT_HIP(hipEventRecord(scr_end[b], sm));
       GMAT_HIP(hipMemcpyAsync(pin_cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
       GMAT_HIP(hipEventRecord(screen_end[b], sm));
       }
@@ -5483,16 +5350,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
           S = S == 0 ? std::min(2, e->n_slice) : S + 1;
           S_max_used = std::max(S_max_used, S);
         } else {  // the finest screen still overflows on one launch (large p_cut): grow the buffer
-          const int64_t cap = std::max<int64_t>(2 * e->cand_cap, (int64_t)(1.25 * (double)count) + 1024);
-          for (DBuf *bf : {&e->cand_i, &e->cand_j, &e->ceff, &e->cvar, &e->cchi, &e->cp})
-            GMAT_TRY(bf->alloc((size_t)cap * 8));
-          if (use_ps)
-            for (DBuf *bf : {&e->cand2_i, &e->cand2_j}) GMAT_TRY(bf->alloc((size_t)cap * 8));
-          e->cand_cap = cap;
-          sa.cap = cap;
+          GMAT_TRY(grow_candidates(e, std::max<int64_t>(2 * e->cand_cap, (int64_t)(1.25 * (double)count) + 1024), use_ps));
+          sa.cap = e->cand_cap;
           sa.cand_i = e->cand_i.as<int64_t>();
           sa.cand_j = e->cand_j.as<int64_t>();
-          if (getenv("GMAT_DEBUG")) fprintf(stderr, "candidate buffer grown to %lld\n", (long long)cap);
         }
       }
       GMAT_TRY(flush(pending));
@@ -5506,37 +5367,10 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
                            pending - ps_done, chi_cut, nullptr, ps_done == 0));
       ps_done = pending;
     }
-    if (stamps_on && li == 5 && S == 0 && use_lr) {  // per-workgroup phase durations (diagnostics)
-      const size_t g = mx_tiles.size() / MX_TE;
-      std::vector<unsigned long long> hs(6 * g);
-      GMAT_HIP(hipMemcpy(hs.data(), dstamp.p, hs.size() * 8, hipMemcpyDeviceToHost));
-      std::vector<double> ph[5];
-      unsigned long long t_min = ~0ull, t_max = 0;
-      for (size_t q = 0; q < g; ++q) {
-        if (mx_tiles[MX_TE * q] < 0) continue;
-        const unsigned long long *st = &hs[6 * q];
-        ph[0].push_back((double)(st[1] - st[0]) * 10.0);  // 100 MHz -> ns
-        ph[1].push_back((double)(st[2] - st[1]) * 10.0);
-        ph[2].push_back((double)(st[3] - st[2]) * 10.0);
-        ph[3].push_back((double)(st[4] - st[3]) * 10.0);
-        ph[4].push_back((double)(st[5] - st[4]) * 10.0);
-        t_min = std::min(t_min, st[0]);
-        t_max = std::max(t_max, st[5]);
-      }
-      const char *nm[5] = {"prologue", "first stage", "other stages", "epilogue", "tests"};
-      for (int k = 0; k < 5; ++k) {
-        std::sort(ph[k].begin(), ph[k].end());
-        if (!ph[k].empty())
-          fprintf(stderr, "lr stamps %-16s median %8.0f ns  p10 %8.0f  p90 %8.0f\n", nm[k], ph[k][ph[k].size() / 2],
-                  ph[k][ph[k].size() / 10], ph[k][ph[k].size() * 9 / 10]);
-      }
-      fprintf(stderr, "lr stamps: %zu workgroups, first start -> last end %.0f us, %d chunks x %d stages\n", ph[0].size(),
-              (double)(t_max - t_min) * 0.01, (int)lx.nC, (int)lx.nK);
-    }
     float ms_side, ms_screen;
     GMAT_HIP(hipEventSynchronize(side_end[b]));
     GMAT_HIP(hipEventElapsedTime(&ms_side, side_beg[b], side_end[b]));
-    GMAT_HIP(hipEventElapsedTime(&ms_screen, evs7[b], evs2[b]));
+    GMAT_HIP(hipEventElapsedTime(&ms_screen, scr_beg[b], scr_end[b]));
     t_side += ms_side * 1e-3;
     t_screen += ms_screen * 1e-3;
     // int8 MFMA ops issued: per tile and slice, sum over K-blocks of (n_pad - K) x MT MACs per
@@ -5558,47 +5392,49 @@ extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t
   }
   GMAT_HIP(hipStreamSynchronize(S2));
   GMAT_TRY(flush(pending));
-  // sort hits by (i, j)
-  std::vector<int64_t> ord(e->hit_i.size());
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
-  });
-  auto apply = [&](auto &v) {
-    auto c2 = v;
-    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
-  };
-  apply(e->hit_i);
-  apply(e->hit_j);
-  apply(e->hit_eff);
-  apply(e->hit_var);
-  apply(e->hit_chi);
-  apply(e->hit_p);
-  *n_hits = (int64_t)e->hit_i.size();
+  *n_hits = sort_hits(e);
   e->stats[0] = pairs_tested;
-  e->stats[1] = ncand_total;
+  e->stats[1] = tally.n_cand;
   e->stats[2] = ops;
   e->stats[3] = t_screen;
-  e->stats[4] = t_ref;
+  e->stats[4] = tally.t_ref;
   e->stats[5] = t_side;
-  if (getenv("GMAT_DEBUG"))
-    fprintf(stderr, "gmat_epi_scan: %lld launches, tile-list building %.3f s on the host, total %.3f s\n",
-            (long long)launches_done, t_build, e->stats[6]);
-  if (getenv("GMAT_DEBUG"))
-    fprintf(stderr, "gmat_epi_scan: %.0f screen candidates, %.0f refined%s\n", ncand_total, n_refined,
-            use_ps ? " (pair screen)" : "");
   e->stats[6] = now() - t_start;
   e->stats[7] = (double)launches_done;
+  if (getenv("GMAT_DEBUG"))
+    fprintf(stderr, "gmat_epi_scan: %lld launches, tile-list building %.3f s on the host, total %.3f s, %.0f screen "
+            "candidates, %.0f refined%s\n", (long long)launches_done, t_build, e->stats[6], tally.n_cand,
+            tally.n_refined, use_ps ? " (pair screen)" : "");
   if (live_cnt.p) {
-    unsigned long long lc = 0;
-    GMAT_HIP(hipMemcpy(&lc, live_cnt.p, 8, hipMemcpyDeviceToHost));
+    unsigned long long lcnt = 0;
+    GMAT_HIP(hipMemcpy(&lcnt, live_cnt.p, 8, hipMemcpyDeviceToHost));
     fprintf(stderr, "gmat_epi_scan: %.0f pairs, prefilter keeps %llu pairs (%.4f%%), %.0f low-rank candidates\n",
-            pairs_tested, lc, 100.0 * (double)lc / std::max(pairs_tested, 1.0), ncand_total);
+            pairs_tested, lcnt, 100.0 * (double)lcnt / std::max(pairs_tested, 1.0), tally.n_cand);
   }
   const bool lr_only = use_lr && S_max_used == 0;
   e->stats[8] = lr_only ? -1 : S_max_used;
   e->stats[9] = lr_only ? e->lr_lam : (S_max_used == 0 ? e->rho_mx : e->rho[S_max_used]);
   return GMAT_OK;
+}
+
+}  // namespace
+
+extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+                             int n_slice, int64_t *n_hits) {
+  GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
+  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
+  const int64_t m = e->m, n_pad = e->n_pad;
+  for (int64_t t = 0; t < n_rows; ++t) {
+    GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
+    GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
+  }
+  if (n_slice == GMAT_SCREEN_NONE) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
+  // the compacted low-rank scan serves the low-rank level (automatic at p_cut <= 1e-4, or forced by
+  // n_slice -2); GMAT_LR_BLOCKS=1 keeps the block-granular path below (A/B runs)
+  const bool lr_level = e->lr_R > 0 && e->pf_mu > 0.0 && (n_slice == -2 || (n_slice == 0 && p_cut <= 1e-4));
+  if (lr_level && pair_screen_fits(e) && !getenv("GMAT_LR_BLOCKS") && !getenv("GMAT_NO_PREFILTER"))
+    return scan_lowrank(e, kind, rows, n_rows, p_cut, chi_cut, n_hits);
+  return scan_blocks(e, kind, rows, n_rows, p_cut, chi_cut, n_slice, n_hits);
 }
 
 extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,
