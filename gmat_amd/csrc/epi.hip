@@ -194,6 +194,8 @@ struct SideArgs {
   int blocked;          // prefilter_pass_kernel: rs[0..E3_PF), rs4, cs4 are stage-blocked panels
                         // ([n_pad / 64][m][64 B] int8, [n_pad / 64][m][32 B] fp4; block_panel_kernel)
   const float *recL, *recR;  // prefilter_pass_kernel: test records, row / column role (pf_rec_kernel)
+  const int *tile_list;      // prefilter_pass_kernel: the launch's running tiles (rt + n_rt ct, ascending),
+  int n_list;                // dealt to the XCDs in contiguous eighths; null: one tile per workgroup
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
@@ -342,17 +344,37 @@ __device__ __forceinline__ v4i i8x2_of_fp4_eo(unsigned x0, unsigned x1) {
 __device__ __forceinline__ void lds_dma16_m0(const void *g, unsigned m0) {
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(m0) : "memory");
 }
+template <bool LIST>
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const ScreenArgs &a = x.a;
-  const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
-  const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
-  const int rt = tile % x.n_rt, ct = tile / x.n_rt;
-  const int r0 = rt * PF_TR;
-  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PF_TC;
-  if (r0 >= a.n_rows || c0 >= a.m) return;
-  if (a.tri && c0 + PF_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
-  auto pstamp = [&](int k) __attribute__((always_inline)) {
-    if (a.pf_stamp && threadIdx.x == 0) a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+  // The workgroup's tiles.  With a tile list (the launch's running tiles), XCD x (workgroup b runs on
+  // XCD b mod 8) takes the list's x-th eighth and its G workgroups stride through it: a persistent
+  // grid, in which the next tile's records and first stages stream into LDS while the current tile's
+  // epilogue runs.  Without one, the workgroup's single tile of the XCD-aware remap, if it has a pair.
+  const int xcd = (int)blockIdx.x % 8, kw = (int)blockIdx.x / 8, G = (int)gridDim.x / 8;
+  const int l_lo = LIST ? (int)(((int64_t)x.n_list * xcd) / 8) : 0;
+  const int l_hi = LIST ? (int)(((int64_t)x.n_list * (xcd + 1)) / 8) : 0;
+  auto tile_at = [&](int i) __attribute__((always_inline)) -> int {
+    if (LIST) {
+      const int q = l_lo + kw + i * G;
+      return q < l_hi ? __builtin_amdgcn_readfirstlane(x.tile_list[q]) : -1;
+    }
+    if (i > 0) return -1;
+    const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8;
+    const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + kw;
+    const int tr0 = (t % x.n_rt) * PF_TR;
+    const int64_t tc0 = (a.j_lo / 32) * 32 + (int64_t)(t / x.n_rt) * PF_TC;
+    if (tr0 >= a.n_rows || tc0 >= a.m) return -1;
+    if (a.tri && tc0 + PF_TC - 1 <= a.rows[tr0]) return -1;  // rows ascend within a launch
+    return t;
+  };
+  int it = 0, tile = tile_at(0);
+  if (tile < 0) return;
+  int r0 = (tile % x.n_rt) * PF_TR;
+  int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PF_TC;
+  auto pstamp = [&](int k) __attribute__((always_inline)) {  // the workgroup's first tile only
+    if (!LIST && a.pf_stamp && threadIdx.x == 0)
+      a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
   };
   pstamp(0);
   // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
@@ -368,20 +390,23 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // an instruction's 1 KB comes from 8 whole 128-byte lines (int8 pieces in the even / odd
   // individual order of i8x2_of_fp4_eo)
   constexpr int64_t rstride = SG_K, fstride = SG_K / 2;
+  auto set_src = [&](int r0, int64_t c0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int u = 0; u < PF_Q; ++u) {
-    const int q = min(w, PF_QW - 1) + PF_QW * u;
-    if (q < 8) {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
-      const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-      src[u] = (const uint8_t *)x.rs[q >> 2] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
-      stp[u] = a.m * SG_K;
-    } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 8, 9 rows, 10..17 columns)
-      const int qq = q < 10 ? q - 8 : q - 10, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-      const int64_t idx = q < 10 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-      src[u] = (q < 10 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
-      stp[u] = a.m * (SG_K / 2);
+    for (int u = 0; u < PF_Q; ++u) {
+      const int q = min(w, PF_QW - 1) + PF_QW * u;
+      if (q < 8) {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
+        const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+        src[u] = (const uint8_t *)x.rs[q >> 2] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
+        stp[u] = a.m * SG_K;
+      } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 8, 9 rows, 10..17 columns)
+        const int qq = q < 10 ? q - 8 : q - 10, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
+        const int64_t idx = q < 10 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
+        src[u] = (q < 10 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
+        stp[u] = a.m * (SG_K / 2);
+      }
     }
-  }
+  };
+  set_src(r0, c0);
   typedef __attribute__((address_space(3))) const void *lds_ct;
   const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
   // stage st into ring slot `slot` (= st % PF_NS, kept by the caller)
@@ -411,190 +436,218 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   };
   v16i acc[2][E3_PF];
   v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-#pragma unroll
-    for (int p = 0; p < E3_PF; ++p)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[q][p][e] = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc4[q][p][e] = 0.f;
-  }
   const int S = (int)(x.n_pad / SG_K);
   const int pre = min(S, PF_NS - 1);
   // the epilogue's test records (32 B per row / column) by LDS-DMA ahead of the stages: wave w the
   // 32 columns 32 w .., waves 0 and 1 also the 32 rows 32 w ..; lane l half l & 1 of record l / 2.
   // They retire before stage 0 (in-order vmcnt), so the stage waits cover them.
-  __shared__ __attribute__((aligned(16))) float rec[PF_TR + PF_TC][PF_REC];
-  {
+  // Two record buffers: the next tile's land while the current tile's epilogue reads its own.
+  __shared__ __attribute__((aligned(16))) float rec[2][PF_TR + PF_TC][PF_REC];
+  auto issue_rec = [&](int r0, int64_t c0, int rb) __attribute__((always_inline)) {
     const int k = 32 * w + (lane >> 1);
     if (w < PF_TR / 32)
-      lds_dma16(x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC + 4 * (lane & 1), &rec[32 * w][0]);
-    lds_dma16(x.recR + min(c0 + k, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[PF_TR + 32 * w][0]);
-  }
+      lds_dma16(x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC + 4 * (lane & 1), &rec[rb][32 * w][0]);
+    lds_dma16(x.recR + min(c0 + k, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[rb][PF_TR + 32 * w][0]);
+  };
+  issue_rec(r0, c0, 0);
   for (int st = 0; st < pre; ++st) issue(st, st);
-  wait_for(0, pre - 1);
-  pstamp(1);
-  const int rrow = 32 * wr + c;
-  int slot = 0, slot_ahead = PF_NS - 1;  // ring slots of stage st and of stage st + 4
-  for (int st = 0; st < S; ++st) {
-    const uint8_t *bf = ring[slot];
-    // slot (st + 4) % 5 was read in stage st - 1, which every wave has left (barrier)
-    if (st + PF_NS - 1 < S) issue(st + PF_NS - 1, slot_ahead);
-    slot = slot == PF_NS - 1 ? 0 : slot + 1;
-    slot_ahead = slot_ahead == PF_NS - 1 ? 0 : slot_ahead + 1;
-    // lane (c, h) holds the fp4 codes of individuals 32h .. 32h + 31 of the stage; the int8 E3
-    // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
-    v4i rb4[2];
+  for (;; ++it) {
+    // per-lane values re-derived from an opaque copy of the thread index each tile: hoisted out of
+    // the tile loop, the epilogue's would stay live through the main loop (256-VGPR budget)
+    int tid_o = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid_o));
+    const int lane = tid_o & 63, h = lane >> 5, c = lane & 31;
+    const int rrow = 32 * wr + c;
+    const int rb = it & 1;
+    if (it == 0) {
+      wait_for(0, pre - 1);
+    } else {  // the prefetched stages, records and the previous epilogue's stores (vmcnt counts those too)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    pstamp(1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
-      rb4[q] = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
-    }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
-      const v4i f0 = *(const v4i *)&bf[O_R8 + rrow * 64 + 16 * lr];
-      const v4i f1 = *(const v4i *)&bf[O_R8S + rrow * 64 + 16 * lr];
+      for (int p = 0; p < E3_PF; ++p)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[q][p][e] = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc4[q][p][e] = 0.f;
+    }
+    int slot = 0, slot_ahead = PF_NS - 1;  // ring slots of stage st and of stage st + 4
+    for (int st = 0; st < S; ++st) {
+      const uint8_t *bf = ring[slot];
+      // slot (st + 4) % 5 was read in stage st - 1, which every wave has left (barrier)
+      if (st + PF_NS - 1 < S) issue(st + PF_NS - 1, slot_ahead);
+      slot = slot == PF_NS - 1 ? 0 : slot + 1;
+      slot_ahead = slot_ahead == PF_NS - 1 ? 0 : slot_ahead + 1;
+      // lane (c, h) holds the fp4 codes of individuals 32h .. 32h + 31 of the stage; the int8 E3
+      // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
+      v4i rb4[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const v4i fc = i8x2_of_fp4_eo((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
-        acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
-        acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
+        const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
+        rb4[q] = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
       }
-    }
-    {
-      const int lr = h ^ ((rrow >> 3) & 1);
-      v8i_ fa[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
+        const v4i f0 = *(const v4i *)&bf[O_R8 + rrow * 64 + 16 * lr];
+        const v4i f1 = *(const v4i *)&bf[O_R8S + rrow * 64 + 16 * lr];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const v4i fc = i8x2_of_fp4_eo((unsigned)rb4[q][2 * kk], (unsigned)rb4[q][2 * kk + 1]);
+          acc[q][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f0, fc, acc[q][0], 0, 0, 0);
+          acc[q][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f1, fc, acc[q][1], 0, 0, 0);
+        }
+      }
       {
-        const v4i ra4 = *(const v4i *)&bf[O_R4 + rrow * 32 + 16 * lr];
-        fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
-        fa[1] = sq4(ra4);
-      }
+        const int lr = h ^ ((rrow >> 3) & 1);
+        v8i_ fa[2];
+        {
+          const v4i ra4 = *(const v4i *)&bf[O_R4 + rrow * 32 + 16 * lr];
+          fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
+          fa[1] = sq4(ra4);
+        }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        v8i_ fb[2];
-        fb[0] = v8i_{rb4[q][0], rb4[q][1], rb4[q][2], rb4[q][3], 0, 0, 0, 0};
-        fb[1] = sq4(rb4[q]);
+        for (int q = 0; q < 2; ++q) {
+          v8i_ fb[2];
+          fb[0] = v8i_{rb4[q][0], rb4[q][1], rb4[q][2], rb4[q][3], 0, 0, 0, 0};
+          fb[1] = sq4(rb4[q]);
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-          acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
+          for (int p = 0; p < 4; ++p)
+            acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
+        }
       }
+      wait_for(st + 1, min(st + PF_NS - 1, S - 1));
     }
-    wait_for(st + 1, min(st + PF_NS - 1, S - 1));
-  }
-  pstamp(2);
-  // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
-  // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
-  // The test runs in fp32 with a certified slack (fp64 costs twice the issue slots and two registers
-  // per value): every quantity below is a signed sum of the monomials of (a - alpha)^2 (b - beta)^2 or
-  // (a - alpha)(b - beta) over the individuals, whose absolute values add up to at most
-  //   M = sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2   (|1'e| <= sqrt(n M)),
-  // so the fp32 evaluation (about a dozen roundings of 2^-24 each, inputs rounded from fp64 included)
-  // is off by at most 2^-20 M for |e|^2 and 2^-21 sqrt(n M) for 1'e, and vlo = (mu - eps)|e|^2 -
-  // (mu + tau)(1'e)^2/n by at most 2^-19 (2 mu + tau) M: vlo is lowered by 2^-17 (2 mu + tau) M.  eff
-  // = sL3 c3 - beta sa + alpha (beta spy - sb) is off by at most 2^-20 times the sum of the three
-  // terms' magnitudes, which is added to eff_hi with the int8 slicing bound.  The final comparison's
-  // three roundings are covered by the factor 1 + 2^-18.
-  // per-row / per-column values: the records in rec[] (pf_rec_kernel).  Two passes: the tests of all
-  // 32 (row, column block) elements of a lane as straight-line code (no branch between them, so the
-  // row records' LDS reads are scheduled ahead of their use), collecting the live masks and a per-lane
-  // bit per element for the stores; then the stores of the live blocks' products (a few per cent).
-  const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id);
-  const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
-  const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
-  constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f;
-  const float4 *rv = (const float4 *)&rec[0][0];
-  int jq[2];  // SNP indices < 2^31
-  bool cok[2];
-  float cbe[2], ccb[2], cC1n[2], cnb[2], cbsb[2], cmag[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int cl = 64 * wc + 32 * q + c;
-    jq[q] = (int)(c0 + cl);
-    // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
-    const float4 cv0 = rv[2 * (PF_TR + cl)], cv1 = rv[2 * (PF_TR + cl) + 1];
-    cbe[q] = cv0.x;
-    ccb[q] = cv0.y;
-    cC1n[q] = cv0.z;
-    cnb[q] = cv0.w;
-    cbsb[q] = cv1.x;
-    cmag[q] = cv1.y;
-    cok[q] = (jq[q] < a.m) & (jq[q] >= a.j_lo) & (cv1.z == 0.0f);
-  }
-  // masks: lane t < 32 of the wave writes the word of (e = t / 2, half t % 2) of each column block
-  const int te = (lane >> 1) & 15, th = lane & 1;
-  unsigned mine[2] = {0u, 0u}, n_live = 0, st_bits = 0u;
-  pstamp(3);
-  const int rw = r0 + 32 * wr;
-  const int64_t cw = c0 + 64 * wc - a.j_lo;
-  const uint32_t voff = (uint32_t)(4 * h * a.ld_e + c);
-  int *const b13 = (int *)a.c13 + ((int64_t)a.n_rows + rw) * a.ld_e + cw;
-  int *const bpf = (int *)a.pfc + (int64_t)rw * a.ld_e + cw;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int kr = (e & 3) + 8 * (e >> 2);
-    const int rl = 32 * wr + kr + 4 * h, r = r0 + rl;
-    const float4 r0v = rv[2 * rl], r1v = rv[2 * rl + 1];  // i, alpha, csum, R1 | sL3, sa, (2 + alpha)^2
-    const int iv = __float_as_int(r0v.x);
-    const float al = r0v.y, sL3 = r1v.x, sL3h = 0.5f * sL3;
-    const bool rok = (r < a.n_rows) & (iv >= 0);
+    pstamp(2);
+    // every wave has passed the last stage's barrier (its vmcnt(0) wait): the ring is free, so the
+    // next tile's records and first stages go out now and land while this tile's epilogue runs
+    const int nxt = tile_at(it + 1);
+    if (nxt >= 0) {
+      const int nr0 = (nxt % x.n_rt) * PF_TR;
+      const int64_t nc0 = (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PF_TC;
+      set_src(nr0, nc0);
+      issue_rec(nr0, nc0, rb ^ 1);
+      for (int st = 0; st < pre; ++st) issue(st, st);
+    }
+    // epilogue: lane (c, h) holds rows 32 wr + (e & 3) + 8 (e >> 2) + 4h, column 64 wc + 32 q + c; a
+    // half-wave covers one 32-column block.  Per-row scalars staged in LDS, per-column ones in registers.
+    // The test runs in fp32 with a certified slack (fp64 costs twice the issue slots and two registers
+    // per value): every quantity below is a signed sum of the monomials of (a - alpha)^2 (b - beta)^2 or
+    // (a - alpha)(b - beta) over the individuals, whose absolute values add up to at most
+    //   M = sum_k (a_k + alpha)^2 (b_k + beta)^2 <= (2 + alpha)^2 sum_k (b_k + beta)^2   (|1'e| <= sqrt(n M)),
+    // so the fp32 evaluation (about a dozen roundings of 2^-24 each, inputs rounded from fp64 included)
+    // is off by at most 2^-20 M for |e|^2 and 2^-21 sqrt(n M) for 1'e, and vlo = (mu - eps)|e|^2 -
+    // (mu + tau)(1'e)^2/n by at most 2^-19 (2 mu + tau) M: vlo is lowered by 2^-17 (2 mu + tau) M.  eff
+    // = sL3 c3 - beta sa + alpha (beta spy - sb) is off by at most 2^-20 times the sum of the three
+    // terms' magnitudes, which is added to eff_hi with the int8 slicing bound.  The final comparison's
+    // three roundings are covered by the factor 1 + 2^-18.
+    // per-row / per-column values: the records in rec[] (pf_rec_kernel).  Two passes: the tests of all
+    // 32 (row, column block) elements of a lane as straight-line code (no branch between them, so the
+    // row records' LDS reads are scheduled ahead of their use), collecting the live masks and a per-lane
+    // bit per element for the stores; then the stores of the live blocks' products (a few per cent).
+    const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / a.n_id);
+    const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
+    const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
+    constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f;
+    const float4 *rv = (const float4 *)&rec[rb][0][0];
+    int jq[2];  // SNP indices < 2^31
+    bool cok[2];
+    float cbe[2], ccb[2], cC1n[2], cnb[2], cbsb[2], cmag[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const bool ok = rok & cok[q] & !(a.tri & (jq[q] <= iv));
-      const float be = cbe[q];
-      float c3 = 0.0f;  // twice the E3 slice sum (the doubled int8 b), halved through sL3h
-#pragma unroll
-      for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
-      const float t1 = sL3h * c3, t2 = be * r1v.y, t3 = al * cbsb[q];
-      const float eff = t1 - t2 + t3;
-      const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb[q] + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
-      const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
-      // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
-      const float ee = sa2b2 + be * (be * r0v.w - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n[q]);
-      const float se = sab - be * r0v.z + al * cnb[q];
-      const float vlo = mu_e * ee - k1 * se * se - k2 * r1v.z * cmag[q];
-      const bool lv = ok & (!(vlo > 0.0f) | (eff_hi * eff_hi * CMP >= chi_cut * vlo));
-      const unsigned long long bal = __ballot(lv);
-      n_live += (unsigned)__popcll(bal);
-      const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
-      mine[q] = te == e ? (th ? w1 : w0) : mine[q];
-      // a live block (its row r < n_rows: some lane of the half passed rok) whose column this lane holds
-      st_bits |= ((((h ? w1 : w0) != 0u) & cok[q]) ? 1u : 0u) << (2 * e + q);
+      const int cl = 64 * wc + 32 * q + c;
+      jq[q] = (int)(c0 + cl);
+      // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
+      const float4 cv0 = rv[2 * (PF_TR + cl)], cv1 = rv[2 * (PF_TR + cl) + 1];
+      cbe[q] = cv0.x;
+      ccb[q] = cv0.y;
+      cC1n[q] = cv0.z;
+      cnb[q] = cv0.w;
+      cbsb[q] = cv1.x;
+      cmag[q] = cv1.y;
+      cok[q] = (jq[q] < a.m) & (jq[q] >= a.j_lo) & (cv1.z == 0.0f);
     }
-  }
-  pstamp(4);
-  // a live block's E3 (and code products) for the low-rank / pair screens (cok: j in range; a
-  // monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+    // masks: lane t < 32 of the wave writes the word of (e = t / 2, half t % 2) of each column block
+    const int te = (lane >> 1) & 15, th = lane & 1;
+    unsigned mine[2] = {0u, 0u}, n_live = 0, st_bits = 0u;
+    pstamp(3);
+    const int rw = r0 + 32 * wr;
+    const int64_t cw = c0 + 64 * wc - a.j_lo;
+    const uint32_t voff = (uint32_t)(4 * h * a.ld_e + c);
+    int *const b13 = (int *)a.c13 + ((int64_t)a.n_rows + rw) * a.ld_e + cw;
+    int *const bpf = (int *)a.pfc + (int64_t)rw * a.ld_e + cw;
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int kr = (e & 3) + 8 * (e >> 2);
+    for (int e = 0; e < 16; ++e) {
+      const int kr = (e & 3) + 8 * (e >> 2);
+      const int rl = 32 * wr + kr + 4 * h, r = r0 + rl;
+      const float4 r0v = rv[2 * rl], r1v = rv[2 * rl + 1];  // i, alpha, csum, R1 | sL3, sa, (2 + alpha)^2
+      const int iv = __float_as_int(r0v.x);
+      const float al = r0v.y, sL3 = r1v.x, sL3h = 0.5f * sL3;
+      const bool rok = (r < a.n_rows) & (iv >= 0);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if ((st_bits >> (2 * e + q)) & 1u) {
-        const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
+      for (int q = 0; q < 2; ++q) {
+        const bool ok = rok & cok[q] & !(a.tri & (jq[q] <= iv));
+        const float be = cbe[q];
+        float c3 = 0.0f;  // twice the E3 slice sum (the doubled int8 b), halved through sL3h
 #pragma unroll
-        for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e] >> 1;  // exact
-        if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
-#pragma unroll
-          for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
+        for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0f / 128.0f) + (float)acc[q][t][e];
+        const float t1 = sL3h * c3, t2 = be * r1v.y, t3 = al * cbsb[q];
+        const float eff = t1 - t2 + t3;
+        const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb[q] + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
+        const float sab = acc4[q][0][e], sa2b = acc4[q][1][e], sab2 = acc4[q][2][e], sa2b2 = acc4[q][3][e];
+        // |e|^2 = sa2b2 - 2b sa2b - 2a sab2 + 4ab sab + b^2 R1 + a^2 C1n;  1'e = sab - b ca + a (n b - cb)
+        const float ee = sa2b2 + be * (be * r0v.w - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n[q]);
+        const float se = sab - be * r0v.z + al * cnb[q];
+        const float vlo = mu_e * ee - k1 * se * se - k2 * r1v.z * cmag[q];
+        const bool lv = ok & (!(vlo > 0.0f) | (eff_hi * eff_hi * CMP >= chi_cut * vlo));
+        const unsigned long long bal = __ballot(lv);
+        n_live += (unsigned)__popcll(bal);
+        const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
+        mine[q] = te == e ? (th ? w1 : w0) : mine[q];
+        // a live block (its row r < n_rows: some lane of the half passed rok) whose column this lane holds
+        st_bits |= ((((h ? w1 : w0) != 0u) & cok[q]) ? 1u : 0u) << (2 * e + q);
       }
-  }
-  pstamp(5);
-  const int tr = r0 + 32 * wr + (te & 3) + 8 * (te >> 2) + 4 * th;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
-    if (lane < 32 && tr < a.n_rows && J < a.nJ) {
-      if (a.flags) a.flags[(int64_t)tr * a.nJ + J] = mine[q] != 0;
-      if (a.lmask) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
     }
+    pstamp(4);
+    // a live block's E3 (and code products) for the low-rank / pair screens (cok: j in range; a
+    // monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int kr = (e & 3) + 8 * (e >> 2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if ((st_bits >> (2 * e + q)) & 1u) {
+          const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
+#pragma unroll
+          for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e] >> 1;  // exact
+          if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+#pragma unroll
+            for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
+        }
+    }
+    pstamp(5);
+    const int tr = r0 + 32 * wr + (te & 3) + 8 * (te >> 2) + 4 * th;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
+      if (lane < 32 && tr < a.n_rows && J < a.nJ) {
+        if (a.flags) a.flags[(int64_t)tr * a.nJ + J] = mine[q] != 0;
+        if (a.lmask) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
+      }
+    }
+    if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
+    if (!LIST && a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
+    pstamp(6);
+    if (nxt < 0) break;
+    r0 = (nxt % x.n_rt) * PF_TR;
+    c0 = (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PF_TC;
+    set_src(r0, c0);  // again: the source addresses stay out of the epilogue's registers
   }
-  if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
-  if (a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
-  pstamp(6);
 }
 
 // ------------------------------------------------------------------ prefilter pass, covariate designs
@@ -3021,6 +3074,7 @@ struct gmat_epi {
   double setup[8] = {0};
   uint64_t p_hash = 0;  // fingerprint of P (guards imported spectral state)
   int imported = 0;     // spectral state imported from another plan (gmat_epi_create_with)
+  int n_cu = 0;         // compute units of the device (persistent prefilter grid), queried on first use
   hipStream_t s = 0;
   // scan work buffers, two sets (kept across scans of the plan: allocation is not free)
   struct ScanBufs {
@@ -3028,12 +3082,12 @@ struct gmat_epi {
   } sb;
   // pinned host staging of the scan pipeline (hipHostMalloc is slow: allocated once per plan)
   struct ScanPins {
-    Pinned res, rows[3], flags[3], mxt[3], mxr[3], t2[3], cnt[3], count2;
+    Pinned res, rows[3], flags[3], mxt[3], mxr[3], t2[3], cnt[3], count2, tl[3];
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
   struct LrcBuffers {  // three sets: the prefilters of launches L + 1 and L + 2 are queued while L screens
-    DBuf drows[3], lmask[3], e13[3], pfc[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3];
+    DBuf drows[3], lmask[3], e13[3], pfc[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3], tlist[3];
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
@@ -4452,6 +4506,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_TRY(B.cnt[b].alloc(RL * sizeof(int)));
     GMAT_TRY(B.soff[b].alloc(RL * sizeof(int)));
     GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
+    GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(RL, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
+    GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(RL, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
     GMAT_TRY(e->pins.rows[b].reserve(RL * 8));
     GMAT_TRY(e->pins.cnt[b].reserve(8));
     GMAT_TRY(e->pins.t2[b].reserve(16));
@@ -4466,6 +4522,17 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   DBuf pf_st;  // GMAT_PF_STAMPS: per-workgroup phase stamps of the prefilter of launch 5
   const size_t stamp_launch = 5;
   int64_t stamp_grid = 0;
+  // the prefilter as a persistent grid over each launch's tile list (GMAT_PF_NOLIST: one workgroup
+  // per tile, as the per-tile phase stamps need)
+  const bool pf_list = !getenv("GMAT_PF_NOLIST") && !getenv("GMAT_PF_STAMPS");
+  // GMAT_PF_WG caps the persistent grid (tests: many tiles per workgroup at small cohorts)
+  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : 0;
+  if (!e->n_cu) {
+    int dev = 0, cus = 0;
+    GMAT_HIP(hipGetDevice(&dev));
+    GMAT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    e->n_cu = std::max(cus, 8);
+  }
   if (getenv("GMAT_PF_STAMPS")) {
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
@@ -4568,6 +4635,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     x.rs4 = L.p4.as<uint8_t>();
     x.cs4 = R.p4.as<uint8_t>();
     x.blocked = 0;
+    x.tile_list = nullptr;
+    x.n_list = 0;
     x.recL = L.pfRecL.as<float>();
     x.recR = R.pfRecR.as<float>();
     if (e->pf_ncov == 0) {  // prefilter_pass_kernel reads stage-blocked operands
@@ -4576,18 +4645,32 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       x.rs4 = L.p4b.as<uint8_t>();
       x.cs4 = R.p4b.as<uint8_t>();
       x.n_rt = (int)cdiv(Rn, PF_TR);
-      // MFMA work of the tiles that run (a tile entirely left of the diagonal exits at once): per pair
-      // 4 fp4 code products + 2 int8 E3 slices over n_pad individuals = 16 n_pad fp4-equivalent ops
-      int64_t run = 0;
-      for (int rt = 0; rt < x.n_rt; ++rt)
-        for (int64_t ct = 0; ct < cdiv(ncols, PF_TC); ++ct) {
+      // the tiles that run (a tile entirely left of the diagonal has no pair), in tile order
+      // rt + n_rt ct; MFMA work per pair: 4 fp4 code products + 2 int8 E3 slices over n_pad
+      // individuals = 16 n_pad fp4-equivalent ops
+      int *tl = e->pins.tl[b].as<int>();
+      int run = 0;
+      for (int64_t ct = 0; ct < cdiv(ncols, PF_TC); ++ct)
+        for (int rt = 0; rt < x.n_rt; ++rt) {
           const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_TC;
-          if (c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR])) ++run;
+          if (c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR])) tl[run++] = rt + x.n_rt * (int)ct;
         }
       pf_ops_of[li] = (double)run * PF_TR * PF_TC * 16.0 * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
-      if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
-      hipLaunchKernelGGL(prefilter_pass_kernel, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512), 0, S2, x);
+      if (pf_list) {
+        // persistent grid over the list: one workgroup per CU (a multiple of 8).  (Same-box A/B: 27.6
+        // against 27.7 ms per configs[2] step for as few workgroups as finish in the same number of
+        // tile rounds, and 28.0 against 28.2 for one workgroup per tile, GMAT_PF_NOLIST.)
+        GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
+        x.tile_list = B.tlist[b].as<int>();
+        x.n_list = run;
+        const int g = 8 * (int)std::min<int64_t>(cdiv(pf_wg ? pf_wg : e->n_cu, 8), cdiv(run, 8));
+        if (run > 0) hipLaunchKernelGGL(prefilter_pass_kernel<true>, dim3((unsigned)g), dim3(512), 0, S2, x);
+      } else {
+        if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
+        hipLaunchKernelGGL(prefilter_pass_kernel<false>, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512), 0,
+                           S2, x);
+      }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
       for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
@@ -5003,6 +5086,8 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
       x.a = make_args(li, b);
       x.n_pad = n_pad;
       x.blocked = 0;
+      x.tile_list = nullptr;
+      x.n_list = 0;
       x.recL = L.pfRecL.as<float>();
       x.recR = R.pfRecR.as<float>();
       x.n_rt = (int)cdiv(Rn, SG_T);
@@ -5021,7 +5106,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.cs4 = R.p4b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
-        hipLaunchKernelGGL(prefilter_pass_kernel, dim3(gp), dim3(512), 0, S2, xp);
+        hipLaunchKernelGGL(prefilter_pass_kernel<false>, dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
         for (int k = 0; k < e->pf_ncov; ++k) xp.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;

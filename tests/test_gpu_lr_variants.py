@@ -1,9 +1,11 @@
 """Scan-schedule variants of the low-rank screen path give byte-identical results: the compacted
 screen (default) against the block-granular one (GMAT_LR_BLOCKS=1: lr_screen_kernel over every
-flagged 32-pair block), and the pair screen run in chunks beside the later launches (GMAT_PS_CHUNK
-small, or 0: all at flush time).  The default is checked against the oracle (remma_epiAA.py:71-82 and the
-epiAD sibling) on sampled rows, every variant against the default on the whole scan (several
-launches, so the next-tile prefetch and the chunked pair screen both run)."""
+flagged 32-pair block), the pair screen run in chunks beside the later launches (GMAT_PS_CHUNK small,
+or 0: all at flush time), and the prefilter's persistent grid against one workgroup per tile
+(GMAT_PF_NOLIST) and against a few workgroups looping over many tiles (GMAT_PF_WG).  The default is
+checked against the oracle (remma_epiAA.py:71-82 and the epiAD sibling) on sampled rows, every
+variant against the default on the whole scan (several launches, so the next-tile prefetch and the
+chunked pair screen both run)."""
 import os
 
 import numpy as np
@@ -12,7 +14,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{"GMAT_LR_BLOCKS": "1"}, {"GMAT_PS_CHUNK": "700"}, {"GMAT_PS_CHUNK": "0"},
-            {"GMAT_LR_BLOCKS": "1", "GMAT_PS_CHUNK": "300"}]
+            {"GMAT_LR_BLOCKS": "1", "GMAT_PS_CHUNK": "300"},
+            {"GMAT_PF_NOLIST": "1"},  # prefilter: one workgroup per tile
+            {"GMAT_PF_WG": "8"},      # prefilter: 8 persistent workgroups, ~10 tiles each per launch
+            {"GMAT_PF_WG": "24"}]
 
 
 @pytest.fixture(scope="module")
