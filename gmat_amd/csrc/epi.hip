@@ -48,7 +48,8 @@ typedef float v2f_ __attribute__((ext_vector_type(2)));
 constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
-constexpr int ROWS_PER_LAUNCH = 512;
+constexpr int ROWS_PER_LAUNCH = 512;       // first SNPs per launch of the block-granular scan
+constexpr int LRC_ROWS_PER_LAUNCH = 4096;  // ... and of the compacted low-rank scan
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
 constexpr int E3_PF = 2;         // L3 slices of the prefilter pass (eff to ~2^-14: enough to screen)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld
@@ -4251,13 +4252,14 @@ struct ScanLaunch {
   int64_t j_lo = 0;
 };
 
-// launches of ROWS_PER_LAUNCH rows: chunk k of half that size folded with chunk NC-1-k (equal work
-// per launch, as the triangle's rows shrink); launches without a pair are dropped.  *pairs = the
-// pairs the launches test.
-std::vector<ScanLaunch> fold_launches(const int64_t *rows, int64_t n_rows, int64_t m, int tri, double *pairs) {
+// launches of `rl` rows: chunk k of half that size folded with chunk NC-1-k (equal work per launch,
+// as the triangle's rows shrink); launches without a pair are dropped.  *pairs = the pairs the
+// launches test.
+std::vector<ScanLaunch> fold_launches(const int64_t *rows, int64_t n_rows, int64_t m, int tri, double *pairs,
+                                      int64_t rl = ROWS_PER_LAUNCH) {
   std::vector<ScanLaunch> plan;
   *pairs = 0;
-  const int64_t half = ROWS_PER_LAUNCH / 2, nc = cdiv(n_rows, half);
+  const int64_t half = rl / 2, nc = cdiv(n_rows, half);
   for (int64_t k = 0, l = nc - 1; k <= l; ++k, --l) {
     ScanLaunch ln;
     for (int64_t t = k * half; t < std::min(n_rows, (k + 1) * half); ++t) ln.rows.push_back(rows[t]);
@@ -4474,11 +4476,13 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
 }
 
 // ---- the compacted low-rank scan (default level for p_cut <= 1e-4 when the plan has the low-rank
-// certificate): per launch of 512 first SNPs (two folded 256-row chunks, equal work)
+// certificate): per launch of 4,096 first SNPs (two folded 2,048-row chunks, equal work; fewer rows
+// when the scan would have fewer than eight launches)
 //   S2: prefilter (live-pair masks, E3 slices and code products of live blocks) -> slot lists (lc_*)
 //   sm: compacted low-rank screen of the launch's slots (candidates appended to cand)
 //   S3: pair screen of the candidates in chunks beside the later launches, the exact refine at flush
-// Launch L + 1's prefilter runs beside launch L's screen (two buffer sets); the host reads a
+// The prefilters of launches L + 1 and L + 2 are queued beside launch L's screen (three buffer sets,
+// even and odd launches on two streams); the host reads a
 // launch's slot count (pinned) to reserve candidate room before queueing its screen, so the
 // candidate buffer can never overflow (a screen adds at most 32 per slot).
 int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
@@ -4490,9 +4494,15 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const Coding &L = *c.L, &R = *c.R;
   const int8_t *slp = c.slp, *srp = c.srp;
   const int tri = c.tri;
+  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least eight launches down to 512 rows (a rank's
+  // part of a multi-GPU split keeps the prefilter-ahead pipeline filled); GMAT_LRC_ROWS forces it for
+  // A/B runs (a multiple of 128, at most 4096)
+  const int64_t RL = getenv("GMAT_LRC_ROWS")
+                         ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
+                         : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / 8 / 128 * 128));
   double pairs_tested = 0;
-  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested);
-  const int64_t nJ = cdiv(m, BJ), RL = ROWS_PER_LAUNCH;
+  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL);
+  const int64_t nJ = cdiv(m, BJ);
   const int64_t max_slots = RL * cdiv(m, 32) + LC_SLOTS;
   auto &B = e->lrc;
   constexpr int NBUF = 3;  // buffer sets: launch L uses set L % 3
