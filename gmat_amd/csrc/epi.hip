@@ -4306,23 +4306,24 @@ struct RefineTally {
   double t_ref = 0, n_cand = 0, n_refined = 0;  // seconds on the refine stream, candidates, refined pairs
 };
 
-// The flush of a screened scan, on stream st: the pair screen (use_ps) of candidates [ps_done, count)
-// (those below ps_done were pair-screened beside the launches), the exact fp64 refine of the
-// survivors, and the hits p < p_cut appended to the plan's lists.  The candidate buffer is free
-// afterwards.
-int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, int64_t count, int64_t ps_done,
+// The flush of a screened scan, on stream st, of candidates [lo, hi): the pair screen (use_ps) of
+// [ps_done, hi) (those in [lo, ps_done) were pair-screened into cand2 beside the launches), the exact
+// fp64 refine of the survivors, and the hits p < p_cut appended to the plan's lists.  Candidates
+// below hi are free afterwards.
+int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, int64_t lo, int64_t hi, int64_t ps_done,
                    double chi_cut, double p_cut, hipEvent_t beg, hipEvent_t end, RefineTally *tl) {
-  if (count <= 0) return GMAT_OK;
-  const int64_t *fi = e->cand_i.as<int64_t>(), *fj = e->cand_j.as<int64_t>();
-  int64_t nf = count;
+  if (hi <= lo) return GMAT_OK;
+  ps_done = std::max(ps_done, lo);
+  const int64_t *fi = e->cand_i.as<int64_t>() + lo, *fj = e->cand_j.as<int64_t>() + lo;
+  int64_t nf = hi - lo;
   GMAT_HIP(hipEventRecord(beg, st));
   if (use_ps) {
-    GMAT_TRY(pair_screen(e, st, *c.L, *c.R, c.slp, c.srp, fi + ps_done, fj + ps_done, count - ps_done, chi_cut, &nf,
-                         ps_done == 0));
+    GMAT_TRY(pair_screen(e, st, *c.L, *c.R, c.slp, c.srp, e->cand_i.as<int64_t>() + ps_done,
+                         e->cand_j.as<int64_t>() + ps_done, hi - ps_done, chi_cut, &nf, ps_done == lo));
     fi = e->cand2_i.as<int64_t>();
     fj = e->cand2_j.as<int64_t>();
   }
-  tl->n_cand += (double)count;
+  tl->n_cand += (double)(hi - lo);
   tl->n_refined += (double)nf;
   Pinned &pin = e->pins.res;
   if (nf > 0) {
@@ -4535,6 +4536,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // the prefilter as a persistent grid over each launch's tile list (GMAT_PF_NOLIST: one workgroup
   // per tile, as the per-tile phase stamps need)
   const bool pf_list = !getenv("GMAT_PF_NOLIST") && !getenv("GMAT_PF_STAMPS");
+  // (A/B: 23.8 against 24.2 ms per configs[2] step for the column-tile-major list, GMAT_PF_COLORDER)
+  const bool pf_blocked_order = !getenv("GMAT_PF_COLORDER");
   // GMAT_PF_WG caps the persistent grid (tests: many tiles per workgroup at small cohorts)
   const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : 0;
   if (!e->n_cu) {
@@ -4660,11 +4663,25 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       // individuals = 16 n_pad fp4-equivalent ops
       int *tl = e->pins.tl[b].as<int>();
       int run = 0;
-      for (int64_t ct = 0; ct < cdiv(ncols, PF_TC); ++ct)
-        for (int rt = 0; rt < x.n_rt; ++rt) {
-          const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_TC;
-          if (c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR])) tl[run++] = rt + x.n_rt * (int)ct;
-        }
+      const int64_t n_ct = cdiv(ncols, PF_TC);
+      auto runs = [&](int rt, int64_t ct) {
+        const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_TC;
+        return c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR]);
+      };
+      if (pf_blocked_order) {
+        // blocks of 4 row tiles x 8 column tiles (the 32 workgroups of an XCD run one block at a time:
+        // 4 row and 8 column panels per stage instead of 32 + 1), blocks of a row group consecutive
+        // (its rows stay in L2 while the columns stream), row groups dealt to the XCDs in eighths
+        for (int rg = 0; rg < x.n_rt; rg += 4)
+          for (int64_t cg = 0; cg < n_ct; cg += 8)
+            for (int64_t ct = cg; ct < std::min(n_ct, cg + 8); ++ct)
+              for (int rt = rg; rt < std::min(x.n_rt, rg + 4); ++rt)
+                if (runs(rt, ct)) tl[run++] = rt + x.n_rt * (int)ct;
+      } else {
+        for (int64_t ct = 0; ct < n_ct; ++ct)
+          for (int rt = 0; rt < x.n_rt; ++rt)
+            if (runs(rt, ct)) tl[run++] = rt + x.n_rt * (int)ct;
+      }
       pf_ops_of[li] = (double)run * PF_TR * PF_TC * 16.0 * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
       if (pf_list) {
@@ -4708,11 +4725,13 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // (Refining each pair-screen chunk's survivors beside the later launches instead of all of them at
   // flush time was measured slower: 32.7 vs 28.4 ms per configs[2] step -- refine workgroups hold
   // CUs that the whole-CU prefilter workgroups then wait for.)
-  // pair screen of what is left, refine of candidates [0, count), hits collected
+  // pair screen of what is left, refine of candidates [0, count), hits collected.  (Refining what
+  // the earlier launches left beside the last launch's screen, so that the refine does not run alone
+  // at the end, was measured slower too: 24.4 vs 22.7 ms per configs[2] step on one box.)
   auto flush = [&](int64_t count) -> int {
     const int64_t done = ps_done;
     ps_done = 0;
-    return refine_collect(e, c, S3, use_ps, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
+    return refine_collect(e, c, S3, use_ps, 0, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
   };
   auto read_count = [&](int b) -> int64_t { return (int64_t)*e->pins.cnt[b].as<unsigned long long>(); };
   ScreenArgs sa;
@@ -4977,7 +4996,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   auto flush = [&](int64_t count) -> int {
     const int64_t done = ps_done;
     ps_done = 0;
-    return refine_collect(e, c, S3, use_ps, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
+    return refine_collect(e, c, S3, use_ps, 0, count, done, chi_cut, p_cut, ref_beg, ref_end, &tally);
   };
 
   // the int8 screen's (row offset, J) tile list of a launch, built when a level >= 1 needs it

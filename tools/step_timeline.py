@@ -1,6 +1,7 @@
 """Kernel time of the last timed scan step from a rocprofv3 --kernel-trace CSV: the window from the
-first of the last 98 prefilter passes to the last refine, its busy union and per-kernel totals, and
-the time in which each kernel ran alone.   python tools/step_timeline.py run_kernel_trace.csv [launches]"""
+first prefilter pass after the previous step's refine (or the first of the last `launches` passes,
+when given) to the last refine, its busy union and per-kernel totals, and the time in which each
+kernel ran alone.   python tools/step_timeline.py run_kernel_trace.csv [launches]"""
 import csv
 import re
 import sys
@@ -13,11 +14,14 @@ def short(name):
 
 def main():
     path = sys.argv[1]
-    nl = int(sys.argv[2]) if len(sys.argv) > 2 else 98
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in csv.DictReader(open(path)))
-    pf = [k for k, e in enumerate(ev) if e[2].startswith("prefilter_pass")][-nl:]
     rf = [k for k, e in enumerate(ev) if e[2].startswith("refine_kernel")]
+    pf = [k for k, e in enumerate(ev) if e[2].startswith("prefilter_pass")]
+    if len(sys.argv) > 2:
+        pf = pf[-int(sys.argv[2]):]
+    elif len(rf) >= 2:  # the last step: the passes after the previous step's refine
+        pf = [k for k in pf if ev[k][0] >= ev[rf[-2]][1]]
     lo, hi = ev[pf[0]][0], max(ev[rf[-1]][1], ev[pf[-1]][1])
     win = [(max(s, lo), min(e, hi), n) for s, e, n in ev if e > lo and s < hi]
     pts = sorted({t for s, e, _ in win for t in (s, e)})
