@@ -4478,7 +4478,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
 
 // ---- the compacted low-rank scan (default level for p_cut <= 1e-4 when the plan has the low-rank
 // certificate): per launch of 4,096 first SNPs (two folded 2,048-row chunks, equal work; fewer rows
-// when the scan would have fewer than four launches)
+// when the scan would have fewer than eight launches)
 //   S2: prefilter (live-pair masks, E3 slices and code products of live blocks) -> slot lists (lc_*)
 //   sm: compacted low-rank screen of the launch's slots (candidates appended to cand)
 //   S3: pair screen of the candidates in chunks beside the later launches, the exact refine at flush
@@ -4495,15 +4495,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const Coding &L = *c.L, &R = *c.R;
   const int8_t *slp = c.slp, *srp = c.srp;
   const int tri = c.tri;
-  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least four launches down to 512 rows (a rank's
-  // part of a multi-GPU split keeps the prefilter-ahead pipeline filled; an eighth of the configs[2]
-  // triangle: 3.8 ms with four launches, 4.0 with eight); GMAT_LRC_ROWS forces it for A/B runs (a
-  // multiple of 128, at most 4096)
-  constexpr int64_t lrc_min_launches = 4;
+  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least eight launches down to 512 rows (a rank's
+  // part of a multi-GPU split keeps the prefilter-ahead pipeline filled); GMAT_LRC_ROWS forces it for
+  // A/B runs (a multiple of 128, at most 4096)
   const int64_t RL = getenv("GMAT_LRC_ROWS")
                          ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
-                         : std::min<int64_t>(LRC_ROWS_PER_LAUNCH,
-                                             std::max<int64_t>(512, n_rows / lrc_min_launches / 128 * 128));
+                         : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / 8 / 128 * 128));
   double pairs_tested = 0;
   const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL);
   const int64_t nJ = cdiv(m, BJ);
