@@ -239,25 +239,34 @@ def reml_bench(k, seed):
             "flop_convention": "n^3/3 potrf + 2n^3/3 inverse + 2n^2(2c+1) per iteration"}
 
 
-def e2e_bench(geno, ka, y, var, p_cut, hits_step):
+def e2e_bench(geno, ka, y, var, p_cut, hits_step, reps=3):
     """User-facing remma_epiAA end to end (SURVEY.md 8(b) signature): .bed/.bim/.fam/pheno on
     disk -> design matrix -> P, Py on the device -> genotype decode -> plan (certificates)
-    -> exhaustive scan -> hits file.  Same cohort and hits as the timed step."""
+    -> exhaustive scan -> hits file.  Same cohort and hits as the timed step.  `reps` calls, the
+    median wall time and the median of each phase (remma._scan.LAST_PHASES)."""
     import tempfile
     from gmat_amd import synth
     from gmat_amd.remma import remma_epiAA
+    from gmat_amd.remma import _scan
     n = geno.shape[1]
+    walls, phases = [], []
     with tempfile.TemporaryDirectory() as d:
         prefix = os.path.join(d, "c")
         synth.write_plink(prefix, geno)
         synth.write_pheno(prefix + ".pheno", [("F%d" % (i // 10), "I%d" % i) for i in range(n)], y)
-        t0 = time.perf_counter()
-        remma_epiAA(prefix + ".pheno", prefix, [ka, ka * ka], var, p_cut=p_cut, out_file=prefix + ".epiAA")
-        wall = time.perf_counter() - t0
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            remma_epiAA(prefix + ".pheno", prefix, [ka, ka * ka], var, p_cut=p_cut, out_file=prefix + ".epiAA")
+            walls.append(time.perf_counter() - t0)
+            ph = dict(_scan.LAST_PHASES)
+            ph["design_and_other"] = walls[-1] - sum(ph.values())
+            phases.append(ph)
         with open(prefix + ".epiAA") as f:
             n_hits = sum(1 for _ in f) - 1
-    return {"wall_s": wall, "hits": n_hits, "hits_match_step": bool(n_hits == hits_step),
-            "what": "remma_epiAA(pheno, bed, [A, AxA], var, p_cut) from files to the hits file"}
+    return {"wall_s": float(np.median(walls)), "wall_s_all": walls, "hits": n_hits,
+            "hits_match_step": bool(n_hits == hits_step),
+            "phases_s_median": {k: float(np.median([p[k] for p in phases])) for k in phases[0]},
+            "what": "remma_epiAA(pheno, bed, [A, AxA], var, p_cut) from files to the hits file, median of %d" % reps}
 
 
 def covariate_bench(g, ka, y0, n, m, p_cut, seed, steps, ms_intercept):
@@ -393,12 +402,16 @@ def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), rep
     return out
 
 
-def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
-    """BASELINE configs[4]: synthetic related 5,000 x 100,000 cohort, 5-GRM model [A, D, AxA, AxD, DxD]:
-    GRMs (agmat / dgmat_as products), weighted EM-AI
-    REML (uvlmm_varcom.py:41-99, up to reml_iters iterations or convergence), P / Py, then the
-    exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included) scans at p_cut, rows
-    sharded over the ranks like configs[3] (GRM and REML on rank 0).  Returns the record on rank 0."""
+def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=5, reps=3):
+    """BASELINE configs[4]: synthetic related 5,000 x 100,000 cohort (the last generation in full-sib
+    families of `family_size`, so that D, AxD and DxD differ from A, AxA and I and the 5-GRM model is
+    identifiable -- SURVEY.md 7.3 item 4), 5-GRM model [A, D, AxA, AxD, DxD]: GRMs (agmat / dgmat_as
+    products), weighted EM-AI REML (uvlmm_varcom.py:41-99, up to reml_iters iterations or
+    convergence), P / Py from the REML ESTIMATE (as remma_epiAD / remma_epiDD get var_com from
+    wemai_multi_gmat in the reference workflow), then the exhaustive epiDD (j > i) and epiAD (every
+    ordered pair, i == j included) scans at p_cut, rows sharded over the ranks like configs[3] (GRM
+    and REML on rank 0).  Each scan: one untimed full scan (codings and buffers at the timed size),
+    then `reps` timed scans, median reported.  Returns the record on rank 0."""
     import ctypes
     from gmat_amd import dist, synth
     from gmat_amd import _native as N
@@ -409,16 +422,17 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
     nb = (n + 3) // 4
     t0 = time.time()
     lo, hi = dist.snp_shard(m, rank, ws)
-    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed)
+    shard, n_bad = synth.simulate_genotype_shard(n, m, lo, hi, seed=seed, family_size=family_size)
     if dist.allreduce_sum(n_bad) > 0:
-        shard = synth.simulate_genotypes(n, m, seed=seed)[lo:hi]
+        shard = synth.simulate_genotypes(n, m, seed=seed, family_size=family_size)[lo:hi]
     local = np.frombuffer(synth.pack_bed(shard)[3:], dtype=np.uint8).reshape(hi - lo, nb)
     del shard
     g = Geno(body=dist.allgather_packed(local, m, nb), n_id=n, n_snp=m)
     t_cohort = time.time() - t0
     log("cfg5 cohort %d x %d in %.1f s" % (n, m, t_cohort))
     var = np.array([0.3, 0.1, 0.1, 0.05, 0.05, 0.4])
-    out = {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP, p_cut=%g" % (n, m, p_cut),
+    out = {"workload": "configs[4]: 5-GRM REML + exhaustive epiDD / epiAD, %d ind x %d SNP (full-sib families of %d), "
+                       "p_cut=%g" % (n, m, family_size, p_cut),
            "n_gpus": ws,
            "parallelism": "scan rows folded over %d rank(s), backend %s; GRM and REML on rank 0" % (ws, backend or "single"),
            "cohort_s": t_cohort}
@@ -451,9 +465,12 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
                        "ms_per_iter": st[2] * 1e3, "wall_s": time.perf_counter() - t1,
                        "fp64_tflops": st[3] / st[2] / 1e12 if st[2] else None,
                        "frac": st[3] / st[2] / 1e12 / FP64_PEAK_TFLOPS if st[2] else None,
-                       "var": [float(v) for v in est], "simulated": var.tolist()}
+                       "var": [float(v) for v in est], "simulated": var.tolist(),
+                       "scans_use": "the REML estimate (var)"}
         out["grm"] = grm
-        pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), gl, var)
+        t1 = time.perf_counter()
+        pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), gl, np.asarray(est, dtype=float))
+        out["projection_s"] = time.perf_counter() - t1
     pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
     py = dist.broadcast_array(py, 0, shape=(n,))
     t1 = time.perf_counter()
@@ -464,17 +481,22 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend):
     total = t_all = 0.0
     for kind in ("DD", "AD"):
         rows = dist.rank_rows(kind, m, rank, ws)
-        plan.scan(kind, rows[:8], p_cut)  # builds the coding (side vectors) outside the timing
-        lib.gmat_device_synchronize()
-        dist.barrier()
         t1 = time.perf_counter()
-        res = plan.scan(kind, rows, p_cut)
+        plan.scan(kind, rows, p_cut)  # codings (side vectors) and scan buffers at the timed size, untimed
         lib.gmat_device_synchronize()
-        dist.barrier()
-        dt = dist.allreduce_max(time.perf_counter() - t1)
+        t_first = time.perf_counter() - t1
+        times = []
+        for _ in range(reps):
+            dist.barrier()
+            t1 = time.perf_counter()
+            res = plan.scan(kind, rows, p_cut)
+            lib.gmat_device_synchronize()
+            dist.barrier()
+            times.append(dist.allreduce_max(time.perf_counter() - t1))
+        dt = float(np.median(times))
         pairs = float(m) * (m - 1) / 2 if kind == "DD" else float(m) * m
         st = plan.stats()
-        out["epi" + kind] = {"pairs": pairs, "s": dt, "pairs_per_s": pairs / dt,
+        out["epi" + kind] = {"pairs": pairs, "s": dt, "s_all": times, "first_scan_s": t_first, "pairs_per_s": pairs / dt,
                              "hits": int(dist.allreduce_sum(res[0].size)),
                              "candidates": int(dist.allreduce_sum(st["candidates"])), "screen_level": int(st["n_slice"])}
         total += pairs
@@ -499,6 +521,22 @@ def cfg5_main(args):
                                                    "parallelism": rec["parallelism"]}}
         out.update({k: v for k, v in rec.items() if k not in ("workload", "parallelism")})
         print(json.dumps(out), flush=True)
+
+
+def dry_run(args):
+    """Every rank initialises the process group (the backend bench.py would use), the ranks
+    all-reduce their rank numbers, and rank 0 prints one JSON line."""
+    from gmat_amd import dist
+    backend = dist.init()
+    rank, ws, local = dist.world()
+    total = dist.allreduce_sum(rank)
+    mx = dist.allreduce_max(rank)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": ws, "backend": backend, "rank_sum": total, "rank_max": mx,
+                          "launcher": os.environ.get("GMAT_LAUNCHER", "external" if ws > 1 else "none")}), flush=True)
+    if total != ws * (ws - 1) / 2 or mx != ws - 1:
+        sys.exit(4)
 
 
 def main():
@@ -526,7 +564,19 @@ def main():
     ap.add_argument("--no-cfg5", action="store_true", help="skip the configs[4] leg of the default line")
     ap.add_argument("--covariates", action="store_true",
                     help="profiling: the timed step uses the covariate design of the covariates leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group check only: every rank joins the group, exchanges its rank and "
+                         "exits (no GPU work)")
     args = ap.parse_args()
+    # --gpus N without a launcher: start N ranks of this script now, before anything in this process
+    # touches the GPU (gmat_amd.launch), and exit with their status; a WORLD_SIZE that contradicts
+    # --gpus is an error
+    from gmat_amd import launch
+    rc = launch.main_or_spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_run:
+        return dry_run(args)
     if args.config == "cfg5":
         if args.n_id == 2000:
             args.n_id = 5000

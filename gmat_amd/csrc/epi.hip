@@ -116,7 +116,17 @@ struct ScreenArgs {
   unsigned long long *pf_stamp;    // diagnostics (GMAT_PF_STAMPS): 4 s_memrealtime stamps per workgroup, or null
   uint32_t *lmask;  // compacted low-rank path: per (band row, 32-column block) the prefilter's live
                     // pairs as a bit mask (bit c = column 32 J + c), or null
+  // compacted low-rank path: the live pairs' test operands as OPS_REC-int records {E3 slice 0, E3
+  // slice 1, Sab, Sa2b, Sab2, Sa2b2, j, 0} appended at ops (a wave reserves its records with one
+  // atomic on ops_count; nothing is stored past ops_cap: the host sees the count, grows the buffer
+  // and reruns the launch); lbase[(band row, block)] = the index of a live block's first record (its
+  // pairs' records are consecutive, ascending j)
+  int *ops;
+  unsigned *ops_count;
+  int64_t ops_cap;
+  uint32_t *lbase;
 };
+constexpr int OPS_REC = 8;  // ints per live-pair record (32 bytes: two 16-byte stores / loads)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
   const uint64_t b = (uint64_t)base;
@@ -345,7 +355,9 @@ __device__ __forceinline__ v4i i8x2_of_fp4_eo(unsigned x0, unsigned x1) {
 __device__ __forceinline__ void lds_dma16_m0(const void *g, unsigned m0) {
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "{m0}"(m0) : "memory");
 }
-template <bool LIST>
+// COMPACT: the compacted low-rank path's output (live masks + one record per live pair at a.ops); else
+// the block-granular path's (flags + E3 and code products of every pair of a live block, dense)
+template <bool LIST, bool COMPACT>
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const ScreenArgs &a = x.a;
   // The workgroup's tiles.  With a tile list (the launch's running tiles), XCD x (workgroup b runs on
@@ -610,26 +622,65 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
         n_live += (unsigned)__popcll(bal);
         const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
         mine[q] = te == e ? (th ? w1 : w0) : mine[q];
-        // a live block (its row r < n_rows: some lane of the half passed rok) whose column this lane holds
-        st_bits |= ((((h ? w1 : w0) != 0u) & cok[q]) ? 1u : 0u) << (2 * e + q);
+        // COMPACT: this lane's pair is live; else: a live block (its row r < n_rows: some lane of the half
+        // passed rok) whose column this lane holds
+        st_bits |= ((COMPACT ? lv : (((h ? w1 : w0) != 0u) & cok[q])) ? 1u : 0u) << (2 * e + q);
       }
     }
     pstamp(4);
-    // a live block's E3 (and code products) for the low-rank / pair screens (cok: j in range; a
-    // monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+    if (COMPACT) {
+      // one record per live pair: the wave reserves its n_live records with one atomic, then each
+      // (row pair, block) ballot places its pairs in lane order (h = 0 row first, ascending columns)
+      unsigned base = 0u;
+      if (n_live) {
+        if (lane == 0) base = atomicAdd(a.ops_count, n_live);
+        base = __builtin_amdgcn_readfirstlane(base);
+      }
+      const bool fits = (int64_t)base + n_live <= a.ops_cap;
+      unsigned run = base;
+      int *const ops = a.ops;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kr = (e & 3) + 8 * (e >> 2);
+      for (int e = 0; e < 16; ++e) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if ((st_bits >> (2 * e + q)) & 1u) {
-          const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
-#pragma unroll
-          for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e] >> 1;  // exact
-          if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
-#pragma unroll
-            for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
+        for (int q = 0; q < 2; ++q) {
+          const bool lv = (st_bits >> (2 * e + q)) & 1u;
+          const unsigned long long bal = __ballot(lv);
+          if (bal) {
+            // the first record of each live (row, block) of the ballot: lane 2 e + th writes row th's
+            const unsigned word = th ? (unsigned)(bal >> 32) : (unsigned)bal;
+            const int trr = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * th;
+            const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
+            if (te == e && lane < 32 && word && trr < a.n_rows && J < a.nJ)
+              a.lbase[(int64_t)trr * a.nJ + J] = run + (th ? (unsigned)__popc((unsigned)bal) : 0u);
+            if (lv && fits) {
+              const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+              v4i r0v = {acc[q][0][e] >> 1, acc[q][1][e] >> 1, (int)acc4[q][0][e], (int)acc4[q][1][e]};  // exact
+              v4i r1v = {(int)acc4[q][2][e], (int)acc4[q][3][e], jq[q], 0};
+              *(v4i *)(ops + (int64_t)k * OPS_REC) = r0v;
+              *(v4i *)(ops + (int64_t)k * OPS_REC + 4) = r1v;
+            }
+            run += (unsigned)__popcll(bal);
+          }
         }
+      }
+    } else {
+      // a live block's E3 (and code products) for the low-rank / pair screens (cok: j in range; a
+      // monomorphic j is never live).  Wave-uniform base + 32-bit lane offset.
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if ((st_bits >> (2 * e + q)) & 1u) {
+            const int64_t ou = (int64_t)kr * a.ld_e + 32 * q;
+#pragma unroll
+            for (int t = 0; t < E3_PF; ++t) (b13 + t * a.c13_stride + ou)[voff] = acc[q][t][e] >> 1;  // exact
+            if (a.pf_store)  // the low-rank screen's |e|^2 and 1'e come from these code products
+#pragma unroll
+              for (int p = 0; p < 4; ++p) (bpf + p * a.pfc_stride + ou)[voff] = (int)acc4[q][p][e];
+          }
+      }
     }
     pstamp(5);
     const int tr = r0 + 32 * wr + (te & 3) + 8 * (te >> 2) + 4 * th;
@@ -804,6 +855,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
 #pragma unroll
   for (int k = 0; k < NC; ++k) cub[k] = 0.0;
+  unsigned own = 0u, n_live = 0u;  // compacted path: this lane's live elements, the wave's live pairs
   bool cmono = true;
   if (jok) {
     cbe = a.beta[j];
@@ -857,7 +909,10 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
       if (a.lmask) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
     }
-    if (blk && rok && jok) {
+    if (a.ops) {  // compacted path: records below
+      own |= (live ? 1u : 0u) << e;
+      n_live += (unsigned)__popcll(bal);
+    } else if (blk && rok && jok) {
       const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
       for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
@@ -866,6 +921,34 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
         for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[p][e];
     }
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if (a.ops) {  // one record per live pair, placed as in prefilter_pass_kernel (one atomic per wave)
+    unsigned base = 0u;
+    if (n_live) {
+      if (lane == 0) base = atomicAdd(a.ops_count, n_live);
+      base = __builtin_amdgcn_readfirstlane(base);
+    }
+    const bool fits = (int64_t)base + n_live <= a.ops_cap;
+    unsigned run = base;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const bool lv = (own >> e) & 1u;
+      const unsigned long long bal = __ballot(lv);
+      const unsigned lo = (unsigned)bal, word = h ? (unsigned)(bal >> 32) : lo;
+      if (word && c == 0 && r < a.n_rows && J < a.nJ)
+        a.lbase[(int64_t)r * a.nJ + J] = run + (h ? (unsigned)__popc(lo) : 0u);
+      if (bal) {
+        if (lv && fits) {
+          const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo(lo, 0u));
+          const v4i r0v = {acc[0][e], acc[1][e], (int)acc4[0][e], (int)acc4[1][e]};
+          const v4i r1v = {(int)acc4[2][e], (int)acc4[3][e], (int)j, 0};
+          *(v4i *)(a.ops + (int64_t)k * OPS_REC) = r0v;
+          *(v4i *)(a.ops + (int64_t)k * OPS_REC + 4) = r1v;
+        }
+        run += (unsigned)__popcll(bal);
+      }
+    }
   }
 }
 
@@ -1715,6 +1798,7 @@ struct LrcArgs {
   const uint8_t *nib_i, *nib_j;
   int nK, nC, R;
   const int *slot_row, *slot_j;  // slot lists of the launch
+  const int *slot_ops;           // the slot pairs' records (OPS_REC ints each, lc_fill)
   const float *G, *H;            // [m][R]: left G' = Q'a - alpha Q'1, right H = Q'b
   const double *recL, *recR;     // per-SNP test records (LR_REC doubles each)
   double lam, tau, eps, E;
@@ -1722,14 +1806,13 @@ struct LrcArgs {
 constexpr int LRC_NSL = 3, LRC_JB = 64;          // ring slots; j-side bytes per column and stage (S1 plane)
 constexpr int LRC_SJ = MX_BI * 32 * LRC_JB;      // j-side bytes per stage (32 KB)
 
-__device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, int ri, int64_t i, int64_t j,
+// slot pair p's record (lc_fill: the prefilter's E3 slices and code products of the pair)
+__device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, int64_t p, int64_t i, int64_t j,
                                          double lowrank) {
-  const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e;
-  double c3 = 0.0;
-#pragma unroll
-  for (int t = SIDE_T - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (t < a.e3_t ? (double)a.c13[t * a.c13_stride + o3] : 0.0);
-  const double sab = (double)a.pfc[o1], sa2b = (double)a.pfc[a.pfc_stride + o1],
-               sab2 = (double)a.pfc[2 * a.pfc_stride + o1], sa2b2 = (double)a.pfc[3 * a.pfc_stride + o1];
+  static_assert(E3_PF == 2, "record layout");
+  const v4i r0v = *(const v4i *)(x.slot_ops + p * OPS_REC), r1v = *(const v4i *)(x.slot_ops + p * OPS_REC + 4);
+  const double c3 = (double)r0v[0] + (double)r0v[1] * (1.0 / 128.0);
+  const double sab = (double)r0v[2], sa2b = (double)r0v[3], sab2 = (double)r1v[0], sa2b2 = (double)r1v[1];
   const double *rl = x.recL + i * LR_REC, *rr = x.recR + j * LR_REC;
   const double al = rl[0], ca = rl[1], ca2 = rl[2], sl3 = rl[3], sai = rl[4];
   const double be = rr[0], cb = rr[1], cb2 = rr[2], sbj = rr[3];
@@ -1898,7 +1981,7 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
   const double tot = (h ? lowrank[1] : lowrank[0]) + __shfl_xor(h ? lowrank[0] : lowrank[1], 32);
   const int ri = h ? rr1 : rr0;
   const int64_t i = h ? i1 : i0, j = h ? jc[1] : jc[0];
-  if (ri >= 0 && j >= 0) lrc_test(a, x, ri, i, j, tot);
+  if (ri >= 0 && j >= 0) lrc_test(a, x, (int64_t)(sbase + PB * w + h) * 32 + c, i, j, tot);
 }
 
 // Left / right test records of a coding (lr_screen_kernel's per-SNP test operands in one 64-byte
@@ -2925,7 +3008,8 @@ __global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint32_t *__restri
 // one workgroup: exclusive scan of the rows' slot counts (soff), info = {slots, tiles}, the padding
 // slots of the last tile
 __global__ __launch_bounds__(1024) void lc_scan_kernel(const int *__restrict__ cnt, int Rn, int *__restrict__ soff,
-                                                       int *__restrict__ info, int *__restrict__ slot_row) {
+                                                       int *__restrict__ info, int *__restrict__ slot_row,
+                                                       int64_t slot_cap) {
   __shared__ int part[1024];
   const int t = threadIdx.x, per = (Rn + 1023) / 1024, r0 = t * per, r1 = min(Rn, r0 + per);
   int sum = 0;
@@ -2947,14 +3031,18 @@ __global__ __launch_bounds__(1024) void lc_scan_kernel(const int *__restrict__ c
     const int slots = part[1023], tiles = (slots + LC_SLOTS - 1) / LC_SLOTS;
     info[0] = slots;
     info[1] = tiles;
-    for (int q = slots; q < tiles * LC_SLOTS; ++q) slot_row[q] = -1;
+    for (int q = slots; q < tiles * LC_SLOTS && q < slot_cap; ++q) slot_row[q] = -1;
   }
 }
 // lc_fill: band row r's live second SNPs in ascending order into its slots (one workgroup per row;
-// each thread takes a contiguous range of column blocks, a block-wide scan places its pairs)
+// each thread takes a contiguous range of column blocks, a block-wide scan places its pairs), and
+// each live pair's record (the prefilter's, at lbase of its block + its rank in the block) copied to
+// its slot position in slot_ops
 __global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restrict__ lmask, int nJ,
                                                        const int *__restrict__ cnt, const int *__restrict__ soff,
-                                                       int *__restrict__ slot_row, int *__restrict__ slot_j) {
+                                                       int *__restrict__ slot_row, int *__restrict__ slot_j,
+                                                       const uint32_t *__restrict__ lbase, const int *__restrict__ ops,
+                                                       int64_t ops_cap, int *__restrict__ slot_ops, int64_t slot_cap) {
   __shared__ int part[LC_T];
   const int r = blockIdx.x, tid = threadIdx.x;
   const int per = (nJ + LC_T - 1) / LC_T, J0 = min(nJ, tid * per), J1 = min(nJ, J0 + per);
@@ -2970,12 +3058,23 @@ __global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restric
     __syncthreads();
   }
   const int base = soff[r] * 32, n_live = cnt[r], n_slots = (n_live + 31) / 32;
+  if ((int64_t)soff[r] + n_slots > slot_cap) return;  // records overflowed: the host reruns the launch
   int k = part[tid] - c;
+  const uint32_t *lb = lbase + (int64_t)r * nJ;
   for (int J = J0; J < J1; ++J) {
     uint32_t w = mk[J];
+    if (!w) continue;
+    uint32_t src = lb[J];
     while (w) {
       const int b = __ffs(w) - 1;
       w &= w - 1;
+      if ((int64_t)src < ops_cap) {  // else the records overflowed: the host reruns the launch
+        const v4i *s4 = (const v4i *)(ops + (int64_t)src * OPS_REC);
+        v4i *d4 = (v4i *)(slot_ops + (int64_t)(base + k) * OPS_REC);
+        d4[0] = s4[0];
+        d4[1] = s4[1];
+      }
+      ++src;
       slot_j[base + k++] = 32 * J + b;
     }
   }
@@ -3088,7 +3187,10 @@ struct gmat_epi {
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
   struct LrcBuffers {  // three sets: the prefilters of launches L + 1 and L + 2 are queued while L screens
-    DBuf drows[3], lmask[3], e13[3], pfc[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3], tlist[3];
+    DBuf drows[3], lmask[3], lbase[3], ops[3], opc[3], slot_ops[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3],
+        tlist[3];
+    int64_t rl = 0, ops_cap = 0, slot_cap = 0;  // the sets' rows per launch, record and slot capacities
+                                                // (grown, never shrunk)
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     if (s1) (void)hipStreamDestroy(s1);
@@ -4495,34 +4597,60 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const Coding &L = *c.L, &R = *c.R;
   const int8_t *slp = c.slp, *srp = c.srp;
   const int tri = c.tri;
-  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least eight launches down to 512 rows (a rank's
-  // part of a multi-GPU split keeps the prefilter-ahead pipeline filled); GMAT_LRC_ROWS forces it for
-  // A/B runs (a multiple of 128, at most 4096)
-  const int64_t RL = getenv("GMAT_LRC_ROWS")
-                         ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
-                         : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / 8 / 128 * 128));
-  double pairs_tested = 0;
-  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL);
   const int64_t nJ = cdiv(m, BJ);
-  const int64_t max_slots = RL * cdiv(m, 32) + LC_SLOTS;
   auto &B = e->lrc;
   constexpr int NBUF = 3;  // buffer sets: launch L uses set L % 3
-  for (int b = 0; b < NBUF; ++b) {
-    GMAT_TRY(B.drows[b].alloc(RL * 8));
-    GMAT_TRY(B.lmask[b].alloc((size_t)RL * nJ * 4));
-    GMAT_TRY(B.e13[b].alloc((size_t)E3_PF * 2 * RL * m * sizeof(int)));
-    GMAT_TRY(B.pfc[b].alloc((size_t)4 * RL * m * sizeof(int)));
-    GMAT_TRY(B.slot_row[b].alloc((size_t)max_slots * sizeof(int)));
-    GMAT_TRY(B.slot_j[b].alloc((size_t)max_slots * 32 * sizeof(int)));
-    GMAT_TRY(B.cnt[b].alloc(RL * sizeof(int)));
-    GMAT_TRY(B.soff[b].alloc(RL * sizeof(int)));
-    GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
-    GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(RL, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
-    GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(RL, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
-    GMAT_TRY(e->pins.rows[b].reserve(RL * 8));
-    GMAT_TRY(e->pins.cnt[b].reserve(8));
-    GMAT_TRY(e->pins.t2[b].reserve(16));
+  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least GMAT_LRC_MIN_LAUNCHES (4) launches down to
+  // 512 rows (a rank's part of a multi-GPU split keeps the prefilter-ahead pipeline filled), and no more
+  // than the three sets' live masks and record bases (8 bytes per (row, 32-column block)) fit in an
+  // eighth of the free HBM; GMAT_LRC_ROWS forces it for A/B runs (a multiple of 128, at most 4096)
+  int64_t RL = 0;
+  {
+    const int64_t min_launches = getenv("GMAT_LRC_MIN_LAUNCHES") ? std::max(1, atoi(getenv("GMAT_LRC_MIN_LAUNCHES"))) : 4;
+    RL = getenv("GMAT_LRC_ROWS")
+             ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
+             : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / min_launches / 128 * 128));
+    if (RL > B.rl) {  // buffers sized for fewer rows than this scan wants: is there room?
+      size_t free_b = 0, total_b = 0;
+      GMAT_HIP(hipMemGetInfo(&free_b, &total_b));
+      const int64_t room = (int64_t)((free_b + (size_t)NBUF * 8 * B.rl * nJ) / 8 / (NBUF * 8 * nJ)) / 128 * 128;
+      RL = std::max<int64_t>(std::max<int64_t>(B.rl, 128), std::min(RL, room));
+    }
   }
+  double pairs_tested = 0;
+  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL);
+  // live-pair records per launch: an initial capacity of 1/128 of a launch's pairs (at least 2^20; the
+  // configs[2] prefilter keeps 1/250), grown (and the launch rerun) when a launch keeps more
+  const int64_t rl_sets = std::max(RL, B.rl);
+  auto alloc_sets = [&](int64_t rl, int64_t cap) -> int {
+    const int64_t max_slots = cap / 32 + rl + 2 * LC_SLOTS;  // a row's last slot may be partial
+    for (int b = 0; b < NBUF; ++b) {
+      GMAT_TRY(B.drows[b].alloc(rl * 8));
+      GMAT_TRY(B.lmask[b].alloc((size_t)rl * nJ * 4));
+      GMAT_TRY(B.lbase[b].alloc((size_t)rl * nJ * 4));
+      GMAT_TRY(B.ops[b].alloc((size_t)cap * OPS_REC * sizeof(int)));
+      GMAT_TRY(B.opc[b].alloc(16));
+      GMAT_TRY(B.slot_ops[b].alloc((size_t)max_slots * 32 * OPS_REC * sizeof(int)));
+      GMAT_TRY(B.slot_row[b].alloc((size_t)max_slots * sizeof(int)));
+      GMAT_TRY(B.slot_j[b].alloc((size_t)max_slots * 32 * sizeof(int)));
+      GMAT_TRY(B.cnt[b].alloc(rl * sizeof(int)));
+      GMAT_TRY(B.soff[b].alloc(rl * sizeof(int)));
+      GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
+      GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(rl, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
+      GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(rl, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
+      GMAT_TRY(e->pins.rows[b].reserve(rl * 8));
+      GMAT_TRY(e->pins.cnt[b].reserve(8));
+      GMAT_TRY(e->pins.t2[b].reserve(32));
+    }
+    B.rl = rl;
+    B.ops_cap = cap;
+    B.slot_cap = max_slots;
+    return GMAT_OK;
+  };
+  // (GMAT_LRC_OPS_CAP: a smaller logical capacity for this scan -- tests of the grow-and-rerun path)
+  GMAT_TRY(alloc_sets(rl_sets, getenv("GMAT_LRC_OPS_CAP")
+                                   ? std::max<int64_t>(32, atoll(getenv("GMAT_LRC_OPS_CAP")))
+                                   : std::max(B.ops_cap, std::min<int64_t>(1 << 23, std::max<int64_t>(1 << 20, RL * m / 128)))));
   const bool use_ps = pair_screen_fits(e) && !getenv("GMAT_NO_PAIR_SCREEN");
   GMAT_TRY(ensure_candidates(e, 1 << 24, use_ps));
   DBuf live_cnt;  // GMAT_LIVE_COUNT: pairs the prefilter keeps (diagnostics, printed at the end)
@@ -4593,6 +4721,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_HIP(hipMemcpyAsync(B.drows[b].p, e->pins.rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
     GMAT_HIP(hipMemsetAsync(B.lmask[b].p, 0, (size_t)Rn * nJ * 4, S2));
+    GMAT_HIP(hipMemsetAsync(B.opc[b].p, 0, 16, S2));
     SideArgs x;
     ScreenArgs &a = x.a;
     std::memset(&a, 0, sizeof(a));
@@ -4603,16 +4732,15 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     a.rows = B.drows[b].as<int64_t>();
     a.n_rows = Rn;
     a.tri = tri;
-    a.c13 = B.e13[b].as<int>();
-    a.c13_stride = (int64_t)2 * Rn * m;
     a.sL3 = L.sL3.as<double>();
     a.csum_l = L.csum.as<double>();
     a.csum_r = R.csum.as<double>();
     a.csq_l = L.csq.as<double>();
     a.csq_r = R.csq.as<double>();
-    a.pf_store = 1;
-    a.pfc = B.pfc[b].as<int>();
-    a.pfc_stride = (int64_t)Rn * m;
+    a.ops = B.ops[b].as<int>();  // one record per live pair (no dense per-pair arrays)
+    a.ops_count = B.opc[b].as<unsigned>();
+    a.ops_cap = B.ops_cap;
+    a.lbase = B.lbase[b].as<uint32_t>();
     a.pf_mu = e->pf_mu;
     a.pf_eps = e->pf_eps;
     a.pf_tau = e->pf_tau;
@@ -4692,11 +4820,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         x.tile_list = B.tlist[b].as<int>();
         x.n_list = run;
         const int g = 8 * (int)std::min<int64_t>(cdiv(pf_wg ? pf_wg : e->n_cu, 8), cdiv(run, 8));
-        if (run > 0) hipLaunchKernelGGL(prefilter_pass_kernel<true>, dim3((unsigned)g), dim3(512), 0, S2, x);
+        if (run > 0) hipLaunchKernelGGL((prefilter_pass_kernel<true, true>), dim3((unsigned)g), dim3(512), 0, S2, x);
       } else {
         if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
-        hipLaunchKernelGGL(prefilter_pass_kernel<false>, dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512), 0,
-                           S2, x);
+        hipLaunchKernelGGL((prefilter_pass_kernel<false, true>), dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512),
+                           0, S2, x);
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
@@ -4714,11 +4842,13 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
                        B.cnt[b].as<int>());
     hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, S2, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
-                       B.info[b].as<int>(), B.slot_row[b].as<int>());
+                       B.info[b].as<int>(), B.slot_row[b].as<int>(), B.slot_cap);
     hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
-                       B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>());
+                       B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>(),
+                       B.lbase[b].as<uint32_t>(), B.ops[b].as<int>(), B.ops_cap, B.slot_ops[b].as<int>(), B.slot_cap);
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].p, B.info[b].p, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
+    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].as<int>() + 4, B.opc[b].p, sizeof(int), hipMemcpyDeviceToHost, S2));
     GMAT_HIP(hipEventRecord(side_end[b], S2));
     return GMAT_OK;
   };
@@ -4771,6 +4901,16 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     const ScanLaunch &ln = plan[li];
     if (li + ahead < plan.size()) GMAT_TRY(enqueue_side(li + ahead, (int)((li + ahead) % NBUF)));
     GMAT_HIP(hipEventSynchronize(side_end[b]));
+    // the prefilter kept more pairs than the record buffers hold: grow them and rerun the launches
+    // whose side passes are queued (none of their records can be trusted; the screens before are done)
+    while ((int64_t)e->pins.t2[b].as<unsigned>()[4] > B.ops_cap) {
+      const int64_t need = (int64_t)e->pins.t2[b].as<unsigned>()[4];
+      GMAT_HIP(hipDeviceSynchronize());
+      GMAT_TRY(alloc_sets(B.rl, std::max<int64_t>(2 * B.ops_cap, need + need / 4)));
+      if (getenv("GMAT_DEBUG")) fprintf(stderr, "live-pair records grown to %lld\n", (long long)B.ops_cap);
+      for (size_t lj = li; lj < std::min(plan.size(), li + ahead + 1); ++lj) GMAT_TRY(enqueue_side(lj, (int)(lj % NBUF)));
+      GMAT_HIP(hipEventSynchronize(side_end[b]));
+    }
     const int *info = e->pins.t2[b].as<int>();
     const int64_t slots = info[0], tiles = info[1];
     float ms_side;
@@ -4797,15 +4937,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     sa.rows = B.drows[b].as<int64_t>();
     sa.n_rows = (int)ln.rows.size();
     sa.j_lo = ln.j_lo;
-    sa.c13 = B.e13[b].as<int>();
-    sa.c13_stride = (int64_t)2 * sa.n_rows * m;
-    sa.pfc = B.pfc[b].as<int>();
-    sa.pfc_stride = (int64_t)sa.n_rows * m;
     sa.cap = e->cand_cap;
     sa.cand_i = e->cand_i.as<int64_t>();
     sa.cand_j = e->cand_j.as<int64_t>();
     lx.slot_row = B.slot_row[b].as<int>();
     lx.slot_j = B.slot_j[b].as<int>();
+    lx.slot_ops = B.slot_ops[b].as<int>();
     GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
     GMAT_HIP(hipEventRecord(scr_beg[b], sm));
     if (tiles > 0) hipLaunchKernelGGL(lrc_screen_kernel, dim3((unsigned)tiles), dim3(512), 0, sm, sa, lx);
@@ -5014,7 +5151,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   };
   // kernel arguments of launch li on buffer set b
   auto make_args = [&](size_t li, int b) -> ScreenArgs {
-    ScreenArgs sa;
+    ScreenArgs sa{};  // value-initialised: unset pointers (lmask, ops, ...) are null
     const ScanLaunch &ln = plan[li];
     const int Rn = (int)ln.rows.size();
     sa.slices = e->slices.as<int8_t>();
@@ -5135,7 +5272,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.cs4 = R.p4b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
-        hipLaunchKernelGGL(prefilter_pass_kernel<false>, dim3(gp), dim3(512), 0, S2, xp);
+        hipLaunchKernelGGL((prefilter_pass_kernel<false, false>), dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
         for (int k = 0; k < e->pf_ncov; ++k) xp.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;

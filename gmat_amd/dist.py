@@ -99,10 +99,11 @@ def _init_rccl(rank, ws):
             pass
 
 
-def choose_backend(explicit=None, gpu_visible=None):
+def choose_backend(explicit=None, gpu_visible=None, n_devices=None, world_size=None):
     """The backend every rank uses: GMAT_DIST_BACKEND / the argument when given, else ``rccl``
-    when a GPU is visible (the product path) and ``gloo`` otherwise (CPU test harness).  The
-    choice depends only on the launch environment, identical on all ranks of a node."""
+    when every rank has a GPU of its own (the product path) and ``gloo`` otherwise (the CPU test
+    harness, or more ranks than GPUs: RCCL refuses two ranks on one device).  The choice depends
+    only on the launch environment, identical on all ranks of a node."""
     if explicit is None:
         explicit = os.environ.get("GMAT_DIST_BACKEND")
     if explicit is not None:
@@ -112,7 +113,12 @@ def choose_backend(explicit=None, gpu_visible=None):
     if gpu_visible is None:
         from . import _native as N
         lib = N.load(required=False)
-        gpu_visible = lib is not None and N.device_count() > 0
+        n_devices = N.device_count() if lib is not None else 0
+        gpu_visible = n_devices > 0
+    if world_size is None:
+        world_size = world()[1]
+    if gpu_visible and n_devices is not None and n_devices < world_size:
+        return "gloo"
     return "rccl" if gpu_visible else "gloo"
 
 

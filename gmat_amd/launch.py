@@ -1,0 +1,112 @@
+"""One process per GPU without an external launcher (bench.py's contract).
+
+``python bench.py --gpus N`` with no WORLD_SIZE in the environment starts N fresh child
+processes of the same script, one per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT set exactly as ``torch.distributed.run`` would set them, and waits for
+them.  The parent never touches the GPU (it imports nothing from the HIP library): the children
+are started before any HIP call in this process, so no GPU state is inherited or exec'd over.
+
+The reference's own multi-process mode is the user-launched ``parallel=[N, k]`` split
+(remma_epiAA.py:109-161): N independent invocations, one per part.  Here the parts are the
+ranks of one job (dist.rank_rows) and their hits are merged on rank 0.
+
+Failure behaviour: if any child exits non-zero, the others are terminated (their exact PIDs)
+and the parent exits with the first failing child's code; a WORLD_SIZE that disagrees with
+``--gpus`` is an error, never a silent single-rank run.
+"""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+
+class LaunchError(RuntimeError):
+    pass
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def resolve(n_gpus, environ=None):
+    """What this process is, given ``--gpus n_gpus``: "spawn" (no launcher: start n_gpus ranks),
+    "single" (one process, no process group) or "rank" (a rank of an n_gpus-process job).
+    Raises LaunchError when an existing WORLD_SIZE contradicts n_gpus."""
+    env = os.environ if environ is None else environ
+    if n_gpus < 1:
+        raise LaunchError("--gpus %d: need at least one GPU" % n_gpus)
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if n_gpus > 1 else "single"
+    ws = int(ws)
+    if ws != n_gpus:
+        raise LaunchError("--gpus %d but WORLD_SIZE=%d (set by the launcher): refusing to run a different number "
+                          "of ranks than asked for" % (n_gpus, ws))
+    return "rank" if ws > 1 else "single"
+
+
+def rank_env(base, rank, world_size, port, addr="127.0.0.1"):
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world_size),
+                "LOCAL_WORLD_SIZE": str(world_size), "GROUP_RANK": "0", "MASTER_ADDR": addr,
+                "MASTER_PORT": str(port), "GMAT_LAUNCHER": "gmat_amd.launch"})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    return env
+
+
+def spawn(argv, n_procs, environ=None, poll_s=0.2, timeout_s=None):
+    """Run ``argv`` (a full command line, e.g. [sys.executable, script, ...]) as ranks 0..n_procs-1
+    of one job and return 0, or the exit code of the first rank that failed (the others are
+    terminated).  stdout / stderr are inherited: rank 0's JSON line reaches the caller's stdout."""
+    base = dict(os.environ if environ is None else environ)
+    port = int(base.get("MASTER_PORT") or free_port())
+    procs = []
+    try:
+        for r in range(n_procs):
+            procs.append(subprocess.Popen(argv, env=rank_env(base, r, n_procs, port)))
+        t0 = time.time()
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print("gmat_amd.launch: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr,
+                      flush=True)
+                return c if c > 0 else 128 - c
+            if all(c == 0 for c in codes):
+                return 0
+            if timeout_s is not None and time.time() - t0 > timeout_s:
+                print("gmat_amd.launch: ranks still running after %.0f s; stopping them" % timeout_s, file=sys.stderr,
+                      flush=True)
+                return 124
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+
+def main_or_spawn(n_gpus, script, argv):
+    """bench.py's entry: returns None when this process should do the work itself (a single
+    process, or a rank started by a launcher), else spawns the ranks and returns their exit
+    code for the caller to exit with."""
+    try:
+        what = resolve(n_gpus)
+    except LaunchError as exc:
+        print("error: %s" % exc, file=sys.stderr, flush=True)
+        return 2
+    if what != "spawn":
+        return None
+    return spawn([sys.executable, script] + list(argv), n_gpus)

@@ -136,14 +136,27 @@ class EpiPlan:
         self.close()
 
 
-def open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file):
+# wall seconds of the phases of the last run_scan call in this process (bench.py's end-to-end leg):
+# projection (V, P, Py), decode (.bed read, checked, decoded on the device), plan (certificates),
+# scan (the device scan, hits on the host), write (the hits file)
+LAST_PHASES = {}
+
+
+def open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file, phases=None):
     """P / Py on the device (remma_epiAA.py:33-49), genotype panel decoded on the device."""
+    phases = {} if phases is None else phases
     logging.info("Calculate the phenotypic covariance matrix and inversion")
+    t0 = time.perf_counter()
     pvp, py = projection(y, xmat, zmat, gmat_lst, var_com)
+    t1 = time.perf_counter()
     geno = Geno(bed_file)
+    t2 = time.perf_counter()
+    phases["projection"], phases["decode"] = t1 - t0, t2 - t1
     if geno.n != pvp.shape[0]:
         raise ValueError("Z has %d individuals, the .fam has %d" % (pvp.shape[0], geno.n))
-    return EpiPlan(geno, pvp, py)
+    plan = EpiPlan(geno, pvp, py)
+    phases["plan"] = time.perf_counter() - t2
+    return plan
 
 
 def format_rows(cols, n_float):
@@ -184,16 +197,20 @@ def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut,
         f.write(SCAN_HEADER + "\n")
     num_snp = count_lines(bed_file + ".bim")
     rows = resolve_rows(kind, num_snp, snp_lst_0)
-    plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file)
+    phases = {}
+    plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file, phases)
     try:
         uniq = np.unique(rows)
         t0 = time.perf_counter()
         hi, hj, eff, var, chi, p = plan.scan(kind, uniq, p_cut)
-        logging.info("Running time: Clock time, {:.5f} sec.".format(time.perf_counter() - t0))
+        phases["scan"] = time.perf_counter() - t0
+        logging.info("Running time: Clock time, {:.5f} sec.".format(phases["scan"]))
         logging.info("scan stats: %s" % plan.stats())
     finally:
+        t0 = time.perf_counter()
         plan.close()
         plan.geno.close()
+        phases["release"] = time.perf_counter() - t0
     if rows.size == uniq.size and np.all(np.diff(rows) > 0):
         order = np.arange(hi.size)
     else:  # replay the caller's row order (and duplicates) like the reference's loop
@@ -201,7 +218,11 @@ def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut,
         ends = np.searchsorted(hi, uniq, side="right")
         pos = np.searchsorted(uniq, rows)
         order = np.concatenate([np.arange(starts[k], ends[k]) for k in pos]) if rows.size else np.zeros(0, int)
+    t0 = time.perf_counter()
     append_rows(out_file, [hi[order], hj[order], eff[order], chi[order], p[order]], 3)
+    phases["write"] = time.perf_counter() - t0
+    LAST_PHASES.clear()
+    LAST_PHASES.update(phases)
     return 0
 
 

@@ -1,0 +1,96 @@
+"""bench.py --gpus N without an external launcher (gmat_amd/launch.py).
+
+CPU: the launch decision, two ranks reaching dist.init() over gloo through bench.py itself,
+failure propagation.  GPU: the real sharded scan through the same launcher (two ranks on the
+box's one GPU exchange over gloo) returns the single-process hit count."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+import time
+
+import pytest
+
+from gmat_amd import launch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _clean_env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR", "GMAT_DIST_BACKEND")}
+    env.update(OMP_NUM_THREADS="1", **kw)
+    return env
+
+
+def test_resolve():
+    assert launch.resolve(1, {}) == "single"
+    assert launch.resolve(4, {}) == "spawn"
+    assert launch.resolve(4, {"WORLD_SIZE": "4"}) == "rank"
+    assert launch.resolve(1, {"WORLD_SIZE": "1"}) == "single"
+    with pytest.raises(launch.LaunchError):
+        launch.resolve(8, {"WORLD_SIZE": "1"})  # driver asked for 8, the launcher made 1: never silent
+    with pytest.raises(launch.LaunchError):
+        launch.resolve(2, {"WORLD_SIZE": "4"})
+    with pytest.raises(launch.LaunchError):
+        launch.resolve(0, {})
+
+
+def test_rank_env():
+    env = launch.rank_env({"X": "1"}, 3, 8, 29511)
+    assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"], env["MASTER_PORT"]) == ("3", "3", "8", "29511")
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["X"] == "1"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_gpus2_reaches_dist_init_on_two_ranks():
+    """python bench.py --gpus 2 (no WORLD_SIZE): two ranks join one gloo group on this CPU box."""
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], env=_clean_env(), cwd=REPO,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 2 and rec["rank_sum"] == 1.0 and rec["backend"] == "gloo"
+    assert rec["launcher"] == "gmat_amd.launch"
+
+
+def test_bench_refuses_mismatched_world_size():
+    env = _clean_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run"], env=env, cwd=REPO,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+def test_failing_rank_stops_the_job(tmp_path):
+    """Rank 1 fails at once, rank 0 would run for a minute: the launcher returns rank 1's code and
+    terminates rank 0."""
+    script = tmp_path / "worker.py"
+    script.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(7)
+        time.sleep(60)
+    """))
+    t0 = time.time()
+    rc = launch.spawn([sys.executable, str(script)], 2, environ=_clean_env())
+    assert rc == 7
+    assert time.time() - t0 < 30
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_sharded_scan_matches_one_rank():
+    """The sharded configs[3] path through bench.py's own launcher on this box: two ranks (one GPU,
+    so the exchanges go over gloo) scan a 2,000 x 6,000 cohort; the merged hit count equals the
+    single-process run's."""
+    small = ["--n-snp", "6000", "--steps", "1", "--warmup", "1", "--no-cpu", "--no-grm", "--no-eff", "--no-e2e",
+             "--no-cov", "--no-split", "--no-cfg5"]
+    res = {}
+    for g in (1, 2):
+        out = subprocess.run([sys.executable, BENCH, "--gpus", str(g)] + small, env=_clean_env(), cwd=REPO,
+                             capture_output=True, text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-3000:]
+        res[g] = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res[2]["n_gpus"] == 2 and res[1]["n_gpus"] == 1
+    assert res[2]["scan"]["hits_per_step"] == res[1]["scan"]["hits_per_step"]
+    assert res[1]["scan"]["hits_per_step"] > 0
