@@ -29,6 +29,7 @@ _PROTOS = {
     "gmat_set_device": (_INT, [_INT]),
     "gmat_device_synchronize": (_INT, []),
     "gmat_reml_stats": (_INT, [_P]),
+    "gmat_reml_trace": (_INT, [_INT, _P, _P, _P, _P]),
     "gmat_epi_setup_stats": (_INT, [_P, _P]),
     "gmat_geno_create": (_INT, [_P, _P, _I64, _I64, _I64]),
     "gmat_geno_counts": (_INT, [_P, _P, _P, _P]),

@@ -241,12 +241,25 @@ double wall_now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 double g_reml_stats[4] = {0, 0, 0, 0};
+// per iteration of the last gmat_reml call: gradient norm, update norm, EM weight
+std::vector<double> g_reml_trace[3];
 
 }  // namespace
 
 extern "C" int gmat_reml_stats(double *out4) {
   GMAT_CHECK(out4, GMAT_E_ARG, "gmat_reml_stats: null");
   for (int k = 0; k < 4; ++k) out4[k] = g_reml_stats[k];
+  return GMAT_OK;
+}
+
+extern "C" int gmat_reml_trace(int cap, double *grad_norm, double *update_norm, double *em_weight, int *count) {
+  GMAT_CHECK(cap >= 0 && count, GMAT_E_ARG, "gmat_reml_trace: bad arguments");
+  const int k = (int)g_reml_trace[0].size();
+  *count = k;
+  double *out[3] = {grad_norm, update_norm, em_weight};
+  for (int t = 0; t < 3; ++t)
+    if (out[t])
+      for (int i = 0; i < std::min(cap, k); ++i) out[t][i] = g_reml_trace[t][i];
   return GMAT_OK;
 }
 
@@ -270,6 +283,7 @@ extern "C" int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat,
     for (int k = 0; k < c1; ++k) var[k] = init[k];
   int it = 0;
   double cc_gra_val = 1000.0, cc_par_val = 1000.0;
+  for (auto &v : g_reml_trace) v.clear();
   while (it < maxiter) {
     ++it;
     GMAT_TRY(md.projection(var.data(), nullptr));
@@ -277,8 +291,9 @@ extern "C" int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat,
     for (int a = 0; a < c1; ++a)
       for (int b = 0; b < c1; ++b) em[a * c1 + b] = (a == b) ? (double)n_rec / (var[a] * var[a]) : 0.0;
     // EM weight grid (uvlmm_varcom.py:82-89): first weight giving all-positive variances
+    double wt = 0.0;
     for (int j = 0; j <= 100; ++j) {
-      const double wt = j * 0.01;
+      wt = j * 0.01;
       for (int e = 0; e < c1 * c1; ++e) wm[e] = (1.0 - wt) * ai[e] + wt * em[e];
       GMAT_CHECK(small_inverse(c1, wm.data(), wi.data(), nullptr), GMAT_E_NOTPD, "singular EM/AI matrix");
       double mn = 1e300;
@@ -300,6 +315,9 @@ extern "C" int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat,
     cc_par_val = std::sqrt(dd / vv);
     var = nv;
     cc_gra_val = std::sqrt(gg);
+    g_reml_trace[0].push_back(cc_gra_val);
+    g_reml_trace[1].push_back(cc_par_val);
+    g_reml_trace[2].push_back(wt);
     if (history)
       for (int a = 0; a < c1; ++a) history[(int64_t)(it - 1) * c1 + a] = var[a];
     if (cc_gra_val < cc_gra && cc_par_val < cc_par) break;

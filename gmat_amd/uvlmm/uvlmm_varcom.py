@@ -45,6 +45,12 @@ def _wemai_multi_gmat(y, xmat, zmat, gmat_lst, init=None, maxiter=200, cc_par=1.
     for k in range(it.value):
         logging.info("Updated variances: " + " ".join(map(str, hist[k])))
     _wemai_multi_gmat.last_history = hist[: it.value].copy()
+    tr = np.zeros((3, max(1, it.value)))
+    cnt = ctypes.c_int(0)
+    N.check(lib.gmat_reml_trace(tr.shape[1], N.ptr(tr[0]), N.ptr(tr[1]), N.ptr(tr[2]), ctypes.byref(cnt)),
+            "gmat_reml_trace")
+    # per iteration: norm of the gradient vector, norm of the update vector, EM weight (uvlmm_varcom.py:90-96)
+    _wemai_multi_gmat.last_trace = tr[:, : it.value].copy()
     return var
 
 

@@ -83,6 +83,11 @@ int gmat_reml(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const doub
  * + 2n^2(2c+1) traces / AI) */
 int gmat_reml_stats(double *out4);
 
+/* per iteration of the last gmat_reml call on this process (the quantities the reference logs,
+ * uvlmm_varcom.py:90-96): norm of the gradient vector, norm of the update vector, and the EM weight
+ * the step used; up to cap values each into the non-NULL arrays, *count = iterations run. */
+int gmat_reml_trace(int cap, double *grad_norm, double *update_norm, double *em_weight, int *count);
+
 /* pvp = Z'PZ (n_id x n_id) and py = Z'Py (n_id) of the scans' setup (remma_epiAA.py:33-49). */
 int gmat_projection(int64_t n_rec, int64_t n_fix, int64_t n_id, int n_gmat, const double *y,
                     const double *xmat, const int64_t *z_col, const double *const *gmat,

@@ -17,12 +17,16 @@ for st in "$@"; do
     quick)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/quick.json 2> $OUT/quick.log || { tail -30 $OUT/quick.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/quick.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
-    cfg5)
-      timeout -k 10 600 python -u bench.py --config cfg5 > $OUT/cfg5.json 2> $OUT/cfg5.log || { tail -30 $OUT/cfg5.log; exit 1; }
-      tail -c 1500 $OUT/cfg5.json ;;
-    prof)
-      cd /tmp && rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $GRAFT_REPO_ROOT/$OUT/prof_bench.json 2> $GRAFT_REPO_ROOT/$OUT/prof.log || { tail -30 $GRAFT_REPO_ROOT/$OUT/prof.log; exit 1; }
-      cd $GRAFT_REPO_ROOT ;;
+    cfg5|cfg5f0|cfg5f2|cfg5f10)
+      FS=5; case $st in cfg5f0) FS=0;; cfg5f2) FS=2;; cfg5f10) FS=10;; esac
+      timeout -k 10 600 python -u bench.py --config cfg5 --family-size $FS --cfg5-reps ${CFG5_REPS:-3} > $OUT/$st.json 2> $OUT/$st.log || { tail -30 $OUT/$st.log; exit 1; }
+      python -c "import json; d=json.load(open('$OUT/$st.json')); r=d['reml']; print('$st', 'value %.3g' % d['value'], 'iters', r['iters'], 'var', [round(v, 4) for v in r['var']], 'grad', r.get('grad_norm_last5'), 'upd', r.get('update_norm_last5'), 'emw', r.get('em_weight_last5'), 'DD cand', d['epiDD']['candidates'], 'AD cand', d['epiAD']['candidates'], 'DD s', d['epiDD']['s'])" ;;
+    prof|serial)
+      # kernel trace + stats of a short scan run and the step timeline of its last step; serial: the
+      # same with kernels serialised (AMD_SERIALIZE_KERNEL=3), so the per-kernel sums are standalone times
+      SER=""; [ $st = serial ] && SER="AMD_SERIALIZE_KERNEL=3"
+      env $SER timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$st -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/${st}_bench.json 2> $OUT/$st.log || { tail -30 $OUT/$st.log; exit 1; }
+      python3 tools/step_timeline.py $(find $OUT/$st -name "*kernel_trace.csv" | head -1) | tee $OUT/${st}_timeline.txt ;;
     *)
       echo "unknown stage $st"; exit 2 ;;
   esac
