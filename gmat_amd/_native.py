@@ -28,6 +28,7 @@ _PROTOS = {
     "gmat_device_count": (_INT, [_P]),
     "gmat_set_device": (_INT, [_INT]),
     "gmat_device_synchronize": (_INT, []),
+    "gmat_empty_cache": (_INT, []),
     "gmat_reml_stats": (_INT, [_P]),
     "gmat_reml_trace": (_INT, [_INT, _P, _P, _P, _P]),
     "gmat_epi_setup_stats": (_INT, [_P, _P]),

@@ -3,6 +3,10 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "common.h"
 
@@ -14,9 +18,95 @@ void set_error(const char *fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+// ---- device memory cache behind DBuf (common.h)
+namespace {
+struct Pool {
+  std::mutex mu;
+  std::multimap<std::pair<int, size_t>, void *> free_blocks;  // (device, bytes) -> block
+  size_t cached = 0;
+  size_t limit() const {  // bytes kept cached at most (GMAT_POOL_MAX_GB, default 64)
+    const char *e = getenv("GMAT_POOL_MAX_GB");
+    return (size_t)((e ? atof(e) : 64.0) * (double)(1ull << 30));
+  }
+  void trim_all() {  // caller holds mu
+    for (auto &kv : free_blocks) (void)hipFree(kv.second);
+    free_blocks.clear();
+    cached = 0;
+  }
+};
+Pool &pool() {
+  static Pool *p = new Pool;  // never destroyed: blocks may be released during static destruction
+  return *p;
+}
+// size classes: 256 B granules below 1 MiB, 2 MiB granules above
+size_t size_class(size_t n) {
+  return n < (1u << 20) ? (n + 255) / 256 * 256 : (n + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+}
+}  // namespace
+
+void *pool_alloc(size_t n, size_t *got) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const size_t c = size_class(n);
+  Pool &pl = pool();
+  {
+    std::lock_guard<std::mutex> lk(pl.mu);
+    // the smallest cached block of this device that fits and wastes at most an eighth
+    auto it = pl.free_blocks.lower_bound({dev, c});
+    if (it != pl.free_blocks.end() && it->first.first == dev && it->first.second <= c + c / 8) {
+      void *p = it->second;
+      *got = it->first.second;
+      pl.cached -= it->first.second;
+      pl.free_blocks.erase(it);
+      return p;
+    }
+  }
+  void *p = nullptr;
+  hipError_t e = hipMalloc(&p, c);
+  if (e != hipSuccess) {  // out of memory: give the cached blocks back and try once more
+    (void)hipGetLastError();
+    {
+      std::lock_guard<std::mutex> lk(pl.mu);
+      (void)hipDeviceSynchronize();
+      pl.trim_all();
+    }
+    e = hipMalloc(&p, c);
+    if (e != hipSuccess) {
+      set_error("hipMalloc(%zu bytes): %s", c, hipGetErrorString(e));
+      return nullptr;
+    }
+  }
+  *got = c;
+  return p;
+}
+
+void pool_free(void *p, size_t bytes) {
+  if (!p) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceSynchronize();  // no kernel still uses the block when it is handed out again
+  Pool &pl = pool();
+  std::lock_guard<std::mutex> lk(pl.mu);
+  if (pl.cached + bytes > pl.limit()) {
+    (void)hipFree(p);
+    return;
+  }
+  pl.free_blocks.insert({{dev, bytes}, p});
+  pl.cached += bytes;
+}
+
 }  // namespace gmat
 
 extern "C" const char *gmat_last_error(void) { return gmat::g_err; }
+
+extern "C" int gmat_empty_cache(void) {
+  gmat::Pool &pl = gmat::pool();
+  std::lock_guard<std::mutex> lk(pl.mu);
+  GMAT_HIP(hipDeviceSynchronize());
+  pl.trim_all();
+  return GMAT_OK;
+}
 
 extern "C" int gmat_version(void) { return 1; }
 

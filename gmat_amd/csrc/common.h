@@ -15,6 +15,14 @@ namespace gmat {
 
 void set_error(const char *fmt, ...);
 
+// Device memory through a process-wide cache (capi.cpp): freed blocks stay reserved per device and
+// size class and are handed out again, so a plan created and destroyed per call (remma_epiAA end to
+// end) does not pay hipMalloc / hipFree each time.  pool_alloc returns the block and its real size
+// (>= n) or nullptr with the error set; pool_free synchronises the device first (the implicit
+// synchronisation of hipFree that callers rely on) and returns the block to the cache.
+void *pool_alloc(size_t n, size_t *got);
+void pool_free(void *p, size_t bytes);
+
 #define GMAT_HIP(x)                                                                        \
   do {                                                                                     \
     hipError_t e_ = (x);                                                                   \
@@ -41,26 +49,23 @@ void set_error(const char *fmt, ...);
 // Owning device allocation (hipMalloc'd, freed on destruction).
 struct DBuf {
   void *p = nullptr;
-  size_t bytes = 0;
+  size_t bytes = 0;  // the size asked for (kernels and the plan state use it as the buffer's size)
+  size_t cap = 0;    // the block's real size (the cache's size class)
   DBuf() = default;
   DBuf(const DBuf &) = delete;
   DBuf &operator=(const DBuf &) = delete;
   ~DBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) pool_free(p, cap);
     p = nullptr;
-    bytes = 0;
+    bytes = cap = 0;
   }
   int alloc(size_t n) {
     if (n <= bytes && p) return GMAT_OK;
     release();
     if (n == 0) n = 16;
-    hipError_t e = hipMalloc(&p, n);
-    if (e != hipSuccess) {
-      p = nullptr;
-      set_error("hipMalloc(%zu bytes): %s", n, hipGetErrorString(e));
-      return GMAT_E_NOMEM;
-    }
+    p = pool_alloc(n, &cap);
+    if (!p) return GMAT_E_NOMEM;
     bytes = n;
     return GMAT_OK;
   }

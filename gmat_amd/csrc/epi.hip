@@ -2184,6 +2184,203 @@ __global__ void pvalue_kernel(int64_t np, const double *eff, const double *var, 
   p[t] = (c < 0.0) ? 1.0 : erfc(sqrt(0.5 * c));
 }
 
+// ------------------------------------------------------------------ exact refine on int8 slices
+// var = e'Pe for the candidates with the O(n^2) part on the int8 matrix cores.  With the screen codes
+// a, b (integers), w = a o b and v = -beta a - alpha b + alpha beta 1 (the pair screen's expansion):
+//   e'Pe = w'P_off w + sum_q P_qq w_q^2 + 2 v'Pw + v'Pv.
+// w'P_off w: P_off in storage order is cut into R8_S int8 slices of one unit u = 2 qmax / 127,
+//   P' = u sum_s 128^-s A_s + R,  |R_kl| <= u 128^-(R8_S-1) / 2  (~1e-15 qmax),
+// of the block-upper form at 32-row granularity (diagonal blocks as they are, blocks right of the
+// diagonal doubled -- hence 2 qmax in the unit --, blocks left of it zero), so that w'P_off w = w'P'w
+// and w'A_s w is an exact integer: int32 MFMA accumulation per row (|sum| < 2^21), int32 fold with w
+// per row tile, fp64 sums of integers (< 2^53) per slice; the only roundings are the final fp64
+// combination sum_s 2^-7s T_s and R (|w'Rw| <= 8e-16 qmax |w|_1^2).  The O(n) terms are fp64 dot
+// products with U = P x codes (refine8_side_kernel), eff = e'Py in fp64 from the reference codes.
+// Tiles: (32-row block kb, 64-column stage cs >= kb / 2), R8_S slices x 2 row tiles x 16 rows x 64
+// bytes, 16-byte chunks XOR-swizzled by row; a workgroup = 8 waves x 16 pairs (v_mfma_i32_16x16x64_i8,
+// w as the B fragments in registers: n_pad <= 64 R8_NC), the tiles stream through a four-slot LDS-DMA
+// ring (three in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
+// folds the row block).
+constexpr int R8_S = 7, R8_TB = 2048, R8_TILE = R8_S * R8_TB, R8_NC = 32, R8_PP = 128;
+__host__ __device__ inline int64_t r8_toff(int64_t kb, int64_t NS) {  // tiles of the row blocks before kb
+  const int64_t h = kb >> 1;
+  return kb * NS - ((kb & 1) ? h * h : h * (h - 1));
+}
+__global__ void r8_image_kernel(int64_t n_pad, const double *__restrict__ Ps, double inv_unit, int8_t *__restrict__ tiles) {
+  const int64_t NB = n_pad / 32, NS = n_pad / 64;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, column) of a tile row
+  const int64_t rs = idx / n_pad, cc = idx % n_pad;  // storage row, column
+  if (rs >= n_pad) return;
+  const int64_t kb = rs / 32, cs = cc / 64;
+  if (cs < kb / 2) return;
+  const int64_t bc = cc / 32;
+  const double f = bc > kb ? 2.0 : (bc == kb ? 1.0 : 0.0);
+  double r = (rs != cc) ? f * Ps[rs * n_pad + cc] * inv_unit : 0.0;
+  const int rt = (int)((rs % 32) / 16), row = (int)(rs % 16), k = (int)(cc % 64);
+  int8_t *t = tiles + (r8_toff(kb, NS) + cs - kb / 2) * R8_TILE + (rt * 16 + row) * 64 + 16 * ((k / 16) ^ (row & 3)) + k % 16;
+  for (int s = 0; s < R8_S; ++s) {
+    const double q = rint(r);
+    t[s * R8_TB] = (int8_t)q;
+    r = (r - q) * 128.0;
+  }
+  (void)NB;
+}
+
+__global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const int8_t *__restrict__ tiles,
+                                                         const int8_t *__restrict__ sl, const int8_t *__restrict__ sr,
+                                                         const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
+                                                         int64_t np, double unit, double *__restrict__ varw) {
+  constexpr int NSL = 4, LA = 3;
+  __shared__ __attribute__((aligned(16))) int8_t sA[NSL][R8_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NB = (int)(n_pad / 32), NS = (int)(n_pad / 64);
+  const int N = (int)r8_toff(NB, NS);
+  const int64_t p = (int64_t)blockIdx.x * R8_PP + 16 * w + c;
+  const bool valid = p < np;
+  // w = a o b (screen codes 0 / 1 / 2): chunk kc holds individuals 64 kc + 16 g .. + 15 of pair c
+  v4i wf[R8_NC];
+  const int8_t *ra = sl + (valid ? pi[p] : 0) * n_pad, *rb = sr + (valid ? pj[p] : 0) * n_pad;
+  {
+#pragma unroll
+    for (int kc = 0; kc < R8_NC; ++kc) {
+      v4i v = {0, 0, 0, 0};
+      if (valid && kc < NS) {
+        const v4i va = *(const v4i *)(ra + 64 * kc + 16 * g), vb = *(const v4i *)(rb + 64 * kc + 16 * g);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          v[d] = (int)__builtin_amdgcn_perm(T_HI, T_LO, to_offset((unsigned)va[d]) + (unsigned)vb[d]);
+      }
+      wf[kc] = v;
+    }
+  }
+  // tile ring: visit v reads slot v % NSL; tile v + LA goes out at visit v into the slot of visit v - 1.
+  // Past the last tile the DMAs repeat tile 0 into slots no visit reads again, so that every visit
+  // waits with the same vmcnt (one static wait: the unrolled loop stays small enough to unroll fully)
+  const bool two = w + 8 < R8_TILE / 1024;  // this wave moves two 1-KB pieces per tile, else one
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&sA[0][0]) + w * 1024;
+  int kb_p = 0, cs_p = NS - 1, issued = 0;
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    const int8_t *src = issued < N ? tiles + (r8_toff(kb_p, NS) + cs_p - kb_p / 2) * R8_TILE : tiles;
+    const unsigned dst = ring_m0 + (unsigned)(issued % NSL) * R8_TILE;
+    lds_dma16_m0(src + (w * 64 + lane) * 16, dst);
+    if (two) lds_dma16_m0(src + ((w + 8) * 64 + lane) * 16, dst + 8 * 1024);
+    if (issued < N && --cs_p < kb_p / 2) {
+      ++kb_p;
+      cs_p = NS - 1;
+    }
+    ++issued;
+  };
+  for (int q = 0; q < LA; ++q) issue_next();
+  const v4i zv = {0, 0, 0, 0};
+  v4i acc[R8_S][2];
+  double T[R8_S];
+#pragma unroll
+  for (int s = 0; s < R8_S; ++s) T[s] = 0.0;
+  const int swz = 16 * (g ^ (c & 3));
+  int v = 0;
+  for (int kb = 0; kb < NB; ++kb) {
+    const int c0 = kb >> 1;
+    // w at this lane's fold rows 32 kb + 16 rt + 4 g .. + 3 (re-read from the panels: taken from wf
+    // the compiler would merge the 32 fold copies into one with a dynamic register index)
+    unsigned wfold[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int64_t o = 32 * kb + 16 * rt + 4 * g;
+      const unsigned da = valid ? *(const unsigned *)(ra + o) : 0u, db = valid ? *(const unsigned *)(rb + o) : 0u;
+      wfold[rt] = __builtin_amdgcn_perm(T_HI, T_LO, to_offset(da) + db);
+    }
+#pragma unroll
+    for (int cs = R8_NC - 1; cs >= 0; --cs) {
+      if (cs < NS && cs >= c0) {
+        // tile v has landed (the LA - 1 younger tiles may be in flight)
+        static_assert(LA == 3, "vmcnt values");
+        if (two)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue_next();
+        const int8_t *tb = sA[v % NSL];
+        const bool first = cs == NS - 1;
+#pragma unroll
+        for (int s = 0; s < R8_S; ++s)
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) {
+            const v4i fa = *(const v4i *)(tb + s * R8_TB + (rt * 16 + c) * 64 + swz);
+            acc[s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[cs], first ? zv : acc[s][rt], 0, 0, 0);
+          }
+        if (cs == c0) {  // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) {
+            const unsigned wd = wfold[rt];
+            const int w0 = (int)(wd & 0xff), w1 = (int)((wd >> 8) & 0xff), w2 = (int)((wd >> 16) & 0xff),
+                      w3 = (int)(wd >> 24);
+#pragma unroll
+            for (int s = 0; s < R8_S; ++s)
+              T[s] += (double)(w0 * acc[s][rt][0] + w1 * acc[s][rt][1] + w2 * acc[s][rt][2] + w3 * acc[s][rt][3]);
+          }
+        }
+        ++v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the workgroup ends
+#pragma unroll
+  for (int s = 0; s < R8_S; ++s) {
+    T[s] += __shfl_xor(T[s], 16);
+    T[s] += __shfl_xor(T[s], 32);
+  }
+  if (g || !valid) return;
+  double sum = 0.0;
+#pragma unroll
+  for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + T[s];
+  varw[p] = unit * sum;
+}
+
+// The O(n) terms of e'Pe in fp64 (refine8_kernel's expansion) and eff = e'Py from the reference
+// codes; one wave per pair, lanes over individuals, lane partials added in a fixed tree.
+__global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const int8_t *__restrict__ sl,
+                                                           const int8_t *__restrict__ sr, const double *__restrict__ Ua,
+                                                           const double *__restrict__ Ub, const double *__restrict__ z,
+                                                           const double *__restrict__ dg, const double *__restrict__ py,
+                                                           const int8_t *__restrict__ lp, const int8_t *__restrict__ rp,
+                                                           const double *soff_l, const double *soff_r, const double *off_l,
+                                                           const double *off_r, const double *qa, const double *ra,
+                                                           const double *qb, const double *rb, double zz,
+                                                           const uint8_t *mono_l, const uint8_t *mono_r,
+                                                           const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
+                                                           int64_t np, const double *varw, double *eff, double *var) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= np) return;
+  const int64_t i = pi[p], j = pj[p];
+  const double al = soff_l[i], be = soff_r[j], ab = al * be, ral = off_l[i], rbe = off_r[j];
+  const int8_t *a = sl + i * n_pad, *b = sr + j * n_pad, *la = lp + i * n_pad, *lb = rp + j * n_pad;
+  const double *ua = Ua + i * n_pad, *ub = Ub + j * n_pad;
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0, ef = 0.0;
+  for (int64_t q = lane; q < n_pad; q += 64) {
+    const double av = (double)a[q], bv = (double)b[q], wv = av * bv;
+    s1 += wv * ((ab * z[q] - be * ua[q]) - al * ub[q]);
+    s2 += av * ub[q];
+    s3 += dg[q] * (wv * wv);
+    ef += (((double)la[q] - ral) * ((double)lb[q] - rbe)) * py[q];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+    s3 += __shfl_xor(s3, off);
+    ef += __shfl_xor(ef, off);
+  }
+  if (lane) return;
+  const double t3 = be * be * qa[i], t5 = al * al * qb[j], t7 = ab * ab * zz, t8 = 2.0 * ab * s2, t4 = -2.0 * ab * be * ra[i],
+               t6 = -2.0 * ab * al * rb[j];
+  // x == 0 (monomorphic): e = 0 exactly, var = 0 as the reference computes it (its chi and p are NaN)
+  var[p] = (mono_l[i] || mono_r[j]) ? 0.0 : varw[p] + s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
+  eff[p] = ef;
+}
+
 // ------------------------------------------------------------------ pair screen
 // The screens' candidates re-tested one pair at a time before the fp64 refine (the low-rank
 // screen's bound is loose by design: most of its candidates fail a sharper test).  With screen
@@ -2379,6 +2576,125 @@ __global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
   const int64_t p = p0 + tid;
   if (p >= x.np) return;
   const double M = (red[tid] + red[PP + tid]) + (red[2 * PP + tid] + red[3 * PP + tid]);
+  const double var = M + x.side[p], sw = x.side[4 * x.np + p];
+  const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
+  const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
+  if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
+    const unsigned long long k = atomicAdd(x.counter, 1ULL);
+    x.oi[k] = x.ci[p];
+    x.oj[k] = x.cj[p];
+  }
+}
+
+// The same quadratic form with each pair's w held in REGISTERS (n_pad <= 128 PXR_NK): a wave owns 32
+// pairs, lane (c, h) holds pair c's fp4 w for 32 individuals of every 64-individual chunk (the MFMA
+// B fragments, 4 registers per chunk), so 8 waves carry 256 pairs and the P tile images stream
+// through LDS once per 256 pairs (pair_mx_kernel: once per 96, from its LDS-resident w planes) in a
+// four-slot LDS-DMA ring, three tiles in flight.  Visit order: row block kb, then column stage cs from
+// the last down to kb (the inner loop is unrolled so that every register index is static; its last
+// visit, the diagonal tile, folds the row block's accumulators with w of block kb, fetched from the
+// lane half that holds them).  Same operands, scales and test as pair_mx_kernel.
+constexpr int PXR_NK = 16;
+__global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
+  constexpr int NSL = 4, LA = 3;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][MX_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nK = x.nK, N = nK * (nK + 1) / 2;
+  const int64_t p = (int64_t)blockIdx.x * 256 + 32 * w + c;
+  const bool valid = p < x.np;
+  v4i wf[2 * PXR_NK];
+  const uint8_t *ri = x.nib_i + (valid ? x.ci[p] : 0) * nK * NB_REC, *rj = x.nib_j + (valid ? x.cj[p] : 0) * nK * NB_REC;
+  {
+#pragma unroll
+    for (int g = 0; g < 2 * PXR_NK; ++g) {
+      v4i v = {0, 0, 0, 0};
+      if (valid && g < 2 * nK) {  // chunk g = stage g / 2, 16-byte piece 2 (g % 2) + h of its planes
+        const int s = g >> 1, q = 2 * (g & 1) + h;
+        const v4i m1 = *(const v4i *)(ri + s * NB_REC + 16 * q), m2 = *(const v4i *)(ri + s * NB_REC + 64 + 16 * q);
+        const v4i s1 = *(const v4i *)(rj + s * NB_REC + 16 * q);
+        v = (m1 & s1) | (m2 & (s1 << 1));
+      }
+      wf[g] = v;
+    }
+  }
+  // tile ring: visit v reads slot v % NSL; the DMA of tile v + LA goes out at visit v into the slot
+  // visit v - 1 read (every wave has passed visit v's barrier)
+  int kb_p = 0, cs_p = nK - 1, issued = 0;
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    if (issued < N) {
+      const uint8_t *src = x.tiles + (int64_t)(kb_p * nK + cs_p) * MX_TILE;
+      uint8_t *dst = sA[issued % NSL];
+      lds_dma16(src + (w * 64 + lane) * 16, dst + w * 1024);
+      lds_dma16(src + ((8 + w) * 64 + lane) * 16, dst + (8 + w) * 1024);
+      if (--cs_p < kb_p) {
+        ++kb_p;
+        cs_p = nK - 1;
+      }
+    }
+    ++issued;
+  };
+  for (int q = 0; q < LA; ++q) issue_next();
+  const int sw16 = 16 * ((c >> 3) & 1);
+  const v16f_ zv = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  v16f_ acc[MX_RB];
+  double tot = 0.0;
+  int v = 0;
+  for (int kb = 0; kb < nK; ++kb) {
+    // w at this lane's fold rows (storage slots 32 r + 16 h .. + 15 of block kb), from the nibble planes
+    // (taken from wf the compiler would merge the fold copies into one with a dynamic register index)
+    v2i_ wfold[MX_RB];
+#pragma unroll
+    for (int r = 0; r < MX_RB; ++r) {
+      const int o = kb * NB_REC + 16 * r + 8 * h;
+      const v2i_ m1 = valid ? *(const v2i_ *)(ri + o) : v2i_{0, 0}, m2 = valid ? *(const v2i_ *)(ri + o + 64) : v2i_{0, 0};
+      const v2i_ s1 = valid ? *(const v2i_ *)(rj + o) : v2i_{0, 0};
+      wfold[r] = (m1 & s1) | (m2 & (s1 << 1));
+    }
+#pragma unroll
+    for (int cs = PXR_NK - 1; cs >= 0; --cs) {
+      if (cs < nK && cs >= kb) {
+        vm_wait_barrier(2 * min(LA - 1, N - 1 - v));  // tile v has landed (younger DMAs may be in flight)
+        issue_next();
+        const uint8_t *tb = sA[v % NSL];
+        const int bs = cs == kb ? 128 : 129;  // off-diagonal tiles count twice
+        const bool first = cs == nK - 1;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const v4i wb = wf[2 * cs + kk];
+          const v8i_ fb = {wb[0], wb[1], wb[2], wb[3], 0, 0, 0, 0};
+#pragma unroll
+          for (int r = 0; r < MX_RB; ++r) {
+            const uint8_t *ar = tb + (2 * kk + h) * 4096 + (32 * r + c) * 32;
+            const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
+            const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            acc[r] = mfma_mx(fa, fb, (first && kk == 0) ? zv : acc[r], hi[2], bs);
+          }
+        }
+        if (cs == kb) {  // row block kb complete: sum_rows w[row] acc[row] (register e <-> slot 16 h + e)
+#pragma unroll
+          for (int r = 0; r < MX_RB; ++r) {
+            const unsigned m[2] = {(unsigned)wfold[r][0], (unsigned)wfold[r][1]};
+            v2f_ s2 = {0.f, 0.f};
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+#pragma unroll
+              for (int bb = 0; bb < 4; ++bb) {
+                const v2f_ wv = bb == 0 ? fp4_pair<0>(m[d]) : bb == 1 ? fp4_pair<1>(m[d]) : bb == 2 ? fp4_pair<2>(m[d]) : fp4_pair<3>(m[d]);
+                const v2f_ av = {acc[r][8 * d + 2 * bb], acc[r][8 * d + 2 * bb + 1]};
+                s2 = __builtin_elementwise_fma(wv, av, s2);
+              }
+            }
+            tot += (double)s2[0] + (double)s2[1];
+          }
+        }
+        ++v;
+      }
+    }
+  }
+  tot += __shfl_xor(tot, 32);
+  if (h || !valid) return;
+  const double M = tot;
   const double var = M + x.side[p], sw = x.side[4 * x.np + p];
   const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
   const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
@@ -3151,6 +3467,8 @@ struct gmat_epi {
   DBuf lr_tiles, lr_Bs, lr_q1;      // Q' tile images; Q fp64 [n_pad][lr_R] storage order; Q'1 (fp64)
   int nK = 0;                       // 128-individual stages
   DBuf rf_part;                     // refine segment partials [2][nseg][np]
+  DBuf r8_tiles, r8_varw;           // refine8: int8 slice tiles of the block-upper P_off; w'P_off w per pair
+  double r8_unit = 0;               // their unit (2 qmax / 127)
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
   DBuf spanels;  // screen codes, one allocation: [0] minor-allele dosage, [1] heterozygote [m][n_pad]
@@ -3352,8 +3670,23 @@ int build_coding_impl(gmat_epi *e, int which) {
                      cd.U.as<double>(), cd.U32.as<float>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipStreamSynchronize(e->s));
-  cd.U.release();
+  // (U = P x codes stays in fp64: the int8 refine's O(n) terms, refine8_side_kernel)
   cd.ready = true;
+  return GMAT_OK;
+}
+
+// the int8 refine serves plans with n_pad <= 64 R8_NC (w in registers) and a nonzero P_off;
+// GMAT_REFINE64 selects the fp64 MFMA refine (refine_kernel) for A/B runs
+bool refine8_fits(const gmat_epi *e) { return e->n_pad <= 64 * R8_NC && e->qmax > 0 && !getenv("GMAT_REFINE64"); }
+int refine8_setup(gmat_epi *e) {
+  if (e->r8_tiles.p) return GMAT_OK;
+  const int64_t n_pad = e->n_pad, NS = n_pad / 64, N = r8_toff(n_pad / 32, NS);
+  GMAT_TRY(e->r8_tiles.alloc((size_t)N * R8_TILE));
+  e->r8_unit = 2.0 * e->qmax / 127.0;
+  hipLaunchKernelGGL(r8_image_kernel, dim3((unsigned)cdiv(n_pad * n_pad, 256)), dim3(256), 0, e->s, n_pad,
+                     e->Ps.as<double>(), 1.0 / e->r8_unit, e->r8_tiles.as<int8_t>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipStreamSynchronize(e->s));
   return GMAT_OK;
 }
 
@@ -3361,6 +3694,27 @@ int build_coding_impl(gmat_epi *e, int which) {
 int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *lp, const int8_t *rp,
            const int64_t *pi, const int64_t *pj, int64_t np, double *eff, double *var, double *chi, double *p) {
   if (np <= 0) return GMAT_OK;
+  if (refine8_fits(e) && L.U.p && R.U.p) {
+    GMAT_TRY(refine8_setup(e));
+    if (e->r8_varw.bytes < (size_t)np * sizeof(double)) {
+      GMAT_HIP(hipStreamSynchronize(st));  // an earlier refine queued on st may still use the old buffer
+      GMAT_TRY(e->r8_varw.alloc((size_t)np * sizeof(double)));
+    }
+    const int li = (int)(&L - e->code), ri = (int)(&R - e->code);
+    const int8_t *sl = screen_panel(e, li), *sr = screen_panel(e, ri);
+    hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)cdiv(np, R8_PP)), dim3(512), 0, st, e->n_pad,
+                       e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>());
+    GMAT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(refine8_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, e->n_pad, sl, sr,
+                       L.U.as<double>(), R.U.as<double>(), e->z.as<double>(), e->dg.as<double>(), e->py.as<double>(), lp,
+                       rp, L.soff.as<double>(), R.soff.as<double>(), L.off.as<double>(), R.off.as<double>(),
+                       L.qa.as<double>(), L.ra.as<double>(), R.qb.as<double>(), R.rb.as<double>(), e->zz,
+                       L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj, np, e->r8_varw.as<double>(), eff, var);
+    GMAT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
+    GMAT_HIP(hipGetLastError());
+    return GMAT_OK;
+  }
   // a fixed number of segments per pair tile (not one chosen from np: a pair's numbers must not
   // depend on the length of the list it came in, scan vs pairs); 4 segments fill >= 90 % of the
   // last round of resident workgroups (two per CU) from about 1,000 tiles up
@@ -3469,7 +3823,9 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4 * PS_PPW)), dim3(256),
                      (size_t)3 * e->n_pad * sizeof(float), st, x);
   GMAT_HIP(hipGetLastError());
-  if (pp == 96)
+  if (nK <= PXR_NK && !getenv("GMAT_PS_OLD"))  // w in registers: 256 pairs per workgroup
+    hipLaunchKernelGGL(pair_mxr_kernel, dim3((unsigned)cdiv(np, 256)), dim3(512), 0, st, x);
+  else if (pp == 96)
     hipLaunchKernelGGL(pair_mx_kernel<96>, dim3((unsigned)cdiv(np, 96)), dim3(768), lds, st, x);
   else if (pp == 64)
     hipLaunchKernelGGL(pair_mx_kernel<64>, dim3((unsigned)cdiv(np, 64)), dim3(512), lds, st, x);

@@ -41,6 +41,9 @@ int gmat_device_count(int *n);
 int gmat_set_device(int device);
 /* wait for all work queued by this process on the current device (hipDeviceSynchronize) */
 int gmat_device_synchronize(void);
+/* device memory freed by the library stays cached for reuse (up to GMAT_POOL_MAX_GB, default 64);
+ * this returns every cached block to the device */
+int gmat_empty_cache(void);
 
 /* ---------------------------------------------------------------- genotype panel
  * Uploads the packed .bed body once and decodes it on the device into SNP-major int8

@@ -21,7 +21,8 @@ VARIANTS = [{"GMAT_LR_BLOCKS": "1"}, {"GMAT_PS_CHUNK": "700"}, {"GMAT_PS_CHUNK":
             {"GMAT_LRC_ROWS": "256"},  # compacted scan: 256-row launches (default: 512 at this size)
             {"GMAT_PF_COLORDER": "1"},  # prefilter tile list in column-tile order
             {"GMAT_LRC_OPS_CAP": "64"},  # live-pair records overflow: grown and the launches rerun
-            {"GMAT_LRC_MIN_LAUNCHES": "1"}]  # one launch of all rows (no prefilter-ahead pipeline)
+            {"GMAT_LRC_MIN_LAUNCHES": "1"},  # one launch of all rows (no prefilter-ahead pipeline)
+            {"GMAT_PS_OLD": "1"}]  # pair screen with LDS-resident w planes (pair_mx_kernel)
 
 
 @pytest.fixture(scope="module")
