@@ -7,15 +7,14 @@ from scipy.sparse import csr_matrix
 _NA = ("NA", "NaN", "nan", "na")
 
 
-def design_matrix_wemai_multi_gmat(pheno_file, bed_file):
-    """y, X and the record->individual incidence Z (csr), in .fam order
-    (design_matrix.py:7-57).  A genotyped id without a phenotype raises ValueError
-    (the reference logs it and calls sys.exit(), :31-34)."""
-    fam = []
+def _fam_keys(bed_file):
+    """'FID IID' of every genotyped individual, in .fam order."""
     with open(bed_file + ".fam") as f:
-        for line in f:
-            a = line.split()
-            fam.append(a[0] + " " + a[1])
+        return [" ".join(line.split()[:2]) for line in f]
+
+
+def _records(pheno_file):
+    """Phenotype records (split lines) by 'FID IID', missing phenotypes (NA) dropped."""
     recs = {}
     with open(pheno_file) as f:
         for line in f:
@@ -23,24 +22,31 @@ def design_matrix_wemai_multi_gmat(pheno_file, bed_file):
             if a[-1] in _NA:
                 continue
             recs.setdefault(a[0] + " " + a[1], []).append(a)
+    return recs
+
+
+def _y_x(rows):
+    """y (column) and the covariate columns of the records in `rows`."""
+    y = np.array([float(a[-1]) for a in rows]).reshape(-1, 1)
+    xmat = np.array([a[2:-1] for a in rows], dtype=float).reshape(y.shape[0], -1)
+    return y, xmat
+
+
+def design_matrix_wemai_multi_gmat(pheno_file, bed_file):
+    """y, X and the record->individual incidence Z (csr), in .fam order
+    (design_matrix.py:7-57).  A genotyped id without a phenotype raises ValueError
+    (the reference logs it and calls sys.exit(), :31-34)."""
+    fam, recs = _fam_keys(bed_file), _records(pheno_file)
     missing = set(fam) - set(recs)
     if missing:
         msg = "The below genotyped id is not in the phenotype file:\n {}".format("\n".join(sorted(missing)))
         logging.error(msg)
         raise ValueError(msg)
-    y, x, iid = [], [], []
-    for key in fam:
-        for a in recs[key]:
-            y.append(float(a[-1]))
-            x.append(a[2:-1])
-            iid.append(a[1])
-    y = np.array(y).reshape(-1, 1)
-    xmat = np.array(x, dtype=float).reshape(y.shape[0], -1)
+    rows = [a for key in fam for a in recs[key]]
+    y, xmat = _y_x(rows)
     order, col = {}, []
-    for v in iid:
-        if v not in order:
-            order[v] = len(order)
-        col.append(order[v])
+    for a in rows:
+        col.append(order.setdefault(a[1], len(order)))
     zmat = csr_matrix((np.ones(len(col)), (np.arange(len(col)), col)))
     return y, xmat, zmat
 
@@ -60,39 +66,18 @@ def design_matrix_wemai_multi_gmat_pred(pheno_file, bed_file):
     """As design_matrix_wemai_multi_gmat, but genotyped ids without a phenotype are allowed:
     they keep a (record-less) column of Z so that their random effects are predicted
     (design_matrix.py:60-113)."""
-    fam = []
-    with open(bed_file + ".fam") as f:
-        for line in f:
-            a = line.split()
-            fam.append(a[0] + " " + a[1])
-    recs = {}
-    with open(pheno_file) as f:
-        for line in f:
-            a = line.split()
-            if a[-1] in _NA:
-                continue
-            recs.setdefault(a[0] + " " + a[1], []).append(a)
-    y, x, iid = [], [], []
+    fam, recs = _fam_keys(bed_file), _records(pheno_file)
+    rows = [a for key in fam for a in recs.get(key, [])]
+    y, xmat = _y_x(rows)
+    order, col, n_col = {}, [], 0
     for key in fam:
-        if key in recs:
-            for a in recs[key]:
-                y.append(float(a[-1]))
-                x.append(a[2:-1])
-                iid.append(a[1])
-        else:
-            iid.append(None)
-    y = np.array(y).reshape(-1, 1)
-    xmat = np.array(x, dtype=float).reshape(y.shape[0], -1)
-    order, rows, col = {}, 0, []
-    n_col = 0
-    for v in iid:
-        if v is None:
+        if key not in recs:  # a record-less id: its own column
             n_col += 1
             continue
-        if v not in order:
-            order[v] = n_col
-            n_col += 1
-        col.append(order[v])
-        rows += 1
-    zmat = csr_matrix((np.ones(rows), (np.arange(rows), col)), shape=(rows, n_col))
+        for a in recs[key]:
+            if a[1] not in order:
+                order[a[1]] = n_col
+                n_col += 1
+            col.append(order[a[1]])
+    zmat = csr_matrix((np.ones(len(col)), (np.arange(len(col)), col)), shape=(len(col), n_col))
     return y, xmat, zmat

@@ -11,6 +11,9 @@ for st in "$@"; do
     tests)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
       tail -3 $OUT/tests.log ;;
+    scantests)
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_pair_screen.py tests/test_gpu_lr_variants.py tests/test_gpu_parity.py tests/test_gpu_full_triangle.py -x -q --timeout 240 --timeout-method thread > $OUT/scantests.log 2>&1 || { tail -40 $OUT/scantests.log; exit 1; }
+      tail -2 $OUT/scantests.log ;;
     bench)
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.log || { tail -30 $OUT/bench.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/bench.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;

@@ -16,7 +16,7 @@ def main():
     path = sys.argv[1]
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in csv.DictReader(open(path)))
-    rf = [k for k, e in enumerate(ev) if e[2].startswith("refine_kernel")]
+    rf = [k for k, e in enumerate(ev) if e[2].startswith(("refine_kernel", "refine8_side_kernel"))]
     pf = [k for k, e in enumerate(ev) if e[2].startswith("prefilter_pass")]
     if len(sys.argv) > 2:
         pf = pf[-int(sys.argv[2]):]
