@@ -644,10 +644,14 @@ def main():
     sync()
     t0 = time.perf_counter()
     screen_s = launches = ops = cands = hits = side_s = ref_s = 0.0
-    ks = {}
+    ks, kx = {}, {}
     n_slice = 0
     for _ in range(args.steps):
         res = step()
+        for name, v in plan.kernel_stats_ext().items():
+            acc = kx.setdefault(name, {"s": 0.0, "launches": 0.0, "pairs": 0.0})
+            for key in acc:
+                acc[key] += v[key]
         st = plan.stats()
         screen_s += st["screen_s"]
         launches += st["launches"]
@@ -685,28 +689,53 @@ def main():
             kern_rec[name] = {"kernel_s_per_step": ks[t_key] / args.steps, "avg_launch_ms": t_launch * 1e3,
                               "ops_per_launch": ks[o_key] / ks[n_key],
                               "achieved": ks[o_key] / ks[n_key] / t_launch / 1e12, "ops_note": what}
-    if kern_rec:
-        dom = max(kern_rec, key=lambda k: kern_rec[k]["kernel_s_per_step"])
+    # the candidate kernels (HIP events around each launch, gmat_epi_kernel_stats_ext), each against the
+    # roof that binds it: pair_mxr_kernel issues n_pad^2 (1 + 1 / nK) fp6 x fp4 MACs x 2 per pair (the
+    # block-upper P tiles), refine8_kernel R8_S = 7 int8 slices over the block-upper 32 x 64 tiles
+    # (1,056 at n_pad 2,048) x 2 ops per pair; pair_side_kernel and refine8_side_kernel gather rows
+    # (fp16 P x codes + int8 codes: 6 n_pad bytes per pair; fp64 P x codes + int8 codes: 20 n_pad)
+    n_pad_k = -(-n // 256) * 256
+    nK_k, NS_k, NB_k = n_pad_k // 128, n_pad_k // 64, n_pad_k // 32
+    r8_tiles = NB_k * NS_k - ((NB_k // 2) * (NB_k // 2 - 1) if NB_k % 2 == 0 else (NB_k // 2) ** 2)
+    for name, kname, per_pair, peak, unit, what in (
+            ("pair_mx", "pair_mxr_kernel", 2.0 * 128 * 128 * nK_k * (nK_k + 1) / 2, MX_PEAK_TFLOPS, "TFLOP/s",
+             "fp6 x fp4 ops of the block-upper P tiles per pair"),
+            ("refine", "refine8_kernel", 2.0 * 7 * r8_tiles * 32 * 64, INT8_PEAK_TOPS, "TOP/s",
+             "int8 ops: 7 slices of the block-upper 32 x 64 tiles per pair"),
+            ("pair_side", "pair_side_kernel", 6.0 * n_pad_k, 8000.0, "GB/s", "gathered bytes per pair (HBM roof)"),
+            ("refine_side", "refine8_side_kernel", 20.0 * n_pad_k, 8000.0, "GB/s", "gathered bytes per pair (HBM roof)")):
+        v = kx.get(name)
+        if not v or v["s"] <= 0:
+            continue
+        rate = v["pairs"] * per_pair / v["s"] / (1e12 if unit != "GB/s" else 1e9)
+        kern_rec[kname] = {"kernel_s_per_step": v["s"] / args.steps, "launches_per_step": v["launches"] / args.steps,
+                           "pairs_per_step": v["pairs"] / args.steps, "avg_launch_ms": v["s"] / v["launches"] * 1e3,
+                           "achieved": rate, "unit": unit, "peak": peak, "frac": rate / peak, "ops_note": what,
+                           "work_per_pair": per_pair}
+    screens = [k for k in ("prefilter_pass_kernel", "lrc_screen_kernel") if k in kern_rec]
+    if screens:
+        dom = max(screens, key=lambda k: kern_rec[k]["kernel_s_per_step"])
         kr = kern_rec[dom]
         # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
         # WRITE_SIZE); used only when recorded on the same kernel source (sha256 of epi.hip), kernel,
         # rank and cohort size (else traffic stays null)
-        traffic, traffic_src = None, None
-        tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % dom)
-        want = {"kernel": dom, "lowrank_rank": plan.lowrank_rank(), "n_id": n, "n_snp": m,
-                "source_sha256": source_sha256()}
-        if os.path.exists(tpath):
+        def traffic_of(kname):
+            tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % kname)
+            want = {"kernel": kname, "lowrank_rank": plan.lowrank_rank(), "n_id": n, "n_snp": m,
+                    "source_sha256": source_sha256()}
+            if not os.path.exists(tpath):
+                return None, "no PMC record %s" % os.path.relpath(tpath, REPO)
             try:
                 tj = json.load(open(tpath))
-                if all(tj.get(k) == v for k, v in want.items()):
-                    traffic, traffic_src = tj.get("hbm_bytes_per_launch"), os.path.relpath(tpath, REPO)
-                else:
-                    traffic_src = "dropped: %s was recorded for %s" % (os.path.relpath(tpath, REPO),
-                                                                       {k: tj.get(k) for k in want})
             except Exception as exc:
-                traffic_src = "unreadable: %s" % exc
-        else:
-            traffic_src = "no PMC record %s" % os.path.relpath(tpath, REPO)
+                return None, "unreadable: %s" % exc
+            if all(tj.get(k) == v for k, v in want.items()):
+                return tj.get("hbm_bytes_per_launch"), os.path.relpath(tpath, REPO)
+            return None, "dropped: %s was recorded for %s" % (os.path.relpath(tpath, REPO), {k: tj.get(k) for k in want})
+
+        traffic, traffic_src = traffic_of(dom)
+        for kname, rec in kern_rec.items():
+            rec["traffic_per_launch"], rec["traffic_source"] = traffic_of(kname)
         roofline = {"bound": "mfma", "achieved": kr["achieved"], "peak": MX_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": kr["achieved"] / MX_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": dom, "ops_note": kr["ops_note"], "avg_launch_ms": kr["avg_launch_ms"],

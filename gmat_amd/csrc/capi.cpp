@@ -96,6 +96,54 @@ void pool_free(void *p, size_t bytes) {
   pl.cached += bytes;
 }
 
+namespace {
+struct PinnedPool {
+  std::mutex mu;
+  std::multimap<size_t, void *> free_blocks;
+  size_t cached = 0;
+};
+PinnedPool &pinned_pool() {
+  static PinnedPool *p = new PinnedPool;
+  return *p;
+}
+}  // namespace
+
+void *pinned_alloc(size_t n, size_t *got) {
+  const size_t c = n < 4096 ? 4096 : (n + 65535) / 65536 * 65536;
+  PinnedPool &pl = pinned_pool();
+  {
+    std::lock_guard<std::mutex> lk(pl.mu);
+    auto it = pl.free_blocks.lower_bound(c);
+    if (it != pl.free_blocks.end() && it->first <= 2 * c) {
+      void *p = it->second;
+      *got = it->first;
+      pl.cached -= it->first;
+      pl.free_blocks.erase(it);
+      return p;
+    }
+  }
+  void *p = nullptr;
+  hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    set_error("hipHostMalloc(%zu bytes): %s", c, hipGetErrorString(e));
+    return nullptr;
+  }
+  *got = c;
+  return p;
+}
+
+void pinned_free(void *p, size_t bytes) {
+  if (!p) return;
+  PinnedPool &pl = pinned_pool();
+  std::lock_guard<std::mutex> lk(pl.mu);
+  if (pl.cached + bytes > (size_t)1 << 30) {  // keep at most 1 GiB of pinned memory cached
+    (void)hipHostFree(p);
+    return;
+  }
+  pl.free_blocks.insert({bytes, p});
+  pl.cached += bytes;
+}
+
 }  // namespace gmat
 
 extern "C" const char *gmat_last_error(void) { return gmat::g_err; }
@@ -105,6 +153,11 @@ extern "C" int gmat_empty_cache(void) {
   std::lock_guard<std::mutex> lk(pl.mu);
   GMAT_HIP(hipDeviceSynchronize());
   pl.trim_all();
+  gmat::PinnedPool &pp = gmat::pinned_pool();
+  std::lock_guard<std::mutex> lk2(pp.mu);
+  for (auto &kv : pp.free_blocks) (void)hipHostFree(kv.second);
+  pp.free_blocks.clear();
+  pp.cached = 0;
   return GMAT_OK;
 }
 

@@ -22,6 +22,9 @@ void set_error(const char *fmt, ...);
 // synchronisation of hipFree that callers rely on) and returns the block to the cache.
 void *pool_alloc(size_t n, size_t *got);
 void pool_free(void *p, size_t bytes);
+// the same for pinned host staging buffers (hipHostMalloc / hipHostFree take about a millisecond each)
+void *pinned_alloc(size_t n, size_t *got);
+void pinned_free(void *p, size_t bytes);
 
 #define GMAT_HIP(x)                                                                        \
   do {                                                                                     \

@@ -489,6 +489,8 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc4[q][p][e] = 0.f;
     }
+    // (two stages per barrier, a six-slot ring, measured slower: 11.7 against 11.0 ms of prefilter per
+    // configs[2] step, serialised)
     int slot = 0, slot_ahead = PF_NS - 1;  // ring slots of stage st and of stage st + 4
     for (int st = 0; st < S; ++st) {
       const uint8_t *bf = ring[slot];
@@ -708,17 +710,18 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
 // orthonormal null directions, so every pair also needs u_k'e = (a o u_k).b - beta u_k.a - alpha
 // u_k.b + alpha beta 1'u_k for k < NC.  (a o u_k) is a one-slice int8 row image (per-row scale sU):
 // |u_k'e - c~_k| <= sU/2 sum_t b_t = sU csum_r / 2, so |U'e|^2 <= sum_k (|c~_k| + err_k)^2.
-// 64 x 128 (row, column) tiles, 8 waves of 32 x 32 at two waves per SIMD (a 32 x 32 wave tile keeps
-// the NC extra int32 accumulator sets within two waves' registers); stage image (14 + 4 NC KB, 64
-// individuals):
-// L3 slices 0, 1 and the NC direction images (64 rows x 64 B each), fp4 codes of a (64 rows x 32 B)
-// and b (128 columns x 32 B); DMA instruction q (1 KB) lands at q KB, wave w issuing q = w + 8u.
-// Five-slot LDS-DMA ring, four stages in flight.
-constexpr int PC_TR = 64, PC_TC = 128, PC_NS = 5, PF_NCOV_MAX = 4;
+// 32 x 256 (row, column) tiles, 8 waves of 32 x 32 (one row band, wave w the columns 32 w ..) at two
+// waves per SIMD (a 32 x 32 wave tile keeps the NC extra int32 accumulator sets within two waves'
+// registers).  A row brings 64 B per int8 region and stage, a column 32 B, so the tall side of the tile
+// is the columns: 32 x 256 streams 2 KB NREG + 9 KB per stage for 8,192 pairs (the round-3 64 x 128
+// tile: 4 KB NREG + 6 KB).  Stage image (64 individuals): L3 slices 0, 1 and the NC direction images
+// (32 rows x 64 B each), fp4 codes of a (32 rows x 32 B) and b (256 columns x 32 B); DMA instruction q
+// (1 KB) lands at q KB, wave w issuing q = w + 8u.  Five-slot LDS-DMA ring, four stages in flight.
+constexpr int PC_TR = 32, PC_TC = 256, PC_NS = 5, PF_NCOV_MAX = 4;
 template <int NC>
 struct PcShape {
   static constexpr int NREG = 2 + NC;                  // int8 row regions: L3 slices + directions
-  static constexpr int O_A4 = 4096 * NREG, O_B4 = O_A4 + 2048, ST = O_B4 + 4096;
+  static constexpr int O_A4 = 2048 * NREG, O_B4 = O_A4 + 1024, ST = O_B4 + 8192;
   static constexpr int QT = ST / 1024;                 // DMA instructions per stage
   static constexpr int QW = (QT + 3) / 4;              // per wave (the last ones partly idle)
 };
@@ -737,49 +740,78 @@ __device__ __forceinline__ void vm_wait_barrier(int n) {
   }
 #undef VMW
 }
-template <int NC>
+// LIST: a persistent grid over the launch's tile list (as prefilter_pass_kernel<true>: XCD x takes the
+// list's x-th eighth, its workgroups stride through it, and the next tile's first stages stream into
+// the ring while this tile's epilogue runs); else one workgroup per tile of the XCD-aware remap.
+template <int NC, bool LIST>
 __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   using SH = PcShape<NC>;
   constexpr int NW = 8;
   const ScreenArgs &a = x.a;
-  const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = (int)blockIdx.x % 8;
-  const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (int)blockIdx.x / 8;
-  const int rt = tile % x.n_rt, ct = tile / x.n_rt;
-  const int r0 = rt * PC_TR;
-  const int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)ct * PC_TC;
-  if (r0 >= a.n_rows || c0 >= a.m) return;
-  if (a.tri && c0 + PC_TC - 1 <= a.rows[r0]) return;  // rows ascend within a launch
-  // 8 waves at two per SIMD: wave w = rows 32 (w >> 2) .. +32 x columns 32 (w & 3) .. +32
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, h = lane >> 5, c = lane & 31;
+  const int xcd = (int)blockIdx.x % 8, kw = (int)blockIdx.x / 8, G = (int)gridDim.x / 8;
+  const int l_lo = LIST ? (int)(((int64_t)x.n_list * xcd) / 8) : 0;
+  const int l_hi = LIST ? (int)(((int64_t)x.n_list * (xcd + 1)) / 8) : 0;
+  auto tile_at = [&](int i) __attribute__((always_inline)) -> int {
+    if (LIST) {
+      const int q = l_lo + kw + i * G;
+      return q < l_hi ? __builtin_amdgcn_readfirstlane(x.tile_list[q]) : -1;
+    }
+    if (i > 0) return -1;
+    const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8;
+    const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + kw;
+    const int r0_ = (t % x.n_rt) * PC_TR;
+    const int64_t c0_ = (a.j_lo / 32) * 32 + (int64_t)(t / x.n_rt) * PC_TC;
+    if (r0_ >= a.n_rows || c0_ >= a.m) return -1;
+    if (a.tri && c0_ + PC_TC - 1 <= a.rows[r0_]) return -1;  // rows ascend within a launch
+    return t;
+  };
+  int tile = tile_at(0);
+  if (tile < 0) return;
+  // 8 waves at two per SIMD: wave w = the tile's 32 rows x columns 32 w .. +32
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = 0, wc = w, h = lane >> 5, c = lane & 31;
   __shared__ __attribute__((aligned(16))) uint8_t ring[PC_NS][SH::ST];
   constexpr int QW = (SH::QT + NW - 1) / NW;
   const uint8_t *src[QW];
   int stp[QW];
   int nq = 0;  // DMA instructions this wave issues per stage
+  auto set_src = [&](int r0, int64_t c0) __attribute__((always_inline)) {
+    nq = 0;
 #pragma unroll
-  for (int u = 0; u < QW; ++u) {
-    const int q = w + NW * u;
-    src[u] = nullptr;
-    stp[u] = 0;
-    if (q < 4 * SH::NREG) {  // int8 rows: region q / 4, 16 rows x 4 chunks per instruction
-      const int g = q >> 2, row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-      src[u] = (const uint8_t *)x.rs[g] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
-      stp[u] = SG_K;
-      ++nq;
-    } else if (q < SH::QT) {  // fp4 codes: 32 rows x 2 chunks per instruction (2 for a, 4 for b)
-      const int qq = q - 4 * SH::NREG, isb = qq >= 2, row = (isb ? qq - 2 : qq) * 32 + (lane >> 1);
-      const int lg = (lane & 1) ^ ((row >> 3) & 1);
-      const int64_t idx = isb ? min(c0 + row, a.m - 1) : a.rows[min(r0 + row, a.n_rows - 1)];
-      src[u] = (isb ? x.cs4 : x.rs4) + idx * (x.n_pad / 2) + 16 * lg;
-      stp[u] = SG_K / 2;
-      ++nq;
+    for (int u = 0; u < QW; ++u) {
+      const int q = w + NW * u;
+      src[u] = nullptr;
+      stp[u] = 0;
+      if (q < 2 * SH::NREG) {  // int8 rows: region q / 2, 16 rows x 4 chunks per instruction
+        const int g = q >> 1, row = (q & 1) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+        src[u] = (const uint8_t *)x.rs[g] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
+        stp[u] = SG_K;
+        ++nq;
+      } else if (q < SH::QT) {  // fp4 codes: 32 rows x 2 chunks per instruction (1 for a, 8 for b)
+        const int qq = q - 2 * SH::NREG, isb = qq >= 1, row = (isb ? qq - 1 : qq) * 32 + (lane >> 1);
+        const int lg = (lane & 1) ^ ((row >> 3) & 1);
+        const int64_t idx = isb ? min(c0 + row, a.m - 1) : a.rows[min(r0 + row, a.n_rows - 1)];
+        src[u] = (isb ? x.cs4 : x.rs4) + idx * (x.n_pad / 2) + 16 * lg;
+        stp[u] = SG_K / 2;
+        ++nq;
+      }
     }
-  }
+  };
   auto issue = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < QW; ++u)
       if (w + NW * u < SH::QT) lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PC_NS][(w + NW * u) * 1024]);
   };
+  const int S = (int)(x.n_pad / SG_K);
+  const int pre = min(S, PC_NS - 1);
+  int r0 = (tile % x.n_rt) * PC_TR;
+  int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PC_TC;
+  set_src(r0, c0);
+  for (int st = 0; st < pre; ++st) issue(st);
+  for (int it = 0;; ++it) {
+  if (it == 0)
+    vm_wait_barrier(nq * (pre - 1));
+  else  // the prefetched stages and the previous epilogue's stores (vmcnt counts those too)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   v16i acc[E3_PF], accu[NC];
   v16f_ acc4[4];  // a.b, a^2.b, a.b^2, a^2.b^2
 #pragma unroll
@@ -791,10 +823,6 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc4[p][e] = 0.f;
   }
-  const int S = (int)(x.n_pad / SG_K);
-  const int pre = min(S, PC_NS - 1);
-  for (int st = 0; st < pre; ++st) issue(st);
-  vm_wait_barrier(nq * (pre - 1));
   const int rrow = 32 * wr + c;
   const int crow = 32 * wc + c, lcb = h ^ ((crow >> 3) & 1);
   for (int st = 0; st < S; ++st) {
@@ -807,7 +835,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       const v4i fc = i8_of_fp4((unsigned)rb4[2 * kk], (unsigned)rb4[2 * kk + 1]);
 #pragma unroll
       for (int g = 0; g < SH::NREG; ++g) {
-        const v4i f = *(const v4i *)&bf[4096 * g + rrow * 64 + 16 * lr];
+        const v4i f = *(const v4i *)&bf[2048 * g + rrow * 64 + 16 * lr];
         if (g < E3_PF)
           acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, fc, acc[g], 0, 0, 0);
         else
@@ -868,6 +896,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     cmono = a.mono_r[j];
 #pragma unroll
     for (int k = 0; k < NC; ++k) cub[k] = a.pf_ub[k * a.m + j];
+  }
+  // every wave has passed the last stage's barrier (and the records' barrier): the ring is free for the
+  // next tile's first stages, which land while the tests below run.  (Issued after the per-row and
+  // per-column loads have been consumed: the compiler's waits for those count the DMAs as well.)
+  const int nxt = tile_at(it + 1);
+  if (nxt >= 0) {
+    set_src((nxt % x.n_rt) * PC_TR, (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PC_TC);
+    asm volatile("" ::"v"(cbe), "v"(ccb), "v"(cC1n), "v"(cnb), "v"(cbsb), "v"(cmag), "v"(cub[0]), "v"((int)cmono));
+    for (int st = 0; st < pre; ++st) issue(st);
   }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -950,6 +987,11 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       }
     }
   }
+  if (nxt < 0) break;
+  tile = nxt;
+  r0 = (tile % x.n_rt) * PC_TR;
+  c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PC_TC;
+  }  // tile loop
 }
 
 // Tile shapes (SH): the K-block height MT (rows of A_s per accumulator set) and the pair blocks
@@ -2198,8 +2240,8 @@ __global__ void pvalue_kernel(int64_t np, const double *eff, const double *var, 
 // products with U = P x codes (refine8_side_kernel), eff = e'Py in fp64 from the reference codes.
 // Tiles: (32-row block kb, 64-column stage cs >= kb / 2), R8_S slices x 2 row tiles x 16 rows x 64
 // bytes, 16-byte chunks XOR-swizzled by row; a workgroup = 8 waves x 16 pairs (v_mfma_i32_16x16x64_i8,
-// w as the B fragments in registers: n_pad <= 64 R8_NC), the tiles stream through a four-slot LDS-DMA
-// ring (three in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
+// w as the B fragments in registers: n_pad <= 64 R8_NC), the tiles stream through an eight-slot
+// LDS-DMA ring (six in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
 // folds the row block).
 constexpr int R8_S = 7, R8_TB = 2048, R8_TILE = R8_S * R8_TB, R8_NC = 32, R8_PP = 128;
 __host__ __device__ inline int64_t r8_toff(int64_t kb, int64_t NS) {  // tiles of the row blocks before kb
@@ -2229,19 +2271,29 @@ __global__ void r8_image_kernel(int64_t n_pad, const double *__restrict__ Ps, do
 __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const int8_t *__restrict__ tiles,
                                                          const int8_t *__restrict__ sl, const int8_t *__restrict__ sr,
                                                          const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
-                                                         int64_t np, double unit, double *__restrict__ varw) {
-  constexpr int NSL = 4, LA = 3;
+                                                         int64_t np, double unit, double *__restrict__ varw,
+                                                         double *__restrict__ tpart) {
+  constexpr int NSL = 8, LA = 6;  // ring slots, tiles in flight (112 KB of LDS)
   __shared__ __attribute__((aligned(16))) int8_t sA[NSL][R8_TILE];
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NB = (int)(n_pad / 32), NS = (int)(n_pad / 64);
-  const int N = (int)r8_toff(NB, NS);
+  // segment blockIdx.y of gridDim.y: the row blocks [kb_lo, kb_hi) holding its share of the tiles (a
+  // short pair list is spread over more workgroups); its per-slice integer sums go to tpart, added by
+  // r8_combine_kernel (exact: the same bits for any number of segments)
+  const int nseg = (int)gridDim.y, seg = (int)blockIdx.y;
+  const int64_t N_all = r8_toff(NB, NS);
+  int kb_lo = 0, kb_hi = 0;
+  while (kb_lo < NB && r8_toff(kb_lo, NS) * nseg < N_all * seg) ++kb_lo;
+  kb_hi = kb_lo;
+  while (kb_hi < NB && r8_toff(kb_hi, NS) * nseg < N_all * (seg + 1)) ++kb_hi;
+  const int N = (int)(r8_toff(kb_hi, NS) - r8_toff(kb_lo, NS));
   const int64_t p = (int64_t)blockIdx.x * R8_PP + 16 * w + c;
   const bool valid = p < np;
   // w = a o b (screen codes 0 / 1 / 2): chunk kc holds individuals 64 kc + 16 g .. + 15 of pair c
   v4i wf[R8_NC];
-  const int8_t *ra = sl + (valid ? pi[p] : 0) * n_pad, *rb = sr + (valid ? pj[p] : 0) * n_pad;
   {
+    const int8_t *ra = sl + (valid ? pi[p] : 0) * n_pad, *rb = sr + (valid ? pj[p] : 0) * n_pad;
 #pragma unroll
     for (int kc = 0; kc < R8_NC; ++kc) {
       v4i v = {0, 0, 0, 0};
@@ -2260,7 +2312,7 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   const bool two = w + 8 < R8_TILE / 1024;  // this wave moves two 1-KB pieces per tile, else one
   typedef __attribute__((address_space(3))) const void *lds_ct;
   const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&sA[0][0]) + w * 1024;
-  int kb_p = 0, cs_p = NS - 1, issued = 0;
+  int kb_p = kb_lo, cs_p = NS - 1, issued = 0;
   auto issue_next = [&]() __attribute__((always_inline)) {
     const int8_t *src = issued < N ? tiles + (r8_toff(kb_p, NS) + cs_p - kb_p / 2) * R8_TILE : tiles;
     const unsigned dst = ring_m0 + (unsigned)(issued % NSL) * R8_TILE;
@@ -2280,26 +2332,19 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   for (int s = 0; s < R8_S; ++s) T[s] = 0.0;
   const int swz = 16 * (g ^ (c & 3));
   int v = 0;
-  for (int kb = 0; kb < NB; ++kb) {
+  for (int kb = kb_lo; kb < kb_hi; ++kb) {
     const int c0 = kb >> 1;
-    // w at this lane's fold rows 32 kb + 16 rt + 4 g .. + 3 (re-read from the panels: taken from wf
-    // the compiler would merge the 32 fold copies into one with a dynamic register index)
-    unsigned wfold[2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int64_t o = 32 * kb + 16 * rt + 4 * g;
-      const unsigned da = valid ? *(const unsigned *)(ra + o) : 0u, db = valid ? *(const unsigned *)(rb + o) : 0u;
-      wfold[rt] = __builtin_amdgcn_perm(T_HI, T_LO, to_offset(da) + db);
-    }
 #pragma unroll
     for (int cs = R8_NC - 1; cs >= 0; --cs) {
-      if (cs < NS && cs >= c0) {
+      int cq = c0;  // opaque per unrolled copy (see pair_mxr_kernel)
+      asm volatile("" : "+s"(cq));
+      if (cs < NS && cs >= cq) {
         // tile v has landed (the LA - 1 younger tiles may be in flight)
-        static_assert(LA == 3, "vmcnt values");
+        static_assert(LA == 6, "vmcnt values");
         if (two)
-          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else
-          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue_next();
         const int8_t *tb = sA[v % NSL];
         const bool first = cs == NS - 1;
@@ -2310,10 +2355,14 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
             const v4i fa = *(const v4i *)(tb + s * R8_TB + (rt * 16 + c) * 64 + swz);
             acc[s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[cs], first ? zv : acc[s][rt], 0, 0, 0);
           }
-        if (cs == c0) {  // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile
+        if (cs == cq) {  // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) {
-            const unsigned wd = wfold[rt];
+            const int sl_ = c + 16 * (2 * (kb & 1) + rt);  // the lanes holding the row tile's w
+            const v4i src = wf[cs];
+            const int d0 = __shfl(src[0], sl_), d1 = __shfl(src[1], sl_), d2 = __shfl(src[2], sl_),
+                      d3 = __shfl(src[3], sl_);
+            const unsigned wd = (unsigned)(g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3);
             const int w0 = (int)(wd & 0xff), w1 = (int)((wd >> 8) & 0xff), w2 = (int)((wd >> 16) & 0xff),
                       w3 = (int)(wd >> 24);
 #pragma unroll
@@ -2332,9 +2381,31 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
     T[s] += __shfl_xor(T[s], 32);
   }
   if (g || !valid) return;
+  if (nseg > 1) {
+#pragma unroll
+    for (int s = 0; s < R8_S; ++s) tpart[((int64_t)seg * R8_S + s) * np + p] = T[s];
+    return;
+  }
   double sum = 0.0;
 #pragma unroll
   for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + T[s];
+  varw[p] = unit * sum;
+}
+// the segments' integer sums added (exactly, in fp64) and combined as refine8_kernel does for one
+// the most row-block segments a short refine8 / pair_mxr list is split into (GMAT_SEG_MAX, default 8)
+int seg_max() {
+  const char *s = getenv("GMAT_SEG_MAX");
+  return s ? std::max(1, std::min(8, atoi(s))) : 8;
+}
+__global__ void r8_combine_kernel(int64_t np, int nseg, const double *tpart, double unit, double *varw) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  double sum = 0.0;
+  for (int s = R8_S - 1; s >= 0; --s) {
+    double t = 0.0;
+    for (int k = 0; k < nseg; ++k) t += tpart[((int64_t)k * R8_S + s) * np + p];
+    sum = sum * (1.0 / 128.0) + t;
+  }
   varw[p] = unit * sum;
 }
 
@@ -2397,7 +2468,7 @@ struct PairArgs {
   const int64_t *ci, *cj;  // candidates [np]
   int64_t np, n_pad;
   const int8_t *a, *b;        // screen panels (left, right coding) [m][n_pad]
-  const float *Ua, *Ub;       // P x panel rounded to fp32 [m][n_pad]
+  const _Float16 *Ua, *Ub;    // P x panel rounded to fp16 [m][n_pad]
   const double *alpha, *beta;  // screen-code offsets
   const double *qa, *ra, *qb, *rb;
   const double *z, *dg, *py;
@@ -2409,7 +2480,20 @@ struct PairArgs {
   double rho, chi_cut;
   unsigned long long *counter;
   int64_t *oi, *oj;  // surviving pairs
+  double *mpart;     // pair_mxr_kernel with segments: w'P~w per (segment, pair), added by pair_test_kernel
 };
+
+// the pair screen's test of pair p given M = w'P~w: kept unless its p-value is certainly >= p_cut
+__device__ __forceinline__ void pair_test(const PairArgs &x, int64_t p, double M) {
+  const double var = M + x.side[p], sw = x.side[4 * x.np + p];
+  const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
+  const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
+  if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
+    const unsigned long long k = atomicAdd(x.counter, 1ULL);
+    x.oi[k] = x.ci[p];
+    x.oj[k] = x.cj[p];
+  }
+}
 
 // One wave per pair, PS_PPW pairs per wave; z, diag(P) and Py staged once per workgroup in LDS as
 // fp32.  The sums run in fp32 with a certified slack: each lane adds its n_pad / 64 terms per
@@ -2434,15 +2518,19 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
     const double dal = x.alpha[i], dbe = x.beta[j], dab = dal * dbe;
     const float al = (float)dal, be = (float)dbe, ab = (float)dab;
     const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
-    const float *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
+    const _Float16 *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
     float s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
     for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
       const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
       const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
-      const float4 u0 = *(const float4 *)(ua + q0), u1 = *(const float4 *)(ua + q0 + 4);
-      const float4 v0 = *(const float4 *)(ub + q0), v1 = *(const float4 *)(ub + q0 + 4);
-      const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      typedef _Float16 h8_ __attribute__((ext_vector_type(8)));
+      const h8_ u8 = *(const h8_ *)(ua + q0), v8 = *(const h8_ *)(ub + q0);
+      float uu[8], vv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        uu[t] = (float)u8[t];
+        vv[t] = (float)v8[t];
+      }
 #pragma unroll
       for (int h = 0; h < 8; ++h) {
         const float av = (float)ca[h], bv = (float)cb[h], w = av * bv;  // exact small integers
@@ -2470,12 +2558,16 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
                  t4 = -2.0 * dab * dbe * x.ra[i], t6 = -2.0 * dab * dal * x.rb[j];
     x.side[p] = r[4] + 2.0 * r[0] + t3 + t5 + t7 + t8 + t4 + t6;
     // fp32 sums: a lane adds n_pad / 64 terms of at most 4 roundings each, so a sum is within
-    // (n_pad / 64 + 4) 2^-24 of its absolute sum (the lane reduction is fp64); fsl doubles that.  Plus
-    // U itself in fp32 and the fp64 rounding of U = P x codes and of the host terms (far inside 1e-10
-    // of the magnitudes).  side[3 np + p] is the eff bound's slack.
+    // (n_pad / 64 + 4) 2^-24 of its absolute sum (the lane reduction is fp64); fsl doubles that.  U is
+    // stored in fp16: a normal value is within 2^-11 of U, relative, so the U terms (su, their magnitudes
+    // from the rounded values) are within 2^-10.9 su; a subnormal one within 2^-25 absolute, at most
+    // 2^-25 (|alpha| + |beta|) 4 n_pad in total (an overflow gives inf / NaN: the pair is kept).  Plus
+    // the fp64 rounding of U = P x codes and of the host terms (far inside 1e-10 of the magnitudes).
+    // side[3 np + p] is the eff bound's slack.
     const double fsl = 2.0 * (double)(n_pad / 64 + 8) * 0x1p-24;
     const double su = 2.0 * r[1] + 2.0 * fabs(dab) * r[3];
-    x.side[x.np + p] = fsl * (su + r[5]) + 1e-10 * (r[5] + su + fabs(t3) + fabs(t5) + fabs(t7) + fabs(t4) + fabs(t6));
+    x.side[x.np + p] = fsl * (su + r[5]) + 0x1p-10 * su + 0x1p-23 * (fabs(dal) + fabs(dbe)) * 4.0 * (double)n_pad +
+                       1e-10 * (r[5] + su + fabs(t3) + fabs(t5) + fabs(t7) + fabs(t4) + fabs(t6));
     x.side[2 * x.np + p] = r[6];
     x.side[3 * x.np + p] = (fsl + 1e-10) * r[7];
     x.side[4 * x.np + p] = r[8];
@@ -2575,37 +2667,39 @@ __global__ __launch_bounds__(PP * 8) void pair_mx_kernel(PairArgs x) {
   if (tid >= PP) return;
   const int64_t p = p0 + tid;
   if (p >= x.np) return;
-  const double M = (red[tid] + red[PP + tid]) + (red[2 * PP + tid] + red[3 * PP + tid]);
-  const double var = M + x.side[p], sw = x.side[4 * x.np + p];
-  const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
-  const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
-  if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
-    const unsigned long long k = atomicAdd(x.counter, 1ULL);
-    x.oi[k] = x.ci[p];
-    x.oj[k] = x.cj[p];
-  }
+  pair_test(x, p, (red[tid] + red[PP + tid]) + (red[2 * PP + tid] + red[3 * PP + tid]));
 }
 
 // The same quadratic form with each pair's w held in REGISTERS (n_pad <= 128 PXR_NK): a wave owns 32
 // pairs, lane (c, h) holds pair c's fp4 w for 32 individuals of every 64-individual chunk (the MFMA
 // B fragments, 4 registers per chunk), so 8 waves carry 256 pairs and the P tile images stream
-// through LDS once per 256 pairs (pair_mx_kernel: once per 96, from its LDS-resident w planes) in a
-// four-slot LDS-DMA ring, three tiles in flight.  Visit order: row block kb, then column stage cs from
+// through LDS once per 256 pairs (pair_mx_kernel: once per 96, from its LDS-resident w planes) in an
+// eight-slot LDS-DMA ring, six tiles in flight (the tiles compete for L2 with the pairs' record
+// gathers).  Visit order: row block kb, then column stage cs from
 // the last down to kb (the inner loop is unrolled so that every register index is static; its last
 // visit, the diagonal tile, folds the row block's accumulators with w of block kb, fetched from the
 // lane half that holds them).  Same operands, scales and test as pair_mx_kernel.
-constexpr int PXR_NK = 16;
+constexpr int PXR_NK = 16, PXR_NSL = 8;  // w chunks in registers (n_pad <= 2048); LDS ring slots
 __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
-  constexpr int NSL = 4, LA = 3;
+  constexpr int NSL = PXR_NSL, LA = PXR_NSL - 2;
   __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][MX_TILE];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nK = x.nK, N = nK * (nK + 1) / 2;
+  const int nK = x.nK;
+  // segment blockIdx.y of gridDim.y: the row blocks [kb_lo, kb_hi) holding its share of the tiles (a
+  // short candidate list is spread over more workgroups); partial sums to x.mpart (pair_test_kernel)
+  const int nseg = (int)gridDim.y, seg = (int)blockIdx.y, N_all = nK * (nK + 1) / 2;
+  auto toff = [&](int kb) __attribute__((always_inline)) { return kb * nK - kb * (kb - 1) / 2; };
+  int kb_lo = 0;
+  while (kb_lo < nK && toff(kb_lo) * nseg < N_all * seg) ++kb_lo;
+  int kb_hi = kb_lo;
+  while (kb_hi < nK && toff(kb_hi) * nseg < N_all * (seg + 1)) ++kb_hi;
+  const int N = toff(kb_hi) - toff(kb_lo);
   const int64_t p = (int64_t)blockIdx.x * 256 + 32 * w + c;
   const bool valid = p < x.np;
   v4i wf[2 * PXR_NK];
-  const uint8_t *ri = x.nib_i + (valid ? x.ci[p] : 0) * nK * NB_REC, *rj = x.nib_j + (valid ? x.cj[p] : 0) * nK * NB_REC;
   {
+    const uint8_t *ri = x.nib_i + (valid ? x.ci[p] : 0) * nK * NB_REC, *rj = x.nib_j + (valid ? x.cj[p] : 0) * nK * NB_REC;
 #pragma unroll
     for (int g = 0; g < 2 * PXR_NK; ++g) {
       v4i v = {0, 0, 0, 0};
@@ -2620,7 +2714,7 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
   }
   // tile ring: visit v reads slot v % NSL; the DMA of tile v + LA goes out at visit v into the slot
   // visit v - 1 read (every wave has passed visit v's barrier)
-  int kb_p = 0, cs_p = nK - 1, issued = 0;
+  int kb_p = kb_lo, cs_p = nK - 1, issued = 0;
   auto issue_next = [&]() __attribute__((always_inline)) {
     if (issued < N) {
       const uint8_t *src = x.tiles + (int64_t)(kb_p * nK + cs_p) * MX_TILE;
@@ -2640,20 +2734,15 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
   v16f_ acc[MX_RB];
   double tot = 0.0;
   int v = 0;
-  for (int kb = 0; kb < nK; ++kb) {
-    // w at this lane's fold rows (storage slots 32 r + 16 h .. + 15 of block kb), from the nibble planes
-    // (taken from wf the compiler would merge the fold copies into one with a dynamic register index)
-    v2i_ wfold[MX_RB];
-#pragma unroll
-    for (int r = 0; r < MX_RB; ++r) {
-      const int o = kb * NB_REC + 16 * r + 8 * h;
-      const v2i_ m1 = valid ? *(const v2i_ *)(ri + o) : v2i_{0, 0}, m2 = valid ? *(const v2i_ *)(ri + o + 64) : v2i_{0, 0};
-      const v2i_ s1 = valid ? *(const v2i_ *)(rj + o) : v2i_{0, 0};
-      wfold[r] = (m1 & s1) | (m2 & (s1 << 1));
-    }
+  for (int kb = kb_lo; kb < kb_hi; ++kb) {
 #pragma unroll
     for (int cs = PXR_NK - 1; cs >= 0; --cs) {
-      if (cs < nK && cs >= kb) {
+      // an opaque copy of kb per unrolled copy: with kb itself the compiler turns the copies' kb == cs
+      // tests into one switch and merges the fold copies into one block that indexes wf dynamically
+      // (through scratch)
+      int kq = kb;
+      asm volatile("" : "+s"(kq));
+      if (cs < nK && cs >= kq) {
         vm_wait_barrier(2 * min(LA - 1, N - 1 - v));  // tile v has landed (younger DMAs may be in flight)
         issue_next();
         const uint8_t *tb = sA[v % NSL];
@@ -2671,10 +2760,14 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
             acc[r] = mfma_mx(fa, fb, (first && kk == 0) ? zv : acc[r], hi[2], bs);
           }
         }
-        if (cs == kb) {  // row block kb complete: sum_rows w[row] acc[row] (register e <-> slot 16 h + e)
+        if (cs == kq) {  // row block kb complete: sum_rows w[row] acc[row] (register e <-> slot 16 h + e)
 #pragma unroll
           for (int r = 0; r < MX_RB; ++r) {
-            const unsigned m[2] = {(unsigned)wfold[r][0], (unsigned)wfold[r][1]};
+            const v4i src = wf[2 * cs + (r >> 1)];  // row tile r: lanes of half r & 1 hold its 32 slots
+            const int sl = c + 32 * (r & 1);
+            const int a0 = __shfl(src[0], sl), a1 = __shfl(src[1], sl), a2 = __shfl(src[2], sl),
+                      a3 = __shfl(src[3], sl);
+            const unsigned m[2] = {(unsigned)(h ? a2 : a0), (unsigned)(h ? a3 : a1)};
             v2f_ s2 = {0.f, 0.f};
 #pragma unroll
             for (int d = 0; d < 2; ++d) {
@@ -2694,15 +2787,17 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
   }
   tot += __shfl_xor(tot, 32);
   if (h || !valid) return;
-  const double M = tot;
-  const double var = M + x.side[p], sw = x.side[4 * x.np + p];
-  const double var_lo = var - x.rho * sw - x.side[x.np + p] - 1e-12 * fabs(M);
-  const double eff_hi = fabs(x.side[2 * x.np + p]) + x.side[3 * x.np + p];
-  if (!(var_lo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= x.chi_cut * var_lo) {
-    const unsigned long long k = atomicAdd(x.counter, 1ULL);
-    x.oi[k] = x.ci[p];
-    x.oj[k] = x.cj[p];
-  }
+  if (nseg > 1)
+    x.mpart[(int64_t)seg * x.np + p] = tot;
+  else
+    pair_test(x, p, tot);
+}
+__global__ void pair_test_kernel(PairArgs x, int nseg) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= x.np) return;
+  double M = 0.0;
+  for (int k = 0; k < nseg; ++k) M += x.mpart[(int64_t)k * x.np + p];
+  pair_test(x, p, M);
 }
 
 // ------------------------------------------------------------------ setup kernels
@@ -2760,9 +2855,9 @@ __global__ __launch_bounds__(256) void left_side_kernel(int64_t n_pad, const int
   for (int64_t q = threadIdx.x; q < n_pad; q += 256) {
     const double av = (double)panel[j * n_pad + q];
     const double u = U[j * n_pad + q];
-    Lp[j * n_pad + q] = av * (u - al * z[q]);
-    L3[j * n_pad + q] = av * py[q];
-    Ld[j * n_pad + q] = av * av * dg[q];
+    if (Lp) Lp[j * n_pad + q] = av * (u - al * z[q]);  // Lp, Ld: the block-granular screens only
+    if (L3) L3[j * n_pad + q] = av * py[q];
+    if (Ld) Ld[j * n_pad + q] = av * av * dg[q];
     s1 += av * u;
     s2 += av * z[q];
     s3 += av * py[q];
@@ -2795,7 +2890,7 @@ __global__ __launch_bounds__(256) void right_side_kernel(int64_t n_pad, const in
   for (int64_t q = threadIdx.x; q < n_pad; q += 256) {
     const double bv = (double)panel[j * n_pad + q];
     const double v = V[j * n_pad + q];
-    Rp[j * n_pad + q] = (bv - be) * v;
+    if (Rp) Rp[j * n_pad + q] = (bv - be) * v;
     s1 += bv * v;
     s2 += bv * z[q];
     s3 += bv * py[q];
@@ -3191,6 +3286,10 @@ __global__ void lr_adjust_kernel(int64_t m, int64_t R, const double *G, const do
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < m * R) out[idx] = (float)(G[idx] - soff[idx / R] * q1[idx % R]);
 }
+__global__ void f64_to_f16_kernel(int64_t count, const double *src, _Float16 *dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < count) dst[t] = (_Float16)src[t];  // |U| << 65504 (P entries ~ 1 / sigma, codes <= 2)
+}
 __global__ void f64_to_f32_kernel(int64_t count, const double *src, float *dst) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < count) dst[idx] = (float)src[idx];
@@ -3400,8 +3499,9 @@ __global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restric
 
 struct Coding {
   bool ready = false;
+  bool side_ready = false;        // Lq / Ldq / Rq built (block_sides)
   DBuf U;                         // P * screen code panel  [m][n_pad] (fp64, while the coding is built)
-  DBuf U32;                       // the same rounded to fp32 (pair screen side terms)
+  DBuf U16;                       // the same rounded to fp16 (pair screen side terms)
   DBuf off;                       // alpha/beta of the reference codes (refine) [m]
   DBuf soff;                      // centring offsets of the screen codes [m]
   DBuf sq;                        // squared screen codes (additive coding only) [m][n_pad]
@@ -3425,16 +3525,16 @@ struct Coding {
 struct Pinned {
   void *p = nullptr;
   size_t cap = 0;
-  ~Pinned() {
-    if (p) (void)hipHostFree(p);
-  }
+  ~Pinned() { pinned_free(p, cap); }
   int reserve(size_t n) {
     if (n <= cap) return GMAT_OK;
-    if (p) GMAT_HIP(hipHostFree(p));
+    pinned_free(p, cap);
     p = nullptr;
     cap = 0;
-    GMAT_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
-    cap = n;
+    size_t got = 0;
+    p = pinned_alloc(n, &got);
+    if (!p) return GMAT_E_NOMEM;
+    cap = got;
     return GMAT_OK;
   }
   template <class T>
@@ -3476,6 +3576,7 @@ struct gmat_epi {
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
   DBuf cand2_i, cand2_j, counter2, ps_side;  // pair screen survivors; its per-pair side terms
+  DBuf ps_mpart;                              // pair_mxr_kernel's segment partials
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
   std::vector<double> hit_eff, hit_var, hit_chi, hit_p;
@@ -3486,6 +3587,16 @@ struct gmat_epi {
   // [5] its fp6 x fp4 ops (R n_pad MACs x 2 per slot pair, empty slots included), [6] pair screen +
   // refine seconds at flush, [7] live pairs (GMAT_LIVE_COUNT) or -1
   double kstats[8] = {0};
+  // per-kernel timers of the candidate kernels (gmat_epi_kernel_stats_ext): HIP event pairs recorded on
+  // the kernel's stream around each launch, read after the scan; kernel ids KT_*
+  std::vector<hipEvent_t> kev;
+  size_t kev_used = 0;
+  struct KMark {
+    int kernel;
+    size_t ev;
+    double pairs;
+  };
+  std::vector<KMark> kmarks;
   // plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition,
   // [3] low-rank certificate, [4] slices + residual bounds, [5] coding builds (side vectors, lazily
   // in the first scan of a kind), [6] Cholesky factorisations run by the certificates
@@ -3511,6 +3622,7 @@ struct gmat_epi {
                                                 // (grown, never shrunk)
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
+    for (auto ev : kev) (void)hipEventDestroy(ev);
     if (s1) (void)hipStreamDestroy(s1);
     if (s2) (void)hipStreamDestroy(s2);
     if (s3) (void)hipStreamDestroy(s3);
@@ -3522,6 +3634,27 @@ namespace {
 
 // screen panel of a coding (inside e->spanels) and its squared codes (B operand of the Ld term)
 const int8_t *screen_panel(const gmat_epi *e, int which) { return e->spanels.as<int8_t>() + which * e->m * e->n_pad; }
+
+// kernel timers: kt_begin records the start event of a launch on st, kt_end its end event
+enum { KT_PAIR_SIDE = 0, KT_PAIR_MX = 1, KT_REFINE = 2, KT_REFINE_SIDE = 3, KT_N = 4 };
+int kt_event(gmat_epi *e, hipStream_t st, size_t *idx) {
+  if (e->kev_used == e->kev.size()) {
+    hipEvent_t ev;
+    GMAT_HIP(hipEventCreate(&ev));
+    e->kev.push_back(ev);
+  }
+  *idx = e->kev_used++;
+  GMAT_HIP(hipEventRecord(e->kev[*idx], st));
+  return GMAT_OK;
+}
+int kt_begin(gmat_epi *e, hipStream_t st, size_t *idx) { return kt_event(e, st, idx); }
+int kt_end(gmat_epi *e, hipStream_t st, int kernel, size_t beg, double pairs) {
+  size_t end;
+  GMAT_TRY(kt_event(e, st, &end));
+  e->kmarks.push_back({kernel, beg, pairs});  // marks come in (start, end) pairs
+  e->kmarks.push_back({-1, end, 0.0});
+  return GMAT_OK;
+}
 const int8_t *screen_sq(const gmat_epi *e, int which) {
   return which == 0 ? e->code[0].sq.as<int8_t>() : screen_panel(e, 1);  // 0/1 codes: a^2 = a
 }
@@ -3571,16 +3704,14 @@ int build_coding_impl(gmat_epi *e, int which) {
     GMAT_HIP(hipMemcpyAsync(panel, e->g->het_ptr(), (size_t)m * n_pad, hipMemcpyDeviceToDevice, e->s));
   }
   const size_t vb = (size_t)m * n_pad * sizeof(double);
-  DBuf Lp, L3, Ld, Rp;  // fp64 side vectors, sliced to int8 below
+  DBuf L3;  // fp64 side vector L3 = a o Py, sliced to int8 below (L', Ld, R' of the block-granular
+            // screens: block_sides, when a scan first needs them)
   GMAT_TRY(cd.U.alloc(vb));
-  GMAT_TRY(Lp.alloc(vb));
   GMAT_TRY(L3.alloc(vb));
-  GMAT_TRY(Ld.alloc(vb));
-  GMAT_TRY(Rp.alloc(vb));
   for (DBuf *b : {&cd.off, &cd.soff, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb, &cd.sL, &cd.sL3, &cd.sLd, &cd.sR,
                   &cd.csum, &cd.csq})
     GMAT_TRY(b->alloc(m * sizeof(double)));
-  for (DBuf *b : {&cd.Lq, &cd.L3q, &cd.Ldq, &cd.Rq}) GMAT_TRY(b->alloc((size_t)SIDE_T * m * n_pad));
+  GMAT_TRY(cd.L3q.alloc((size_t)SIDE_T * m * n_pad));
   GMAT_HIP(hipMemcpy(cd.csum.p, csum.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.csq.p, csq.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_TRY(cd.mono.alloc(m));
@@ -3591,22 +3722,16 @@ int build_coding_impl(gmat_epi *e, int which) {
   GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
                      cd.U.as<double>(), n_pad));
   hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), e->dg.as<double>(), cd.soff.as<double>(), Lp.as<double>(),
-                     L3.as<double>(), Ld.as<double>(), cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
+                     e->z.as<double>(), e->py.as<double>(), e->dg.as<double>(), cd.soff.as<double>(), nullptr,
+                     L3.as<double>(), nullptr, cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
   GMAT_HIP(hipGetLastError());
   hipLaunchKernelGGL(right_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
-                     e->z.as<double>(), e->py.as<double>(), cd.soff.as<double>(), Rp.as<double>(),
-                     cd.qb.as<double>(), cd.rb.as<double>(), cd.sb.as<double>());
+                     e->z.as<double>(), e->py.as<double>(), cd.soff.as<double>(), nullptr, cd.qb.as<double>(),
+                     cd.rb.as<double>(), cd.sb.as<double>());
   GMAT_HIP(hipGetLastError());
   const int64_t ss = m * n_pad;
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Lp.as<double>(),
-                     cd.Lq.as<int8_t>(), cd.sL.as<double>());
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, L3.as<double>(),
                      cd.L3q.as<int8_t>(), cd.sL3.as<double>());
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Ld.as<double>(),
-                     cd.Ldq.as<int8_t>(), cd.sLd.as<double>());
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
-                     cd.Rq.as<int8_t>(), cd.sR.as<double>());
   GMAT_HIP(hipGetLastError());
   GMAT_TRY(cd.p4.alloc((size_t)m * n_pad / 2));
   hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
@@ -3665,9 +3790,9 @@ int build_coding_impl(gmat_epi *e, int which) {
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipStreamSynchronize(e->s));
   }
-  GMAT_TRY(cd.U32.alloc((size_t)m * n_pad * sizeof(float)));
-  hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)cdiv(m * n_pad, 256)), dim3(256), 0, e->s, m * n_pad,
-                     cd.U.as<double>(), cd.U32.as<float>());
+  GMAT_TRY(cd.U16.alloc((size_t)m * n_pad * sizeof(_Float16)));
+  hipLaunchKernelGGL(f64_to_f16_kernel, dim3((unsigned)cdiv(m * n_pad, 256)), dim3(256), 0, e->s, m * n_pad,
+                     cd.U.as<double>(), cd.U16.as<_Float16>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipStreamSynchronize(e->s));
   // (U = P x codes stays in fp64: the int8 refine's O(n) terms, refine8_side_kernel)
@@ -3696,21 +3821,42 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
   if (np <= 0) return GMAT_OK;
   if (refine8_fits(e) && L.U.p && R.U.p) {
     GMAT_TRY(refine8_setup(e));
-    if (e->r8_varw.bytes < (size_t)np * sizeof(double)) {
-      GMAT_HIP(hipStreamSynchronize(st));  // an earlier refine queued on st may still use the old buffer
-      GMAT_TRY(e->r8_varw.alloc((size_t)np * sizeof(double)));
+    // segments: short lists spread over more workgroups (one workgroup per CU holds its LDS ring)
+    if (!e->n_cu) {
+      int dev = 0, cus = 0;
+      GMAT_HIP(hipGetDevice(&dev));
+      GMAT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      e->n_cu = std::max(cus, 8);
     }
+    const int64_t wgs = cdiv(np, R8_PP);
+    const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(seg_max(), e->n_cu / wgs));
+    const size_t need = (size_t)np * sizeof(double) * (nseg > 1 ? 1 + R8_S * nseg : 1);
+    if (e->r8_varw.bytes < need) {
+      GMAT_HIP(hipStreamSynchronize(st));  // an earlier refine queued on st may still use the old buffer
+      GMAT_TRY(e->r8_varw.alloc(std::max(need, (size_t)np * sizeof(double) * (1 + R8_S * 8))));
+    }
+    double *tpart = e->r8_varw.as<double>() + np;
     const int li = (int)(&L - e->code), ri = (int)(&R - e->code);
     const int8_t *sl = screen_panel(e, li), *sr = screen_panel(e, ri);
-    hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)cdiv(np, R8_PP)), dim3(512), 0, st, e->n_pad,
-                       e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>());
+    size_t kt0;
+    GMAT_TRY(kt_begin(e, st, &kt0));
+    hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
+                       e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>(), tpart);
     GMAT_HIP(hipGetLastError());
+    if (nseg > 1) {
+      hipLaunchKernelGGL(r8_combine_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, nseg, tpart,
+                         e->r8_unit, e->r8_varw.as<double>());
+      GMAT_HIP(hipGetLastError());
+    }
+    GMAT_TRY(kt_end(e, st, KT_REFINE, kt0, (double)np));
+    GMAT_TRY(kt_begin(e, st, &kt0));
     hipLaunchKernelGGL(refine8_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, e->n_pad, sl, sr,
                        L.U.as<double>(), R.U.as<double>(), e->z.as<double>(), e->dg.as<double>(), e->py.as<double>(), lp,
                        rp, L.soff.as<double>(), R.soff.as<double>(), L.off.as<double>(), R.off.as<double>(),
                        L.qa.as<double>(), L.ra.as<double>(), R.qb.as<double>(), R.rb.as<double>(), e->zz,
                        L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj, np, e->r8_varw.as<double>(), eff, var);
     GMAT_HIP(hipGetLastError());
+    GMAT_TRY(kt_end(e, st, KT_REFINE_SIDE, kt0, (double)np));
     hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
     GMAT_HIP(hipGetLastError());
     return GMAT_OK;
@@ -3762,12 +3908,12 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   const int pp_cap = getenv("GMAT_PS_PP") ? atoi(getenv("GMAT_PS_PP")) : 96;
   const int pp = (pp_cap >= 96 && lds_of(96) <= 160 * 1024 - 256) ? 96 : (lds_of(64) <= 160 * 1024 - 256 && pp_cap >= 64) ? 64 : 32;
   GMAT_CHECK(nK <= 63, GMAT_E_ARG, "pair screen: %d stages exceed the LDS", nK);
-  GMAT_CHECK(L.U32.p && R.U32.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
+  GMAT_CHECK(L.U16.p && R.U16.p && L.nibI.p && R.nibJ.p && e->mx_tiles.p && e->z.p && e->dg.p && e->py.p && L.qa.p &&
                  R.qb.p && e->cand2_i.p && e->cand2_j.p && e->counter2.p &&
-                 e->cand2_i.bytes >= (size_t)np * 8 && L.U32.bytes >= (size_t)e->m * e->n_pad * 4 &&
-                 R.U32.bytes >= (size_t)e->m * e->n_pad * 4 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
-             GMAT_E_ARG, "pair screen: plan buffers missing (U32 %d %d nib %d %d mx %zu z %d cand2 %zu / %lld counter2 %d)",
-             L.U32.p != nullptr, R.U32.p != nullptr, L.nibI.p != nullptr, R.nibJ.p != nullptr, e->mx_tiles.bytes,
+                 e->cand2_i.bytes >= (size_t)np * 8 && L.U16.bytes >= (size_t)e->m * e->n_pad * 2 &&
+                 R.U16.bytes >= (size_t)e->m * e->n_pad * 2 && e->mx_tiles.bytes >= (size_t)nK * nK * MX_TILE,
+             GMAT_E_ARG, "pair screen: plan buffers missing (U16 %d %d nib %d %d mx %zu z %d cand2 %zu / %lld counter2 %d)",
+             L.U16.p != nullptr, R.U16.p != nullptr, L.nibI.p != nullptr, R.nibJ.p != nullptr, e->mx_tiles.bytes,
              e->z.p != nullptr, e->cand2_i.bytes, (long long)np, e->counter2.p != nullptr);
   // the side-term buffer is sized for the largest call once (calls queued on one stream share it)
   if (e->ps_side.bytes < (size_t)5 * np * sizeof(double)) {
@@ -3782,8 +3928,8 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
   x.n_pad = e->n_pad;
   x.a = slp;
   x.b = srp;
-  x.Ua = L.U32.as<float>();
-  x.Ub = R.U32.as<float>();
+  x.Ua = L.U16.as<_Float16>();
+  x.Ub = R.U16.as<_Float16>();
   x.alpha = L.soff.as<double>();
   x.beta = R.soff.as<double>();
   x.qa = L.qa.as<double>();
@@ -3820,18 +3966,41 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
                                  160 * 1024 - 256));
     attr = true;
   }
+  size_t kt0;
+  GMAT_TRY(kt_begin(e, st, &kt0));
   hipLaunchKernelGGL(pair_side_kernel, dim3((unsigned)cdiv(np, 4 * PS_PPW)), dim3(256),
                      (size_t)3 * e->n_pad * sizeof(float), st, x);
   GMAT_HIP(hipGetLastError());
-  if (nK <= PXR_NK && !getenv("GMAT_PS_OLD"))  // w in registers: 256 pairs per workgroup
-    hipLaunchKernelGGL(pair_mxr_kernel, dim3((unsigned)cdiv(np, 256)), dim3(512), 0, st, x);
-  else if (pp == 96)
+  GMAT_TRY(kt_end(e, st, KT_PAIR_SIDE, kt0, (double)np));
+  GMAT_TRY(kt_begin(e, st, &kt0));
+  if (nK <= PXR_NK && !getenv("GMAT_PS_OLD")) {  // w in registers: 256 pairs per workgroup
+    // a short list in row-block segments over more workgroups (one per CU holds its LDS ring)
+    if (!e->n_cu) {
+      int dev = 0, cus = 0;
+      GMAT_HIP(hipGetDevice(&dev));
+      GMAT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      e->n_cu = std::max(cus, 8);
+    }
+    const int64_t wgs = cdiv(np, 256);
+    const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(seg_max(), nK), e->n_cu / wgs));
+    if (nseg > 1 && e->ps_mpart.bytes < (size_t)nseg * np * sizeof(double)) {
+      GMAT_HIP(hipStreamSynchronize(st));
+      GMAT_TRY(e->ps_mpart.alloc((size_t)8 * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
+    }
+    x.mpart = e->ps_mpart.as<double>();
+    hipLaunchKernelGGL(pair_mxr_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, x);
+    if (nseg > 1) {
+      GMAT_HIP(hipGetLastError());
+      hipLaunchKernelGGL(pair_test_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, x, nseg);
+    }
+  } else if (pp == 96)
     hipLaunchKernelGGL(pair_mx_kernel<96>, dim3((unsigned)cdiv(np, 96)), dim3(768), lds, st, x);
   else if (pp == 64)
     hipLaunchKernelGGL(pair_mx_kernel<64>, dim3((unsigned)cdiv(np, 64)), dim3(512), lds, st, x);
   else
     hipLaunchKernelGGL(pair_mx_kernel<32>, dim3((unsigned)cdiv(np, 32)), dim3(256), lds, st, x);
   GMAT_HIP(hipGetLastError());
+  GMAT_TRY(kt_end(e, st, KT_PAIR_MX, kt0, (double)np));
   }
   if (!n_out) return GMAT_OK;
   GMAT_HIP(hipMemcpyAsync(e->pins.count2.p, e->counter2.p, 8, hipMemcpyDeviceToHost, st));
@@ -4683,6 +4852,40 @@ struct ScanSide {
   const int8_t *slp = nullptr, *srp = nullptr;  // screen codes
 };
 
+// the block-granular screens' side vectors of a built coding (int8 slices of L' = a o (Pa - alpha z),
+// Ld = a^2 o diag(P) and R' = (b - beta) o Pb), made when a scan first uses those screens
+int block_sides(gmat_epi *e, int which) {
+  Coding &cd = e->code[which];
+  if (cd.side_ready) return GMAT_OK;
+  const int64_t m = e->m, n_pad = e->n_pad, ss = m * n_pad;
+  const size_t vb = (size_t)m * n_pad * sizeof(double);
+  const int8_t *panel = screen_panel(e, which);
+  DBuf Lp, Ld, Rp;
+  GMAT_TRY(Lp.alloc(vb));
+  GMAT_TRY(Ld.alloc(vb));
+  GMAT_TRY(Rp.alloc(vb));
+  for (DBuf *b : {&cd.Lq, &cd.Ldq, &cd.Rq}) GMAT_TRY(b->alloc((size_t)SIDE_T * m * n_pad));
+  DBuf scratch;  // the kernels' per-SNP scalars again (discarded: the coding has them)
+  GMAT_TRY(scratch.alloc((size_t)6 * m * sizeof(double)));
+  double *sc = scratch.as<double>();
+  hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), e->dg.as<double>(), cd.soff.as<double>(), Lp.as<double>(),
+                     nullptr, Ld.as<double>(), sc, sc + m, sc + 2 * m);
+  hipLaunchKernelGGL(right_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
+                     e->z.as<double>(), e->py.as<double>(), cd.soff.as<double>(), Rp.as<double>(), sc + 3 * m,
+                     sc + 4 * m, sc + 5 * m);
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Lp.as<double>(),
+                     cd.Lq.as<int8_t>(), cd.sL.as<double>());
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Ld.as<double>(),
+                     cd.Ldq.as<int8_t>(), cd.sLd.as<double>());
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, Rp.as<double>(),
+                     cd.Rq.as<int8_t>(), cd.sR.as<double>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_HIP(hipStreamSynchronize(e->s));
+  cd.side_ready = true;
+  return GMAT_OK;
+}
+
 // builds the codings `kind` needs and clears the previous scan's hits and counters
 int scan_begin(gmat_epi *e, int kind, ScanSide *c) {
   kind_codings(kind, &c->lc, &c->rc);
@@ -4697,6 +4900,8 @@ int scan_begin(gmat_epi *e, int kind, ScanSide *c) {
   c->tri = kind != GMAT_AD;
   for (double &v : e->stats) v = 0.0;
   for (double &v : e->kstats) v = 0.0;
+  e->kev_used = 0;
+  e->kmarks.clear();
   for (auto *v : {&e->hit_i, &e->hit_j}) v->clear();
   for (auto *v : {&e->hit_eff, &e->hit_var, &e->hit_chi, &e->hit_p}) v->clear();
   return GMAT_OK;
@@ -4992,8 +5197,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_TRY(B.cnt[b].alloc(rl * sizeof(int)));
       GMAT_TRY(B.soff[b].alloc(rl * sizeof(int)));
       GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
-      GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(rl, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
-      GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(rl, PF_TR) * (cdiv(m, PF_TC) + 1) * sizeof(int)));
+      GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(rl, PC_TR) * (cdiv(m, PC_TC) + 1) * sizeof(int)));  // PC tiles: the most
+      GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(rl, PC_TR) * (cdiv(m, PC_TC) + 1) * sizeof(int)));
       GMAT_TRY(e->pins.rows[b].reserve(rl * 8));
       GMAT_TRY(e->pins.cnt[b].reserve(8));
       GMAT_TRY(e->pins.t2[b].reserve(32));
@@ -5078,7 +5283,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
     GMAT_HIP(hipMemsetAsync(B.lmask[b].p, 0, (size_t)Rn * nJ * 4, S2));
     GMAT_HIP(hipMemsetAsync(B.opc[b].p, 0, 16, S2));
-    SideArgs x;
+    SideArgs x{};
     ScreenArgs &a = x.a;
     std::memset(&a, 0, sizeof(a));
     a.n_pad = n_pad;
@@ -5186,13 +5391,42 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     } else {
       for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
       x.n_rt = (int)cdiv(Rn, PC_TR);
-      const dim3 gp((unsigned)(x.n_rt * cdiv(ncols, PC_TC)));
-      switch (e->pf_ncov) {
-        case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, gp, dim3(512), 0, S2, x); break;
-        case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, gp, dim3(512), 0, S2, x); break;
-        case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, gp, dim3(512), 0, S2, x); break;
-        default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, gp, dim3(512), 0, S2, x); break;
+      // the running 64 x 128 tiles in blocks of 4 row x 8 column tiles (as the intercept-only prefilter's
+      // list), a persistent grid of one workgroup per CU over them (GMAT_PF_NOLIST: one per tile)
+      int *tl = e->pins.tl[b].as<int>();
+      int run = 0;
+      const int64_t n_ct = cdiv(ncols, PC_TC);
+      for (int rg = 0; rg < x.n_rt; rg += 4)
+        for (int64_t cg = 0; cg < n_ct; cg += 8)
+          for (int64_t ct = cg; ct < std::min(n_ct, cg + 8); ++ct)
+            for (int rt = rg; rt < std::min(x.n_rt, rg + 4); ++rt) {
+              const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PC_TC;
+              if (c0 < m && !(tri && c0 + PC_TC - 1 <= ln.rows[rt * PC_TR])) tl[run++] = rt + x.n_rt * (int)ct;
+            }
+      // MFMA work per pair: 4 fp4 code products + (2 + K0) int8 products over n_pad individuals
+      pf_ops_of[li] = (double)run * PC_TR * PC_TC * (8.0 + 4.0 * (2 + e->pf_ncov)) * (double)n_pad;
+      GMAT_HIP(hipEventRecord(pf_beg[b], S2));
+      if (run > 0 && pf_list) {
+        GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
+        x.tile_list = B.tlist[b].as<int>();
+        x.n_list = run;
+        const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pf_wg ? pf_wg : e->n_cu, 8), cdiv(run, 8))));
+        switch (e->pf_ncov) {
+          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, true>), gp, dim3(512), 0, S2, x); break;
+          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, true>), gp, dim3(512), 0, S2, x); break;
+          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, true>), gp, dim3(512), 0, S2, x); break;
+          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, true>), gp, dim3(512), 0, S2, x); break;
+        }
+      } else if (run > 0) {
+        const dim3 gp((unsigned)(x.n_rt * n_ct));
+        switch (e->pf_ncov) {
+          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false>), gp, dim3(512), 0, S2, x); break;
+          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false>), gp, dim3(512), 0, S2, x); break;
+          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, false>), gp, dim3(512), 0, S2, x); break;
+          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, false>), gp, dim3(512), 0, S2, x); break;
+        }
       }
+      GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
     GMAT_HIP(hipGetLastError());
     hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
@@ -5399,6 +5633,12 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   ScanSide c;
   GMAT_TRY(scan_begin(e, kind, &c));
   const int lc = c.lc, rc = c.rc;
+  {
+    const double t0 = now();
+    GMAT_TRY(block_sides(e, lc));
+    GMAT_TRY(block_sides(e, rc));
+    e->setup[5] += now() - t0;
+  }
   const Coding &L = *c.L, &R = *c.R;
   const int8_t *slp = c.slp, *srp = c.srp, *srq = screen_sq(e, rc), *slq = screen_sq(e, lc);  // screen codes
   const int tri = c.tri;
@@ -5604,7 +5844,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
       GMAT_HIP(hipMemcpyAsync(drows[b].p, pin_rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
       GMAT_HIP(hipEventRecord(side_beg[b], S2));
       GMAT_HIP(hipMemsetAsync(flags[b].p, 0, (size_t)Rn * nJ, S2));
-      SideArgs x;
+      SideArgs x{};
       x.a = make_args(li, b);
       x.n_pad = n_pad;
       x.blocked = 0;
@@ -5635,10 +5875,10 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.n_rt = (int)cdiv(Rn, PC_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PC_TC));
         switch (e->pf_ncov) {
-          case 1: hipLaunchKernelGGL(prefilter_cov_kernel<1>, dim3(gp), dim3(512), 0, S2, xp); break;
-          case 2: hipLaunchKernelGGL(prefilter_cov_kernel<2>, dim3(gp), dim3(512), 0, S2, xp); break;
-          case 3: hipLaunchKernelGGL(prefilter_cov_kernel<3>, dim3(gp), dim3(512), 0, S2, xp); break;
-          default: hipLaunchKernelGGL(prefilter_cov_kernel<4>, dim3(gp), dim3(512), 0, S2, xp); break;
+          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false>), dim3(gp), dim3(512), 0, S2, xp); break;
+          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false>), dim3(gp), dim3(512), 0, S2, xp); break;
+          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, false>), dim3(gp), dim3(512), 0, S2, xp); break;
+          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, false>), dim3(gp), dim3(512), 0, S2, xp); break;
         }
       }
       GMAT_HIP(hipGetLastError());
@@ -6063,6 +6303,23 @@ extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, d
 extern "C" int gmat_epi_kernel_stats(const gmat_epi *e, double *out8) {
   GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_kernel_stats: bad arguments");
   for (int k = 0; k < 8; ++k) out8[k] = e->kstats[k];
+  return GMAT_OK;
+}
+
+extern "C" int gmat_epi_kernel_stats_ext(const gmat_epi *e, double *out, int cap, int *count) {
+  GMAT_CHECK(e && out && count && cap >= 0, GMAT_E_ARG, "gmat_epi_kernel_stats_ext: bad arguments");
+  double v[3 * KT_N] = {0};
+  for (size_t k = 0; k + 1 < e->kmarks.size(); k += 2) {
+    const auto &b = e->kmarks[k], &en = e->kmarks[k + 1];
+    float ms = 0.f;
+    GMAT_HIP(hipEventSynchronize(e->kev[en.ev]));
+    GMAT_HIP(hipEventElapsedTime(&ms, e->kev[b.ev], e->kev[en.ev]));
+    v[3 * b.kernel] += ms * 1e-3;
+    v[3 * b.kernel + 1] += 1.0;
+    v[3 * b.kernel + 2] += b.pairs;
+  }
+  *count = 3 * KT_N;
+  for (int k = 0; k < std::min(cap, 3 * KT_N); ++k) out[k] = v[k];
   return GMAT_OK;
 }
 

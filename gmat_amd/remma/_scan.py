@@ -102,6 +102,18 @@ class EpiPlan:
                 "flush_s", "live_pairs")
         return dict(zip(keys, s.tolist()))
 
+    def kernel_stats_ext(self):
+        """The candidate kernels of the last scan (gmat_epi_kernel_stats_ext): seconds, launches and pairs
+        of pair_side, pair_mx, refine and refine_side."""
+        s = np.zeros(12)
+        cnt = ctypes.c_int()
+        N.check(self._lib.gmat_epi_kernel_stats_ext(self._h, N.ptr(s), s.size, ctypes.byref(cnt)),
+                "gmat_epi_kernel_stats_ext")
+        out = {}
+        for k, name in enumerate(("pair_side", "pair_mx", "refine", "refine_side")):
+            out[name] = {"s": float(s[3 * k]), "launches": float(s[3 * k + 1]), "pairs": float(s[3 * k + 2])}
+        return out
+
     def setup_stats(self):
         """Plan setup seconds (gmat_epi_setup_stats): create total, prefilter certificate,
         eigendecomposition, low-rank certificate, slices/residual bounds, coding builds, and

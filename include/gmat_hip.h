@@ -137,6 +137,10 @@ int gmat_epi_stats(const gmat_epi *e, double *out10);
  * 2 x int8 ops), [3] low-rank screen seconds, [4] its launches, [5] its fp6 x fp4 ops, [6] pair screen
  * + refine seconds at flush, [7] pairs kept by the prefilter (GMAT_LIVE_COUNT set) or -1 */
 int gmat_epi_kernel_stats(const gmat_epi *e, double *out8);
+/* the candidate kernels of the last scan, timed with HIP events on their streams: per kernel
+ * (pair_side, pair_mx, refine, refine_side) seconds, launches and pairs, in that order; up to cap
+ * values, *count = 12 */
+int gmat_epi_kernel_stats_ext(const gmat_epi *e, double *out, int cap, int *count);
 /* Diagnostic: the certified lower bounds of e'Pe that the screens test with, evaluated exactly in
  * fp64 for listed pairs (i, j) (e = the screen codes' centred product over the real individuals):
  * out5[5 t ..] = {prefilter bound, low-rank bound, |e|^2, 1'e, |Q'e|^2} (-inf where the plan has no

@@ -20,10 +20,34 @@ for st in "$@"; do
     quick)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/quick.json 2> $OUT/quick.log || { tail -30 $OUT/quick.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/quick.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
+    pmc)
+      # counter passes of the six scan kernels (one rocprofv3 run per counter group) and their traffic
+      # records keyed by epi.hip's sha256 (bench.py attaches them to roofline.kernels)
+      K="prefilter_pass_kernel|lrc_screen_kernel|pair_side_kernel|pair_mxr_kernel|refine8_kernel|refine8_side_kernel"
+      KEY="$K" bash tools/pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+      for k in prefilter_pass_kernel lrc_screen_kernel pair_side_kernel pair_mxr_kernel refine8_kernel refine8_side_kernel; do
+        python3 tools/pmc_summary.py $OUT/pmc $k --out $OUT/traffic_$k.json --level -1 --rank 128 --n-id 2000 --n-snp 50000 > $OUT/pmc_$k.txt || exit 1
+        tail -12 $OUT/pmc_$k.txt
+      done ;;
+    part)
+      # one rank's part of the 8-way split (rank 0), traced: the timeline of a multi-GPU step
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/part -o run -- python3 tools/split_part.py 0 8 5 > $OUT/part.log 2>&1 || { tail -30 $OUT/part.log; exit 1; }
+      grep "part 0" $OUT/part.log | tail -3
+      python3 tools/step_timeline.py $(find $OUT/part -name "*kernel_trace.csv" | head -1) | tee $OUT/part_timeline.txt ;;
+    cov)
+      timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --covariates --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/cov.json 2> $OUT/cov.log || { tail -30 $OUT/cov.log; exit 1; }
+      python -c "import json; d=json.load(open('$OUT/cov.json')); print('covariates: value %.4g ms %.2f' % (d['value'], d['ms_per_step']))" ;;
+    covtests)
+      timeout -k 10 500 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_parity.py tests/test_gpu_workflow.py -x -q --timeout 300 --timeout-method thread > $OUT/covtests.log 2>&1 || { tail -40 $OUT/covtests.log; exit 1; }
+      tail -2 $OUT/covtests.log ;;
     cfg5|cfg5f0|cfg5f2|cfg5f10)
       FS=5; case $st in cfg5f0) FS=0;; cfg5f2) FS=2;; cfg5f10) FS=10;; esac
       timeout -k 10 600 python -u bench.py --config cfg5 --family-size $FS --cfg5-reps ${CFG5_REPS:-3} > $OUT/$st.json 2> $OUT/$st.log || { tail -30 $OUT/$st.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/$st.json')); r=d['reml']; print('$st', 'value %.3g' % d['value'], 'iters', r['iters'], 'var', [round(v, 4) for v in r['var']], 'grad', r.get('grad_norm_last5'), 'upd', r.get('update_norm_last5'), 'emw', r.get('em_weight_last5'), 'DD cand', d['epiDD']['candidates'], 'AD cand', d['epiAD']['candidates'], 'DD s', d['epiDD']['s'])" ;;
+    covprof)
+      # kernel trace of the covariate step (prefilter_cov_kernel) and its timeline
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/covprof -o run -- python3 bench.py --steps 3 --warmup 1 --covariates --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/covprof_bench.json 2> $OUT/covprof.log || { tail -30 $OUT/covprof.log; exit 1; }
+      python3 tools/step_timeline.py $(find $OUT/covprof -name "*kernel_trace.csv" | head -1) | tee $OUT/covprof_timeline.txt ;;
     prof|serial)
       # kernel trace + stats of a short scan run and the step timeline of its last step; serial: the
       # same with kernels serialised (AMD_SERIALIZE_KERNEL=3), so the per-kernel sums are standalone times

@@ -17,7 +17,7 @@ def main():
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in csv.DictReader(open(path)))
     rf = [k for k, e in enumerate(ev) if e[2].startswith(("refine_kernel", "refine8_side_kernel"))]
-    pf = [k for k, e in enumerate(ev) if e[2].startswith("prefilter_pass")]
+    pf = [k for k, e in enumerate(ev) if e[2].startswith(("prefilter_pass", "prefilter_cov"))]
     if len(sys.argv) > 2:
         pf = pf[-int(sys.argv[2]):]
     elif len(rf) >= 2:  # the last step: the passes after the previous step's refine
