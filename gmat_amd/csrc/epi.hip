@@ -3576,6 +3576,7 @@ struct gmat_epi {
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
   DBuf cand2_i, cand2_j, counter2, ps_side;  // pair screen survivors; its per-pair side terms
+  DBuf cpack;                                 // refined candidates packed for the read-back
   DBuf ps_mpart;                              // pair_mxr_kernel's segment partials
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
@@ -3591,6 +3592,7 @@ struct gmat_epi {
   // the kernel's stream around each launch, read after the scan; kernel ids KT_*
   std::vector<hipEvent_t> kev;
   size_t kev_used = 0;
+  std::vector<hipEvent_t> sev;  // the scans' pipeline events (ScanEvents), created once
   struct KMark {
     int kernel;
     size_t ev;
@@ -3623,6 +3625,7 @@ struct gmat_epi {
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     for (auto ev : kev) (void)hipEventDestroy(ev);
+    for (auto ev : sev) (void)hipEventDestroy(ev);
     if (s1) (void)hipStreamDestroy(s1);
     if (s2) (void)hipStreamDestroy(s2);
     if (s3) (void)hipStreamDestroy(s3);
@@ -4973,6 +4976,19 @@ struct RefineTally {
 // [ps_done, hi) (those in [lo, ps_done) were pair-screened into cand2 beside the launches), the exact
 // fp64 refine of the survivors, and the hits p < p_cut appended to the plan's lists.  Candidates
 // below hi are free afterwards.
+// [i | j | eff | var | chi | p] of n refined candidates in one buffer (one read-back copy)
+__global__ void cand_pack_kernel(int64_t n, const int64_t *ci, const int64_t *cj, const double *eff, const double *var,
+                                 const double *chi, const double *p, double *out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  ((int64_t *)out)[k] = ci[k];
+  ((int64_t *)out)[n + k] = cj[k];
+  out[2 * n + k] = eff[k];
+  out[3 * n + k] = var[k];
+  out[4 * n + k] = chi[k];
+  out[5 * n + k] = p[k];
+}
+
 int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, int64_t lo, int64_t hi, int64_t ps_done,
                    double chi_cut, double p_cut, hipEvent_t beg, hipEvent_t end, RefineTally *tl) {
   if (hi <= lo) return GMAT_OK;
@@ -4995,12 +5011,16 @@ int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, 
     GMAT_TRY(pin.reserve((size_t)nf * 48));
     int64_t *ci = pin.as<int64_t>(), *cj = ci + nf;
     double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cq = cc + nf;
-    GMAT_HIP(hipMemcpyAsync(ci, fi, nf * 8, hipMemcpyDeviceToHost, st));
-    GMAT_HIP(hipMemcpyAsync(cj, fj, nf * 8, hipMemcpyDeviceToHost, st));
-    GMAT_HIP(hipMemcpyAsync(ce, e->ceff.p, nf * 8, hipMemcpyDeviceToHost, st));
-    GMAT_HIP(hipMemcpyAsync(cv, e->cvar.p, nf * 8, hipMemcpyDeviceToHost, st));
-    GMAT_HIP(hipMemcpyAsync(cc, e->cchi.p, nf * 8, hipMemcpyDeviceToHost, st));
-    GMAT_HIP(hipMemcpyAsync(cq, e->cp.p, nf * 8, hipMemcpyDeviceToHost, st));
+    // the six candidate arrays packed on the device and read back in one copy (six copies cost ~0.1 ms
+    // of a step: each is a round trip)
+    if (e->cpack.bytes < (size_t)nf * 48) {
+      GMAT_HIP(hipStreamSynchronize(st));
+      GMAT_TRY(e->cpack.alloc((size_t)std::max<int64_t>(nf, 1 << 16) * 48));
+    }
+    hipLaunchKernelGGL(cand_pack_kernel, dim3((unsigned)cdiv(nf, 256)), dim3(256), 0, st, nf, fi, fj, e->ceff.as<double>(),
+                       e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>(), e->cpack.as<double>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_HIP(hipMemcpyAsync(ci, e->cpack.p, (size_t)nf * 48, hipMemcpyDeviceToHost, st));
     GMAT_HIP(hipEventRecord(end, st));
     GMAT_HIP(hipStreamSynchronize(st));
     for (int64_t k = 0; k < nf; ++k)
@@ -5043,14 +5063,18 @@ int64_t sort_hits(gmat_epi *e) {
 }
 
 // owner of the events a scan creates
+// a scan's pipeline events, handed out from the plan's pool (event creation costs ~10 us each: ~0.2 ms
+// of host time per scan when the compacted scan created its 20 per call)
 struct ScanEvents {
-  std::vector<hipEvent_t> v;
-  ~ScanEvents() {
-    for (auto x : v) (void)hipEventDestroy(x);
-  }
+  gmat_epi *e;
+  size_t used = 0;
   int make(hipEvent_t *x) {
-    GMAT_HIP(hipEventCreate(x));
-    v.push_back(*x);
+    if (used == e->sev.size()) {
+      hipEvent_t ev;
+      GMAT_HIP(hipEventCreate(&ev));
+      e->sev.push_back(ev);
+    }
+    *x = e->sev[used++];
     return GMAT_OK;
   }
 };
@@ -5071,7 +5095,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   GMAT_TRY(drows.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
   GMAT_TRY(doffs.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
   GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
-  ScanEvents evs;
+  ScanEvents evs{e};
   hipEvent_t ev0, ev1;
   GMAT_TRY(evs.make(&ev0));
   GMAT_TRY(evs.make(&ev1));
@@ -5228,13 +5252,16 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // (A/B: 23.8 against 24.2 ms per configs[2] step for the column-tile-major list, GMAT_PF_COLORDER)
   const bool pf_blocked_order = !getenv("GMAT_PF_COLORDER");
   // GMAT_PF_WG caps the persistent grid (tests: many tiles per workgroup at small cohorts)
-  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : 0;
   if (!e->n_cu) {
     int dev = 0, cus = 0;
     GMAT_HIP(hipGetDevice(&dev));
     GMAT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     e->n_cu = std::max(cus, 8);
   }
+  // by default 7/8 of the CUs (28 of an XCD's 32): the slot lists and the low-rank screens of the
+  // launches before run on the rest instead of waiting for a whole prefilter launch (one-box A/Bs,
+  // configs[2]: 18.4 against 19.2 ms per step at 224 against 256 workgroups; 240 and 232 were slower)
+  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : std::max(8, e->n_cu * 7 / 8);
   if (getenv("GMAT_PF_STAMPS")) {
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
@@ -5249,7 +5276,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, getenv("GMAT_PF_ONE_STREAM") ? e->s2 : e->s4};
   GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
-  ScanEvents evs;
+  ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
   double t_pf = 0, pf_ops = 0;
   std::vector<double> pf_ops_of(plan.size(), 0.0);
@@ -5380,7 +5407,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
         x.tile_list = B.tlist[b].as<int>();
         x.n_list = run;
-        const int g = 8 * (int)std::min<int64_t>(cdiv(pf_wg ? pf_wg : e->n_cu, 8), cdiv(run, 8));
+        const int g = 8 * (int)std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8));
         if (run > 0) hipLaunchKernelGGL((prefilter_pass_kernel<true, true>), dim3((unsigned)g), dim3(512), 0, S2, x);
       } else {
         if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
@@ -5410,7 +5437,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
         x.tile_list = B.tlist[b].as<int>();
         x.n_list = run;
-        const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pf_wg ? pf_wg : e->n_cu, 8), cdiv(run, 8))));
+        const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8))));
         switch (e->pf_ncov) {
           case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, true>), gp, dim3(512), 0, S2, x); break;
           case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, true>), gp, dim3(512), 0, S2, x); break;
@@ -5481,10 +5508,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   lx.eps = e->lr_eps;
   lx.E = e->lr_E;
   int64_t prev_count = 0;  // candidates after the previous launch's screen (known once it completed)
-  // two launches' prefilters queued ahead of the screen being launched (the prefilter streams never
-  // wait for a host round trip between launches)
-  // (same-box A/B: 28.0 ms per configs[2] step two launches ahead against 28.6 one ahead)
-  constexpr size_t ahead = 2;
+  // the prefilters of the next launch(es) queued ahead of the screen being launched (the prefilter
+  // streams never wait for a host round trip between launches).  Round 3, every CU in the prefilter
+  // grid: 28.0 ms per configs[2] step two launches ahead against 28.6 one ahead; round 4
+  // (one-box A/Bs with the 7/8 prefilter grid: 18.25 against 18.41 ms per configs[2] step one launch
+  // ahead against two; 3.12 against 3.14-3.19 ms for rank 0's part of an 8-way split)
+  const size_t ahead = getenv("GMAT_LRC_AHEAD") ? (size_t)std::max(1, std::min(NBUF - 1, atoi(getenv("GMAT_LRC_AHEAD")))) : 1;
   for (size_t li = 0; li < std::min<size_t>(ahead, plan.size()); ++li) GMAT_TRY(enqueue_side(li, (int)li));
   for (size_t li = 0; li < plan.size(); ++li) {
     const int b = (int)(li % NBUF);
@@ -5710,7 +5739,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
   const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
   GMAT_HIP(hipDeviceSynchronize());
-  ScanEvents evs;
+  ScanEvents evs{e};
   // per buffer set: side pass begin / end, screen begin / end (+ its count copy); refine begin / end
   hipEvent_t side_beg[2], side_end[2], scr_beg[2], scr_end[2], screen_end[2], ref_beg, ref_end;
   for (int b = 0; b < 2; ++b)

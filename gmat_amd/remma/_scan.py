@@ -6,6 +6,7 @@ hits; this module keeps the reference's argument handling, defaults, error condi
 output files and row order.
 """
 import ctypes
+import functools
 import os
 import logging
 import time
@@ -22,6 +23,12 @@ SCAN_HEADER = "snp_0 snp_1 eff chi p_val"
 PAIR_HEADER = "snp_0 snp_1 eff var chi p"
 N_SLICE = 3  # slices kept; each scan uses 1, 2 or 3 by p_cut (gmat_epi_scan n_slice=0)
 
+
+
+@functools.lru_cache(maxsize=64)
+def _chi_cut(p_cut):
+    """chi2(1) quantile of p_cut (scipy's isf costs ~50 us: cached, the multi-GPU steps are ~3 ms)"""
+    return float(chi2.isf(p_cut, 1)) if p_cut < 1 else 0.0
 
 class EpiPlan:
     """gmat_epi handle: a genotype panel plus Z'PZ and Z'Py resident on the device."""
@@ -61,7 +68,7 @@ class EpiPlan:
         computation, remma_epiAA.py:71-82) -- the audit of the screens."""
         rows = N.i64(rows)
         n_hits = ctypes.c_int64()
-        chi_cut = float(chi2.isf(p_cut, 1)) if p_cut < 1 else 0.0
+        chi_cut = _chi_cut(float(p_cut))
         N.check(self._lib.gmat_epi_scan(self._h, KINDS[kind], N.ptr(rows), rows.size, float(p_cut), chi_cut,
                                         int(n_slice), ctypes.byref(n_hits)), "gmat_epi_scan")
         k = n_hits.value

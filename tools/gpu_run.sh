@@ -34,6 +34,10 @@ for st in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/part -o run -- python3 tools/split_part.py 0 8 5 > $OUT/part.log 2>&1 || { tail -30 $OUT/part.log; exit 1; }
       grep "part 0" $OUT/part.log | tail -3
       python3 tools/step_timeline.py $(find $OUT/part -name "*kernel_trace.csv" | head -1) | tee $OUT/part_timeline.txt ;;
+    parthost)
+      # host API trace of rank 0's part (which HIP calls sit between the steps' kernels)
+      timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --output-format csv -d $OUT/parthost -o run -- python3 tools/split_part.py 0 8 5 > $OUT/parthost.log 2>&1 || { tail -30 $OUT/parthost.log; exit 1; }
+      grep "part 0" $OUT/parthost.log | tail -2; ls $OUT/parthost/*/ 2>/dev/null | head; find $OUT/parthost -name "*.csv" | head ;;
     cov)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --covariates --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/cov.json 2> $OUT/cov.log || { tail -30 $OUT/cov.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/cov.json')); print('covariates: value %.4g ms %.2f' % (d['value'], d['ms_per_step']))" ;;
