@@ -105,11 +105,11 @@ struct ScreenArgs {
   int nJ;
   int pf_store;  // side pass 1 also writes the code products of flagged blocks to pfc
   // covariate directions of the prefilter certificate (P's null space besides 1, pf_ncov of them):
-  // per direction k, the left coding's int8 row images are in SideArgs rs[E3_PF + k] with scales
-  // pf_sU[k][i]; pf_ua[k][i] = u_k . a_i (left screen codes), pf_ub[k][j] = u_k . b_j (right);
-  // pf_su[k] = 1'u_k; the certificate's coefficient of |U'e|^2 is pf_ku
-  const double *pf_sU, *pf_ua, *pf_ub;
-  double pf_su[4];
+  // direction k quantised to int8 q_k = rint(u_k / pf_sq[k]) (SideArgs qimg); pf_ua[k][i] = u_k . a_i
+  // (left screen codes), pf_ub[k][j] = u_k . b_j (right); pf_su[k] = 1'u_k; the certificate's
+  // coefficient of |U'e|^2 is pf_ku
+  const double *pf_ua, *pf_ub;
+  double pf_sq[4], pf_su[4];
   double pf_ku;
   int pf_ncov;
   unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
@@ -118,7 +118,8 @@ struct ScreenArgs {
                     // pairs as a bit mask (bit c = column 32 J + c), or null
   // compacted low-rank path: the live pairs' test operands as OPS_REC-int records {E3 slice 0, E3
   // slice 1, Sab, Sa2b, Sab2, Sa2b2, j, 0} appended at ops (a wave reserves its records with one
-  // atomic on ops_count; nothing is stored past ops_cap: the host sees the count, grows the buffer
+  // atomic on ops_count, a persistent one in chunks of PF_CHUNK or more; nothing is stored past
+  // ops_cap: the host sees the count (records reserved, a little above those written), grows the buffer
   // and reruns the launch); lbase[(band row, block)] = the index of a live block's first record (its
   // pairs' records are consecutive, ascending j)
   int *ops;
@@ -200,13 +201,15 @@ struct SideArgs {
   const int8_t *rs[7];  // row-side sets [m][n_pad] (slices: stride slice_stride)
   const int8_t *cs[5];  // column-side sets
   const uint8_t *rs4, *cs4;  // prefilter: fp4 code panels (a | b) [m][n_pad / 2]
+  const uint8_t *rs2, *cs2;  // prefilter: stage-blocked 2-bit code panels (a | b) [n_pad / 64][m][16 B]
   int64_t n_pad;
   int n_rt;             // row tiles
   int blocked;          // prefilter_pass_kernel: rs[0..E3_PF), rs4, cs4 are stage-blocked panels
-                        // ([n_pad / 64][m][64 B] int8, [n_pad / 64][m][32 B] fp4; block_panel_kernel)
+                        // ([n_pad / 64][m][64 B] int8, block_panel_perm8_kernel; the codes: rs2 / cs2)
   const float *recL, *recR;  // prefilter_pass_kernel: test records, row / column role (pf_rec_kernel)
   const int *tile_list;      // prefilter_pass_kernel: the launch's running tiles (rt + n_rt ct, ascending),
   int n_list;                // dealt to the XCDs in contiguous eighths; null: one tile per workgroup
+  const uint8_t *qimg;       // prefilter_cov_kernel: the quantised covariate directions [ncov][n_pad] int8
 };
 template <int PASS>
 __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
@@ -311,13 +314,16 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 // the bytes per pair at the register file's limit of 16,384 pairs (six accumulators each): a row
 // brings 160 B per stage (two int8 L3 slices + fp4 codes), a column 32 B, so 64 x 256 streams 18 KB
 // per stage where 128 x 128 streamed 24 KB.  Stage image (64 individuals), five-slot LDS-DMA ring
-// (90 KB), four stages in flight: int8 L3 slices 0, 1 (64 rows x 64 B each), fp4 codes a (64 rows x
-// 32 B) and b (256 columns x 32 B).  The squares' fp4 codes (sq4) and the int8 b of the E3 products
-// (i8_of_fp4) come from the codes in registers.  16-byte chunks XOR-swizzled through the DMA source
-// address (int8: chunk ^ (row >> 2) & 3, fp4: chunk ^ (row >> 3) & 1); the image holds DMA
-// instruction q (1 KB) at q KB, wave w < 6 issuing q = w + 6u (u < 3), waves 6 and 7 none.
-constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 18 * 1024, PF_NS = 5, PF_Q = 3, PF_QW = 6;
+// (65 KB), four stages in flight: int8 L3 slices 0, 1 (64 rows x 64 B each), then the genotype codes
+// of a (64 rows) and b (256 columns) at 2 bits each (16 B per SNP and stage, code2_panel_kernel: the
+// codes take 0, 1, 2; round 3 streamed them as fp4, 32 B, so that a stage is 13 instead of 18 KB).  The
+// fp4 codes (fp4_of_code2: two VALU per dword), their squares (sq4) and the int8 b of the E3 products
+// (i8x2_of_fp4_eo) come from them in registers.  The int8 16-byte chunks XOR-swizzled through the
+// DMA source address (chunk ^ (row >> 2) & 3); the image holds DMA instruction q (1 KB) at q KB, wave w
+// issuing q = w + 8u (u < 2; waves 0-4 two, 5-7 one).
+constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 13 * 1024, PF_NS = 5, PF_NQ = 13;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
+constexpr int PF_CHUNK = 128;  // live-pair records a persistent prefilter wave reserves at a time
 constexpr int PF_NSTAMP = 7;  // GMAT_PF_STAMPS: start, prologue, main loop, column records, tests, stores, end
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
@@ -325,6 +331,14 @@ __device__ __forceinline__ v8i_ sq4(v4i x) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) r[q] = x[q] | ((x[q] >> 1) & 0x22222222);
   return r;
+}
+// fp4 codes (e2m1 nibble 2c: 0, 1, 2 -> 0x0, 0x2, 0x4) of 32 genotype codes c stored at 2 bits
+// (code2_panel_kernel: per 16 individuals a dword whose nibble k holds c[k] | c[8 + k] << 2), as the
+// four nibble-per-individual dwords of individuals 0-7, 8-15, 16-23, 24-31
+__device__ __forceinline__ v4i fp4_of_code2(v2i_ d) {
+  const unsigned d0 = (unsigned)d[0], d1 = (unsigned)d[1];
+  return v4i{(int)((d0 << 1) & 0x66666666u), (int)((d0 >> 1) & 0x66666666u), (int)((d1 << 1) & 0x66666666u),
+             (int)((d1 >> 1) & 0x66666666u)};
 }
 // int8 values of 16 fp4 codes (two dwords, individual i at nibble i): code >> 1, in order
 __device__ __forceinline__ v4i i8_of_fp4(unsigned x0, unsigned x1) {
@@ -349,6 +363,11 @@ __device__ __forceinline__ v4i i8x2_of_fp4_eo(unsigned x0, unsigned x1) {
   r[2] = (int)(x1 & 0x0f0f0f0fu);
   r[3] = (int)((x1 >> 4) & 0x0f0f0f0fu);
   return r;
+}
+// LDS-DMA from a wave-uniform 64-bit base (SGPRs) + a 32-bit per-lane byte offset (one VGPR per
+// source instead of two), LDS destination m0
+__device__ __forceinline__ void lds_dma16_sv(unsigned voff, const void *sbase, unsigned m0) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
 }
 // LDS-DMA with the LDS destination given as a wave-uniform byte address (m0), no per-call
 // generic -> LDS address conversion
@@ -393,59 +412,64 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wr = w >> 2, wc = w & 3;  // wave-uniform (SGPR)
-  constexpr int O_R8 = 0, O_R8S = 4096, O_R4 = 8192, O_C4 = 10240;
-  static_assert(O_C4 + PF_TC * 32 == PF_ST && PF_ST == 1024 * PF_Q * PF_QW, "prefilter stage image");
-  const bool dma_wave = w < PF_QW;  // waves 0..5 issue the stage DMAs
+  constexpr int O_R8 = 0, O_R8S = 4096, O_R4 = 8192, O_C4 = 9216;
+  static_assert(O_C4 + PF_TC * 16 == PF_ST && PF_ST == 1024 * PF_NQ, "prefilter stage image");
+  const int nq = w + 8 < PF_NQ ? 2 : 1;  // stage DMAs of this wave (q = w, w + 8)
   __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
-  const uint8_t *src[PF_Q];
-  int64_t stp[PF_Q];
-  // stage-blocked panels: a stage's 64-byte / 32-byte pieces of consecutive SNPs are contiguous, so
+  // stage-blocked panels: a stage's 64-byte / 16-byte pieces of consecutive SNPs are contiguous, so
   // an instruction's 1 KB comes from 8 whole 128-byte lines (int8 pieces in the even / odd
-  // individual order of i8x2_of_fp4_eo)
-  constexpr int64_t rstride = SG_K, fstride = SG_K / 2;
+  // individual order of i8x2_of_fp4_eo).  Sources: a wave-uniform base per instruction (the panel's
+  // stage st, SGPRs) + a 32-bit lane offset
+  constexpr int64_t rstride = SG_K, cstride = SG_K / 4;
+  const uint8_t *sbase0 = (const uint8_t *)x.rs[w >> 2];           // q = w: L3 slice w / 4
+  const uint8_t *sbase1 = w == 0 ? x.rs2 : x.cs2;                  // q = w + 8: codes
+  const int64_t sstep0 = a.m * SG_K, sstep1 = a.m * cstride;
+  unsigned voff[2];
   auto set_src = [&](int r0, int64_t c0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < PF_Q; ++u) {
-      const int q = min(w, PF_QW - 1) + PF_QW * u;
-      if (q < 8) {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
-        const int row = (q & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-        src[u] = (const uint8_t *)x.rs[q >> 2] + a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg;
-        stp[u] = a.m * SG_K;
-      } else {  // fp4 codes: 32 rows x 2 chunks per instruction (q 8, 9 rows, 10..17 columns)
-        const int qq = q < 10 ? q - 8 : q - 10, row = qq * 32 + (lane >> 1), lg = (lane & 1) ^ ((row >> 3) & 1);
-        const int64_t idx = q < 10 ? a.rows[min(r0 + row, a.n_rows - 1)] : min(c0 + row, a.m - 1);
-        src[u] = (q < 10 ? x.rs4 : x.cs4) + idx * fstride + 16 * lg;
-        stp[u] = a.m * (SG_K / 2);
-      }
+    {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
+      const int row = (w & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+      voff[0] = (unsigned)(a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg);
     }
+    if (w == 0)  // q 8: 2-bit codes of the 64 rows, one per lane
+      voff[1] = (unsigned)(a.rows[min(r0 + lane, a.n_rows - 1)] * cstride);
+    else  // q 9..12: 2-bit codes of 64 columns per instruction
+      voff[1] = (unsigned)(min(c0 + 64 * (w - 1) + lane, a.m - 1) * cstride);
   };
   set_src(r0, c0);
   typedef __attribute__((address_space(3))) const void *lds_ct;
   const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
   // stage st into ring slot `slot` (= st % PF_NS, kept by the caller)
   auto issue = [&](int st, int slot) __attribute__((always_inline)) {
-    if (dma_wave)
-#pragma unroll
-      for (int u = 0; u < PF_Q; ++u)
-        lds_dma16_m0(src[u] + (int64_t)st * stp[u], ring_m0 + slot * PF_ST + PF_QW * u * 1024);
+    lds_dma16_sv(voff[0], sbase0 + st * sstep0, ring_m0 + slot * PF_ST);
+    if (nq == 2) lds_dma16_sv(voff[1], sbase1 + st * sstep1, ring_m0 + slot * PF_ST + 8 * 1024);
   };
-  // wait until stage `st` has landed given the stages issued up to `last` (PF_Q = 3 DMAs per stage),
-  // then the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm
-  // writes LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist
-  // the next stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations
-  // retire in order (they do on gfx9 for loads).  Waves 6 and 7 issue no stage DMA: they wait for
-  // nothing of their own (their record DMA is older than any stage) and meet the others at the barrier.
-  static_assert(PF_Q == 3 && PF_NS == 5, "wait_for's vmcnt values");
+  // wait until stage `st` has landed given the stages issued up to `last` (nq DMAs per stage), then
+  // the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm writes
+  // LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist the next
+  // stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations retire in order
+  // (they do on gfx9 for loads).  (The record DMAs are older than any stage.)
+  static_assert(PF_NS == 5, "wait_for's vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
-    const int ahead = dma_wave ? last - st : 0;
-    if (ahead >= 3)
-      asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (ahead == 2)
-      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int ahead = last - st;
+    if (nq == 2) {
+      if (ahead >= 3)
+        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (ahead == 2)
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (ahead >= 3)
+        asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (ahead == 2)
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
   };
   v16i acc[2][E3_PF];
   v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
@@ -464,6 +488,10 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   };
   issue_rec(r0, c0, 0);
   for (int st = 0; st < pre; ++st) issue(st, st);
+  // COMPACT + LIST: the wave's live-pair records are placed in chunks of at least PF_CHUNK records
+  // reserved with one atomic (a tile keeps ~8 per wave at configs[2]: an atomic every ~16 tiles instead
+  // of a round trip in every epilogue; the unused tails count against ops_cap)
+  unsigned ch_cur = 0u, ch_end = 0u;
   for (;; ++it) {
     // per-lane values re-derived from an opaque copy of the thread index each tile: hoisted out of
     // the tile loop, the epilogue's would stay live through the main loop (256-VGPR budget)
@@ -502,10 +530,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
       v4i rb4[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int crow = 64 * wc + 32 * q + c, lc = h ^ ((crow >> 3) & 1);
-        rb4[q] = *(const v4i *)&bf[O_C4 + crow * 32 + 16 * lc];
-      }
+      for (int q = 0; q < 2; ++q) rb4[q] = fp4_of_code2(*(const v2i_ *)&bf[O_C4 + (64 * wc + 32 * q + c) * 16 + 8 * h]);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
@@ -519,10 +544,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
         }
       }
       {
-        const int lr = h ^ ((rrow >> 3) & 1);
         v8i_ fa[2];
         {
-          const v4i ra4 = *(const v4i *)&bf[O_R4 + rrow * 32 + 16 * lr];
+          const v4i ra4 = fp4_of_code2(*(const v2i_ *)&bf[O_R4 + rrow * 16 + 8 * h]);
           fa[0] = v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0};
           fa[1] = sq4(ra4);
         }
@@ -635,8 +659,20 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       // (row pair, block) ballot places its pairs in lane order (h = 0 row first, ascending columns)
       unsigned base = 0u;
       if (n_live) {
-        if (lane == 0) base = atomicAdd(a.ops_count, n_live);
-        base = __builtin_amdgcn_readfirstlane(base);
+        if (!LIST) {
+          if (lane == 0) base = atomicAdd(a.ops_count, n_live);
+          base = __builtin_amdgcn_readfirstlane(base);
+        } else {
+          if (ch_cur + n_live > ch_end) {
+            const unsigned want = max(n_live, (unsigned)PF_CHUNK);
+            unsigned b0 = 0u;
+            if (lane == 0) b0 = atomicAdd(a.ops_count, want);
+            ch_cur = __builtin_amdgcn_readfirstlane(b0);
+            ch_end = ch_cur + want;
+          }
+          base = ch_cur;
+          ch_cur += n_live;
+        }
       }
       const bool fits = (int64_t)base + n_live <= a.ops_cap;
       unsigned run = base;
@@ -708,22 +744,28 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
 // The same prefilter when P has null directions besides 1 (covariate columns of X): the certificate
 // (gmat_epi_create) is  e'Pe >= mu |e|^2 - (mu + tau)(1'e)^2/n - ku |U'e|^2 - eps |e|^2  with U the
 // orthonormal null directions, so every pair also needs u_k'e = (a o u_k).b - beta u_k.a - alpha
-// u_k.b + alpha beta 1'u_k for k < NC.  (a o u_k) is a one-slice int8 row image (per-row scale sU):
-// |u_k'e - c~_k| <= sU/2 sum_t b_t = sU csum_r / 2, so |U'e|^2 <= sum_k (|c~_k| + err_k)^2.
-// 32 x 256 (row, column) tiles, 8 waves of 32 x 32 (one row band, wave w the columns 32 w ..) at two
-// waves per SIMD (a 32 x 32 wave tile keeps the NC extra int32 accumulator sets within two waves'
-// registers).  A row brings 64 B per int8 region and stage, a column 32 B, so the tall side of the tile
-// is the columns: 32 x 256 streams 2 KB NREG + 9 KB per stage for 8,192 pairs (the round-3 64 x 128
-// tile: 4 KB NREG + 6 KB).  Stage image (64 individuals): L3 slices 0, 1 and the NC direction images
-// (32 rows x 64 B each), fp4 codes of a (32 rows x 32 B) and b (256 columns x 32 B); DMA instruction q
-// (1 KB) lands at q KB, wave w issuing q = w + 8u.  Five-slot LDS-DMA ring, four stages in flight.
-constexpr int PC_TR = 32, PC_TC = 256, PC_NS = 5, PF_NCOV_MAX = 4;
+// u_k.b + alpha beta 1'u_k for k < NC.  u_k is quantised once per plan to q_k = rint(u_k / sq_k),
+// sq_k = max |u_k| / 63 (ensure_pf_q), so that a o q_k is an exact int8 vector (|a q| <= 126) and
+// |(a o u_k).b - sq_k (a o q_k).b| <= sq_k / 2 sum_t a_t b_t = sq_k Sab / 2 (Sab: the exact code product
+// the kernel computes anyway).  The images a o q_k are formed ON CHIP, once per stage and workgroup,
+// from the streamed fp4 codes of a and a 64-byte q slice per direction (round 3 streamed per-row int8
+// images a o u_k from HBM: 64 B per row, stage and direction, 2.1x the bytes per pair of the
+// intercept-only prefilter).  32 x 256 (row, column) tiles, 8 waves of 32 x 32 (one row band, wave w
+// the columns 32 w ..) at two waves per SIMD (the NC extra int32 accumulator sets keep a wave at 1,024
+// pairs).  Stage slot (64 individuals), all from stage-blocked panels: DMA instruction q (1 KB) at q KB:
+// L3 slices 0, 1 (q 0-3, 32 rows x 64 B each), the 2-bit codes of a (q 4, 32 rows x 16 B; lanes 32-63
+// load a copy into the unused half) and b (q 5-8, 256 columns x 16 B), the q slices (q 9: direction k at
+// 64 k).  The NC direction images (32 rows x 64 B each, same swizzle as
+// the L3 slices) are written by the workgroup into a double buffer: the image of stage s + 1 is formed
+// while stage s multiplies.  Eight-slot ring: stage s + 7 streams while stage s multiplies (stages up
+// to s + 2 have landed at its closing barrier, five more in flight: the loop is bound by the latency of
+// the LDS-DMA stream as much as by its rate).
+constexpr int PC_TR = 32, PC_TC = 256, PC_NS = 8, PF_NCOV_MAX = 4;
 template <int NC>
 struct PcShape {
-  static constexpr int NREG = 2 + NC;                  // int8 row regions: L3 slices + directions
-  static constexpr int O_A4 = 2048 * NREG, O_B4 = O_A4 + 1024, ST = O_B4 + 8192;
-  static constexpr int QT = ST / 1024;                 // DMA instructions per stage
-  static constexpr int QW = (QT + 3) / 4;              // per wave (the last ones partly idle)
+  static constexpr int O_A2 = 4096, O_B2 = 5120, O_Q = 9216;
+  static constexpr int QT = 10;                        // DMA instructions per stage
+  static constexpr int ST = 10240;                     // slot bytes
 };
 // s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier as ONE asm statement (see prefilter_pass_kernel)
 __device__ __forceinline__ void vm_wait_barrier(int n) {
@@ -739,6 +781,21 @@ __device__ __forceinline__ void vm_wait_barrier(int n) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 #undef VMW
+}
+// a o q for 16 individuals in the stage-blocked panels' even/odd order (i8x2_of_fp4_eo): a from two
+// dwords of fp4 codes (0, 1, 2 as e2m1: nibble = 2a), q as int8 (|q| <= 63, the same order): bytes q
+// where a = 1, 2q where a = 2, 0 where a = 0 (byte-table v_perm masks on 2a + bit select)
+__device__ __forceinline__ v4i aq_of_fp4_eo(unsigned x0, unsigned x1, v4i q) {
+  const v4i av = i8x2_of_fp4_eo(x0, x1);  // 2a: 0, 2, 4
+  v4i r;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const unsigned a = (unsigned)av[d], qd = (unsigned)q[d];
+    const unsigned nz = __builtin_amdgcn_perm(0x000000FFu, 0x00FF0000u, a), two = __builtin_amdgcn_perm(0x000000FFu, 0u, a);
+    const unsigned q2 = (qd & 0x7F7F7F7Fu) << 1;  // 2q per byte (|2q| <= 126: the dropped bit is a sign copy)
+    r[d] = (int)((q2 & two) | (qd & nz & ~two));
+  }
+  return r;
 }
 // LIST: a persistent grid over the launch's tile list (as prefilter_pass_kernel<true>: XCD x takes the
 // list's x-th eighth, its workgroups stride through it, and the next tile's first stages stream into
@@ -765,41 +822,64 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     if (a.tri && c0_ + PC_TC - 1 <= a.rows[r0_]) return -1;  // rows ascend within a launch
     return t;
   };
+  auto pstamp = [&](int st_) __attribute__((always_inline)) {  // GMAT_PF_STAMPS (one tile per workgroup)
+    if (!LIST && a.pf_stamp && threadIdx.x == 0)
+      a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + st_] = __builtin_amdgcn_s_memrealtime();
+  };
+  pstamp(0);
   int tile = tile_at(0);
   if (tile < 0) return;
   // 8 waves at two per SIMD: wave w = the tile's 32 rows x columns 32 w .. +32
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = 0, wc = w, h = lane >> 5, c = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            c = lane & 31;
   __shared__ __attribute__((aligned(16))) uint8_t ring[PC_NS][SH::ST];
-  constexpr int QW = (SH::QT + NW - 1) / NW;
-  const uint8_t *src[QW];
-  int stp[QW];
-  int nq = 0;  // DMA instructions this wave issues per stage
+  __shared__ __attribute__((aligned(16))) uint8_t img[2][NC][2048];  // direction images, stages s % 2
+  // DMA instruction q = w + 8u (u < 2): a wave-uniform base per instruction (the panel at stage st,
+  // SGPRs) + a 32-bit lane offset
+  const int nq = (w + NW < SH::QT) ? 2 : 1;  // DMA instructions this wave issues per stage
+  auto base_of = [&](int q) __attribute__((always_inline)) -> const uint8_t * {
+    return q < 4 ? (const uint8_t *)x.rs[q >> 1] : q == 4 ? x.rs2 : q < 9 ? x.cs2 : x.qimg;
+  };
+  auto step_of = [&](int q) __attribute__((always_inline)) -> int64_t {
+    return q < 4 ? (int64_t)SG_K * a.m : q < 9 ? (int64_t)(SG_K / 4) * a.m : (int64_t)SG_K;
+  };
+  const uint8_t *sbase0 = base_of(w), *sbase1 = base_of(w + NW);
+  const int64_t sstep0 = step_of(w), sstep1 = step_of(w + NW);
+  unsigned voff[2];
   auto set_src = [&](int r0, int64_t c0) __attribute__((always_inline)) {
-    nq = 0;
 #pragma unroll
-    for (int u = 0; u < QW; ++u) {
+    for (int u = 0; u < 2; ++u) {
       const int q = w + NW * u;
-      src[u] = nullptr;
-      stp[u] = 0;
-      if (q < 2 * SH::NREG) {  // int8 rows: region q / 2, 16 rows x 4 chunks per instruction
-        const int g = q >> 1, row = (q & 1) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
-        src[u] = (const uint8_t *)x.rs[g] + a.rows[min(r0 + row, a.n_rows - 1)] * x.n_pad + 16 * lg;
-        stp[u] = SG_K;
-        ++nq;
-      } else if (q < SH::QT) {  // fp4 codes: 32 rows x 2 chunks per instruction (1 for a, 8 for b)
-        const int qq = q - 2 * SH::NREG, isb = qq >= 1, row = (isb ? qq - 1 : qq) * 32 + (lane >> 1);
-        const int lg = (lane & 1) ^ ((row >> 3) & 1);
-        const int64_t idx = isb ? min(c0 + row, a.m - 1) : a.rows[min(r0 + row, a.n_rows - 1)];
-        src[u] = (isb ? x.cs4 : x.rs4) + idx * (x.n_pad / 2) + 16 * lg;
-        stp[u] = SG_K / 2;
-        ++nq;
+      if (q < 4) {  // int8 L3 rows (stage-blocked): slice q / 2, 16 rows x 4 chunks per instruction
+        const int row = (q & 1) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+        voff[u] = (unsigned)(a.rows[min(r0 + row, a.n_rows - 1)] * SG_K + 16 * lg);
+      } else if (q == 4) {  // 2-bit codes of the 32 rows (lanes 32-63: a copy)
+        voff[u] = (unsigned)(a.rows[min(r0 + (lane & 31), a.n_rows - 1)] * (SG_K / 4));
+      } else if (q < 9) {  // 2-bit codes of 64 columns per instruction
+        voff[u] = (unsigned)(min(c0 + 64 * (q - 5) + lane, a.m - 1) * (SG_K / 4));
+      } else {  // the q slices: lane l = direction min(l / 4, NC - 1), chunk l % 4
+        voff[u] = (unsigned)(min(lane >> 2, NC - 1) * x.n_pad + 16 * (lane & 3));
       }
     }
   };
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
   auto issue = [&](int st) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < QW; ++u)
-      if (w + NW * u < SH::QT) lds_dma16(src[u] + (int64_t)st * stp[u], &ring[st % PC_NS][(w + NW * u) * 1024]);
+    const unsigned m0 = ring_m0 + (st % PC_NS) * SH::ST;
+    lds_dma16_sv(voff[0], sbase0 + st * sstep0, m0);
+    if (nq == 2) lds_dma16_sv(voff[1], sbase1 + st * sstep1, m0 + NW * 1024);
+  };
+  // the direction images of stage st (its codes and q slices have landed): thread t < 128 NC forms
+  // direction t / 128, row (t / 4) % 32, 16-individual chunk t % 4
+  auto image = [&](int st) __attribute__((always_inline)) {
+    if (tid < 128 * NC) {
+      uint8_t *sl = ring[st % PC_NS];
+      const int k = tid >> 7, row = (tid >> 2) & 31, ch = tid & 3;
+      const unsigned cw = *(const unsigned *)(sl + SH::O_A2 + row * 16 + 4 * ch);  // 16 individuals, 2 bits each
+      const v4i qv = *(const v4i *)(sl + SH::O_Q + 64 * k + 16 * ch);
+      *(v4i *)(&img[st & 1][k][row * 64 + 16 * (ch ^ ((row >> 2) & 3))]) =
+          aq_of_fp4_eo((cw << 1) & 0x66666666u, (cw >> 1) & 0x66666666u, qv);
+    }
   };
   const int S = (int)(x.n_pad / SG_K);
   const int pre = min(S, PC_NS - 1);
@@ -807,11 +887,15 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PC_TC;
   set_src(r0, c0);
   for (int st = 0; st < pre; ++st) issue(st);
+  unsigned ch_cur = 0u, ch_end = 0u;  // LIST: record chunks (prefilter_pass_kernel)
   for (int it = 0;; ++it) {
   if (it == 0)
-    vm_wait_barrier(nq * (pre - 1));
+    vm_wait_barrier(nq * max(0, pre - 2));  // stages 0 and 1 have landed
   else  // the prefetched stages and the previous epilogue's stores (vmcnt counts those too)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  image(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (no vmcnt wait: later stages stream on)
+  pstamp(1);
   v16i acc[E3_PF], accu[NC];
   v16f_ acc4[4];  // a.b, a^2.b, a.b^2, a^2.b^2
 #pragma unroll
@@ -823,39 +907,40 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc4[p][e] = 0.f;
   }
-  const int rrow = 32 * wr + c;
-  const int crow = 32 * wc + c, lcb = h ^ ((crow >> 3) & 1);
+  const int rrow = c;
+  const int crow = 32 * w + c;
   for (int st = 0; st < S; ++st) {
     const uint8_t *bf = ring[st % PC_NS];
     if (st + PC_NS - 1 < S) issue(st + PC_NS - 1);
-    const v4i rb4 = *(const v4i *)&bf[SH::O_B4 + crow * 32 + 16 * lcb];
+    if (st + 1 < S) image(st + 1);
+    const v4i rb4 = fp4_of_code2(*(const v2i_ *)&bf[SH::O_B2 + crow * 16 + 8 * h]);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int lr = (2 * h + kk) ^ ((rrow >> 2) & 3);
-      const v4i fc = i8_of_fp4((unsigned)rb4[2 * kk], (unsigned)rb4[2 * kk + 1]);
+      const v4i fc = i8x2_of_fp4_eo((unsigned)rb4[2 * kk], (unsigned)rb4[2 * kk + 1]);  // 2b: sums doubled
 #pragma unroll
-      for (int g = 0; g < SH::NREG; ++g) {
-        const v4i f = *(const v4i *)&bf[2048 * g + rrow * 64 + 16 * lr];
-        if (g < E3_PF)
-          acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, fc, acc[g], 0, 0, 0);
-        else
-          accu[g - E3_PF] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f, fc, accu[g - E3_PF], 0, 0, 0);
-      }
+      for (int g = 0; g < E3_PF; ++g)
+        acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const v4i *)&bf[2048 * g + rrow * 64 + 16 * lr], fc, acc[g], 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < NC; ++k)
+        accu[k] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const v4i *)&img[st & 1][k][rrow * 64 + 16 * lr], fc, accu[k], 0,
+                                                        0, 0);
     }
     {
-      const int lr = h ^ ((rrow >> 3) & 1);
-      const v4i ra4 = *(const v4i *)&bf[SH::O_A4 + rrow * 32 + 16 * lr];
+      const v4i ra4 = fp4_of_code2(*(const v2i_ *)&bf[SH::O_A2 + rrow * 16 + 8 * h]);
       const v8i_ fa[2] = {v8i_{ra4[0], ra4[1], ra4[2], ra4[3], 0, 0, 0, 0}, sq4(ra4)};
       const v8i_ fb[2] = {v8i_{rb4[0], rb4[1], rb4[2], rb4[3], 0, 0, 0, 0}, sq4(rb4)};
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         acc4[p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[p], 4, 4, 0, 127, 0, 127);
     }
-    vm_wait_barrier(nq * (min(st + PC_NS - 1, S - 1) - (st + 1)));
+    // stages up to st + 2 have landed (the image of st + 2 is formed in the next iteration)
+    vm_wait_barrier(nq * max(0, min(st + PC_NS - 1, S - 1) - (st + 2)));
   }
+  pstamp(2);
   // epilogue as prefilter_pass_kernel, plus the direction terms
   __shared__ double rowv[7][PC_TR];
-  __shared__ double rowu[2][NC][PC_TR];  // sU, u.a per direction
+  __shared__ double rowu[NC][PC_TR];  // u.a per direction
   const double n = a.n_id;
   if (tid < PC_TR) {
     const int r = min(r0 + tid, a.n_rows - 1);
@@ -869,12 +954,10 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     rowv[5][tid] = a.sa[i];
     rowv[6][tid] = (2.0 + al) * (2.0 + al);
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      rowu[0][k][tid] = a.pf_sU[k * a.m + i];
-      rowu[1][k][tid] = a.pf_ua[k * a.m + i];
-    }
+    for (int k = 0; k < NC; ++k) rowu[k][tid] = a.pf_ua[k * a.m + i];
   }
   __syncthreads();
+  pstamp(3);
   const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
   const double ku = a.pf_ku * (1.0 + 1e-12);
   const int64_t j = c0 + crow;
@@ -908,7 +991,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int rl = 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
+    const int rl = (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
     const bool rok = r < a.n_rows;
     const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
     bool live = false;
@@ -920,7 +1003,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
         double c3 = 0.0;
 #pragma unroll
         for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
-        const double eff = sL3 * c3 - be * rowv[5][rl] + al * cbsb;
+        const double eff = 0.5 * sL3 * c3 - be * rowv[5][rl] + al * cbsb;
         const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
         const double sab = (double)acc4[0][e], sa2b = (double)acc4[1][e], sab2 = (double)acc4[2][e],
                      sa2b2 = (double)acc4[3][e];
@@ -930,9 +1013,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
         double u2 = 0.0;
 #pragma unroll
         for (int k = 0; k < NC; ++k) {
-          const double sU = rowu[0][k][rl], t1 = sU * (double)accu[k][e], t2 = be * rowu[1][k][rl],
-                       t3 = al * cub[k], t4 = al * be * a.pf_su[k];
-          const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sU * ccb * (1.0 + 1e-9) +
+          const double sq = a.pf_sq[k], t1 = 0.5 * sq * (double)accu[k][e], t2 = be * rowu[k][rl], t3 = al * cub[k],
+                       t4 = al * be * a.pf_su[k];
+          const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sq * sab * (1.0 + 1e-9) +
                             1e-12 * (fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4));
           u2 += ck * ck;
         }
@@ -952,24 +1035,37 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     } else if (blk && rok && jok) {
       const int64_t o3 = o1 + (int64_t)a.n_rows * a.ld_e;
 #pragma unroll
-      for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e];
+      for (int t = 0; t < E3_PF; ++t) ((int *)a.c13)[t * a.c13_stride + o3] = acc[t][e] >> 1;  // exact
       if (a.pf_store)
 #pragma unroll
         for (int p = 0; p < 4; ++p) ((int *)a.pfc)[p * a.pfc_stride + o1] = (int)acc4[p][e];
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  pstamp(4);
   if (a.ops) {  // one record per live pair, placed as in prefilter_pass_kernel (one atomic per wave)
     unsigned base = 0u;
     if (n_live) {
-      if (lane == 0) base = atomicAdd(a.ops_count, n_live);
-      base = __builtin_amdgcn_readfirstlane(base);
+      if (!LIST) {
+        if (lane == 0) base = atomicAdd(a.ops_count, n_live);
+        base = __builtin_amdgcn_readfirstlane(base);
+      } else {
+        if (ch_cur + n_live > ch_end) {
+          const unsigned want = max(n_live, (unsigned)PF_CHUNK);
+          unsigned b0 = 0u;
+          if (lane == 0) b0 = atomicAdd(a.ops_count, want);
+          ch_cur = __builtin_amdgcn_readfirstlane(b0);
+          ch_end = ch_cur + want;
+        }
+        base = ch_cur;
+        ch_cur += n_live;
+      }
     }
     const bool fits = (int64_t)base + n_live <= a.ops_cap;
     unsigned run = base;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int r = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int r = r0 + (e & 3) + 8 * (e >> 2) + 4 * h;
       const bool lv = (own >> e) & 1u;
       const unsigned long long bal = __ballot(lv);
       const unsigned lo = (unsigned)bal, word = h ? (unsigned)(bal >> 32) : lo;
@@ -978,7 +1074,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       if (bal) {
         if (lv && fits) {
           const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo(lo, 0u));
-          const v4i r0v = {acc[0][e], acc[1][e], (int)acc4[0][e], (int)acc4[1][e]};
+          const v4i r0v = {acc[0][e] >> 1, acc[1][e] >> 1, (int)acc4[0][e], (int)acc4[1][e]};  // exact
           const v4i r1v = {(int)acc4[2][e], (int)acc4[3][e], (int)j, 0};
           *(v4i *)(a.ops + (int64_t)k * OPS_REC) = r0v;
           *(v4i *)(a.ops + (int64_t)k * OPS_REC + 4) = r1v;
@@ -987,6 +1083,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       }
     }
   }
+  pstamp(5);
+  if (!LIST && a.pf_stamp) __syncthreads();
+  pstamp(6);
   if (nxt < 0) break;
   tile = nxt;
   r0 = (tile % x.n_rt) * PC_TR;
@@ -3177,50 +3276,24 @@ __global__ void pf_shift_u_kernel(int64_t n, const double *P, const double *C, d
   if (idx / n == idx % n) v -= mu;
   A[idx] = v;
 }
-// covariate direction images of a coding: img[j][t] = rint(code[j][t] u[t] / sU[j]) (int8, |.| <= 127),
-// sU[j] = max_t |code u| / 127, dot[j] = sum_t code[j][t] u[t] (fixed-order reduction)
-__global__ __launch_bounds__(256) void cov_image_kernel(int64_t n_pad, const int8_t *panel, const double *u,
-                                                        int8_t *img, double *sU, double *dot) {
+// covariate direction dots of a coding: dot[j] = sum_t code[j][t] u[t] (fixed-order reduction)
+__global__ __launch_bounds__(256) void cov_dot_kernel(int64_t n_pad, const int8_t *panel, const double *u, double *dot) {
   const int64_t j = blockIdx.x;
   const int8_t *pj = panel + j * n_pad;
-  __shared__ double rmax[256], rsum[256];
-  double mx = 0.0, sm = 0.0;
-  for (int64_t t = threadIdx.x; t < n_pad; t += 256) {
-    const double v = (double)pj[t] * u[t];
-    mx = fmax(mx, fabs(v));
-    sm += v;
-  }
-  rmax[threadIdx.x] = mx;
+  __shared__ double rsum[256];
+  double sm = 0.0;
+  for (int64_t t = threadIdx.x; t < n_pad; t += 256) sm += (double)pj[t] * u[t];
   rsum[threadIdx.x] = sm;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
-    if ((int)threadIdx.x < off) {
-      rmax[threadIdx.x] = fmax(rmax[threadIdx.x], rmax[threadIdx.x + off]);
-      rsum[threadIdx.x] += rsum[threadIdx.x + off];
-    }
+    if ((int)threadIdx.x < off) rsum[threadIdx.x] += rsum[threadIdx.x + off];
     __syncthreads();
   }
-  const double sc = rmax[0] > 0.0 ? rmax[0] / 127.0 : 1.0;
-  for (int64_t t = threadIdx.x; t < n_pad; t += 256) {
-    const double v = (double)pj[t] * u[t];
-    img[j * n_pad + t] = (int8_t)fmin(127.0, fmax(-127.0, rint(v / sc)));
-  }
-  if (threadIdx.x == 0) {
-    sU[j] = sc;
-    dot[j] = rsum[0];
-  }
+  if (threadIdx.x == 0) dot[j] = rsum[0];
 }
-// stage-blocked copy of an SNP-major panel: dst[(st m + snp) w + b] = src[snp W + st w + b] for
-// stages st of w bytes (W bytes per SNP); 16 bytes per thread
-__global__ void block_panel_kernel(int64_t m, int64_t W, int64_t w, const uint8_t *__restrict__ src,
-                                   uint8_t *__restrict__ dst) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = W / 16;
-  if (t >= m * per) return;
-  const int64_t snp = t / per, o = (t % per) * 16, st = o / w, b = o % w;
-  *(v4i *)(dst + (st * m + snp) * w + b) = *(const v4i *)(src + snp * W + o);
-}
-// The same for int8 rows with each 8 bytes reordered to individuals 0 2 4 6 1 3 5 7 (the K slot
-// order of i8x2_of_fp4_eo)
+// stage-blocked copy of an SNP-major int8 panel (dst[(st m + snp) w + b] = src[snp W + st w + b] for
+// stages st of w bytes, W bytes per SNP, 16 bytes per thread), each 8 bytes reordered to individuals
+// 0 2 4 6 1 3 5 7 (the K slot order of i8x2_of_fp4_eo)
 __global__ void block_panel_perm8_kernel(int64_t m, int64_t W, int64_t w, const uint8_t *__restrict__ src,
                                          uint8_t *__restrict__ dst) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = W / 16;
@@ -3272,6 +3345,20 @@ __global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, 
   const int v0 = panel[2 * idx], v1 = panel[2 * idx + 1];
   auto code = [](int v) { return v == 0 ? 0 : v == 1 ? 2 : 4; };
   p4[idx] = (uint8_t)(code(v0) | (code(v1) << 4));
+}
+
+// stage-blocked 2-bit genotype codes (the prefilters' code stream): per SNP and 16 individuals a dword
+// whose nibble k holds c[k] | c[8 + k] << 2 (fp4_of_code2 expands it with two VALU per fp4 dword);
+// dst[(st m + snp) 16 B + 4 g] for the stage st's 16-individual group g
+__global__ void code2_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint32_t *dst) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = n_pad / 16;
+  if (idx >= m * per) return;
+  const int64_t snp = idx / per, g = idx % per, st = g >> 2;
+  const int8_t *p = panel + snp * n_pad + 16 * g;
+  unsigned d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d |= (unsigned)((p[k] & 3) | ((p[8 + k] & 3) << 2)) << (4 * k);
+  dst[(st * m + snp) * 4 + (g & 3)] = d;
 }
 
 // A = P + C + (lam + tau) 11'/n - lam I (natural order) for the low-rank screen's certificate
@@ -3511,11 +3598,10 @@ struct Coding {
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
   DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
-  DBuf p4b, L3b;                  // stage-blocked copies for the prefilter pass: p4 [n_pad/64][m][32 B],
-                                  // L3q slices 0 .. E3_PF-1 [E3_PF][n_pad/64][m][64 B]
+  DBuf p2b, L3b;                  // stage-blocked copies for the prefilters: 2-bit codes [n_pad/64][m][16 B]
+                                  // (code2_panel_kernel), L3q slices 0 .. E3_PF-1 [E3_PF][n_pad/64][m][64 B]
   DBuf pfRecL, pfRecR;            // prefilter test records, row / column role [m][PF_REC] fp32
-  DBuf Lu, sU, uc;                // covariate directions: int8 images of (screen code o u_k) [ncov][m][n_pad],
-                                  // their per-row scales and u_k . code [ncov][m]
+  DBuf uc;                        // covariate directions: u_k . code [ncov][m]
   DBuf lrG, lrGa;                 // low-rank screen: Q' x screen codes, fp32 [m][lr_R]; the same minus
                                   // soff x Q'1 (left side: folds the alpha beta q1 term)
   DBuf lrRecL, lrRecR;            // low-rank screen test records [m][LR_REC] (left / right roles)
@@ -3559,6 +3645,8 @@ struct gmat_epi {
   int pf_ncov = 0;
   double pf_ku = 0, pf_su[4] = {0, 0, 0, 0};
   DBuf pf_U;  // [pf_ncov][n_pad] the directions in storage order
+  DBuf pf_q;  // [pf_ncov][n_pad] int8: rint(u_k / pf_sq[k]), |q| <= 63 (ensure_pf_q)
+  double pf_sq[4] = {0, 0, 0, 0};
   // low-rank screen (lr_screen_kernel): e'Pe >= lam |Pi e|^2 - tau (1'e)^2/n - eps |e|^2 - |Q'e|^2
   // with Q = fp6(bottom eigenvectors x sqrt(d)); lr_R = padded rank (0: disabled)
   int lr_R = 0;
@@ -3740,9 +3828,9 @@ int build_coding_impl(gmat_epi *e, int which) {
   hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
                      cd.p4.as<uint8_t>());
   GMAT_HIP(hipGetLastError());
-  GMAT_TRY(cd.p4b.alloc((size_t)m * n_pad / 2));
-  hipLaunchKernelGGL(block_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 32), 256)), dim3(256), 0, e->s, m, n_pad / 2,
-                     (int64_t)SG_K / 2, cd.p4.as<uint8_t>(), cd.p4b.as<uint8_t>());
+  GMAT_TRY(cd.p2b.alloc((size_t)m * n_pad / 4));
+  hipLaunchKernelGGL(code2_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad, panel,
+                     cd.p2b.as<uint32_t>());
   GMAT_TRY(cd.L3b.alloc((size_t)E3_PF * m * n_pad));
   for (int t = 0; t < E3_PF; ++t)
     hipLaunchKernelGGL(block_panel_perm8_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m,
@@ -3761,15 +3849,12 @@ int build_coding_impl(gmat_epi *e, int which) {
   hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
                      panel, cd.nibI.as<uint32_t>(), cd.nibJ.as<uint32_t>());
   GMAT_HIP(hipGetLastError());
-  if (e->pf_ncov > 0) {  // covariate direction images for the prefilter
+  if (e->pf_ncov > 0) {  // covariate directions: u_k . code per SNP (the prefilter forms the images on chip)
     const int K0 = e->pf_ncov;
-    GMAT_TRY(cd.Lu.alloc((size_t)K0 * m * n_pad));
-    GMAT_TRY(cd.sU.alloc((size_t)K0 * m * sizeof(double)));
     GMAT_TRY(cd.uc.alloc((size_t)K0 * m * sizeof(double)));
     for (int k = 0; k < K0; ++k)
-      hipLaunchKernelGGL(cov_image_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel,
-                         e->pf_U.as<double>() + k * n_pad, cd.Lu.as<int8_t>() + (int64_t)k * m * n_pad,
-                         cd.sU.as<double>() + k * m, cd.uc.as<double>() + k * m);
+      hipLaunchKernelGGL(cov_dot_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel,
+                         e->pf_U.as<double>() + k * n_pad, cd.uc.as<double>() + k * m);
     GMAT_HIP(hipGetLastError());
   }
   if (e->lr_R) {  // G = screen codes x B (exact in fp64: fp6 x small integers), kept in fp32
@@ -4890,10 +4975,36 @@ int block_sides(gmat_epi *e, int which) {
 }
 
 // builds the codings `kind` needs and clears the previous scan's hits and counters
+// the covariate directions quantised for prefilter_cov_kernel: q_k = rint(u_k / sq_k), sq_k = max |u_k| / 63
+// (so a o q_k, a in {0, 1, 2}, is an exact int8 vector); from pf_U, once per plan (also after an import)
+int ensure_pf_q(gmat_epi *e) {
+  const int K0 = e->pf_ncov;
+  if (K0 <= 0 || e->pf_q.p) return GMAT_OK;
+  const int64_t n_pad = e->n_pad;
+  std::vector<double> u((size_t)K0 * n_pad);
+  GMAT_HIP(hipMemcpy(u.data(), e->pf_U.p, u.size() * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<int8_t> q(u.size(), 0);
+  for (int k = 0; k < K0; ++k) {
+    double mx = 0.0;
+    for (int64_t t = 0; t < n_pad; ++t) mx = std::max(mx, std::fabs(u[(size_t)k * n_pad + t]));
+    const double sq = mx > 0.0 ? mx / 63.0 : 1.0;
+    e->pf_sq[k] = sq;
+    // stored in the stage-blocked panels' order: per 8 individuals 0 2 4 6 1 3 5 7 (block_panel_perm8_kernel)
+    static const int eo[8] = {0, 2, 4, 6, 1, 3, 5, 7};
+    for (int64_t t = 0; t < n_pad; ++t)
+      q[(size_t)k * n_pad + t] =
+          (int8_t)std::max(-63.0, std::min(63.0, std::rint(u[(size_t)k * n_pad + (t & ~7LL) + eo[t & 7]] / sq)));
+  }
+  GMAT_TRY(e->pf_q.alloc(q.size()));
+  GMAT_HIP(hipMemcpy(e->pf_q.p, q.data(), q.size(), hipMemcpyHostToDevice));
+  return GMAT_OK;
+}
+
 int scan_begin(gmat_epi *e, int kind, ScanSide *c) {
   kind_codings(kind, &c->lc, &c->rc);
   GMAT_TRY(build_coding(e, c->lc));
   GMAT_TRY(build_coding(e, c->rc));
+  GMAT_TRY(ensure_pf_q(e));
   c->L = &e->code[c->lc];
   c->R = &e->code[c->rc];
   c->lp = c->lc == 0 ? e->g->dose_ptr() : e->g->het_ptr();
@@ -5335,9 +5446,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     a.pf_ncov = e->pf_ncov;
     a.pf_ku = e->pf_ku;
     for (int k = 0; k < 4; ++k) a.pf_su[k] = e->pf_su[k];
-    a.pf_sU = e->pf_ncov ? L.sU.as<double>() : nullptr;
+    for (int k = 0; k < 4; ++k) a.pf_sq[k] = e->pf_sq[k];
     a.pf_ua = e->pf_ncov ? L.uc.as<double>() : nullptr;
     a.pf_ub = e->pf_ncov ? R.uc.as<double>() : nullptr;
+    x.qimg = e->pf_q.as<uint8_t>();
     a.n_id = (double)e->n;
     a.flags = nullptr;
     a.lmask = B.lmask[b].as<uint32_t>();
@@ -5371,8 +5483,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     if (e->pf_ncov == 0) {  // prefilter_pass_kernel reads stage-blocked operands
       x.blocked = 1;
       for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
-      x.rs4 = L.p4b.as<uint8_t>();
-      x.cs4 = R.p4b.as<uint8_t>();
+      x.rs2 = L.p2b.as<uint8_t>();
+      x.cs2 = R.p2b.as<uint8_t>();
       x.n_rt = (int)cdiv(Rn, PF_TR);
       // the tiles that run (a tile entirely left of the diagonal has no pair), in tile order
       // rt + n_rt ct; MFMA work per pair: 4 fp4 code products + 2 int8 E3 slices over n_pad
@@ -5416,7 +5528,9 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
-      for (int k = 0; k < e->pf_ncov; ++k) x.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
+      for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;  // stage-blocked operands
+      x.rs2 = L.p2b.as<uint8_t>();
+      x.cs2 = R.p2b.as<uint8_t>();
       x.n_rt = (int)cdiv(Rn, PC_TR);
       // the running 64 x 128 tiles in blocks of 4 row x 8 column tiles (as the intercept-only prefilter's
       // list), a persistent grid of one workgroup per CU over them (GMAT_PF_NOLIST: one per tile)
@@ -5433,6 +5547,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       // MFMA work per pair: 4 fp4 code products + (2 + K0) int8 products over n_pad individuals
       pf_ops_of[li] = (double)run * PC_TR * PC_TC * (8.0 + 4.0 * (2 + e->pf_ncov)) * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
+      // persistent (one-box A/B, covariate configs[2] step: 35.8 against 41.9 ms for one workgroup per
+      // tile, GMAT_PF_NOLIST; the persistent variant spills a few registers at three or four directions)
       if (run > 0 && pf_list) {
         GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
         x.tile_list = B.tlist[b].as<int>();
@@ -5446,6 +5562,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         }
       } else if (run > 0) {
         const dim3 gp((unsigned)(x.n_rt * n_ct));
+        if (li == stamp_launch) stamp_grid = x.n_rt * n_ct;
         switch (e->pf_ncov) {
           case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false>), gp, dim3(512), 0, S2, x); break;
           case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false>), gp, dim3(512), 0, S2, x); break;
@@ -5819,7 +5936,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
     sa.pf_ncov = e->pf_ncov;
     sa.pf_ku = e->pf_ku;
     for (int k = 0; k < 4; ++k) sa.pf_su[k] = e->pf_su[k];
-    sa.pf_sU = e->pf_ncov ? L.sU.as<double>() : nullptr;
+    for (int k = 0; k < 4; ++k) sa.pf_sq[k] = e->pf_sq[k];
     sa.pf_ua = e->pf_ncov ? L.uc.as<double>() : nullptr;
     sa.pf_ub = e->pf_ncov ? R.uc.as<double>() : nullptr;
     sa.n_id = (double)e->n;
@@ -5893,14 +6010,17 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         SideArgs xp = x;
         xp.blocked = 1;
         for (int t = 0; t < E3_PF; ++t) xp.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
-        xp.rs4 = L.p4b.as<uint8_t>();
-        xp.cs4 = R.p4b.as<uint8_t>();
+        xp.rs2 = L.p2b.as<uint8_t>();
+        xp.cs2 = R.p2b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
         hipLaunchKernelGGL((prefilter_pass_kernel<false, false>), dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
-        for (int k = 0; k < e->pf_ncov; ++k) xp.rs[E3_PF + k] = L.Lu.as<int8_t>() + (int64_t)k * ss;
+        xp.qimg = e->pf_q.as<uint8_t>();
+        for (int t = 0; t < E3_PF; ++t) xp.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;  // stage-blocked
+        xp.rs2 = L.p2b.as<uint8_t>();
+        xp.cs2 = R.p2b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PC_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PC_TC));
         switch (e->pf_ncov) {
