@@ -2630,10 +2630,19 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
         uu[t] = (float)u8[t];
         vv[t] = (float)v8[t];
       }
+      // z, diag(P), Py of the lane's 8 individuals as 16-byte LDS reads (a lane's 32 bytes: 8 scalar reads at
+      // a 32-byte lane stride were 8-way bank conflicts)
+      float zz8[8], dd8[8], yy8[8];
+      *(float4 *)&zz8[0] = *(const float4 *)&zdp[q0];
+      *(float4 *)&zz8[4] = *(const float4 *)&zdp[q0 + 4];
+      *(float4 *)&dd8[0] = *(const float4 *)&zdp[n_pad + q0];
+      *(float4 *)&dd8[4] = *(const float4 *)&zdp[n_pad + q0 + 4];
+      *(float4 *)&yy8[0] = *(const float4 *)&zdp[2 * n_pad + q0];
+      *(float4 *)&yy8[4] = *(const float4 *)&zdp[2 * n_pad + q0 + 4];
 #pragma unroll
       for (int h = 0; h < 8; ++h) {
         const float av = (float)ca[h], bv = (float)cb[h], w = av * bv;  // exact small integers
-        const float z = zdp[q0 + h], d = zdp[n_pad + q0 + h], y = zdp[2 * n_pad + q0 + h];
+        const float z = zz8[h], d = dd8[h], y = yy8[h];
         const float tu = be * uu[h], tv = al * vv[h], tz = ab * z;
         s1 += w * ((tz - tu) - tv);
         s1a += w * ((fabsf(tu) + fabsf(tv)) + fabsf(tz));
@@ -5134,14 +5143,20 @@ int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, 
     GMAT_HIP(hipMemcpyAsync(ci, e->cpack.p, (size_t)nf * 48, hipMemcpyDeviceToHost, st));
     GMAT_HIP(hipEventRecord(end, st));
     GMAT_HIP(hipStreamSynchronize(st));
+    // one bulk copy out of the pinned staging block (element-wise reads of it cost ~50 ns each)
+    std::vector<double> hb((size_t)nf * 6);
+    std::memcpy(hb.data(), ci, (size_t)nf * 48);
+    const int64_t *hi_ = (const int64_t *)hb.data(), *hj_ = hi_ + nf;
+    const double *he_ = hb.data() + 2 * nf, *hv_ = he_ + nf, *hc_ = hv_ + nf, *hq_ = hc_ + nf;
+    (void)ce, (void)cv, (void)cc, (void)cq;
     for (int64_t k = 0; k < nf; ++k)
-      if (cq[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
-        e->hit_i.push_back(ci[k]);
-        e->hit_j.push_back(cj[k]);
-        e->hit_eff.push_back(ce[k]);
-        e->hit_var.push_back(cv[k]);
-        e->hit_chi.push_back(cc[k]);
-        e->hit_p.push_back(cq[k]);
+      if (hq_[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
+        e->hit_i.push_back(hi_[k]);
+        e->hit_j.push_back(hj_[k]);
+        e->hit_eff.push_back(he_[k]);
+        e->hit_var.push_back(hv_[k]);
+        e->hit_chi.push_back(hc_[k]);
+        e->hit_p.push_back(hq_[k]);
       }
   } else {
     GMAT_HIP(hipEventRecord(end, st));
