@@ -42,12 +42,23 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
   __shared__ double Ls[NB][NB + 1];
   __shared__ double Xs[NB][NB + 1];
   __shared__ double Ts[NP - 1][PW][PW + 1];
-  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
+  __shared__ double piv[NB];   // L_jj (log-determinant summed at the end, off the pivot chain)
+  __shared__ double ipiv[NB];  // 1 / L_jj (the diagonal inverses multiply by it instead of dividing)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int e = tid; e < NB * NB; e += 256) {
-    const int rr = e / NB, cc = e % NB;
-    Ls[rr][cc] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
-    Xs[rr][cc] = 0.0;
+  {  // the block's 16 values per thread: all loads issued before the first LDS store (a load-store loop
+     // waited for each load in turn: ~16 memory latencies per launch)
+    double v[NB * NB / 256];
+#pragma unroll
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
+      v[u] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
+      Ls[rr][cc] = v[u];
+      Xs[rr][cc] = 0.0;
+    }
   }
   __syncthreads();
   bool bad = false;
@@ -71,7 +82,10 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
         const double ljj = d * inv;
-        if (i == 0) piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
+        if (i == 0) {
+          piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
+          ipiv[c0 + j] = (c0 + j < kb) ? inv : 1.0;
+        }
         r[j] = (i > c0 + j) ? r[j] * inv : (i == c0 + j ? ljj : r[j]);
 #pragma unroll
         for (int k = j + 1; k < PW; ++k) r[k] = fma(-r[j], readlane_d(r[j], c0 + k), r[k]);
@@ -112,7 +126,7 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
 #pragma unroll
       for (int k = 0; k < q; ++k) sacc = fma(Ls[o + q][o + k], x[k], sacc);
       const double v = (q == c) ? 1.0 : -sacc;
-      x[q] = (q >= c) ? v / Ls[o + q][o + q] : 0.0;
+      x[q] = (q >= c) ? v * ipiv[o + q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < PW; ++q) Xs[o + q][o + c] = x[q];
@@ -204,26 +218,40 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
 // a pivot fails (the caller checks *info_dev).
 int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
                      double *linv) {
+  // Optional look-ahead (GMAT_CHOL_LOOKAHEAD): after panel k is solved, the main stream updates only
+  // block column k + 1 of the trailing matrix ("narrow") and goes on to factor it, while the rest of the trailing update
+  // (block columns k + 2 ..) runs on a third stream; the narrow update of step k + 1 waits for that
+  // rest (both write block column k + 2).  The factorisation's critical path per step becomes potf2 +
+  // panel solve + the narrow update instead of potf2 + panel solve + the whole trailing update.
   static std::mutex mu;
-  static hipStream_t side[64] = {nullptr};
+  static hipStream_t side[64] = {nullptr}, rest_s[64] = {nullptr};
   static std::vector<hipEvent_t> evs[64];
   int dev = 0;
   GMAT_HIP(hipGetDevice(&dev));
   GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_ARG, "cholesky_inverse: device %d", dev);
   std::lock_guard<std::mutex> lock(mu);
   if (!side[dev]) GMAT_HIP(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
-  const hipStream_t s2 = side[dev];
+  if (!rest_s[dev]) GMAT_HIP(hipStreamCreateWithFlags(&rest_s[dev], hipStreamNonBlocking));
+  const hipStream_t s2 = side[dev], s3 = rest_s[dev];
   const int64_t nb = cdiv(n, NB);
-  while ((int64_t)evs[dev].size() < nb + 2) {
+  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done, ev[nb + 2 + i]: rest update i done,
+  // ev[2 nb + 2]: all rest updates done
+  while ((int64_t)evs[dev].size() < 2 * nb + 3) {
     hipEvent_t e;
     GMAT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     evs[dev].push_back(e);
   }
-  hipEvent_t *ev = evs[dev].data();  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done
+  hipEvent_t *ev = evs[dev].data();
+  hipEvent_t *ev_rest = ev + nb + 2;
+  // (one-box A/B at n = 2,000: 2.77 ms per REML iteration with the look-ahead against 2.33 without --
+  // the narrow update is as latency-bound as the whole one and the cross-stream waits add their own;
+  // kept behind GMAT_CHOL_LOOKAHEAD)
+  const bool lookahead = getenv("GMAT_CHOL_LOOKAHEAD") != nullptr;
   GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
   GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
   GMAT_HIP(hipEventRecord(ev[0], s));
   GMAT_HIP(hipStreamWaitEvent(s2, ev[0], 0));  // after the caller's earlier work on s
+  GMAT_HIP(hipStreamWaitEvent(s3, ev[0], 0));
   hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s2, linv, n * n);
   GMAT_HIP(hipGetLastError());
   for (int64_t k0 = 0, i = 0; k0 < n; k0 += NB, ++i) {
@@ -245,11 +273,26 @@ int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *d
     if (rem > 0) {
       GMAT_TRY(dgemm(s2, rem, k0 + kb, kb, -1.0, DView{a + (k0 + kb) * lda + k0, lda, 0}, DView{xi, n, 0}, 1.0,
                      linv + (k0 + kb) * n, n));
-      // A22 -= L21 L21'  (lower tiles)
       double *a22 = a + (k0 + kb) * lda + (k0 + kb);
-      GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
+      const int64_t kb1 = std::min<int64_t>(NB, rem), rest = rem - kb1;
+      if (!lookahead || rest <= 0) {  // A22 -= L21 L21'  (lower tiles), all on the main stream
+        if (i > 0 && lookahead) GMAT_HIP(hipStreamWaitEvent(s, ev_rest[i - 1], 0));
+        GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
+      } else {
+        // rest: block columns k + 2 .. (rows k + 2 ..) on the third stream, after panel k
+        GMAT_HIP(hipStreamWaitEvent(s3, ev[1 + i], 0));
+        GMAT_TRY(dgemm(s3, rest, rest, kb, -1.0, DView{panel + kb1 * lda, lda, 0}, DView{panel + kb1 * lda, lda, 1}, 1.0,
+                       a22 + kb1 * lda + kb1, lda, 1));
+        GMAT_HIP(hipEventRecord(ev_rest[i], s3));
+        // narrow: block column k + 1 (rows k + 1 ..) on the main stream, after the previous rest (which
+        // wrote this block column)
+        if (i > 0) GMAT_HIP(hipStreamWaitEvent(s, ev_rest[i - 1], 0));
+        GMAT_TRY(dgemm(s, rem, kb1, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda));
+      }
     }
   }
+  GMAT_HIP(hipEventRecord(ev[2 * nb + 2], s3));
+  GMAT_HIP(hipStreamWaitEvent(s, ev[2 * nb + 2], 0));
   GMAT_HIP(hipEventRecord(ev[nb + 1], s2));
   GMAT_HIP(hipStreamWaitEvent(s, ev[nb + 1], 0));
   return GMAT_OK;

@@ -11,8 +11,10 @@ import bench  # noqa: E402
 def main():
     n, m = (int(a) for a in (sys.argv[1:3] if len(sys.argv) > 2 else (2000, 50000)))
     g = bench.grm_bench(n, m, 1, reps=1)
-    r = bench.reml_bench(bench.grm_bench.last_k, 1)
-    print(json.dumps({"grm_kernel_ms": g["kernel_ms"], "reml": r}), flush=True)
+    bench.reml_bench(bench.grm_bench.last_k, 1)  # first call: workspaces, streams, code objects
+    r = [bench.reml_bench(bench.grm_bench.last_k, 1) for _ in range(3)]
+    r.sort(key=lambda x: x["ms_per_iter"])
+    print(json.dumps({"grm_kernel_ms": g["kernel_ms"], "reml": r[1]}), flush=True)
 
 
 if __name__ == "__main__":
