@@ -1937,6 +1937,7 @@ __global__ __launch_bounds__(MxShape<1>::T, 1) void lr_screen_kernel(ScreenArgs 
 struct LrcArgs {
   const uint8_t *tiles;  // [nC][nK] Q' tile images
   const uint8_t *nib_i, *nib_j;
+  const uint8_t *s1c2;           // the j side's S1 planes at 2 bits (s1_code2_kernel) [m][nK][32 B]
   int nK, nC, R;
   const int *slot_row, *slot_j;  // slot lists of the launch
   const int *slot_ops;           // the slot pairs' records (OPS_REC ints each, lc_fill)
@@ -1944,8 +1945,8 @@ struct LrcArgs {
   const double *recL, *recR;     // per-SNP test records (LR_REC doubles each)
   double lam, tau, eps, E;
 };
-constexpr int LRC_NSL = 3, LRC_JB = 64;          // ring slots; j-side bytes per column and stage (S1 plane)
-constexpr int LRC_SJ = MX_BI * 32 * LRC_JB;      // j-side bytes per stage (32 KB)
+// j-side bytes per column and stage: the S1 plane at 2 bits (J2) or as the nibble plane
+template <bool J2> constexpr int lrc_jb() { return J2 ? 32 : 64; }
 
 // slot pair p's record (lc_fill: the prefilter's E3 slices and code products of the pair)
 __device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, int64_t p, int64_t i, int64_t j,
@@ -1982,11 +1983,13 @@ __device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, 
   }
 }
 
+template <bool J2, int NSL>
 __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArgs x) {
-  constexpr int NSL = LRC_NSL, T = 512, RB = MX_RB, PB = 2, NA = MX_TILE / 16 / T, LA = NSL - 1;
+  constexpr int T = 512, RB = MX_RB, PB = 2, NA = MX_TILE / 16 / T, LA = NSL - 1;
+  constexpr int LRC_JB = lrc_jb<J2>(), NJ = LRC_JB / 16;  // j-side bytes per column and stage; DMAs per wave
   __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][MX_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t sI[NSL][MX_BI * NB_REC];
-  __shared__ __attribute__((aligned(16))) uint8_t sJ[NSL][LRC_SJ];
+  __shared__ __attribute__((aligned(16))) uint8_t sJ[NSL][MX_BI * 32 * LRC_JB];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nK = x.nK, nC = x.nC;
@@ -1996,16 +1999,20 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
   const int rr0 = x.slot_row[sbase + PB * w], rr1 = x.slot_row[sbase + PB * w + 1];
   if (__builtin_amdgcn_readfirstlane(x.slot_row[sbase]) < 0) return;  // empty tile (never queued)
   const int64_t i0 = rr0 >= 0 ? a.rows[rr0] : -1, i1 = rr1 >= 0 ? a.rows[rr1] : -1;
-  // DMA sources.  j side: instruction u of wave w moves its slots' (t, column, chunk) = item 64 u +
-  // lane (t = item / 128, column = item / 4 % 32, physical chunk = item % 4 holding logical chunk
-  // (item % 4) ^ ((column >> 2) & 3): the 16 lanes of a ds_read_b128 group hit 16 distinct slots).
-  unsigned oJ[4];
+  // DMA sources.  j side (round 4: the S1 planes at 2 bits, 32 B per column and stage, half the bytes
+  // of the nibble plane): instruction u of wave w moves its slots' (t, column, 16-byte chunk) = item
+  // 64 u + lane (t = item / 64, column = item / 2 % 32, physical chunk = item % 2 holding logical chunk
+  // (item % 2) ^ ((column >> 3) & 1): 2-way bank conflicts at most on the 8-byte reads).
+  // (!J2: the nibble plane, 64 B, four chunks per column, physical chunk (item % 4) ^ ((column >> 2) & 3))
+  unsigned oJ[NJ];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int item = 64 * u + lane, t = item >> 7, col = (item >> 2) & 31, pc = item & 3;
+  for (int u = 0; u < NJ; ++u) {
+    const int item = 64 * u + lane;
+    const int t = J2 ? item >> 6 : item >> 7, col = J2 ? (item >> 1) & 31 : (item >> 2) & 31;
+    const int pc = J2 ? item & 1 : item & 3, sw = J2 ? (col >> 3) & 1 : (col >> 2) & 3;
     const int rr = t ? rr1 : rr0;
     const int jj = rr >= 0 ? x.slot_j[(sbase + PB * w + t) * 32 + col] : -1;
-    oJ[u] = (unsigned)((jj >= 0 ? jj : 0) * nK * NB_REC + (pc ^ ((col >> 2) & 3)) * 16);
+    oJ[u] = (unsigned)((jj >= 0 ? jj : 0) * nK * (J2 ? LRC_JB : NB_REC) + (pc ^ sw) * 16);
   }
   unsigned oI = 0;  // i side (waves 0, 1): slot tid / 8 of the tile, 16-byte chunk tid % 8 of its record
   if (w < 2) {
@@ -2018,12 +2025,13 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
 #pragma unroll
     for (int u = 0; u < NA; ++u) lds_dma16(src + (tid + u * T) * 16, &sA[nb][(w * 64 + u * T) * 16]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) lds_dma16(x.nib_j + oJ[u] + kc * NB_REC, &sJ[nb][w * 4096 + u * 1024]);
+    for (int u = 0; u < NJ; ++u)
+      lds_dma16((J2 ? x.s1c2 + kc * LRC_JB : x.nib_j + kc * NB_REC) + oJ[u], &sJ[nb][w * NJ * 1024 + u * 1024]);
     if (w < 2) lds_dma16(x.nib_i + oI + kc * NB_REC, &sI[nb][w * 1024]);
   };
-  const int NL = NA + 4 + (w < 2 ? 1 : 0);  // this wave's DMAs per stage
+  const int NL = NA + NJ + (w < 2 ? 1 : 0);  // this wave's DMAs per stage
   v16f_ acc[RB][PB];
-  const int sw16 = 16 * ((c >> 3) & 1), jf = (c >> 2) & 3;
+  const int sw16 = 16 * ((c >> 3) & 1), jf = J2 ? (c >> 3) & 1 : (c >> 2) & 3;
   auto afrag = [&](int b, int kk, int r) __attribute__((always_inline)) {
     const uint8_t *ar = &sA[b][(2 * kk + h) * 4096 + (32 * r + c) * 32];
     const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
@@ -2037,7 +2045,15 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
       v8i_ fb[PB];
 #pragma unroll
       for (int t = 0; t < PB; ++t) {
-        const v4i j1 = *(const v4i *)&sJ[b][(PB * w + t) * 2048 + c * LRC_JB + 16 * ((2 * kk + h) ^ jf)];
+        // logical 8-byte piece 2 kk + h of the column: chunk kk (swizzled), half h; expanded to the
+        // nibble plane's four dwords (piece = D0 | D1 << 2, D2 | D3 << 2)
+        v4i j1;
+        if (J2) {
+          const v2i_ e2 = *(const v2i_ *)&sJ[b][(PB * w + t) * 32 * LRC_JB + c * LRC_JB + 16 * (kk ^ jf) + 8 * h];
+          j1 = v4i{e2[0] & 0x33333333, (e2[0] >> 2) & 0x33333333, e2[1] & 0x33333333, (e2[1] >> 2) & 0x33333333};
+        } else {
+          j1 = *(const v4i *)&sJ[b][(PB * w + t) * 32 * LRC_JB + c * LRC_JB + 16 * ((2 * kk + h) ^ jf)];
+        }
         const v4i j2 = j1 << 1;
         const v4i m1 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 32 * kk + 16 * h];
         const v4i m2 = *(const v4i *)&sI[b][(PB * w + t) * NB_REC + 64 + 32 * kk + 16 * h];
@@ -3265,6 +3281,21 @@ __global__ void nibble_kernel(int64_t m, int64_t n_pad, int nK, const int8_t *pa
   nib_j[rec + 16 + dd] = s2;
 }
 
+// the j side's S1 planes (nibble_kernel: nibble e of dword dd = code of individual 8 dd + e) at 2 bits
+// for the compacted low-rank screen: per (SNP, 128-individual stage) 32 bytes, 8-byte piece k packing
+// the plane's dwords 4k .. 4k + 3 as D0 | D1 << 2, D2 | D3 << 2 (codes 0..2 fit two bits)
+__global__ void s1_code2_kernel(int64_t m, int64_t n_pad, int nK, const int8_t *panel, uint32_t *out) {
+  const int64_t per = n_pad / 16;  // one output dword per 16 individuals
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= m * per) return;
+  const int64_t j = idx / per, g = idx % per;  // g: output dword (16 individuals: plane dwords 2g, 2g + 1)
+  const int8_t *src = panel + j * n_pad + 16 * g;
+  uint32_t d = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) d |= ((uint32_t)(src[e] & 3) | ((uint32_t)(src[8 + e] & 3) << 2)) << (4 * e);
+  out[j * (n_pad / 16) + g] = d;
+}
+
 // A = P + (mu + tau) 11'/n - mu I (natural order, n x n) for the prefilter's Cholesky certificate
 __global__ void pf_shift_kernel(int64_t n, const double *P, double mu, double tau, double *A) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3606,6 +3637,7 @@ struct Coding {
   DBuf qa, ra, sa, qb, rb, sb;    // per-SNP scalars
   DBuf mono;                      // uint8 [m]
   DBuf nibI, nibJ;                // MX screen nibble planes (i side M1/M2, j side S1/S2) [m][nK][128]
+  DBuf s1c2;                      // the S1 planes at 2 bits (compacted low-rank screen) [m][nK][32]
   DBuf p4;                        // screen codes as fp4 e2m1 [m][n_pad / 2] (prefilter)
   DBuf p2b, L3b;                  // stage-blocked copies for the prefilters: 2-bit codes [n_pad/64][m][16 B]
                                   // (code2_panel_kernel), L3q slices 0 .. E3_PF-1 [E3_PF][n_pad/64][m][64 B]
@@ -3857,6 +3889,10 @@ int build_coding_impl(gmat_epi *e, int which) {
   GMAT_TRY(cd.nibJ.alloc((size_t)m * n_pad));
   hipLaunchKernelGGL(nibble_kernel, dim3((unsigned)cdiv(m * (n_pad / 8), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
                      panel, cd.nibI.as<uint32_t>(), cd.nibJ.as<uint32_t>());
+  GMAT_HIP(hipGetLastError());
+  GMAT_TRY(cd.s1c2.alloc((size_t)m * n_pad / 4));
+  hipLaunchKernelGGL(s1_code2_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad, e->nK,
+                     panel, cd.s1c2.as<uint32_t>());
   GMAT_HIP(hipGetLastError());
   if (e->pf_ncov > 0) {  // covariate directions: u_k . code per SNP (the prefilter forms the images on chip)
     const int K0 = e->pf_ncov;
@@ -5625,9 +5661,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   sa.chi_cut = chi_cut;
   sa.counter = e->counter.as<unsigned long long>();
   LrcArgs lx;
+  const bool lrc_j4 = getenv("GMAT_LRC_J4") != nullptr;  // j side as the 4-bit nibble plane (A/B)
   lx.tiles = e->lr_tiles.as<uint8_t>();
   lx.nib_i = L.nibI.as<uint8_t>();
   lx.nib_j = R.nibJ.as<uint8_t>();
+  lx.s1c2 = R.s1c2.as<uint8_t>();
   lx.nK = e->nK;
   lx.nC = e->lr_R / MXK;
   lx.R = e->lr_R;
@@ -5696,7 +5734,14 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     lx.slot_ops = B.slot_ops[b].as<int>();
     GMAT_HIP(hipStreamWaitEvent(sm, side_end[b], 0));
     GMAT_HIP(hipEventRecord(scr_beg[b], sm));
-    if (tiles > 0) hipLaunchKernelGGL(lrc_screen_kernel, dim3((unsigned)tiles), dim3(512), 0, sm, sa, lx);
+    if (tiles > 0) {
+      // (one-box A/Bs: 18.3 against 19.3 ms per configs[2] step for the 2-bit j side against the nibble
+      // plane; a four-slot ring with it measured 18.4 against 18.2 ms)
+      if (lrc_j4)
+        hipLaunchKernelGGL((lrc_screen_kernel<false, 3>), dim3((unsigned)tiles), dim3(512), 0, sm, sa, lx);
+      else
+        hipLaunchKernelGGL((lrc_screen_kernel<true, 3>), dim3((unsigned)tiles), dim3(512), 0, sm, sa, lx);
+    }
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipMemcpyAsync(e->pins.cnt[b].p, e->counter.p, 8, hipMemcpyDeviceToHost, sm));
     GMAT_HIP(hipEventRecord(scr_end[b], sm));
