@@ -132,6 +132,46 @@ void *pinned_alloc(size_t n, size_t *got) {
   return p;
 }
 
+// non-blocking streams, kept per device once created (hipStreamCreate / hipStreamDestroy take ~3 ms
+// each: a plan's five streams cost ~30 ms of every remma_epiAA call end to end)
+namespace {
+struct StreamPool {
+  std::mutex mu;
+  std::multimap<int, hipStream_t> free_streams;  // device -> stream
+};
+StreamPool &stream_pool() {
+  static StreamPool *p = new StreamPool;
+  return *p;
+}
+}  // namespace
+
+int stream_acquire(hipStream_t *out) {
+  int dev = 0;
+  GMAT_HIP(hipGetDevice(&dev));
+  StreamPool &pl = stream_pool();
+  {
+    std::lock_guard<std::mutex> lk(pl.mu);
+    auto it = pl.free_streams.find(dev);
+    if (it != pl.free_streams.end()) {
+      *out = it->second;
+      pl.free_streams.erase(it);
+      return GMAT_OK;
+    }
+  }
+  GMAT_HIP(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+  return GMAT_OK;
+}
+
+void stream_release(hipStream_t s) {
+  if (!s) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  (void)hipStreamSynchronize(s);  // its work is done before another user queues behind it
+  StreamPool &pl = stream_pool();
+  std::lock_guard<std::mutex> lk(pl.mu);
+  pl.free_streams.insert({dev, s});
+}
+
 void pinned_free(void *p, size_t bytes) {
   if (!p) return;
   PinnedPool &pl = pinned_pool();

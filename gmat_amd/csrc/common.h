@@ -25,6 +25,10 @@ void pool_free(void *p, size_t bytes);
 // the same for pinned host staging buffers (hipHostMalloc / hipHostFree take about a millisecond each)
 void *pinned_alloc(size_t n, size_t *got);
 void pinned_free(void *p, size_t bytes);
+// non-blocking HIP streams from a process-wide cache (stream creation / destruction cost milliseconds);
+// stream_release synchronises the stream and keeps it for the next stream_acquire on its device
+int stream_acquire(hipStream_t *out);
+void stream_release(hipStream_t s);
 
 #define GMAT_HIP(x)                                                                        \
   do {                                                                                     \

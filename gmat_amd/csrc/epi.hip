@@ -3755,10 +3755,10 @@ struct gmat_epi {
   ~gmat_epi() {
     for (auto ev : kev) (void)hipEventDestroy(ev);
     for (auto ev : sev) (void)hipEventDestroy(ev);
-    if (s1) (void)hipStreamDestroy(s1);
-    if (s2) (void)hipStreamDestroy(s2);
-    if (s3) (void)hipStreamDestroy(s3);
-    if (s4) (void)hipStreamDestroy(s4);
+    stream_release(s1);
+    stream_release(s2);
+    stream_release(s3);
+    stream_release(s4);
   }
 };
 
@@ -4510,18 +4510,10 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
       (rc = rabs.alloc(n_pad * sizeof(double))))
     return fail(rc);
   hipStream_t sx = nullptr;
-  if (hipStreamCreateWithFlags(&sx, hipStreamNonBlocking) != hipSuccess) {
-    set_error("gmat_epi_create: stream creation failed");
-    return fail(GMAT_E_HIP);
-  }
+  if ((rc = stream_acquire(&sx)) != GMAT_OK) return fail(rc);
   struct StreamGuard {
     hipStream_t s;
-    ~StreamGuard() {
-      if (s) {
-        (void)hipStreamSynchronize(s);
-        (void)hipStreamDestroy(s);
-      }
-    }
+    ~StreamGuard() { stream_release(s); }
   } sx_guard{sx};
   (void)hipDeviceSynchronize();  // P, the slices and z / dg are ready for both streams
   const double os = qmax > 0 ? 15.0 / qmax : 1.0;
@@ -5249,7 +5241,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   const int tri = c.tri;
   // chunks of whole rows of at most `cap` pairs (one row holds at most m)
   const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : (1 << 24));
-  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
   const hipStream_t st = e->s3;
   DBuf di, dj, de, dv, dc, dp, hi, hj, he, hv, hc, hp, cnt, drows, doffs;
   for (DBuf *b : {&di, &dj, &de, &dv, &dc, &dp, &hi, &hj, &he, &hv, &hc, &hp}) GMAT_TRY(b->alloc((size_t)cap * 8));
@@ -5428,10 +5420,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
   }
-  if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
-  if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
-  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
-  if (!e->s4) GMAT_HIP(hipStreamCreateWithFlags(&e->s4, hipStreamNonBlocking));
+  if (!e->s1) GMAT_TRY(stream_acquire(&e->s1));
+  if (!e->s2) GMAT_TRY(stream_acquire(&e->s2));
+  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
+  if (!e->s4) GMAT_TRY(stream_acquire(&e->s4));
   // the prefilter passes of even / odd launches on two streams: launch L + 1 (other buffer set) can
   // start on the CUs that the tail of launch L leaves idle (a launch's ~800 equal tiles fill its last
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
@@ -5911,9 +5903,9 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   // pair screen + refine on S3; ordered after the coding setup by a device synchronisation
   // (Refining launch by launch beside the screens was measured 2.7x slower overall: refine waves
   // occupy CUs that a screen workgroup, which needs a whole CU, then waits for.)
-  if (!e->s1) GMAT_HIP(hipStreamCreateWithFlags(&e->s1, hipStreamNonBlocking));
-  if (!e->s2) GMAT_HIP(hipStreamCreateWithFlags(&e->s2, hipStreamNonBlocking));
-  if (!e->s3) GMAT_HIP(hipStreamCreateWithFlags(&e->s3, hipStreamNonBlocking));
+  if (!e->s1) GMAT_TRY(stream_acquire(&e->s1));
+  if (!e->s2) GMAT_TRY(stream_acquire(&e->s2));
+  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
   const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
   GMAT_HIP(hipDeviceSynchronize());
   ScanEvents evs{e};
