@@ -2635,6 +2635,8 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
     const int8_t *pa = x.a + i * n_pad, *pb = x.b + j * n_pad;
     const _Float16 *ua = x.Ua + i * n_pad, *ub = x.Ub + j * n_pad;
     float s1 = 0, s1a = 0, s2 = 0, s2a = 0, s3 = 0, s3a = 0, ef = 0, efa = 0, sw = 0;
+    // (the codes at 2 bits instead of int8, a quarter of the code bytes, measured the same: 18.3 ms per
+    // configs[2] step either way; the gathers are latency-bound)
     for (int64_t q0 = 8 * lane; q0 < n_pad; q0 += 512) {
       const v2i_ va = *(const v2i_ *)(pa + q0), vb = *(const v2i_ *)(pb + q0);
       const int8_t *ca = (const int8_t *)&va, *cb = (const int8_t *)&vb;
@@ -3294,6 +3296,40 @@ __global__ void s1_code2_kernel(int64_t m, int64_t n_pad, int nK, const int8_t *
 #pragma unroll
   for (int e = 0; e < 8; ++e) d |= ((uint32_t)(src[e] & 3) | ((uint32_t)(src[8 + e] & 3) << 2)) << (4 * e);
   out[j * (n_pad / 16) + g] = d;
+}
+
+// per row i of P (n x n, natural order): max |P_ik| off the diagonal, |P_ii| and the sum (mod 2^64)
+// of a 64-bit mix of every element's bits with its index (the plan's fingerprint of P, order-free)
+__global__ __launch_bounds__(256) void p_scan_kernel(int64_t n, const double *P, double *out) {
+  const int64_t i = blockIdx.x;
+  const double *row = P + i * n;
+  double q = 0.0;
+  uint64_t h = 0;
+  for (int64_t k = threadIdx.x; k < n; k += 256) {
+    const double v = row[k];
+    if (k != i) q = fmax(q, fabs(v));
+    uint64_t z = (uint64_t)__double_as_longlong(v) ^ ((uint64_t)(i * n + k) * 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    h += z ^ (z >> 31);
+  }
+  __shared__ double sq[256];
+  __shared__ uint64_t sh[256];
+  sq[threadIdx.x] = q;
+  sh[threadIdx.x] = h;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      sq[threadIdx.x] = fmax(sq[threadIdx.x], sq[threadIdx.x + off]);
+      sh[threadIdx.x] += sh[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[i] = sq[0];
+    out[n + i] = fabs(row[i]);
+    out[2 * n + i] = __longlong_as_double((long long)sh[0]);
+  }
 }
 
 // A = P + (mu + tau) 11'/n - mu I (natural order, n x n) for the prefilter's Cholesky certificate
@@ -4425,38 +4461,10 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   e->n_slice = n_slice;
   e->nK = (int)(g->n_pad / MXK);
   const int64_t n = e->n, n_pad = e->n_pad;
-  // max |P|, max |P_kl| off the diagonal (contiguous row pieces: vectorised) and the fingerprint of
-  // P as 8 interleaved hash lanes (independent multiply chains; one chain ran 11 ms at n = 2,000)
+  // max |P|, max |P_kl| off the diagonal and the fingerprint of P: on the device after the upload
+  // (p_scan_kernel; the host scan took ~3 ms of every plan at n = 2,000)
   double pmax = 0.0, qmax = 0.0, dmax = 0.0;
-  for (int64_t i = 0; i < n; ++i) {
-    const double *row = pvp + i * n;
-    double q = 0.0;
-    for (int64_t k = 0; k < i; ++k) q = std::max(q, std::fabs(row[k]));
-    for (int64_t k = i + 1; k < n; ++k) q = std::max(q, std::fabs(row[k]));
-    qmax = std::max(qmax, q);
-    dmax = std::max(dmax, std::fabs(row[i]));
-  }
-  pmax = std::max(qmax, dmax);
-  uint64_t hl[8];
-  for (int l = 0; l < 8; ++l) hl[l] = (0x9e3779b97f4a7c15ULL ^ (uint64_t)n) + 0x632be59bd9b4e019ULL * (uint64_t)l;
-  const int64_t nn = n * n, n8 = nn / 8 * 8;
-  for (int64_t k = 0; k < n8; k += 8)
-    for (int l = 0; l < 8; ++l) {
-      uint64_t b;
-      memcpy(&b, &pvp[k + l], 8);
-      hl[l] = (hl[l] ^ b) * 0x100000001b3ULL;
-      hl[l] ^= hl[l] >> 29;
-    }
-  for (int64_t k = n8; k < nn; ++k) {
-    uint64_t b;
-    memcpy(&b, &pvp[k], 8);
-    hl[0] = (hl[0] ^ b) * 0x100000001b3ULL;
-    hl[0] ^= hl[0] >> 29;
-  }
   uint64_t ph = 0;
-  for (int l = 0; l < 8; ++l) ph = (ph ^ hl[l]) * 0x100000001b3ULL ^ (ph >> 31);
-  e->qmax = qmax;
-  e->p_hash = ph;
   double spy = 0.0;
   for (int64_t i = 0; i < n; ++i) spy += py[i];
   e->spy = spy;
@@ -4477,6 +4485,28 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
     set_error("gmat_epi_create: upload failed");
     return fail(GMAT_E_HIP);
   }
+  {
+    DBuf scan;
+    if ((rc = scan.alloc((size_t)3 * n * sizeof(double)))) return fail(rc);
+    hipLaunchKernelGGL(p_scan_kernel, dim3((unsigned)n), dim3(256), 0, 0, n, dp.as<double>(), scan.as<double>());
+    std::vector<double> hs((size_t)3 * n);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpy(hs.data(), scan.p, hs.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("gmat_epi_create: scan of P failed");
+      return fail(GMAT_E_HIP);
+    }
+    ph = 0x9e3779b97f4a7c15ULL ^ (uint64_t)n;
+    for (int64_t i = 0; i < n; ++i) {
+      qmax = std::max(qmax, hs[i]);
+      dmax = std::max(dmax, hs[n + i]);
+      uint64_t h;
+      memcpy(&h, &hs[2 * n + i], 8);
+      ph += h;  // a sum of per-element mixes: independent of the reduction order
+    }
+    pmax = std::max(qmax, dmax);
+  }
+  e->qmax = qmax;
+  e->p_hash = ph;
   const unsigned gb = (unsigned)cdiv(n_pad * n_pad, 256);
   hipLaunchKernelGGL(permute_p_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), e->Ps.as<double>());
   hipLaunchKernelGGL(permute_vec_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n, n_pad, dv.as<double>(),
