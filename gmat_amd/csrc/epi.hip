@@ -2510,7 +2510,7 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
 // the most row-block segments a short refine8 / pair_mxr list is split into (GMAT_SEG_MAX, default 8)
 int seg_max() {
   const char *s = getenv("GMAT_SEG_MAX");
-  return s ? std::max(1, std::min(8, atoi(s))) : 8;
+  return s ? std::max(1, std::min(16, atoi(s))) : 8;
 }
 __global__ void r8_combine_kernel(int64_t np, int nseg, const double *tpart, double unit, double *varw) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4154,7 +4154,7 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
     const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(seg_max(), nK), e->n_cu / wgs));
     if (nseg > 1 && e->ps_mpart.bytes < (size_t)nseg * np * sizeof(double)) {
       GMAT_HIP(hipStreamSynchronize(st));
-      GMAT_TRY(e->ps_mpart.alloc((size_t)8 * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
+      GMAT_TRY(e->ps_mpart.alloc((size_t)std::max(8, nseg) * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
     }
     x.mpart = e->ps_mpart.as<double>();
     hipLaunchKernelGGL(pair_mxr_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, x);
