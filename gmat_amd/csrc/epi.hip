@@ -938,47 +938,61 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     vm_wait_barrier(nq * max(0, min(st + PC_NS - 1, S - 1) - (st + 2)));
   }
   pstamp(2);
-  // epilogue as prefilter_pass_kernel, plus the direction terms
-  __shared__ double rowv[7][PC_TR];
-  __shared__ double rowu[NC][PC_TR];  // u.a per direction
+  // epilogue as prefilter_pass_kernel's (fp32 with its certified slack, straight-line tests), plus the
+  // direction terms: each c_k = t1 - t2 - t3 + t4 (t1 = sq_k / 2 x the doubled integer sum, t2 = beta
+  // u_k.a, t3 = alpha u_k.b, t4 = alpha beta 1'u_k) is off by at most 2^-21 (|t1| + .. + |t4|) in fp32
+  // (inputs rounded from fp64 included), to which the quantisation bound sq_k Sab / 2 is added; |U'e|^2
+  // from those upper bounds carries a relative 2^-20 of its own roundings, covered by ku (1 + 2^-18).
+  // (Round 3 / early round 4: fp64, 13 us of epilogue per tile.)
+  __shared__ float rowf[7][PC_TR];    // i (int bits, -1 monomorphic), alpha, csum, R1, sL3, sa, (2 + alpha)^2
+  __shared__ float rowu[NC][PC_TR];   // u.a per direction
   const double n = a.n_id;
   if (tid < PC_TR) {
     const int r = min(r0 + tid, a.n_rows - 1);
     const int64_t i = a.rows[r];
     const double al = a.alpha[i], ca = a.csum_l[i];
-    rowv[0][tid] = a.mono_l[i] ? -1.0 : (double)i;
-    rowv[1][tid] = al;
-    rowv[2][tid] = ca;
-    rowv[3][tid] = a.csq_l[i] - 2.0 * al * ca;
-    rowv[4][tid] = a.sL3[i];
-    rowv[5][tid] = a.sa[i];
-    rowv[6][tid] = (2.0 + al) * (2.0 + al);
+    rowf[0][tid] = __int_as_float(a.mono_l[i] ? -1 : (int)i);
+    rowf[1][tid] = (float)al;
+    rowf[2][tid] = (float)ca;
+    rowf[3][tid] = (float)(a.csq_l[i] - 2.0 * al * ca);
+    rowf[4][tid] = (float)a.sL3[i];
+    rowf[5][tid] = (float)a.sa[i];
+    rowf[6][tid] = (float)((2.0 + al) * (2.0 + al));
 #pragma unroll
-    for (int k = 0; k < NC; ++k) rowu[k][tid] = a.pf_ua[k * a.m + i];
+    for (int k = 0; k < NC; ++k) rowu[k][tid] = (float)a.pf_ua[k * a.m + i];
   }
   __syncthreads();
   pstamp(3);
-  const double mu_e = a.pf_mu - a.pf_eps, k1 = (a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n, k2 = 1e-12 * a.pf_mu;
-  const double ku = a.pf_ku * (1.0 + 1e-12);
+  const float mu_e = (float)(a.pf_mu - a.pf_eps), k1 = (float)((a.pf_mu + a.pf_tau + 1e-12 * a.pf_mu) / n);
+  const float k2 = (float)(std::ldexp(1.0, -17) * (2.0 * a.pf_mu + a.pf_tau));
+  const float ku = (float)(a.pf_ku * (1.0 + std::ldexp(1.0, -18)));
+  const float chi_cut = (float)a.chi_cut, e3_eps = (float)a.e3_eps;
+  constexpr float EFF_REL = 0x1p-20f, CMP = 1.0f + 0x1p-18f, UREL = 0x1p-21f, QREL = 1.0f + 0x1p-20f;
   const int64_t j = c0 + crow;
   const int J = (int)(j / 32);
   const bool jok = j < a.m && j >= a.j_lo;
-  double cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
+  float cbe = 0, ccb = 0, cC1n = 0, cnb = 0, cbsb = 0, cmag = 0, cub[NC];
 #pragma unroll
-  for (int k = 0; k < NC; ++k) cub[k] = 0.0;
+  for (int k = 0; k < NC; ++k) cub[k] = 0.f;
   unsigned own = 0u, n_live = 0u;  // compacted path: this lane's live elements, the wave's live pairs
   bool cmono = true;
   if (jok) {
-    cbe = a.beta[j];
-    ccb = a.csum_r[j];
-    const double cb2 = a.csq_r[j];
-    cC1n = cb2 - 2.0 * cbe * ccb + n * cbe * cbe;
-    cnb = n * cbe - ccb;
-    cbsb = cbe * a.spy - a.sb[j];
-    cmag = cb2 + 2.0 * cbe * ccb + n * cbe * cbe;
+    const double be = a.beta[j], cb = a.csum_r[j], cb2 = a.csq_r[j];
+    cbe = (float)be;
+    ccb = (float)cb;
+    cC1n = (float)(cb2 - 2.0 * be * cb + n * be * be);
+    cnb = (float)(n * be - cb);
+    cbsb = (float)(be * a.spy - a.sb[j]);
+    cmag = (float)(cb2 + 2.0 * be * cb + n * be * be);
     cmono = a.mono_r[j];
 #pragma unroll
-    for (int k = 0; k < NC; ++k) cub[k] = a.pf_ub[k * a.m + j];
+    for (int k = 0; k < NC; ++k) cub[k] = (float)a.pf_ub[k * a.m + j];
+  }
+  float sqh[NC], su4[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    sqh[k] = (float)(0.5 * a.pf_sq[k]);
+    su4[k] = (float)a.pf_su[k];
   }
   // every wave has passed the last stage's barrier (and the records' barrier): the ring is free for the
   // next tile's first stages, which land while the tests below run.  (Issued after the per-row and
@@ -989,40 +1003,31 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     asm volatile("" ::"v"(cbe), "v"(ccb), "v"(cC1n), "v"(cnb), "v"(cbsb), "v"(cmag), "v"(cub[0]), "v"((int)cmono));
     for (int st = 0; st < pre; ++st) issue(st);
   }
+  const bool cok = jok & !cmono;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int rl = (e & 3) + 8 * (e >> 2) + 4 * h, r = r0 + rl;
     const bool rok = r < a.n_rows;
     const int64_t o1 = (int64_t)(rok ? r : 0) * a.ld_e + (j - a.j_lo);
-    bool live = false;
-    const double iv = rowv[0][rl];
-    if (rok && jok && iv >= 0.0 && !cmono) {
-      const int64_t i = (int64_t)iv;
-      if (!(a.tri && j <= i)) {
-        const double al = rowv[1][rl], sL3 = rowv[4][rl], be = cbe;
-        double c3 = 0.0;
+    const int iv = __float_as_int(rowf[0][rl]);
+    const bool ok = rok & cok & (iv >= 0) & !(a.tri & (j <= (int64_t)iv));
+    const float al = rowf[1][rl], sL3 = rowf[4][rl], be = cbe;
+    const float c3 = (float)acc[1][e] * (1.0f / 128.0f) + (float)acc[0][e];  // twice the E3 slice sums
+    const float t1 = 0.5f * sL3 * c3, t2 = be * rowf[5][rl], t3 = al * cbsb;
+    const float eff = t1 - t2 + t3;
+    const float eff_hi = fabsf(eff) + e3_eps * sL3 * ccb + EFF_REL * (fabsf(t1) + fabsf(t2) + fabsf(t3));
+    const float sab = acc4[0][e], sa2b = acc4[1][e], sab2 = acc4[2][e], sa2b2 = acc4[3][e];
+    const float ee = sa2b2 + be * (be * rowf[3][rl] - 2.0f * sa2b) + al * (4.0f * be * sab - 2.0f * sab2 + al * cC1n);
+    const float se = sab - be * rowf[2][rl] + al * cnb;
+    float u2 = 0.f;
 #pragma unroll
-        for (int t = E3_PF - 1; t >= 0; --t) c3 = c3 * (1.0 / 128.0) + (double)acc[t][e];
-        const double eff = 0.5 * sL3 * c3 - be * rowv[5][rl] + al * cbsb;
-        const double eff_hi = fabs(eff) + a.e3_eps * sL3 * ccb;
-        const double sab = (double)acc4[0][e], sa2b = (double)acc4[1][e], sab2 = (double)acc4[2][e],
-                     sa2b2 = (double)acc4[3][e];
-        const double ee =
-            sa2b2 + be * (be * rowv[3][rl] - 2.0 * sa2b) + al * (4.0 * be * sab - 2.0 * sab2 + al * cC1n);
-        const double se = sab - be * rowv[2][rl] + al * cnb;
-        double u2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-          const double sq = a.pf_sq[k], t1 = 0.5 * sq * (double)accu[k][e], t2 = be * rowu[k][rl], t3 = al * cub[k],
-                       t4 = al * be * a.pf_su[k];
-          const double ck = fabs(t1 - t2 - t3 + t4) + 0.5 * sq * sab * (1.0 + 1e-9) +
-                            1e-12 * (fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4));
-          u2 += ck * ck;
-        }
-        const double vlo = mu_e * ee - k1 * se * se - ku * u2 - k2 * rowv[6][rl] * cmag;
-        live = !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
-      }
+    for (int k = 0; k < NC; ++k) {
+      const float u1 = sqh[k] * (float)accu[k][e], uu2 = be * rowu[k][rl], u3 = al * cub[k], u4 = al * be * su4[k];
+      const float ck = fabsf(u1 - uu2 - u3 + u4) + sqh[k] * sab * QREL + UREL * (fabsf(u1) + fabsf(uu2) + fabsf(u3) + fabsf(u4));
+      u2 += ck * ck;
     }
+    const float vlo = mu_e * ee - k1 * se * se - ku * u2 - k2 * rowf[6][rl] * cmag;
+    const bool live = ok & (!(vlo > 0.0f) | (eff_hi * eff_hi * CMP >= chi_cut * vlo));
     const unsigned long long bal = __ballot(live);
     const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
     if (rok && c == 0 && J < a.nJ) {
