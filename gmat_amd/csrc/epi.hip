@@ -115,7 +115,8 @@ struct ScreenArgs {
   unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
   unsigned long long *pf_stamp;    // diagnostics (GMAT_PF_STAMPS): 4 s_memrealtime stamps per workgroup, or null
   uint32_t *lmask;  // compacted low-rank path: per (band row, 32-column block) the prefilter's live
-                    // pairs as a bit mask (bit c = column 32 J + c), or null
+                    // pairs as a bit mask (bit c = column 32 J + c), or null; only nonzero words are
+                    // written (the caller zeroes the launch's masks)
   // compacted low-rank path: the live pairs' test operands as OPS_REC-int records {E3 slice 0, E3
   // slice 1, Sab, Sa2b, Sab2, Sa2b2, j, 0} appended at ops (a wave reserves its records with one
   // atomic on ops_count, a persistent one in chunks of PF_CHUNK or more; nothing is stored past
@@ -727,7 +728,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
       if (lane < 32 && tr < a.n_rows && J < a.nJ) {
         if (a.flags) a.flags[(int64_t)tr * a.nJ + J] = mine[q] != 0;
-        if (a.lmask) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
+        // live masks: only the nonzero words (the scan zeroes a launch's masks: 8.5 % of the words at
+        // configs[2], 0.3 GB less written per step)
+        if (a.lmask && mine[q]) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
       }
     }
     if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
@@ -1032,7 +1035,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
     if (rok && c == 0 && J < a.nJ) {
       if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
-      if (a.lmask) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
+      if (a.lmask && (uint32_t)(bal >> (32 * h))) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
     }
     if (a.ops) {  // compacted path: records below
       own |= (live ? 1u : 0u) << e;
