@@ -42,8 +42,7 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
   __shared__ double Ls[NB][NB + 1];
   __shared__ double Xs[NB][NB + 1];
   __shared__ double Ts[NP - 1][PW][PW + 1];
-  __shared__ double piv[NB];   // L_jj (log-determinant summed at the end, off the pivot chain)
-  __shared__ double ipiv[NB];  // 1 / L_jj (the diagonal inverses multiply by it instead of dividing)
+  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   {  // the block's 16 values per thread: all loads issued before the first LDS store (a load-store loop
      // waited for each load in turn: ~16 memory latencies per launch)
@@ -82,10 +81,7 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
         const double ljj = d * inv;
-        if (i == 0) {
-          piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
-          ipiv[c0 + j] = (c0 + j < kb) ? inv : 1.0;
-        }
+        if (i == 0) piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
         r[j] = (i > c0 + j) ? r[j] * inv : (i == c0 + j ? ljj : r[j]);
 #pragma unroll
         for (int k = j + 1; k < PW; ++k) r[k] = fma(-r[j], readlane_d(r[j], c0 + k), r[k]);
@@ -126,7 +122,9 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
 #pragma unroll
       for (int k = 0; k < q; ++k) sacc = fma(Ls[o + q][o + k], x[k], sacc);
       const double v = (q == c) ? 1.0 : -sacc;
-      x[q] = (q >= c) ? v * ipiv[o + q] : 0.0;
+      // (a division, not a multiplication by 1 / L_qq: the bits of P = V^-1 .. are pinned by the
+      // recorded exhaustive hit set's cohort fingerprint; the multiplication measured no faster)
+      x[q] = (q >= c) ? v / Ls[o + q][o + q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < PW; ++q) Xs[o + q][o + c] = x[q];

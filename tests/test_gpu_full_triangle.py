@@ -132,3 +132,22 @@ def test_full_triangle_ad_dd(small_cohort, kind):
         with EpiPlan(g, pvp, py) as plan:
             d = plan.scan("AD", np.arange(5, dtype=np.int64), 1.0, n_slice=N.GMAT_SCREEN_NONE)
         assert d[0].size > 0 and np.any(d[0] == d[1])
+
+
+def test_recorded_exhaustive_hit_set_still_applies():
+    """bench.py checks every step against the recorded exhaustive hit set of its cohort
+    (tests/golden/cfg3_exhaustive_hits_AA_2000x50000.npz) only while the cohort fingerprint (per-SNP
+    counts, P, Py) matches: a change that moves a bit of P (the projection's Cholesky and inverse)
+    silently turns that check off, so it fails here instead."""
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    import bench
+    from tools.full_triangle import cohort_fingerprint
+    rec = np.load(os.path.join(repo, bench.EXHAUSTIVE_HITS))
+    _, g, pvp, py, _, _ = bench.build_inputs(2000, 50000, 1, np.array([0.4, 0.2, 0.4]), 0, 1)
+    try:
+        assert bytes(rec["fingerprint"]).hex() == cohort_fingerprint(g, pvp, py)
+    finally:
+        g.close()
