@@ -2362,7 +2362,7 @@ __global__ void pvalue_kernel(int64_t np, const double *eff, const double *var, 
 // combination sum_s 2^-7s T_s and R (|w'Rw| <= 8e-16 qmax |w|_1^2).  The O(n) terms are fp64 dot
 // products with U = P x codes (refine8_side_kernel), eff = e'Py in fp64 from the reference codes.
 // Tiles: (32-row block kb, 64-column stage cs >= kb / 2), R8_S slices x 2 row tiles x 16 rows x 64
-// bytes, 16-byte chunks XOR-swizzled by row; a workgroup = 8 waves x 16 pairs (v_mfma_i32_16x16x64_i8,
+// bytes, 16-byte chunks XOR-swizzled by row (r8_swz); a workgroup = 8 waves x 16 pairs (v_mfma_i32_16x16x64_i8,
 // w as the B fragments in registers: n_pad <= 64 R8_NC), the tiles stream through an eight-slot
 // LDS-DMA ring (six in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
 // folds the row block).
@@ -2371,6 +2371,10 @@ __host__ __device__ inline int64_t r8_toff(int64_t kb, int64_t NS) {  // tiles o
   const int64_t h = kb >> 1;
   return kb * NS - ((kb & 1) ? h * h : h * (h - 1));
 }
+// the 16-byte chunk swizzle of a tile row (row & 15): chunk k of row r sits at k ^ r8_swz(r), so that
+// each 16-lane group of refine8_kernel's ds_read_b128 (rows c, chunks g) covers all 64 banks (k ^ (r & 3)
+// alone left rows r and r + 4 on the same banks: 2-way conflicts, ~20 % of the kernel's cycles)
+__host__ __device__ inline int r8_swz(int r) { return (r & 3) ^ ((r >> 1) & 2); }
 __global__ void r8_image_kernel(int64_t n_pad, const double *__restrict__ Ps, double inv_unit, int8_t *__restrict__ tiles) {
   const int64_t NB = n_pad / 32, NS = n_pad / 64;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, column) of a tile row
@@ -2382,7 +2386,7 @@ __global__ void r8_image_kernel(int64_t n_pad, const double *__restrict__ Ps, do
   const double f = bc > kb ? 2.0 : (bc == kb ? 1.0 : 0.0);
   double r = (rs != cc) ? f * Ps[rs * n_pad + cc] * inv_unit : 0.0;
   const int rt = (int)((rs % 32) / 16), row = (int)(rs % 16), k = (int)(cc % 64);
-  int8_t *t = tiles + (r8_toff(kb, NS) + cs - kb / 2) * R8_TILE + (rt * 16 + row) * 64 + 16 * ((k / 16) ^ (row & 3)) + k % 16;
+  int8_t *t = tiles + (r8_toff(kb, NS) + cs - kb / 2) * R8_TILE + (rt * 16 + row) * 64 + 16 * ((k / 16) ^ r8_swz(row)) + k % 16;
   for (int s = 0; s < R8_S; ++s) {
     const double q = rint(r);
     t[s * R8_TB] = (int8_t)q;
@@ -2453,7 +2457,7 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   double T[R8_S];
 #pragma unroll
   for (int s = 0; s < R8_S; ++s) T[s] = 0.0;
-  const int swz = 16 * (g ^ (c & 3));
+  const int swz = 16 * (g ^ r8_swz(c));
   int v = 0;
   for (int kb = kb_lo; kb < kb_hi; ++kb) {
     const int c0 = kb >> 1;
@@ -2657,14 +2661,23 @@ __global__ __launch_bounds__(256) void pair_side_kernel(PairArgs x) {
         vv[t] = (float)v8[t];
       }
       // z, diag(P), Py of the lane's 8 individuals as 16-byte LDS reads (a lane's 32 bytes: 8 scalar reads at
-      // a 32-byte lane stride were 8-way bank conflicts)
+      // a 32-byte lane stride were 8-way bank conflicts).  Lanes with bit 3 set read their second half
+      // first: each 16-lane group of a ds_read_b128 then covers all 64 banks (in one order the groups'
+      // lanes l and l + 8 or l + 24 met on a bank, 2-way: ~40 % of the kernel's cycles by SQ_LDS_BANK_CONFLICT)
       float zz8[8], dd8[8], yy8[8];
-      *(float4 *)&zz8[0] = *(const float4 *)&zdp[q0];
-      *(float4 *)&zz8[4] = *(const float4 *)&zdp[q0 + 4];
-      *(float4 *)&dd8[0] = *(const float4 *)&zdp[n_pad + q0];
-      *(float4 *)&dd8[4] = *(const float4 *)&zdp[n_pad + q0 + 4];
-      *(float4 *)&yy8[0] = *(const float4 *)&zdp[2 * n_pad + q0];
-      *(float4 *)&yy8[4] = *(const float4 *)&zdp[2 * n_pad + q0 + 4];
+      {
+        const int o1 = (lane & 8) ? 4 : 0, o2 = 4 - o1;
+        const bool sw = lane & 8;
+        auto rd2 = [&](const float *base, float *dst) __attribute__((always_inline)) {
+          const float4 f1 = *(const float4 *)&base[q0 + o1];
+          const float4 f2 = *(const float4 *)&base[q0 + o2];
+          *(float4 *)&dst[0] = sw ? f2 : f1;
+          *(float4 *)&dst[4] = sw ? f1 : f2;
+        };
+        rd2(zdp, zz8);
+        rd2(zdp + n_pad, dd8);
+        rd2(zdp + 2 * n_pad, yy8);
+      }
 #pragma unroll
       for (int h = 0; h < 8; ++h) {
         const float av = (float)ca[h], bv = (float)cb[h], w = av * bv;  // exact small integers
