@@ -2407,7 +2407,7 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   const int NB = (int)(n_pad / 32), NS = (int)(n_pad / 64);
   // segment blockIdx.y of gridDim.y: the row blocks [kb_lo, kb_hi) holding its share of the tiles (a
   // short pair list is spread over more workgroups); its per-slice integer sums go to tpart, added by
-  // r8_combine_kernel (exact: the same bits for any number of segments)
+  // refine8_side_kernel (exact: the same bits for any number of segments)
   const int nseg = (int)gridDim.y, seg = (int)blockIdx.y;
   const int64_t N_all = r8_toff(NB, NS);
   int kb_lo = 0, kb_hi = 0;
@@ -2518,22 +2518,10 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + T[s];
   varw[p] = unit * sum;
 }
-// the segments' integer sums added (exactly, in fp64) and combined as refine8_kernel does for one
 // the most row-block segments a short refine8 / pair_mxr list is split into (GMAT_SEG_MAX, default 8)
 int seg_max() {
   const char *s = getenv("GMAT_SEG_MAX");
   return s ? std::max(1, std::min(16, atoi(s))) : 8;
-}
-__global__ void r8_combine_kernel(int64_t np, int nseg, const double *tpart, double unit, double *varw) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
-  double sum = 0.0;
-  for (int s = R8_S - 1; s >= 0; --s) {
-    double t = 0.0;
-    for (int k = 0; k < nseg; ++k) t += tpart[((int64_t)k * R8_S + s) * np + p];
-    sum = sum * (1.0 / 128.0) + t;
-  }
-  varw[p] = unit * sum;
 }
 
 // The O(n) terms of e'Pe in fp64 (refine8_kernel's expansion) and eff = e'Py from the reference
@@ -2548,7 +2536,9 @@ __global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const 
                                                            const double *qb, const double *rb, double zz,
                                                            const uint8_t *mono_l, const uint8_t *mono_r,
                                                            const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
-                                                           int64_t np, const double *varw, double *eff, double *var) {
+                                                           int64_t np, const double *varw, int nseg, const double *tpart,
+                                                           double unit, double *eff, double *var, double *chi,
+                                                           double *pv) {
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= np) return;
@@ -2574,9 +2564,28 @@ __global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const 
   if (lane) return;
   const double t3 = be * be * qa[i], t5 = al * al * qb[j], t7 = ab * ab * zz, t8 = 2.0 * ab * s2, t4 = -2.0 * ab * be * ra[i],
                t6 = -2.0 * ab * al * rb[j];
+  // w'P_off w: refine8_kernel's value, or its segments' integer sums added exactly in fp64 (integers
+  // < 2^53) and combined in the single-segment order: the same bits for any number of segments
+  double vw;
+  if (nseg > 1) {
+    double sum = 0.0;
+    for (int s = R8_S - 1; s >= 0; --s) {
+      double t = 0.0;
+      for (int k = 0; k < nseg; ++k) t += tpart[((int64_t)k * R8_S + s) * np + p];
+      sum = sum * (1.0 / 128.0) + t;
+    }
+    vw = unit * sum;
+  } else {
+    vw = varw[p];
+  }
   // x == 0 (monomorphic): e = 0 exactly, var = 0 as the reference computes it (its chi and p are NaN)
-  var[p] = (mono_l[i] || mono_r[j]) ? 0.0 : varw[p] + s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
+  const double v = (mono_l[i] || mono_r[j]) ? 0.0 : vw + s3 + 2.0 * s1 + t3 + t5 + t7 + t8 + t4 + t6;
+  var[p] = v;
   eff[p] = ef;
+  // chi and p as pvalue_kernel
+  const double cc = ef * ef / v;
+  chi[p] = cc;
+  pv[p] = (cc < 0.0) ? 1.0 : erfc(sqrt(0.5 * cc));
 }
 
 // ------------------------------------------------------------------ pair screen
@@ -4033,22 +4042,18 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
     hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
                        e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>(), tpart);
     GMAT_HIP(hipGetLastError());
-    if (nseg > 1) {
-      hipLaunchKernelGGL(r8_combine_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, nseg, tpart,
-                         e->r8_unit, e->r8_varw.as<double>());
-      GMAT_HIP(hipGetLastError());
-    }
     GMAT_TRY(kt_end(e, st, KT_REFINE, kt0, (double)np));
     GMAT_TRY(kt_begin(e, st, &kt0));
+    // the O(n) terms, the segments' combination and the p-values in one launch (as three launches they
+    // were two more dependent steps at the end of every scan)
     hipLaunchKernelGGL(refine8_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, e->n_pad, sl, sr,
                        L.U.as<double>(), R.U.as<double>(), e->z.as<double>(), e->dg.as<double>(), e->py.as<double>(), lp,
                        rp, L.soff.as<double>(), R.soff.as<double>(), L.off.as<double>(), R.off.as<double>(),
                        L.qa.as<double>(), L.ra.as<double>(), R.qb.as<double>(), R.rb.as<double>(), e->zz,
-                       L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj, np, e->r8_varw.as<double>(), eff, var);
+                       L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj, np, e->r8_varw.as<double>(), nseg, tpart,
+                       e->r8_unit, eff, var, chi, p);
     GMAT_HIP(hipGetLastError());
     GMAT_TRY(kt_end(e, st, KT_REFINE_SIDE, kt0, (double)np));
-    hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, eff, var, chi, p);
-    GMAT_HIP(hipGetLastError());
     return GMAT_OK;
   }
   // a fixed number of segments per pair tile (not one chosen from np: a pair's numbers must not
@@ -5299,7 +5304,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   GMAT_TRY(cnt.alloc(8));
   GMAT_TRY(drows.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
   GMAT_TRY(doffs.alloc((size_t)std::max<int64_t>(n_rows, 1) * 8));
-  GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
+  GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t ev0, ev1;
   GMAT_TRY(evs.make(&ev0));
@@ -5480,7 +5485,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, getenv("GMAT_PF_ONE_STREAM") ? e->s2 : e->s4};
-  GMAT_HIP(hipDeviceSynchronize());  // the codings were built on the plan's stream
+  GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
   double t_pf = 0, pf_ops = 0;
