@@ -3456,6 +3456,138 @@ __global__ void fp4_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, 
 // stage-blocked 2-bit genotype codes (the prefilters' code stream): per SNP and 16 individuals a dword
 // whose nibble k holds c[k] | c[8 + k] << 2 (fp4_of_code2 expands it with two VALU per fp4 dword);
 // dst[(st m + snp) 16 B + 4 g] for the stage st's 16-individual group g
+// ---- U = codes x P on the int8 matrix cores (the codings' side vectors; fp64 GEMM: 10.5 ms per coding
+// at configs[2], this 2-3 ms).  P in U8_S int8 slices per row q with the row's unit u_q = max_r |P_qr| / 127:
+//   P_qr = u_q sum_s 128^-s B_s[q][r] + R_qr,  |R_qr| <= u_q 128^-(U8_S-1) / 2 = u_q 2^-50,
+// so T_s = codes x B_s' is an exact int32 sum (|T_s| <= 254 n_pad) and U[j][q] = u_q sum_s 128^-s T_s[j][q]
+// is off by at most 2 n_pad u_q 2^-50 (below the fp64 GEMM's own rounding bound, 2 n_pad 2^-53 max |P|
+// per row, times 8 n_pad / 127 -- ~2^-46 relative to the row's largest |P| at n_pad = 2048).  P is
+// symmetric: row q is column q.
+// Operands per stage of 64 individuals (SG_K): the codes from the 2-bit stage-blocked panel (p2b, 16 B per
+// SNP and stage, code2_panel_kernel) expanded to int8 in registers; the slices stage-blocked as
+// [stage][slice][q][64 B] with the 16-byte chunks XOR-swizzled by q & 31 (u8_swz: conflict-free
+// ds_read_b128 of the B fragments) and the bytes of a chunk in the expansion's individual order
+// (0 2 4 6 1 3 5 7 8 10 12 14 9 11 13 15).  A workgroup: 256 SNPs x 32 columns q, 8 waves of 32 SNPs
+// (v_mfma_i32_32x32x32_i8, one accumulator per slice), a four-slot LDS-DMA ring (three stages in
+// flight).
+constexpr int U8_S = 8, U8_J = 256, U8_Q = 32, U8_NS = 4, U8_AB = U8_J * 16, U8_ST = U8_AB + U8_S * U8_Q * 64;
+__host__ __device__ inline int u8_swz(int q) { return (q & 3) ^ ((q >> 3) & 3); }
+__host__ __device__ inline int u8_pos(int t16) {  // byte position of individual t16 (0..15) in its chunk
+  return (t16 & 8) + ((t16 & 1) ? 4 : 0) + ((t16 & 7) >> 1);
+}
+__global__ void u8_unit_kernel(int64_t n_pad, const double *__restrict__ Ps, double *__restrict__ unit) {
+  const int64_t q = blockIdx.x;
+  double mx = 0.0;
+  for (int64_t r = threadIdx.x; r < n_pad; r += blockDim.x) mx = fmax(mx, fabs(Ps[q * n_pad + r]));
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double m4 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    unit[q] = m4 > 0.0 ? m4 / 127.0 : 1.0;
+  }
+}
+__global__ void u8_slice_kernel(int64_t n_pad, const double *__restrict__ Ps, const double *__restrict__ unit,
+                                int8_t *__restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_pad * n_pad) return;
+  const int64_t q = idx / n_pad, r = idx % n_pad;
+  const int64_t st = r / 64;
+  const int rr = (int)(r % 64), chunk = rr >> 4, pos = u8_pos(rr & 15);
+  const int phys = chunk ^ u8_swz((int)(q & 31));
+  double v = Ps[idx] / unit[q];
+  int8_t *o = out + (st * U8_S * n_pad + q) * 64 + phys * 16 + pos;
+  for (int sl = 0; sl < U8_S; ++sl) {
+    const double t = rint(v);
+    o[(int64_t)sl * n_pad * 64] = (int8_t)t;
+    v = (v - t) * 128.0;
+  }
+}
+// int8 values of the 16 genotype codes of one dword of the 2-bit panel (nibble k = c[k] | c[8 + k] << 2),
+// in the order 0 2 4 6 | 1 3 5 7 | 8 10 12 14 | 9 11 13 15
+__device__ __forceinline__ v4i i8_of_code2(unsigned d) {
+  const unsigned lo = d & 0x33333333u, hi = (d >> 2) & 0x33333333u;
+  return v4i{(int)(lo & 0x0f0f0f0fu), (int)((lo >> 4) & 0x0f0f0f0fu), (int)(hi & 0x0f0f0f0fu), (int)((hi >> 4) & 0x0f0f0f0fu)};
+}
+__global__ __launch_bounds__(512, 1) void u8_gemm_kernel(int64_t m, int64_t n_pad, const uint8_t *__restrict__ p2b,
+                                                         const int8_t *__restrict__ slices, const double *__restrict__ unit,
+                                                         double *__restrict__ U) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[U8_NS][U8_ST];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t j0 = (int64_t)blockIdx.x * U8_J, q0 = (int64_t)blockIdx.y * U8_Q;
+  const int S = (int)(n_pad / SG_K);
+  // DMAs per stage: wave w the two 1-KB pieces of slice w (q rows 0-15, 16-31); waves 0-3 also the
+  // codes of SNPs j0 + 64 w .. + 63 (16 B each)
+  const int nq = w < 4 ? 3 : 2;
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]);
+  const int8_t *bsrc = slices + ((int64_t)w * n_pad + q0) * 64 + lane * 16;
+  const uint8_t *asrc = p2b + std::min<int64_t>(j0 + 64 * w + lane, m - 1) * 16;
+  auto issue = [&](int st, int slot) __attribute__((always_inline)) {
+    const unsigned base = ring_m0 + slot * U8_ST;
+    const int8_t *b = bsrc + (int64_t)st * U8_S * n_pad * 64;
+    lds_dma16_m0(b, base + U8_AB + w * 2048);
+    lds_dma16_m0(b + 1024, base + U8_AB + w * 2048 + 1024);
+    if (w < 4) lds_dma16_m0(asrc + (int64_t)st * m * 16, base + w * 1024);
+  };
+  static_assert(U8_NS == 4, "wait_for's vmcnt values");
+  auto wait_for = [&](int ahead) __attribute__((always_inline)) {
+    if (nq == 3) {
+      if (ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+  const int pre = min(S, U8_NS - 1);
+  for (int st = 0; st < pre; ++st) issue(st, st);
+  v16i acc[U8_S];
+#pragma unroll
+  for (int sl = 0; sl < U8_S; ++sl)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[sl][e] = 0;
+  const int sw = u8_swz(c);
+  for (int st = 0; st < S; ++st) {
+    // stage st landed (the younger stages issued may be in flight), then every wave has left stage
+    // st - 1, whose slot the stage issued next reuses
+    wait_for(min(st + U8_NS - 2, S - 1) - st);
+    if (st + U8_NS - 1 < S) issue(st + U8_NS - 1, (st + U8_NS - 1) % U8_NS);
+    const uint8_t *bf = ring[st % U8_NS];
+    const v4i ad = *(const v4i *)&bf[(32 * w + c) * 16];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v4i a8 = i8_of_code2((unsigned)ad[2 * kk + h]);
+#pragma unroll
+      for (int sl = 0; sl < U8_S; ++sl) {
+        const v4i b8 = *(const v4i *)&bf[U8_AB + sl * 2048 + c * 64 + 16 * ((2 * kk + h) ^ sw)];
+        acc[sl] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a8, b8, acc[sl], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int64_t q = q0 + c;
+  const double uq = unit[q];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int64_t j = j0 + 32 * w + (e & 3) + 8 * (e >> 2) + 4 * h;
+    double sum = (double)acc[U8_S - 1][e];
+#pragma unroll
+    for (int sl = U8_S - 2; sl >= 0; --sl) sum = sum * (1.0 / 128.0) + (double)acc[sl][e];
+    if (j < m) U[j * n_pad + q] = uq * sum;
+  }
+}
+
 __global__ void code2_panel_kernel(int64_t m, int64_t n_pad, const int8_t *panel, uint32_t *dst) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, per = n_pad / 16;
   if (idx >= m * per) return;
@@ -3763,6 +3895,7 @@ struct gmat_epi {
   int nK = 0;                       // 128-individual stages
   DBuf rf_part;                     // refine segment partials [2][nseg][np]
   DBuf r8_tiles, r8_varw;           // refine8: int8 slice tiles of the block-upper P_off; w'P_off w per pair
+  DBuf u8_slices, u8_unit;          // U = codes x P on int8 MFMA: the slices of P by row, their units
   double r8_unit = 0;               // their unit (2 qmax / 127)
   DBuf Ps, py, z, dg, slices;
   DBuf mx_tiles;                    // fp6 P_off tile images with e8m0 scales (MX screen)
@@ -3916,9 +4049,30 @@ int build_coding_impl(gmat_epi *e, int which) {
   GMAT_HIP(hipMemcpy(cd.off.p, off.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.soff.p, soff.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.mono.p, mono.data(), m, hipMemcpyHostToDevice));
-  // U[j][q] = sum_q' panel[j][q'] P[q'][q]
-  GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
-                     cd.U.as<double>(), n_pad));
+  // the 2-bit stage-blocked codes (the prefilter's operand; also the int8 U GEMM's)
+  GMAT_TRY(cd.p2b.alloc((size_t)m * n_pad / 4));
+  hipLaunchKernelGGL(code2_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad, panel,
+                     cd.p2b.as<uint32_t>());
+  GMAT_HIP(hipGetLastError());
+  // U[j][q] = sum_q' panel[j][q'] P[q'][q]: on int8 slices of P (u8_gemm_kernel), or as an fp64 GEMM
+  // (GMAT_U_DGEMM, A/B and checks)
+  if (!getenv("GMAT_U_DGEMM") && n_pad % SG_K == 0) {
+    if (!e->u8_slices.p) {
+      GMAT_TRY(e->u8_unit.alloc((size_t)n_pad * sizeof(double)));
+      GMAT_TRY(e->u8_slices.alloc((size_t)U8_S * n_pad * n_pad));
+      hipLaunchKernelGGL(u8_unit_kernel, dim3((unsigned)n_pad), dim3(256), 0, e->s, n_pad, e->Ps.as<double>(),
+                         e->u8_unit.as<double>());
+      hipLaunchKernelGGL(u8_slice_kernel, dim3((unsigned)cdiv(n_pad * n_pad, 256)), dim3(256), 0, e->s, n_pad,
+                         e->Ps.as<double>(), e->u8_unit.as<double>(), e->u8_slices.as<int8_t>());
+      GMAT_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(u8_gemm_kernel, dim3((unsigned)cdiv(m, U8_J), (unsigned)(n_pad / U8_Q)), dim3(512), 0, e->s, m, n_pad,
+                       cd.p2b.as<uint8_t>(), e->u8_slices.as<int8_t>(), e->u8_unit.as<double>(), cd.U.as<double>());
+    GMAT_HIP(hipGetLastError());
+  } else {
+    GMAT_TRY(dgemm_i8a(e->s, m, n_pad, n_pad, 1.0, I8View{panel, n_pad, 0}, DView{e->Ps.as<double>(), n_pad, 0}, 0.0,
+                       cd.U.as<double>(), n_pad));
+  }
   hipLaunchKernelGGL(left_side_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, panel, cd.U.as<double>(),
                      e->z.as<double>(), e->py.as<double>(), e->dg.as<double>(), cd.soff.as<double>(), nullptr,
                      L3.as<double>(), nullptr, cd.qa.as<double>(), cd.ra.as<double>(), cd.sa.as<double>());
@@ -3935,9 +4089,6 @@ int build_coding_impl(gmat_epi *e, int which) {
   hipLaunchKernelGGL(fp4_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 2), 256)), dim3(256), 0, e->s, m, n_pad, panel,
                      cd.p4.as<uint8_t>());
   GMAT_HIP(hipGetLastError());
-  GMAT_TRY(cd.p2b.alloc((size_t)m * n_pad / 4));
-  hipLaunchKernelGGL(code2_panel_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m, n_pad, panel,
-                     cd.p2b.as<uint32_t>());
   GMAT_TRY(cd.L3b.alloc((size_t)E3_PF * m * n_pad));
   for (int t = 0; t < E3_PF; ++t)
     hipLaunchKernelGGL(block_panel_perm8_kernel, dim3((unsigned)cdiv(m * (n_pad / 16), 256)), dim3(256), 0, e->s, m,
