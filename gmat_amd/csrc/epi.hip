@@ -114,20 +114,28 @@ struct ScreenArgs {
   int pf_ncov;
   unsigned long long *live_count;  // diagnostics (GMAT_LIVE_COUNT): pairs the prefilter keeps, or null
   unsigned long long *pf_stamp;    // diagnostics (GMAT_PF_STAMPS): 4 s_memrealtime stamps per workgroup, or null
-  uint32_t *lmask;  // compacted low-rank path: per (band row, 32-column block) the prefilter's live
-                    // pairs as a bit mask (bit c = column 32 J + c), or null; only nonzero words are
-                    // written (the caller zeroes the launch's masks)
+  // compacted low-rank path, per (band row, 32-column block) with a live pair: one 64-bit entry (lm_*)
+  // {live mask (bit c = column 32 J + c), index of the block's first record, launch tag}, or null.  Only
+  // live blocks are written; a reader takes an entry whose tag is not ltag as an empty block, so the
+  // entries need no clearing between launches (the host zeroes a buffer set once per 63 launches)
+  uint64_t *lmask;
+  unsigned ltag;
   // compacted low-rank path: the live pairs' test operands as OPS_REC-int records {E3 slice 0, E3
   // slice 1, Sab, Sa2b, Sab2, Sa2b2, j, 0} appended at ops (a wave reserves its records with one
   // atomic on ops_count, a persistent one in chunks of PF_CHUNK or more; nothing is stored past
   // ops_cap: the host sees the count (records reserved, a little above those written), grows the buffer
-  // and reruns the launch); lbase[(band row, block)] = the index of a live block's first record (its
-  // pairs' records are consecutive, ascending j)
+  // and reruns the launch); a live block's pairs' records are consecutive, ascending j
   int *ops;
   unsigned *ops_count;
   int64_t ops_cap;
-  uint32_t *lbase;
 };
+// the live-block entries of the compacted path: mask | first record << 32 | tag << 58 (records < 2^26)
+constexpr int LM_BASE_BITS = 26;
+__host__ __device__ inline uint64_t lm_entry(uint32_t mask, uint32_t base, unsigned tag) {
+  return (uint64_t)mask | ((uint64_t)(base & ((1u << LM_BASE_BITS) - 1)) << 32) | ((uint64_t)tag << 58);
+}
+__device__ inline uint32_t lm_mask(uint64_t e, unsigned tag) { return (unsigned)(e >> 58) == tag ? (uint32_t)e : 0u; }
+__device__ inline uint32_t lm_base(uint64_t e) { return (uint32_t)(e >> 32) & ((1u << LM_BASE_BITS) - 1); }
 constexpr int OPS_REC = 8;  // ints per live-pair record (32 bytes: two 16-byte stores / loads)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
@@ -690,7 +698,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
             const int trr = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * th;
             const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
             if (te == e && lane < 32 && word && trr < a.n_rows && J < a.nJ)
-              a.lbase[(int64_t)trr * a.nJ + J] = run + (th ? (unsigned)__popc((unsigned)bal) : 0u);
+              a.lmask[(int64_t)trr * a.nJ + J] = lm_entry(word, run + (th ? (unsigned)__popc((unsigned)bal) : 0u), a.ltag);
             if (lv && fits) {
               const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
@@ -728,9 +736,6 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
       if (lane < 32 && tr < a.n_rows && J < a.nJ) {
         if (a.flags) a.flags[(int64_t)tr * a.nJ + J] = mine[q] != 0;
-        // live masks: only the nonzero words (the scan zeroes a launch's masks: 8.5 % of the words at
-        // configs[2], 0.3 GB less written per step)
-        if (a.lmask && mine[q]) a.lmask[(int64_t)tr * a.nJ + J] = mine[q];
       }
     }
     if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
@@ -1035,7 +1040,6 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     const bool blk = ((bal >> (32 * h)) & 0xFFFFFFFFull) != 0;
     if (rok && c == 0 && J < a.nJ) {
       if (a.flags) a.flags[(int64_t)r * a.nJ + J] = blk;
-      if (a.lmask && (uint32_t)(bal >> (32 * h))) a.lmask[(int64_t)r * a.nJ + J] = (uint32_t)(bal >> (32 * h));
     }
     if (a.ops) {  // compacted path: records below
       own |= (live ? 1u : 0u) << e;
@@ -1078,7 +1082,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
       const unsigned long long bal = __ballot(lv);
       const unsigned lo = (unsigned)bal, word = h ? (unsigned)(bal >> 32) : lo;
       if (word && c == 0 && r < a.n_rows && J < a.nJ)
-        a.lbase[(int64_t)r * a.nJ + J] = run + (h ? (unsigned)__popc(lo) : 0u);
+        a.lmask[(int64_t)r * a.nJ + J] = lm_entry(word, run + (h ? (unsigned)__popc(lo) : 0u), a.ltag);
       if (bal) {
         if (lv && fits) {
           const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo(lo, 0u));
@@ -3734,12 +3738,12 @@ __global__ __launch_bounds__(1024) void tl_fill_kernel(const uint8_t *__restrict
 // numbered row by row and grouped 16 to a tile; the padding slots of the last tile have row -1.
 // lc_count: live pairs per band row (one workgroup per row).
 constexpr int LC_T = 256, LC_SLOTS = MX_BI;  // threads per row; slots per tile
-__global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint32_t *__restrict__ lmask, int nJ,
+__global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
                                                         int *__restrict__ cnt) {
   __shared__ int part[LC_T / 64];
   const int r = blockIdx.x, tid = threadIdx.x;
   int c = 0;
-  for (int J = tid; J < nJ; J += LC_T) c += __popc(lmask[(int64_t)r * nJ + J]);
+  for (int J = tid; J < nJ; J += LC_T) c += __popc(lm_mask(lmask[(int64_t)r * nJ + J], tag));
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((tid & 63) == 0) part[tid >> 6] = c;
   __syncthreads();
@@ -3776,19 +3780,19 @@ __global__ __launch_bounds__(1024) void lc_scan_kernel(const int *__restrict__ c
 }
 // lc_fill: band row r's live second SNPs in ascending order into its slots (one workgroup per row;
 // each thread takes a contiguous range of column blocks, a block-wide scan places its pairs), and
-// each live pair's record (the prefilter's, at lbase of its block + its rank in the block) copied to
+// each live pair's record (the prefilter's, at its block's first record + its rank in the block) copied to
 // its slot position in slot_ops
-__global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restrict__ lmask, int nJ,
+__global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
                                                        const int *__restrict__ cnt, const int *__restrict__ soff,
                                                        int *__restrict__ slot_row, int *__restrict__ slot_j,
-                                                       const uint32_t *__restrict__ lbase, const int *__restrict__ ops,
-                                                       int64_t ops_cap, int *__restrict__ slot_ops, int64_t slot_cap) {
+                                                       const int *__restrict__ ops, int64_t ops_cap,
+                                                       int *__restrict__ slot_ops, int64_t slot_cap) {
   __shared__ int part[LC_T];
   const int r = blockIdx.x, tid = threadIdx.x;
   const int per = (nJ + LC_T - 1) / LC_T, J0 = min(nJ, tid * per), J1 = min(nJ, J0 + per);
-  const uint32_t *mk = lmask + (int64_t)r * nJ;
+  const uint64_t *mk = lmask + (int64_t)r * nJ;
   int c = 0;
-  for (int J = J0; J < J1; ++J) c += __popc(mk[J]);
+  for (int J = J0; J < J1; ++J) c += __popc(lm_mask(mk[J], tag));
   part[tid] = c;
   __syncthreads();
   for (int off = 1; off < LC_T; off <<= 1) {
@@ -3800,11 +3804,11 @@ __global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint32_t *__restric
   const int base = soff[r] * 32, n_live = cnt[r], n_slots = (n_live + 31) / 32;
   if ((int64_t)soff[r] + n_slots > slot_cap) return;  // records overflowed: the host reruns the launch
   int k = part[tid] - c;
-  const uint32_t *lb = lbase + (int64_t)r * nJ;
   for (int J = J0; J < J1; ++J) {
-    uint32_t w = mk[J];
+    const uint64_t ent = mk[J];
+    uint32_t w = lm_mask(ent, tag);
     if (!w) continue;
-    uint32_t src = lb[J];
+    uint32_t src = lm_base(ent);
     while (w) {
       const int b = __ffs(w) - 1;
       w &= w - 1;
@@ -3946,10 +3950,11 @@ struct gmat_epi {
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
   struct LrcBuffers {  // three sets: the prefilters of launches L + 1 and L + 2 are queued while L screens
-    DBuf drows[3], lmask[3], lbase[3], ops[3], opc[3], slot_ops[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3],
-        tlist[3];
+    DBuf drows[3], lmask[3], ops[3], opc[3], slot_ops[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3], tlist[3];
     int64_t rl = 0, ops_cap = 0, slot_cap = 0;  // the sets' rows per launch, record and slot capacities
                                                 // (grown, never shrunk)
+    unsigned ltag[3] = {0, 0, 0};               // the live-block entries' tag of each set's last launch
+    void *lm_ptr[3] = {nullptr, nullptr, nullptr};  // the entry buffer that tag refers to
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
     for (auto ev : kev) (void)hipEventDestroy(ev);
@@ -5569,11 +5574,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // configs[2] prefilter keeps 1/250), grown (and the launch rerun) when a launch keeps more
   const int64_t rl_sets = std::max(RL, B.rl);
   auto alloc_sets = [&](int64_t rl, int64_t cap) -> int {
+    GMAT_CHECK(cap <= ((int64_t)1 << LM_BASE_BITS), GMAT_E_ARG, "compacted scan: %lld live-pair records in one launch "
+               "exceed the entries' 2^%d", (long long)cap, LM_BASE_BITS);
     const int64_t max_slots = cap / 32 + rl + 2 * LC_SLOTS;  // a row's last slot may be partial
     for (int b = 0; b < NBUF; ++b) {
       GMAT_TRY(B.drows[b].alloc(rl * 8));
-      GMAT_TRY(B.lmask[b].alloc((size_t)rl * nJ * 4));
-      GMAT_TRY(B.lbase[b].alloc((size_t)rl * nJ * 4));
+      GMAT_TRY(B.lmask[b].alloc((size_t)rl * nJ * sizeof(uint64_t)));
       GMAT_TRY(B.ops[b].alloc((size_t)cap * OPS_REC * sizeof(int)));
       GMAT_TRY(B.opc[b].alloc(16));
       GMAT_TRY(B.slot_ops[b].alloc((size_t)max_slots * 32 * OPS_REC * sizeof(int)));
@@ -5669,7 +5675,14 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     std::memcpy(e->pins.rows[b].p, ln.rows.data(), Rn * 8);
     GMAT_HIP(hipMemcpyAsync(B.drows[b].p, e->pins.rows[b].p, Rn * 8, hipMemcpyHostToDevice, S2));
     GMAT_HIP(hipEventRecord(side_beg[b], S2));
-    GMAT_HIP(hipMemsetAsync(B.lmask[b].p, 0, (size_t)Rn * nJ * 4, S2));
+    // the set's live-block entries: a fresh tag per launch (1..63); a new buffer or a spent tag range
+    // clears the whole buffer first (every 63rd launch of the set, instead of a launch's masks each time)
+    if (B.lm_ptr[b] != B.lmask[b].p || B.ltag[b] >= 63) {
+      GMAT_HIP(hipMemsetAsync(B.lmask[b].p, 0, B.lmask[b].bytes, S2));
+      B.lm_ptr[b] = B.lmask[b].p;
+      B.ltag[b] = 0;
+    }
+    const unsigned tag = ++B.ltag[b];
     GMAT_HIP(hipMemsetAsync(B.opc[b].p, 0, 16, S2));
     SideArgs x{};
     ScreenArgs &a = x.a;
@@ -5689,7 +5702,6 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     a.ops = B.ops[b].as<int>();  // one record per live pair (no dense per-pair arrays)
     a.ops_count = B.opc[b].as<unsigned>();
     a.ops_cap = B.ops_cap;
-    a.lbase = B.lbase[b].as<uint32_t>();
     a.pf_mu = e->pf_mu;
     a.pf_eps = e->pf_eps;
     a.pf_tau = e->pf_tau;
@@ -5702,7 +5714,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     x.qimg = e->pf_q.as<uint8_t>();
     a.n_id = (double)e->n;
     a.flags = nullptr;
-    a.lmask = B.lmask[b].as<uint32_t>();
+    a.lmask = B.lmask[b].as<uint64_t>();
+    a.ltag = tag;
     a.live_count = live_cnt.p ? live_cnt.as<unsigned long long>() : nullptr;
     a.pf_stamp = (pf_st.p && li == stamp_launch) ? pf_st.as<unsigned long long>() : nullptr;
     a.nJ = (int)nJ;
@@ -5823,13 +5836,13 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
     GMAT_HIP(hipGetLastError());
-    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
+    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
                        B.cnt[b].as<int>());
     hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, S2, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
                        B.info[b].as<int>(), B.slot_row[b].as<int>(), B.slot_cap);
-    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint32_t>(), (int)nJ,
+    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
                        B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>(),
-                       B.lbase[b].as<uint32_t>(), B.ops[b].as<int>(), B.ops_cap, B.slot_ops[b].as<int>(), B.slot_cap);
+                       B.ops[b].as<int>(), B.ops_cap, B.slot_ops[b].as<int>(), B.slot_cap);
     GMAT_HIP(hipGetLastError());
     GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].p, B.info[b].p, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
     GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].as<int>() + 4, B.opc[b].p, sizeof(int), hipMemcpyDeviceToHost, S2));
