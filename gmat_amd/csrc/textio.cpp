@@ -125,22 +125,37 @@ extern "C" int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *
   for (int k = 0; k < nf; ++k) GMAT_CHECK(n == 0 || fv[k], GMAT_E_ARG, "gmat_append_hit_rows: column %d missing", k);
   FILE *f = fopen(path, "ab");
   GMAT_CHECK(f, GMAT_E_ARG, "gmat_append_hit_rows: cannot open %s", path);
-  std::string buf;
-  buf.reserve((size_t)std::min<int64_t>(n, 1 << 20) * (16 + 25 * nf));
-  char tmp[96];
+  // rows formatted by up to 16 threads in contiguous chunks of >= 2,048 (the shortest-repr formatting is
+  // ~250 ns a row: 2.8 ms for a configs[2] step's 10,932 hits on one thread), written in order in
+  // blocks of at most 1M rows
+  auto fmt = [&](int64_t r0, int64_t r1, std::string *out) {
+    out->clear();
+    out->reserve((size_t)(r1 - r0) * (16 + 25 * nf));
+    char tmp[96];
+    for (int64_t r = r0; r < r1; ++r) {
+      const int l = snprintf(tmp, sizeof(tmp), "%lld %lld", (long long)i[r], (long long)j[r]);
+      out->append(tmp, l);
+      for (int k = 0; k < nf; ++k) {
+        out->push_back(' ');
+        out->append(tmp, py_repr(fv[k][r], tmp));
+      }
+      out->push_back('\n');
+    }
+  };
+  const int64_t blk = 1 << 20;
+  const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   int rc = GMAT_OK;
-  for (int64_t r = 0; r < n; ++r) {
-    const int l = snprintf(tmp, sizeof(tmp), "%lld %lld", (long long)i[r], (long long)j[r]);
-    buf.append(tmp, l);
-    for (int k = 0; k < nf; ++k) {
-      buf.push_back(' ');
-      buf.append(tmp, py_repr(fv[k][r], tmp));
-    }
-    buf.push_back('\n');
-    if (buf.size() > (8u << 20) || r + 1 == n) {
-      if (fwrite(buf.data(), 1, buf.size(), f) != buf.size()) rc = GMAT_E_ARG;
-      buf.clear();
-    }
+  for (int64_t b0 = 0; b0 < n && rc == GMAT_OK; b0 += blk) {
+    const int64_t b1 = std::min(n, b0 + blk);
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(hw, (b1 - b0) / 2048));
+    std::vector<std::string> bufs(T);
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t)
+      th.emplace_back(fmt, b0 + (b1 - b0) * t / T, b0 + (b1 - b0) * (t + 1) / T, &bufs[t]);
+    fmt(b0, b0 + (b1 - b0) / T, &bufs[0]);
+    for (auto &x : th) x.join();
+    for (auto &s : bufs)
+      if (!s.empty() && fwrite(s.data(), 1, s.size(), f) != s.size()) rc = GMAT_E_ARG;
   }
   if (fclose(f) != 0) rc = GMAT_E_ARG;
   GMAT_CHECK(rc == GMAT_OK, rc, "gmat_append_hit_rows: write to %s failed", path);
