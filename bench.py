@@ -239,7 +239,7 @@ def reml_bench(k, seed):
             "flop_convention": "n^3/3 potrf + 2n^3/3 inverse + 2n^2(2c+1) per iteration"}
 
 
-def e2e_bench(geno, ka, y, var, p_cut, hits_step, reps=3):
+def e2e_bench(geno, ka, y, var, p_cut, hits_step, reps=5):
     """User-facing remma_epiAA end to end (SURVEY.md 8(b) signature): .bed/.bim/.fam/pheno on
     disk -> design matrix -> P, Py on the device -> genotype decode -> plan (certificates)
     -> exhaustive scan -> hits file.  Same cohort and hits as the timed step.  `reps` calls, the
