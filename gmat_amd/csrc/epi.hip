@@ -2522,6 +2522,117 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + T[s];
   varw[p] = unit * sum;
 }
+// refine8_kernel for n_pad > 64 R8_NC (configs[4]: 80 stages), where one wave cannot hold every chunk of
+// its pairs' w: the (row block, column stage) tiles are cut into squares of R8_NC column stages by the
+// 2 R8_NC row blocks beside them, one per segment (gridDim.y: square (qi, qj), qi <= qj, row-major), a
+// wave holds w of its square's column stages only, and a row block's accumulators are folded at the end
+// of its row of the square with w of the block's rows formed from the screen codes in memory.  The
+// per-slice sums are integers, so the segments add up (refine8_side_kernel) to the unsegmented bits.
+__global__ __launch_bounds__(512, 1) void refine8w_kernel(int64_t n_pad, const int8_t *__restrict__ tiles,
+                                                          const int8_t *__restrict__ sl, const int8_t *__restrict__ sr,
+                                                          const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
+                                                          int64_t np, double *__restrict__ tpart) {
+  constexpr int NSL = 8, LA = 6;
+  __shared__ __attribute__((aligned(16))) int8_t sA[NSL][R8_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NB = (int)(n_pad / 32), NS = (int)(n_pad / 64), nQ = (NS + R8_NC - 1) / R8_NC;
+  int sq = (int)blockIdx.y, qi = 0;
+  while (sq >= nQ - qi) {
+    sq -= nQ - qi;
+    ++qi;
+  }
+  const int qj = qi + sq;
+  const int K0 = 2 * R8_NC * qi, K1 = min(NB, K0 + 2 * R8_NC), C0 = R8_NC * qj, C1 = min(NS, C0 + R8_NC);
+  int N = 0;
+  for (int kb = K0; kb < K1; ++kb) N += max(0, C1 - max(C0, kb >> 1));
+  const int64_t p = (int64_t)blockIdx.x * R8_PP + 16 * w + c;
+  const bool valid = p < np;
+  const int8_t *ra = sl + (valid ? pi[p] : 0) * n_pad, *rb = sr + (valid ? pj[p] : 0) * n_pad;
+  v4i wf[R8_NC];  // chunk kc: individuals 64 (C0 + kc) + 16 g .. + 15 of pair c
+#pragma unroll
+  for (int kc = 0; kc < R8_NC; ++kc) {
+    v4i v = {0, 0, 0, 0};
+    if (valid && C0 + kc < C1) {
+      const v4i va = *(const v4i *)(ra + 64 * (C0 + kc) + 16 * g), vb = *(const v4i *)(rb + 64 * (C0 + kc) + 16 * g);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) v[d] = (int)__builtin_amdgcn_perm(T_HI, T_LO, to_offset((unsigned)va[d]) + (unsigned)vb[d]);
+    }
+    wf[kc] = v;
+  }
+  const bool two = w + 8 < R8_TILE / 1024;
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&sA[0][0]) + w * 1024;
+  int kb_p = K0, cs_p = C1 - 1, issued = 0;
+  while (kb_p < K1 && C1 - 1 < max(C0, kb_p >> 1)) ++kb_p;  // row blocks of the square without a tile
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    const int8_t *src = issued < N ? tiles + (r8_toff(kb_p, NS) + cs_p - kb_p / 2) * R8_TILE : tiles;
+    const unsigned dst = ring_m0 + (unsigned)(issued % NSL) * R8_TILE;
+    lds_dma16_m0(src + (w * 64 + lane) * 16, dst);
+    if (two) lds_dma16_m0(src + ((w + 8) * 64 + lane) * 16, dst + 8 * 1024);
+    if (issued < N && --cs_p < max(C0, kb_p >> 1)) {
+      ++kb_p;
+      cs_p = C1 - 1;
+    }
+    ++issued;
+  };
+  for (int q = 0; q < LA; ++q) issue_next();
+  const v4i zv = {0, 0, 0, 0};
+  v4i acc[R8_S][2];
+  double T[R8_S];
+#pragma unroll
+  for (int s2 = 0; s2 < R8_S; ++s2) T[s2] = 0.0;
+  const int swz = 16 * (g ^ r8_swz(c));
+  int v = 0;
+  for (int kb = K0; kb < K1; ++kb) {
+    int lo = max(C0, kb >> 1);
+    asm volatile("" : "+s"(lo));  // opaque per unrolled copy (see pair_mxr_kernel)
+    if (lo > C1 - 1) continue;
+#pragma unroll
+    for (int kc = R8_NC - 1; kc >= 0; --kc) {
+      if (C0 + kc < C1 && C0 + kc >= lo) {
+        static_assert(LA == 6, "vmcnt values");
+        if (two)
+          asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue_next();
+        const int8_t *tb = sA[v % NSL];
+        const bool first = C0 + kc == C1 - 1;
+#pragma unroll
+        for (int s2 = 0; s2 < R8_S; ++s2)
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) {
+            const v4i fa = *(const v4i *)(tb + s2 * R8_TB + (rt * 16 + c) * 64 + swz);
+            acc[s2][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[kc], first ? zv : acc[s2][rt], 0, 0, 0);
+          }
+        ++v;
+      }
+    }
+    // the row block's rows 4 g .. 4 g + 3 of each row tile: w from the screen codes
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      unsigned wd = 0u;
+      if (valid) {
+        const int64_t q0 = 32 * (int64_t)kb + 16 * rt + 4 * g;
+        wd = __builtin_amdgcn_perm(T_HI, T_LO, to_offset(*(const unsigned *)(ra + q0)) + *(const unsigned *)(rb + q0));
+      }
+      const int w0 = (int)(wd & 0xff), w1 = (int)((wd >> 8) & 0xff), w2 = (int)((wd >> 16) & 0xff), w3 = (int)(wd >> 24);
+#pragma unroll
+      for (int s2 = 0; s2 < R8_S; ++s2)
+        T[s2] += (double)(w0 * acc[s2][rt][0] + w1 * acc[s2][rt][1] + w2 * acc[s2][rt][2] + w3 * acc[s2][rt][3]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s2 = 0; s2 < R8_S; ++s2) {
+    T[s2] += __shfl_xor(T[s2], 16);
+    T[s2] += __shfl_xor(T[s2], 32);
+  }
+  if (g || !valid) return;
+#pragma unroll
+  for (int s2 = 0; s2 < R8_S; ++s2) tpart[((int64_t)blockIdx.y * R8_S + s2) * np + p] = T[s2];
+}
 // the most row-block segments a short refine8 / pair_mxr list is split into (GMAT_SEG_MAX, default 8)
 int seg_max() {
   const char *s = getenv("GMAT_SEG_MAX");
@@ -2951,6 +3062,118 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
     x.mpart[(int64_t)seg * x.np + p] = tot;
   else
     pair_test(x, p, tot);
+}
+// pair_mxr_kernel for n_pad > 64 PXR_NK (configs[4]: 40 stages), where one wave cannot hold every
+// stage of its pairs' w: the triangle of (row block, column stage) tiles is cut into squares of
+// PXR_NK x PXR_NK stages, one per segment (gridDim.y: square (qi, qj), qi <= qj, row-major), so a wave
+// holds the w of its square's PXR_NK column stages only; a row block's accumulators are folded at the
+// end of its row of the square with w of that block read from the nibble records (L2).  Per (square,
+// pair) partial sums go to mpart (pair_test_kernel adds them).  The LDS-resident pair_mx_kernel it
+// replaces at these sizes holds 32 pairs per workgroup and streamed the whole tile set per 32 pairs.
+__global__ __launch_bounds__(512, 1) void pair_mxw_kernel(PairArgs x) {
+  constexpr int NSL = PXR_NSL, LA = PXR_NSL - 2;
+  __shared__ __attribute__((aligned(16))) uint8_t sA[NSL][MX_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nK = x.nK, nQ = (nK + PXR_NK - 1) / PXR_NK;
+  int sq = (int)blockIdx.y, qi = 0;
+  while (sq >= nQ - qi) {
+    sq -= nQ - qi;
+    ++qi;
+  }
+  const int qj = qi + sq;
+  const int K0 = qi * PXR_NK, K1 = min(nK, K0 + PXR_NK), C0 = qj * PXR_NK, C1 = min(nK, C0 + PXR_NK);
+  int N = 0;
+  for (int kb = K0; kb < K1; ++kb) N += C1 - max(C0, kb);
+  const int64_t p = (int64_t)blockIdx.x * 256 + 32 * w + c;
+  const bool valid = p < x.np;
+  const uint8_t *ri = x.nib_i + (valid ? x.ci[p] : 0) * nK * NB_REC, *rj = x.nib_j + (valid ? x.cj[p] : 0) * nK * NB_REC;
+  v4i wf[2 * PXR_NK];  // chunk g: column stage C0 + g / 2, 16-byte piece 2 (g % 2) + h
+#pragma unroll
+  for (int g = 0; g < 2 * PXR_NK; ++g) {
+    v4i v = {0, 0, 0, 0};
+    if (valid && C0 + (g >> 1) < C1) {
+      const int s = C0 + (g >> 1), q = 2 * (g & 1) + h;
+      const v4i m1 = *(const v4i *)(ri + s * NB_REC + 16 * q), m2 = *(const v4i *)(ri + s * NB_REC + 64 + 16 * q);
+      const v4i s1 = *(const v4i *)(rj + s * NB_REC + 16 * q);
+      v = (m1 & s1) | (m2 & (s1 << 1));
+    }
+    wf[g] = v;
+  }
+  int kb_p = K0, cs_p = C1 - 1, issued = 0;
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    if (issued < N) {
+      const uint8_t *src = x.tiles + (int64_t)(kb_p * nK + cs_p) * MX_TILE;
+      uint8_t *dst = sA[issued % NSL];
+      lds_dma16(src + (w * 64 + lane) * 16, dst + w * 1024);
+      lds_dma16(src + ((8 + w) * 64 + lane) * 16, dst + (8 + w) * 1024);
+      if (--cs_p < max(C0, kb_p)) {
+        ++kb_p;
+        cs_p = C1 - 1;
+      }
+    }
+    ++issued;
+  };
+  for (int q = 0; q < LA; ++q) issue_next();
+  const int sw16 = 16 * ((c >> 3) & 1);
+  const v16f_ zv = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  v16f_ acc[MX_RB];
+  double tot = 0.0;
+  int v = 0;
+  for (int kb = K0; kb < K1; ++kb) {
+    int lo = max(C0, kb);
+    asm volatile("" : "+s"(lo));  // opaque per unrolled copy (see pair_mxr_kernel)
+#pragma unroll
+    for (int cl = PXR_NK - 1; cl >= 0; --cl) {
+      if (C0 + cl < C1 && C0 + cl >= lo) {
+        vm_wait_barrier(2 * min(LA - 1, N - 1 - v));  // tile v has landed (younger DMAs may be in flight)
+        issue_next();
+        const uint8_t *tb = sA[v % NSL];
+        const int bs = C0 + cl == kb ? 128 : 129;  // off-diagonal tiles count twice
+        const bool first = C0 + cl == C1 - 1;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const v4i wb = wf[2 * cl + kk];
+          const v8i_ fb = {wb[0], wb[1], wb[2], wb[3], 0, 0, 0, 0};
+#pragma unroll
+          for (int r = 0; r < MX_RB; ++r) {
+            const uint8_t *ar = tb + (2 * kk + h) * 4096 + (32 * r + c) * 32;
+            const v4i lo4 = *(const v4i *)(ar + sw16), hi4 = *(const v4i *)(ar + (16 - sw16));
+            const v8i_ fa = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            acc[r] = mfma_mx(fa, fb, (first && kk == 0) ? zv : acc[r], hi4[2], bs);
+          }
+        }
+        ++v;
+      }
+    }
+    // row block kb of the square done: sum_rows w[row] acc[row] with w of block kb (piece r = row tile
+    // r; this lane half's slots 16 h .. 16 h + 15 are dwords 2 h, 2 h + 1 of the piece)
+#pragma unroll
+    for (int r = 0; r < MX_RB; ++r) {
+      v4i wv = {0, 0, 0, 0};
+      if (valid) {
+        const v4i m1 = *(const v4i *)(ri + kb * NB_REC + 16 * r), m2 = *(const v4i *)(ri + kb * NB_REC + 64 + 16 * r);
+        const v4i s1 = *(const v4i *)(rj + kb * NB_REC + 16 * r);
+        wv = (m1 & s1) | (m2 & (s1 << 1));
+      }
+      const unsigned m[2] = {(unsigned)(h ? wv[2] : wv[0]), (unsigned)(h ? wv[3] : wv[1])};
+      v2f_ s2 = {0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const v2f_ wq = bb == 0 ? fp4_pair<0>(m[d]) : bb == 1 ? fp4_pair<1>(m[d]) : bb == 2 ? fp4_pair<2>(m[d]) : fp4_pair<3>(m[d]);
+          const v2f_ av = {acc[r][8 * d + 2 * bb], acc[r][8 * d + 2 * bb + 1]};
+          s2 = __builtin_elementwise_fma(wq, av, s2);
+        }
+      }
+      tot += (double)s2[0] + (double)s2[1];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the workgroup ends
+  tot += __shfl_xor(tot, 32);
+  if (h || !valid) return;
+  x.mpart[(int64_t)blockIdx.y * x.np + p] = tot;
 }
 __global__ void pair_test_kernel(PairArgs x, int nseg) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4157,7 +4380,8 @@ int build_coding_impl(gmat_epi *e, int which) {
 
 // the int8 refine serves plans with n_pad <= 64 R8_NC (w in registers) and a nonzero P_off;
 // GMAT_REFINE64 selects the fp64 MFMA refine (refine_kernel) for A/B runs
-bool refine8_fits(const gmat_epi *e) { return e->n_pad <= 64 * R8_NC && e->qmax > 0 && !getenv("GMAT_REFINE64"); }
+// (n_pad > 64 R8_NC: refine8w_kernel, by squares of stages)
+bool refine8_fits(const gmat_epi *e) { return e->n_pad % 64 == 0 && e->qmax > 0 && !getenv("GMAT_REFINE64"); }
 int refine8_setup(gmat_epi *e) {
   if (e->r8_tiles.p) return GMAT_OK;
   const int64_t n_pad = e->n_pad, NS = n_pad / 64, N = r8_toff(n_pad / 32, NS);
@@ -4184,7 +4408,9 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
       e->n_cu = std::max(cus, 8);
     }
     const int64_t wgs = cdiv(np, R8_PP);
-    const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(seg_max(), e->n_cu / wgs));
+    const bool wide = e->n_pad > 64 * R8_NC;  // w by squares of stages (refine8w_kernel)
+    const int nQ = (int)cdiv(e->n_pad / 64, R8_NC);
+    const int nseg = wide ? nQ * (nQ + 1) / 2 : (int)std::max<int64_t>(1, std::min<int64_t>(seg_max(), e->n_cu / wgs));
     const size_t need = (size_t)np * sizeof(double) * (nseg > 1 ? 1 + R8_S * nseg : 1);
     if (e->r8_varw.bytes < need) {
       GMAT_HIP(hipStreamSynchronize(st));  // an earlier refine queued on st may still use the old buffer
@@ -4195,8 +4421,12 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
     const int8_t *sl = screen_panel(e, li), *sr = screen_panel(e, ri);
     size_t kt0;
     GMAT_TRY(kt_begin(e, st, &kt0));
-    hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
-                       e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>(), tpart);
+    if (wide)
+      hipLaunchKernelGGL(refine8w_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
+                         e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, tpart);
+    else
+      hipLaunchKernelGGL(refine8_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
+                         e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>(), tpart);
     GMAT_HIP(hipGetLastError());
     GMAT_TRY(kt_end(e, st, KT_REFINE, kt0, (double)np));
     GMAT_TRY(kt_begin(e, st, &kt0));
@@ -4344,6 +4574,16 @@ int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, c
       GMAT_HIP(hipGetLastError());
       hipLaunchKernelGGL(pair_test_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, x, nseg);
     }
+  } else if (nK <= 63 && !getenv("GMAT_PS_OLD")) {  // w in registers by squares of stages (pair_mxw_kernel)
+    const int nQ = cdiv(nK, PXR_NK), nseg = nQ * (nQ + 1) / 2;
+    if (e->ps_mpart.bytes < (size_t)nseg * np * sizeof(double)) {
+      GMAT_HIP(hipStreamSynchronize(st));
+      GMAT_TRY(e->ps_mpart.alloc((size_t)std::max(8, nseg) * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
+    }
+    x.mpart = e->ps_mpart.as<double>();
+    hipLaunchKernelGGL(pair_mxw_kernel, dim3((unsigned)cdiv(np, 256), (unsigned)nseg), dim3(512), 0, st, x);
+    GMAT_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pair_test_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, x, nseg);
   } else if (pp == 96)
     hipLaunchKernelGGL(pair_mx_kernel<96>, dim3((unsigned)cdiv(np, 96)), dim3(768), lds, st, x);
   else if (pp == 64)
