@@ -5901,7 +5901,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   GMAT_HIP(hipMemsetAsync(e->counter.p, 0, 8, sm));
   double t_screen = 0, t_side = 0, ops = 0;
   RefineTally tally;
-  const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 65536;
+  // candidates pair-screened beside the launches once at least ps_chunk are pending (one-box A/Bs,
+  // configs[2] at ~60 k candidates per launch: 17.6-17.8 ms per step at 32 k, 48 k and 128 k against
+  // 18.3-18.5 at 64 k and 96 k; rank 0's 8-way part 2.78-2.84 ms at 48 k against 2.76-2.82 at 64 k and
+  // 2.84-2.94 at 32 k, 96 k and 128 k)
+  const int64_t ps_chunk = getenv("GMAT_PS_CHUNK") ? atoll(getenv("GMAT_PS_CHUNK")) : 49152;
   int64_t ps_done = 0;  // candidates [0, ps_done) already pair-screened (queued on S3)
   // candidate room: known_count (exact, after the last screen whose count was read) + inflight (32 per
   // slot of the screen queued since) bounds the buffer's fill
