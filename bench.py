@@ -580,6 +580,9 @@ def main():
     ap.add_argument("--cfg5-reps", type=int, default=3, help="configs[4]: timed scans per kind (median reported)")
     ap.add_argument("--covariates", action="store_true",
                     help="profiling: the timed step uses the covariate design of the covariates leg")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="tests only: let --gpus N exceed the visible GPUs (ranks share devices, exchanges over gloo)")
+    ap.add_argument("--hits-out", default=None, help="rank 0 writes the last step's merged hits to this .npz")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, exchanges its rank and "
                          "exits (no GPU work)")
@@ -588,7 +591,9 @@ def main():
     # touches the GPU (gmat_amd.launch), and exit with their status; a WORLD_SIZE that contradicts
     # --gpus is an error
     from gmat_amd import launch
-    rc = launch.main_or_spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if args.allow_shared_gpu:
+        os.environ["GMAT_ALLOW_SHARED_GPU"] = "1"  # inherited by the ranks
+    rc = launch.main_or_spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:], allow_shared=args.allow_shared_gpu)
     if rc is not None:
         sys.exit(rc)
     if args.dry_run:
@@ -605,6 +610,8 @@ def main():
     backend = dist.init()
     rank, ws, _ = dist.world()
     N.ensure_device()
+    # GPUs this job's ranks run on (one node, rank r on device LOCAL_RANK mod visible)
+    devices_used = min(ws, N.device_count())
     n, m = args.n_id, args.n_snp
     var = np.array([0.4, 0.2, 0.4])
     geno, g, pvp, py, ka, y = build_inputs(n, m, args.seed, var, rank, ws, covariates=args.covariates)
@@ -767,6 +774,8 @@ def main():
         live = dist.gather_hits(ex_local)
         t_live = dist.allreduce_max(t_live)
     full_tri = full_triangle_check(g, pvp, py, merged, args.p_cut, live) if rank == 0 else None
+    if rank == 0 and args.hits_out:
+        np.savez(args.hits_out, i=merged[0], j=merged[1], eff=merged[2], var=merged[3], chi=merged[4], p=merged[5])
     if rank == 0 and t_live is not None:
         full_tri["exhaustive_s"] = t_live
         full_tri["exhaustive_pairs_per_s"] = total_pairs / t_live
@@ -811,7 +820,8 @@ def main():
             parity = {}
         parity["full_triangle"] = full_tri
         value = total_pairs * args.steps / t_max
-        out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "steps": args.steps,
+        out = {"metric": METRIC, "value": value, "unit": "SNP-pairs/s", "n_gpus": ws, "devices_used": devices_used,
+               "backend": backend or "single", "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "fp6xfp4/fp64" if n_slice <= 0 else "int8/fp64", "data": "synthetic",
                "config": {"workload": "configs[2]/[3]: exhaustive exact remma_epiAA, synthetic related cohort "

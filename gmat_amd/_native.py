@@ -125,6 +125,11 @@ def device_count():
     return n.value
 
 
+def shared_gpu_allowed():
+    """Several ranks on one device (the gloo rehearsals of the multi-GPU path on a one-GPU box)."""
+    return os.environ.get("GMAT_ALLOW_SHARED_GPU", "") not in ("", "0")
+
+
 def ensure_device():
     """Bind this process to its GPU (LOCAL_RANK / GMAT_DEVICE, default 0); raise when
     there is none -- the product path never falls back to the CPU."""
@@ -135,7 +140,13 @@ def ensure_device():
     if device_count() < 1:
         raise GmatNativeError("no HIP device visible: the gmat_amd product path needs an MI355X")
     dev = int(os.environ.get("GMAT_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-    check(lib.gmat_set_device(dev % device_count()), "gmat_set_device")
+    n_dev = device_count()
+    if dev >= n_dev and not shared_gpu_allowed():
+        # one process per GPU: a rank without a device of its own would silently share one and the
+        # job would report more GPUs than it used (GMAT_ALLOW_SHARED_GPU=1: test rehearsals only)
+        raise GmatNativeError("device %d requested (LOCAL_RANK / GMAT_DEVICE) but only %d visible; set "
+                              "GMAT_ALLOW_SHARED_GPU=1 to share devices (tests only)" % (dev, n_dev))
+    check(lib.gmat_set_device(dev % n_dev), "gmat_set_device")
     _device_set = True
     return lib
 

@@ -25,9 +25,9 @@ struct Pool {
   std::mutex mu;
   std::multimap<std::pair<int, size_t>, void *> free_blocks;  // (device, bytes) -> block
   size_t cached = 0;
-  size_t limit() const {  // bytes kept cached at most (GMAT_POOL_MAX_GB, default 64)
+  size_t limit() const {  // bytes kept cached at most (GMAT_POOL_MAX_GB, default 32)
     const char *e = getenv("GMAT_POOL_MAX_GB");
-    return (size_t)((e ? atof(e) : 64.0) * (double)(1ull << 30));
+    return (size_t)((e ? atof(e) : 32.0) * (double)(1ull << 30));
   }
   void trim_all() {  // caller holds mu
     for (auto &kv : free_blocks) (void)hipFree(kv.second);
@@ -81,11 +81,13 @@ void *pool_alloc(size_t n, size_t *got) {
   return p;
 }
 
-void pool_free(void *p, size_t bytes) {
+void pool_free(void *p, size_t bytes, int dev) {
   if (!p) return;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
   (void)hipDeviceSynchronize();  // no kernel still uses the block when it is handed out again
+  if (cur != dev) (void)hipSetDevice(cur);
   Pool &pl = pool();
   std::lock_guard<std::mutex> lk(pl.mu);
   if (pl.cached + bytes > pl.limit()) {
@@ -94,6 +96,17 @@ void pool_free(void *p, size_t bytes) {
   }
   pl.free_blocks.insert({{dev, bytes}, p});
   pl.cached += bytes;
+}
+
+size_t pool_cached_bytes() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Pool &pl = pool();
+  std::lock_guard<std::mutex> lk(pl.mu);
+  size_t c = 0;
+  for (auto it = pl.free_blocks.lower_bound({dev, 0}); it != pl.free_blocks.end() && it->first.first == dev; ++it)
+    c += it->first.second;
+  return c;
 }
 
 namespace {

@@ -20,8 +20,11 @@ void set_error(const char *fmt, ...);
 // end) does not pay hipMalloc / hipFree each time.  pool_alloc returns the block and its real size
 // (>= n) or nullptr with the error set; pool_free synchronises the device first (the implicit
 // synchronisation of hipFree that callers rely on) and returns the block to the cache.
+// pool_free files the block under the device it was allocated on (dev); pool_cached_bytes is what the
+// cache holds for the current device (free for the taking: callers sizing buffers from hipMemGetInfo add it)
 void *pool_alloc(size_t n, size_t *got);
-void pool_free(void *p, size_t bytes);
+void pool_free(void *p, size_t bytes, int dev);
+size_t pool_cached_bytes();
 // the same for pinned host staging buffers (hipHostMalloc / hipHostFree take about a millisecond each)
 void *pinned_alloc(size_t n, size_t *got);
 void pinned_free(void *p, size_t bytes);
@@ -58,12 +61,13 @@ struct DBuf {
   void *p = nullptr;
   size_t bytes = 0;  // the size asked for (kernels and the plan state use it as the buffer's size)
   size_t cap = 0;    // the block's real size (the cache's size class)
+  int dev = 0;       // the device it was allocated on
   DBuf() = default;
   DBuf(const DBuf &) = delete;
   DBuf &operator=(const DBuf &) = delete;
   ~DBuf() { release(); }
   void release() {
-    if (p) pool_free(p, cap);
+    if (p) pool_free(p, cap, dev);
     p = nullptr;
     bytes = cap = 0;
   }
@@ -71,6 +75,7 @@ struct DBuf {
     if (n <= bytes && p) return GMAT_OK;
     release();
     if (n == 0) n = 16;
+    (void)hipGetDevice(&dev);
     p = pool_alloc(n, &cap);
     if (!p) return GMAT_E_NOMEM;
     bytes = n;

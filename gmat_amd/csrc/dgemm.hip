@@ -234,13 +234,15 @@ int splitk_workspace(hipStream_t s, size_t bytes, double **out) {
   if (b.second < bytes) {
     if (b.first) {
       GMAT_HIP(hipStreamSynchronize(s));  // the old buffer may still be read by queued work
-      GMAT_HIP(hipFree(b.first));
+      pool_free(b.first, b.second, dev);
       b.first = nullptr;
       b.second = 0;
     }
-    const size_t want = std::max(bytes, (size_t)64 << 20);
-    GMAT_HIP(hipMalloc(&b.first, want));
-    b.second = want;
+    // through the device-memory cache (an allocation failure there trims the cache and retries)
+    size_t got = 0;
+    b.first = pool_alloc(std::max(bytes, (size_t)64 << 20), &got);
+    if (!b.first) return GMAT_E_NOMEM;
+    b.second = got;
   }
   *out = static_cast<double *>(b.first);
   return GMAT_OK;

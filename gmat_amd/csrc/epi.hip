@@ -5254,6 +5254,10 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
   kind_codings(kind, &lc, &rc);
   GMAT_TRY(build_coding(e, lc));
   GMAT_TRY(build_coding(e, rc));
+  // the kernel timers record the calls since the last scan or pairs call only (refine() marks every
+  // chunk's launches: without the reset repeated pairs calls would grow them without bound)
+  e->kev_used = 0;
+  e->kmarks.clear();
   std::vector<int64_t> hi(n_pairs), hj(n_pairs);
   for (int64_t t = 0; t < n_pairs; ++t) {
     hi[t] = pairs[2 * t];
@@ -5804,6 +5808,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     if (RL > B.rl) {  // buffers sized for fewer rows than this scan wants: is there room?
       size_t free_b = 0, total_b = 0;
       GMAT_HIP(hipMemGetInfo(&free_b, &total_b));
+      free_b += pool_cached_bytes();  // blocks the device-memory cache holds are free for the sets
       const int64_t room = (int64_t)((free_b + (size_t)NBUF * 8 * B.rl * nJ) / 8 / (NBUF * 8 * nJ)) / 128 * 128;
       RL = std::max<int64_t>(std::max<int64_t>(B.rl, 128), std::min(RL, room));
     }
@@ -5819,7 +5824,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     const int64_t max_slots = cap / 32 + rl + 2 * LC_SLOTS;  // a row's last slot may be partial
     for (int b = 0; b < NBUF; ++b) {
       GMAT_TRY(B.drows[b].alloc(rl * 8));
+      // a grown entry buffer can be the same block again (the cache hands back what it just took):
+      // its rows past the old size hold stale entries, so any change of size forces the full clear
+      const size_t lm_before = B.lmask[b].bytes;
       GMAT_TRY(B.lmask[b].alloc((size_t)rl * nJ * sizeof(uint64_t)));
+      if (B.lmask[b].bytes != lm_before) B.lm_ptr[b] = nullptr;
       GMAT_TRY(B.ops[b].alloc((size_t)cap * OPS_REC * sizeof(int)));
       GMAT_TRY(B.opc[b].alloc(16));
       GMAT_TRY(B.slot_ops[b].alloc((size_t)max_slots * 32 * OPS_REC * sizeof(int)));

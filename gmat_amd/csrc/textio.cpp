@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -128,7 +129,9 @@ extern "C" int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *
   // rows formatted by up to 16 threads in contiguous chunks of >= 2,048 (the shortest-repr formatting is
   // ~250 ns a row: 2.8 ms for a configs[2] step's 10,932 hits on one thread), written in order in
   // blocks of at most 1M rows
-  auto fmt = [&](int64_t r0, int64_t r1, std::string *out) {
+  // a formatting thread that runs out of memory records it here instead of taking the process down
+  std::atomic<bool> oom{false};
+  auto fmt_rows = [&](int64_t r0, int64_t r1, std::string *out) {
     out->clear();
     out->reserve((size_t)(r1 - r0) * (16 + 25 * nf));
     char tmp[96];
@@ -140,6 +143,14 @@ extern "C" int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *
         out->append(tmp, py_repr(fv[k][r], tmp));
       }
       out->push_back('\n');
+    }
+  };
+  auto fmt = [&](int64_t r0, int64_t r1, std::string *out) {
+    try {
+      fmt_rows(r0, r1, out);
+    } catch (...) {
+      oom = true;
+      std::string().swap(*out);
     }
   };
   const int64_t blk = 1 << 20;
@@ -154,6 +165,10 @@ extern "C" int gmat_append_hit_rows(const char *path, int64_t n, const int64_t *
       th.emplace_back(fmt, b0 + (b1 - b0) * t / T, b0 + (b1 - b0) * (t + 1) / T, &bufs[t]);
     fmt(b0, b0 + (b1 - b0) / T, &bufs[0]);
     for (auto &x : th) x.join();
+    if (oom) {
+      fclose(f);
+      GMAT_CHECK(false, GMAT_E_NOMEM, "gmat_append_hit_rows: out of host memory formatting %lld rows", (long long)n);
+    }
     for (auto &s : bufs)
       if (!s.empty() && fwrite(s.data(), 1, s.size(), f) != s.size()) rc = GMAT_E_ARG;
   }
@@ -180,15 +195,28 @@ extern "C" int gmat_write_grm_text(const char *path, const double *mat, int64_t 
   // row blocks of roughly equal output size, written in order
   const int64_t R = 64;
   int rc = GMAT_OK;
+  std::atomic<bool> oom{false};
   for (int64_t base = 0; base < n && rc == GMAT_OK; base += R * T) {
     std::vector<std::string> bufs(T);
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) {
       const int64_t r0 = std::min(n, base + t * R), r1 = std::min(n, r0 + R);
       if (r0 >= r1) break;
-      th.emplace_back(format_rows, fmt, mat, n, std::cref(ids), r0, r1, &bufs[t]);
+      th.emplace_back(
+          [&, r0, r1, t]() {
+            try {
+              format_rows(fmt, mat, n, ids, r0, r1, &bufs[t]);
+            } catch (...) {
+              oom = true;
+              std::string().swap(bufs[t]);
+            }
+          });
     }
     for (auto &x : th) x.join();
+    if (oom) {
+      fclose(f);
+      GMAT_CHECK(false, GMAT_E_NOMEM, "gmat_write_grm_text: out of host memory");
+    }
     for (auto &b : bufs)
       if (!b.empty() && fwrite(b.data(), 1, b.size(), f) != b.size()) rc = GMAT_E_ARG;
   }

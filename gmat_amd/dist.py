@@ -118,6 +118,10 @@ def choose_backend(explicit=None, gpu_visible=None, n_devices=None, world_size=N
     if world_size is None:
         world_size = world()[1]
     if gpu_visible and n_devices is not None and n_devices < world_size:
+        from . import _native as N
+        if not N.shared_gpu_allowed():
+            raise RuntimeError("%d ranks but %d GPU(s) visible: one process per GPU (GMAT_ALLOW_SHARED_GPU=1 "
+                               "lets ranks share devices over gloo, for tests)" % (world_size, n_devices))
         return "gloo"
     return "rccl" if gpu_visible else "gloo"
 

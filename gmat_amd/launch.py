@@ -98,10 +98,37 @@ def spawn(argv, n_procs, environ=None, poll_s=0.2, timeout_s=None):
                 p.wait()
 
 
-def main_or_spawn(n_gpus, script, argv):
+def visible_devices(environ=None, timeout_s=180):
+    """GPUs a rank of this job would see, counted in a CHILD process (hipGetDeviceCount initialises
+    the runtime; the launcher itself must stay GPU-free because it starts the ranks).  0 when the
+    library or the runtime is missing."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gmat_amd import _native as N\n"
+            "lib = N.load(required=False)\n"
+            "print(N.device_count() if lib is not None else 0)\n" % os.path.dirname(os.path.dirname(
+                os.path.abspath(__file__))))
+    try:
+        out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ if environ is None else environ),
+                             capture_output=True, text=True, timeout=timeout_s)
+        return int(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 and out.stdout.strip() else 0
+    except (subprocess.TimeoutExpired, ValueError):
+        return 0
+
+
+def check_devices(n_gpus, n_visible, allow_shared):
+    """None when n_gpus ranks can each have a GPU of their own (or sharing is allowed, or the job
+    runs on the CPU test harness with no GPU at all); else the error text."""
+    if n_visible == 0 or n_visible >= n_gpus or allow_shared:
+        return None
+    return ("--gpus %d but only %d GPU(s) visible: one process per GPU, so the job would report GPUs it does not "
+            "use (--allow-shared-gpu lets ranks share devices, for tests)" % (n_gpus, n_visible))
+
+
+def main_or_spawn(n_gpus, script, argv, allow_shared=False):
     """bench.py's entry: returns None when this process should do the work itself (a single
     process, or a rank started by a launcher), else spawns the ranks and returns their exit
-    code for the caller to exit with."""
+    code for the caller to exit with.  More ranks than visible GPUs is an error (exit status 2)
+    unless allow_shared."""
     try:
         what = resolve(n_gpus)
     except LaunchError as exc:
@@ -109,4 +136,8 @@ def main_or_spawn(n_gpus, script, argv):
         return 2
     if what != "spawn":
         return None
+    err = check_devices(n_gpus, visible_devices(), allow_shared)
+    if err:
+        print("error: %s" % err, file=sys.stderr, flush=True)
+        return 2
     return spawn([sys.executable, script] + list(argv), n_gpus)

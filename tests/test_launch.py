@@ -1,8 +1,9 @@
 """bench.py --gpus N without an external launcher (gmat_amd/launch.py).
 
 CPU: the launch decision, two ranks reaching dist.init() over gloo through bench.py itself,
-failure propagation.  GPU: the real sharded scan through the same launcher (two ranks on the
-box's one GPU exchange over gloo) returns the single-process hit count."""
+failure propagation, the device-count check.  GPU: --gpus N beyond the visible GPUs is refused; the
+real sharded scan through the same launcher (two ranks on the box's one GPU, --allow-shared-gpu,
+exchanges over gloo) at the bench's full cohort gives the one-rank step's hits byte for byte."""
 import json
 import os
 import subprocess
@@ -10,6 +11,7 @@ import sys
 import textwrap
 import time
 
+import numpy as np
 import pytest
 
 from gmat_amd import launch
@@ -78,19 +80,56 @@ def test_failing_rank_stops_the_job(tmp_path):
     assert time.time() - t0 < 30
 
 
+def test_check_devices():
+    assert launch.check_devices(8, 8, False) is None
+    assert launch.check_devices(2, 8, False) is None
+    assert launch.check_devices(8, 0, False) is None  # no GPU at all: the CPU (gloo) harness
+    assert launch.check_devices(8, 1, True) is None   # --allow-shared-gpu
+    msg = launch.check_devices(8, 1, False)
+    assert msg and "only 1 GPU" in msg
+
+
 @pytest.mark.gpu
-def test_bench_gpus2_sharded_scan_matches_one_rank():
-    """The sharded configs[3] path through bench.py's own launcher on this box: two ranks (one GPU,
-    so the exchanges go over gloo) scan a 2,000 x 6,000 cohort; the merged hit count equals the
-    single-process run's."""
-    small = ["--n-snp", "6000", "--steps", "1", "--warmup", "1", "--no-cpu", "--no-grm", "--no-eff", "--no-e2e",
-             "--no-cov", "--no-split", "--no-cfg5"]
-    res = {}
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py --gpus 8 on a box with fewer GPUs exits with status 2 before starting any rank (it
+    would otherwise report 8 GPUs with ranks sharing devices)."""
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--steps", "1", "--warmup", "0"], env=_clean_env(),
+                         cwd=REPO, capture_output=True, text=True, timeout=240)
+    n = launch.visible_devices(_clean_env())
+    assert n >= 1
+    if n < 8:
+        assert out.returncode == 2, (out.returncode, out.stderr[-2000:])
+        assert "only %d GPU" % n in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_sharded_full_cohort_identical(tmp_path):
+    """configs[3]'s sharded path at the bench's full size (2,000 x 50,000, p_cut 1e-5) through
+    bench.py's own launcher: two ranks (on this box's one GPU, --allow-shared-gpu: the exchanges go over
+    gloo) each scan part k of the reference's folded split (remma_epiAA.py:109-161) and rank 0 merges
+    the hits.  The merged (i, j, eff, var, chi, p) tuples are byte-identical to the one-rank step's,
+    and both equal the exhaustive (unscreened) full-triangle hit set (parity.full_triangle)."""
+    common = ["--steps", "1", "--warmup", "1", "--no-cpu", "--no-grm", "--no-eff", "--no-e2e", "--no-cov",
+              "--no-split", "--no-cfg5"]
+    res, hits = {}, {}
     for g in (1, 2):
-        out = subprocess.run([sys.executable, BENCH, "--gpus", str(g)] + small, env=_clean_env(), cwd=REPO,
-                             capture_output=True, text=True, timeout=240)
+        path = str(tmp_path / ("hits%d.npz" % g))
+        extra = ["--allow-shared-gpu"] if g > 1 else []
+        out = subprocess.run([sys.executable, BENCH, "--gpus", str(g), "--hits-out", path] + extra + common,
+                             env=_clean_env(OMP_NUM_THREADS="16"), cwd=REPO, capture_output=True, text=True,
+                             timeout=420)
         assert out.returncode == 0, out.stderr[-3000:]
         res[g] = json.loads(out.stdout.strip().splitlines()[-1])
+        hits[g] = np.load(path)
     assert res[2]["n_gpus"] == 2 and res[1]["n_gpus"] == 1
-    assert res[2]["scan"]["hits_per_step"] == res[1]["scan"]["hits_per_step"]
-    assert res[1]["scan"]["hits_per_step"] > 0
+    assert res[2]["devices_used"] == min(2, launch.visible_devices(_clean_env()))
+    assert res[2]["backend"] == "gloo" and res[1]["backend"] == "single"
+    for g in (1, 2):
+        ft = res[g]["parity"]["full_triangle"]
+        assert ft["checked"], ft
+        assert ft["identical"] and ft["values_byte_identical"] and ft["symmetric_difference"] == 0, ft
+    assert hits[1]["i"].size == res[1]["scan"]["hits_per_step"] > 10000
+    for key in ("i", "j", "eff", "var", "chi", "p"):
+        a, b = hits[1][key], hits[2][key]
+        assert a.dtype == b.dtype and a.shape == b.shape, key
+        np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64), err_msg=key)
