@@ -724,7 +724,7 @@ def main():
         dom = max(screens, key=lambda k: kern_rec[k]["kernel_s_per_step"])
         kr = kern_rec[dom]
         # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
-        # WRITE_SIZE); used only when recorded on the same kernel source (sha256 of epi.hip), kernel,
+        # WRITE_SIZE); used only when recorded on the same kernel source (sha256 of the epi stage files), kernel,
         # rank and cohort size (else traffic stays null)
         def traffic_of(kname):
             tpath = os.path.join(REPO, "profiles", "traffic_%s.json" % kname)

@@ -1,6 +1,6 @@
 """Plan-buffer reuse and the int8 refine's anchor (round-5 review items).
 
-* Live-block entries of the compacted scan (epi.hip scan_lowrank alloc_sets): when the rows per launch
+* Live-block entries of the compacted scan (epi_scan.hip scan_lowrank alloc_sets): when the rows per launch
   grow within one device-memory size class, the cache hands the same block back; its rows past the old
   size must not be read as live blocks.  A plan that scanned at 640 rows per launch leaves tagged
   entries in its block; a second plan then scans at 512 and again at 640 rows per launch -- every scan

@@ -1,6 +1,6 @@
 """The scan plan's partial symmetric eigensolver (gmat_amd/csrc/eig.hip: Chebyshev-filtered subspace
 iteration, device Rayleigh-Ritz) against numpy's dense decomposition, on projection matrices P of the kind the plan decomposes (uvlmm_varcom.py:
-P = V^-1 - V^-1 X (X'V^-1 X)^-1 X'V^-1, intercept direction lifted as epi.hip eigen_bottom does),
+P = V^-1 - V^-1 X (X'V^-1 X)^-1 X'V^-1, intercept direction lifted as epi_plan.hip eigen_bottom does),
 with and without covariates (P's exact null directions: a repeated eigenvalue 0)."""
 import numpy as np
 import pytest

@@ -19,10 +19,8 @@ VARIANTS = [{"GMAT_LR_BLOCKS": "1"}, {"GMAT_PS_CHUNK": "700"}, {"GMAT_PS_CHUNK":
             {"GMAT_PF_WG": "8"},      # prefilter: 8 persistent workgroups, ~10 tiles each per launch
             {"GMAT_PF_WG": "24"},
             {"GMAT_LRC_ROWS": "256"},  # compacted scan: 256-row launches (default: 512 at this size)
-            {"GMAT_PF_COLORDER": "1"},  # prefilter tile list in column-tile order
             {"GMAT_LRC_OPS_CAP": "64"},  # live-pair records overflow: grown and the launches rerun
             {"GMAT_LRC_MIN_LAUNCHES": "1"},  # one launch of all rows (no prefilter-ahead pipeline)
-            {"GMAT_PS_OLD": "1"},  # pair screen with LDS-resident w planes (pair_mx_kernel)
             {"GMAT_SEG_MAX": "1"},  # refine8 / pair_mxr without row-block segments
             {"GMAT_LRC_J4": "1"}]  # compacted screen reading the j side's 4-bit nibble planes
 

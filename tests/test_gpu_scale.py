@@ -7,7 +7,7 @@ the hardware check of the low-rank screen's fp32 accumulation bound.
   form, int8 slices -- for AA, and on the automatic level for DD and AD (i == j included).
 * cfg2 (2,000 x 20,000): agmat's full matrix and the 2-GRM REML ([A, AxA], uvlmm_varcom.py:41-99)
   against the oracle.
-* The screen's bound |c~_r - c_r| <= eta_r = 2^-24 |Q_r|_1 (8 n_pad + 400) (epi.hip lr_setup) on
+* The screen's bound |c~_r - c_r| <= eta_r = 2^-24 |Q_r|_1 (8 n_pad + 400) (epi_plan.hip lr_setup) on
   adversarial operands (same sign, w = 4, n_pad up to 8,192, block scales 2^16 apart).
 """
 import ctypes

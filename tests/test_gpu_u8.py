@@ -1,4 +1,4 @@
-"""U = codes x P (the codings' side vectors) on int8 slices of P (u8_gemm_kernel in csrc/epi.hip)
+"""U = codes x P (the codings' side vectors) on int8 slices of P (u8_gemm_kernel in csrc/epi_*.hip)
 against the fp64 GEMM it replaced (GMAT_U_DGEMM=1): the scan's hits and statistics and the exact
 refine of sampled pairs agree to fp64 rounding (the slicing error is bounded below 2^-46 of a row's
 largest |P|), and the default path is checked against the oracle (remma_epiAA.py:71-82)."""

@@ -1,4 +1,4 @@
-"""CPU checks of the low-rank spectral screen (epi.hip lr_setup / lr_screen_kernel).
+"""CPU checks of the low-rank spectral screen (epi_plan.hip lr_setup / lr_screen_kernel).
 
 The device screen bounds var = e'Pe from below by
     lam (|e|^2 - (1'e)^2/n) - tau (1'e)^2/n - eps |e|^2 - sum_r d_r (B_r'e)^2,
@@ -13,7 +13,7 @@ from test_prefilter_math import _projection
 
 
 def fp6_block(v):
-    """fp6 e2m3 values with one e8m0 scale per 32 entries (fp6_block in epi.hip)."""
+    """fp6 e2m3 values with one e8m0 scale per 32 entries (fp6_block in epi_plan.hip)."""
     mx = np.abs(v).max()
     if mx == 0:
         return np.zeros_like(v)

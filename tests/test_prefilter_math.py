@@ -1,4 +1,4 @@
-"""CPU checks of the algebra behind the scan's spectral prefilter (epi.hip).
+"""CPU checks of the algebra behind the scan's spectral prefilter (epi_*.hip).
 
 The device code never forms e = x_i o x_j: it expands |e|^2 and 1'e into exact integer code
 products (a.b, a^2.b, a.b^2, a^2.b^2) and per-SNP sums, and bounds e'Pe from below by a

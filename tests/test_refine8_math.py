@@ -1,4 +1,4 @@
-"""The int8-slice refine (refine8_kernel + refine8_side_kernel in csrc/epi.hip) restated in numpy:
+"""The int8-slice refine (refine8_kernel + refine8_side_kernel in csrc/epi_*.hip) restated in numpy:
 the block-upper slice images, the exact integer quadratic forms per slice, the expansion of e'Pe
 around the integer codes, and the tile count r8_toff.  The statistic it feeds is the reference's
 var = e'Pe of remma_epiAA.py:71-82; this checks that the restated arithmetic reproduces it to the

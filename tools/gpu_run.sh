@@ -22,7 +22,7 @@ for st in "$@"; do
       python -c "import json; d=json.load(open('$OUT/quick.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
     pmc)
       # counter passes of the six scan kernels (one rocprofv3 run per counter group) and their traffic
-      # records keyed by epi.hip's sha256 (bench.py attaches them to roofline.kernels)
+      # records keyed by the epi stage files' sha256 (bench.py attaches them to roofline.kernels)
       K="prefilter_pass_kernel|lrc_screen_kernel|pair_side_kernel|pair_mxr_kernel|refine8_kernel|refine8_side_kernel"
       KEY="$K" bash tools/pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
       for k in prefilter_pass_kernel lrc_screen_kernel pair_side_kernel pair_mxr_kernel refine8_kernel refine8_side_kernel; do

@@ -4,7 +4,7 @@
 
 With --out, writes the traffic record bench.py uses for roofline.traffic: fabric bytes per launch
 (FETCH_SIZE x 2, the gfx950 wide-read correction of MI355X_MICROARCH.md "HBM", + WRITE_SIZE), keyed
-by the kernel, its screen level and low-rank rank, the cohort size and the sha256 of epi.hip (the
+by the kernel, its screen level and low-rank rank, the cohort size and the sha256 of the epi stage files (the
 kernels' source), so that a record of other code or another kernel shape is not used (bench.py
 drops it).  Launch times under --pmc are those of serialised kernels (the profiler serialises
 dispatches), so they are recorded but not compared.
@@ -20,10 +20,18 @@ import os
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def source_sha256(path=os.path.join(REPO, "gmat_amd", "csrc", "epi.hip")):
-    """Fingerprint of the scan kernels' source: a traffic record applies only to the code it measured."""
-    with open(path, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+EPI_SOURCES = ("epi.h", "epi_prefilter.hip", "epi_screen.hip", "epi_refine.hip", "epi_setup.hip", "epi_plan.hip",
+               "epi_scan.hip")
+
+
+def source_sha256(paths=None):
+    """Fingerprint of the scan kernels' source (the epi.h / epi_*.hip stage files, in a fixed order): a
+    traffic record applies only to the code it measured."""
+    h = hashlib.sha256()
+    for name in (EPI_SOURCES if paths is None else paths):
+        with open(os.path.join(REPO, "gmat_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 def main():
     ap = argparse.ArgumentParser()
