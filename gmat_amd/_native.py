@@ -51,6 +51,7 @@ _PROTOS = {
     "gmat_epi_kernel_stats": (_INT, [_P, _P]),
     "gmat_epi_kernel_stats_ext": (_INT, [_P, _P, _INT, _P]),
     "gmat_epi_info": (_INT, [_P, _P]),
+    "gmat_epi_layout": (_INT, [_P, _P]),
     "gmat_epi_destroy": (_INT, [_P]),
     "gmat_eff_scan": (_INT, [_P, _INT, _P, _P, _I64, _P, _P, _P, ctypes.c_char_p, _P]),
     "gmat_eff_stats": (_INT, [_P]),

@@ -150,7 +150,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, in
 constexpr int MX_TS = 16 * 32;
 __device__ __forceinline__ void cand_test(const ScreenArgs &a, int ri, int64_t i, int64_t j, double M, double sumw2,
                                           const int *ts = nullptr, int slot = 0, int col = 0) {
-  if (j >= a.m || (a.tri && j <= i)) return;
+  if (j >= a.m || j < a.j_lo || (a.tri && j <= i)) return;  // j_lo: a launch's (or segment's) first column
   if (a.mono_l[i] || a.mono_r[j]) return;  // x == 0: the reference's statistic is NaN
   const int64_t o1 = (int64_t)ri * a.ld_e + (j - a.j_lo), o3 = o1 + (int64_t)a.n_rows * a.ld_e,
                 od = o3 + (int64_t)a.n_rows * a.ld_e;
@@ -543,7 +543,7 @@ struct LrcArgs {
 constexpr int LRC_J2B = 32;  // j-side bytes per column and stage of the compacted screen (2-bit S1 planes)
 
 // slot pair p's record (lc_fill: the prefilter's E3 slices and code products of the pair)
-__device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, int64_t p, int64_t i, int64_t j,
+__device__ __forceinline__ bool lrc_cand(const ScreenArgs &a, const LrcArgs &x, int64_t p, int64_t i, int64_t j,
                                          double lowrank) {
   static_assert(E3_PF == 2, "record layout");
   const v4i r0v = *(const v4i *)(x.slot_ops + p * OPS_REC), r1v = *(const v4i *)(x.slot_ops + p * OPS_REC + 4);
@@ -568,13 +568,7 @@ __device__ __forceinline__ void lrc_test(const ScreenArgs &a, const LrcArgs &x, 
   const double qb = sqrt(lowrank * (1.0 + 1e-4)) + sqrt(x.E);
   const double vlo = x.lam * (ee - se * se / n) - x.tau * se * se / n - x.eps * ee - qb * qb -
                      1e-12 * (x.lam + x.tau) * (mag + se * se / n);
-  if (!(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo) {
-    const unsigned long long k = atomicAdd(a.counter, 1ULL);
-    if ((int64_t)k < a.cap) {
-      a.cand_i[k] = i;
-      a.cand_j[k] = j;
-    }
-  }
+  return !(vlo > 0.0) || eff_hi * eff_hi * (1.0 + 1e-9) >= a.chi_cut * vlo;
 }
 
 
@@ -880,10 +874,26 @@ struct Pinned {
   }
 };
 
+namespace gmat {
+namespace epi {
+struct SegPlan;               // a plan cut into SNP segments (epi_seg.hip)
+void seg_free(SegPlan *sp);
+}  // namespace epi
+}  // namespace gmat
+
 struct gmat_epi {
   gmat_geno *g = nullptr;
   int64_t n = 0, n_pad = 0, m = 0;
   int n_slice = 3;
+  // Past the single-plan limits (epi_seg.hip): a plan whose panels would need byte offsets of 2^32 or
+  // more (2 m n_pad) is cut into SNP segments, each scan running on sub-plans of one or two segments
+  // (seg); a plan with n_pad > EXH_ONLY_NPAD individuals has no screens (the int8 screen's 24-bit
+  // epilogue sums and the pair screen's LDS planes stop there) and scans every pair exactly
+  // (exh_only).  col_lo: the first second SNP a scan of this plan tests (a segment pair's sub-plan
+  // [A, B] scans rows of A against columns of B only); 0 otherwise.
+  gmat::epi::SegPlan *seg = nullptr;
+  bool exh_only = false;
+  int64_t col_lo = 0;
   double qmax = 0, zz = 0, spy = 0;
   double rho[5] = {0, 0, 0, 0, 0};  // rho[S]: upper bound of ||P_off - sum_{s<S} A_s 128^-s qmax/127||_2
                                     // (0: not computed yet, ensure_rho)
@@ -965,6 +975,7 @@ struct gmat_epi {
     void *lm_ptr[3] = {nullptr, nullptr, nullptr};  // the entry buffer that tag refers to
   } lrc;  // compacted low-rank scan buffers (scan_lowrank)
   ~gmat_epi() {
+    gmat::epi::seg_free(seg);
     for (auto ev : kev) (void)hipEventDestroy(ev);
     for (auto ev : sev) (void)hipEventDestroy(ev);
     stream_release(s1);
@@ -981,7 +992,7 @@ namespace epi {
 // ---- kernels (defined in the stage files)
 template <int PASS>
 __global__ void side_gemm_kernel(SideArgs x);
-template <bool LIST, bool COMPACT>
+template <bool LIST, bool COMPACT, bool STAMP>
 __global__ void prefilter_pass_kernel(SideArgs x);
 template <int NC, bool LIST>
 __global__ void prefilter_cov_kernel(SideArgs x);
@@ -1108,7 +1119,7 @@ __global__ void lr_quant_kernel(int64_t n, int64_t n_pad, int nK, int Rp, const 
                                 const double *__restrict__ sd, double *__restrict__ Bn, double *__restrict__ Bs,
                                 uint32_t *__restrict__ img);
 __global__ void all_pairs_kernel(const int64_t *__restrict__ rows, const int64_t *__restrict__ offs, int64_t m, int tri,
-                                 int64_t *__restrict__ pi, int64_t *__restrict__ pj);
+                                 int64_t col_lo, int64_t *__restrict__ pi, int64_t *__restrict__ pj);
 __global__ void hit_compact_kernel(int64_t np, const int64_t *__restrict__ pi,
                                                           const int64_t *__restrict__ pj, const double *__restrict__ eff,
                                                           const double *__restrict__ var, const double *__restrict__ chi,
@@ -1147,6 +1158,25 @@ bool pair_screen_fits(const gmat_epi *e);
 int default_lr_rank(const gmat_epi *e);
 int pair_screen(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const int8_t *slp, const int8_t *srp,
                 const int64_t *pi, const int64_t *pj, int64_t np, double chi_cut, int64_t *n_out, bool reset = true);
+// plan creation (epi_plan.hip): a plan of one panel (state: another plan's spectral state, or null)
+// (allow_seg false: a plan of this one panel even when seg_snps() would cut it -- the segments' sub-plans)
+int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
+                    const uint8_t *state, int64_t state_bytes, bool allow_seg = true);
+constexpr int64_t EXH_ONLY_NPAD = 8192;  // plans past this many (padded) individuals scan exhaustively
+// whether a plan for g is cut into SNP segments, and the segment size (epi_seg.hip)
+int64_t seg_snps(const gmat_geno *g);
+int seg_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice, const uint8_t *state,
+               int64_t state_bytes);
+// the scan of a validated row list on a plan of one panel (gmat_epi_scan without the checks), epi_scan.hip
+int scan_dispatch(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut, int n_slice,
+                  int64_t *n_hits);
+// segmented plans' scan / pair statistics / bound audit (epi_seg.hip)
+int seg_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut, int n_slice,
+             int64_t *n_hits);
+int seg_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *eff, double *var, double *chi,
+              double *p);
+int seg_audit(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *out5);
+const gmat_epi *seg_base(const gmat_epi *e);  // the plan of segment 0 (spectral state, setup statistics)
 // batched int8 GEMM C = A B' (the block-granular scans' side GEMMs), epi_setup.hip
 int i8gemm_nt(hipStream_t st, int Z, int M, int N, int K, const int8_t *A, int64_t lda, int64_t za, const int8_t *B,
               int64_t ldb, int64_t zb, int *C, int64_t ldc, int64_t zc);

@@ -82,7 +82,7 @@ int build_coding_impl(gmat_epi *e, int which) {
   for (DBuf *b : {&cd.off, &cd.soff, &cd.qa, &cd.ra, &cd.sa, &cd.qb, &cd.rb, &cd.sb, &cd.sL, &cd.sL3, &cd.sLd, &cd.sR,
                   &cd.csum, &cd.csq})
     GMAT_TRY(b->alloc(m * sizeof(double)));
-  GMAT_TRY(cd.L3q.alloc((size_t)SIDE_T * m * n_pad));
+  if (!e->exh_only) GMAT_TRY(cd.L3q.alloc((size_t)SIDE_T * m * n_pad));
   GMAT_HIP(hipMemcpy(cd.csum.p, csum.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(cd.csq.p, csq.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_TRY(cd.mono.alloc(m));
@@ -121,6 +121,11 @@ int build_coding_impl(gmat_epi *e, int which) {
                      e->z.as<double>(), e->py.as<double>(), cd.soff.as<double>(), nullptr, cd.qb.as<double>(),
                      cd.rb.as<double>(), cd.sb.as<double>());
   GMAT_HIP(hipGetLastError());
+  if (e->exh_only) {  // the exact refine's operands only (U, the offsets and per-SNP scalars above)
+    GMAT_HIP(hipStreamSynchronize(e->s));
+    cd.ready = true;
+    return GMAT_OK;
+  }
   const int64_t ss = m * n_pad;
   hipLaunchKernelGGL(quantize_rows_kernel, dim3((unsigned)m), dim3(256), 0, e->s, n_pad, ss, L3.as<double>(),
                      cd.L3q.as<int8_t>(), cd.sL3.as<double>());
@@ -640,15 +645,21 @@ int gmat::epi::ensure_rho(gmat_epi *e, int S) {
   return GMAT_OK;
 }
 
-static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
-                           const uint8_t *state, int64_t state_bytes) {
+int gmat::epi::epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice,
+                               const uint8_t *state, int64_t state_bytes, bool allow_seg) {
   GMAT_CHECK(out && g && pvp && py, GMAT_E_ARG, "gmat_epi_create: bad arguments");
   GMAT_CHECK(n_slice >= 1 && n_slice <= 4, GMAT_E_ARG, "gmat_epi_create: n_slice must be 1..4");
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_epi_create: panel has missing genotypes (impute first)");
-  GMAT_CHECK(g->n_pad <= 8192 && 2 * g->m * g->n_pad < (1LL << 32), GMAT_E_ARG,
-             "gmat_epi_create: supports n_id <= 8192 and 2 * n_snp * n_pad < 2^32 (32-bit buffer offsets)");
+  // panels whose byte offsets would reach 2^32 (the kernels' 32-bit lane offsets from a 64-bit base):
+  // a plan of SNP segments, each sub-plan within the limit (epi_seg.hip)
+  if (allow_seg && seg_snps(g) > 0) return seg_create(out, g, pvp, py, n_slice, state, state_bytes);
+  GMAT_CHECK(2 * g->m * g->n_pad < ((int64_t)1 << 32), GMAT_E_ARG, "gmat_epi_create: a single-panel plan of %lld SNPs "
+             "x %lld individuals (2 m n_pad >= 2^32)", (long long)g->m, (long long)g->n_pad);
   const double t_create = now();
   auto *e = new gmat_epi();
+  // past EXH_ONLY_NPAD individuals no screen applies (the int8 slice screen's 24-bit epilogue sums, the
+  // pair screen's LDS-resident planes): every pair is refined exactly (GMAT_EXH_ONLY: the same below it)
+  e->exh_only = g->n_pad > EXH_ONLY_NPAD || getenv("GMAT_EXH_ONLY") != nullptr;
   e->g = g;
   e->n = g->n;
   e->n_pad = g->n_pad;
@@ -673,7 +684,8 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   if ((rc = dp.alloc(n * n * sizeof(double))) || (rc = dv.alloc(n * sizeof(double))) ||
       (rc = e->Ps.alloc(n_pad * n_pad * sizeof(double))) || (rc = e->py.alloc(n_pad * sizeof(double))) ||
       (rc = e->z.alloc(n_pad * sizeof(double))) || (rc = e->dg.alloc(n_pad * sizeof(double))) ||
-      (rc = e->slices.alloc((size_t)n_slice * n_pad * n_pad)) || (rc = e->spanels.alloc((size_t)2 * e->m * n_pad)))
+      (!e->exh_only && (rc = e->slices.alloc((size_t)n_slice * n_pad * n_pad))) ||
+      (rc = e->spanels.alloc((size_t)2 * e->m * n_pad)))
     return fail(rc);
   if (hipMemcpy(dp.p, pvp, n * n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(dv.p, py, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
@@ -707,8 +719,9 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   hipLaunchKernelGGL(permute_vec_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n, n_pad, dv.as<double>(),
                      e->py.as<double>());
   const double unit = qmax > 0 ? 127.0 / qmax : 1.0;
-  hipLaunchKernelGGL(slice_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, n_slice,
-                     e->slices.as<int8_t>());
+  if (!e->exh_only)
+    hipLaunchKernelGGL(slice_kernel, dim3(gb), dim3(256), 0, 0, n, n_pad, dp.as<double>(), unit, n_slice,
+                       e->slices.as<int8_t>());
   hipLaunchKernelGGL(zsum_kernel, dim3((unsigned)cdiv(n_pad, 4)), dim3(256), 0, 0, n_pad, e->Ps.as<double>(),
                      e->z.as<double>());
   hipLaunchKernelGGL(diag_kernel, dim3((unsigned)cdiv(n_pad, 256)), dim3(256), 0, 0, n_pad, e->Ps.as<double>(),
@@ -719,6 +732,26 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
   }
   // the int8 levels' bounds rho[S] are computed on first use (ensure_rho)
   e->pmax = pmax;
+  // the plan's last step: 1'P1 (z summed on the host)
+  auto finish_plan = [&]() -> int {
+    std::vector<double> hz(n_pad);
+    if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("gmat_epi_create: z download failed");
+      return fail(GMAT_E_HIP);
+    }
+    double zz = 0.0;
+    for (double v : hz) zz += v;
+    e->zz = zz;
+    e->setup[0] = now() - t_create;
+    *out = e;
+    return GMAT_OK;
+  };
+  if (e->exh_only) {  // no screens: P, z, diag(P) and Py are all the exact refine reads
+    if (state && (rc = import_state(e, state, state_bytes)) != GMAT_OK) return fail(rc);
+    e->pf_mu = 0.0;
+    e->lr_R = 0;
+    return finish_plan();
+  }
   DBuf r1, r2, rrows;
   if ((rc = r1.alloc(n_pad * n_pad * sizeof(double))) || (rc = r2.alloc(n_pad * n_pad * sizeof(double))) ||
       (rc = rrows.alloc(n_pad * sizeof(double))))
@@ -875,17 +908,7 @@ static int epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, cons
     }
   }  // spectral state computed here
   if ((rc = finish_mx()) != GMAT_OK) return fail(rc);
-  std::vector<double> hz(n_pad);
-  if (hipMemcpy(hz.data(), e->z.p, n_pad * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
-    set_error("gmat_epi_create: z download failed");
-    return fail(GMAT_E_HIP);
-  }
-  double zz = 0.0;
-  for (double v : hz) zz += v;
-  e->zz = zz;
-  e->setup[0] = now() - t_create;
-  *out = e;
-  return GMAT_OK;
+  return finish_plan();
 }
 
 extern "C" int gmat_epi_create(gmat_epi **out, gmat_geno *g, const double *pvp, const double *py, int n_slice) {
@@ -967,6 +990,7 @@ int import_state(gmat_epi *e, const uint8_t *st, int64_t bytes) {
 // and the certificate searches run once per job.  *needed = the size; buf may be null.
 extern "C" int gmat_epi_export(const gmat_epi *e, uint8_t *buf, int64_t cap, int64_t *needed) {
   GMAT_CHECK(e && needed, GMAT_E_ARG, "gmat_epi_export: bad arguments");
+  if (e->seg) return gmat_epi_export(seg_base(e), buf, cap, needed);  // the state of the segments' plans
   const int64_t sz = state_size(e);
   *needed = sz;
   if (!buf) return GMAT_OK;
@@ -1001,6 +1025,7 @@ extern "C" int gmat_epi_export(const gmat_epi *e, uint8_t *buf, int64_t cap, int
 
 extern "C" int gmat_epi_setup_stats(const gmat_epi *e, double *out8) {
   GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_setup_stats: bad arguments");
+  if (e->seg) return gmat_epi_setup_stats(seg_base(e), out8);
   for (int k = 0; k < 7; ++k) out8[k] = e->setup[k];
   out8[7] = e->pf_ncov;
   return GMAT_OK;
@@ -1008,6 +1033,7 @@ extern "C" int gmat_epi_setup_stats(const gmat_epi *e, double *out8) {
 
 extern "C" int gmat_epi_info(const gmat_epi *e, double *out4) {
   GMAT_CHECK(e && out4, GMAT_E_ARG, "gmat_epi_info: bad arguments");
+  if (e->seg) return gmat_epi_info(seg_base(e), out4);
   out4[0] = e->lr_R;
   out4[1] = e->lr_lam;
   out4[2] = e->pf_mu;
@@ -1025,6 +1051,7 @@ extern "C" int gmat_epi_pairs(gmat_epi *e, int kind, const int64_t *pairs, int64
   GMAT_CHECK(e && (n_pairs == 0 || (pairs && eff && var && chi && p)), GMAT_E_ARG, "gmat_epi_pairs: bad arguments");
   GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_pairs: bad kind");
   if (n_pairs == 0) return GMAT_OK;
+  if (e->seg) return seg_pairs(e, kind, pairs, n_pairs, eff, var, chi, p);
   int lc, rc;
   kind_codings(kind, &lc, &rc);
   GMAT_TRY(build_coding(e, lc));
@@ -1084,6 +1111,7 @@ extern "C" int gmat_epi_audit(gmat_epi *e, int kind, const int64_t *pairs, int64
   GMAT_CHECK(e && (n_pairs == 0 || (pairs && out5)), GMAT_E_ARG, "gmat_epi_audit: bad arguments");
   GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_audit: bad kind");
   if (n_pairs == 0) return GMAT_OK;
+  if (e->seg) return seg_audit(e, kind, pairs, n_pairs, out5);
   int lc, rc;
   kind_codings(kind, &lc, &rc);
   GMAT_TRY(build_coding(e, lc));

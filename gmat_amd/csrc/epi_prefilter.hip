@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
 
 // COMPACT: the compacted low-rank path's output (live masks + one record per live pair at a.ops); else
 // the block-granular path's (flags + E3 and code products of every pair of a live block, dense)
-template <bool LIST, bool COMPACT>
+template <bool LIST, bool COMPACT, bool STAMP>
 __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   const ScreenArgs &a = x.a;
   // The workgroup's tiles.  With a tile list (the launch's running tiles), XCD x (workgroup b runs on
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   int r0 = (tile % x.n_rt) * PF_TR;
   int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PF_TC;
   auto pstamp = [&](int k) __attribute__((always_inline)) {  // the workgroup's first tile only
-    if (!LIST && a.pf_stamp && threadIdx.x == 0)
+    if (STAMP && a.pf_stamp && threadIdx.x == 0)
       a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
   };
   pstamp(0);
@@ -194,6 +194,8 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   // They retire before stage 0 (in-order vmcnt), so the stage waits cover them.
   // Two record buffers: the next tile's land while the current tile's epilogue reads its own.
   __shared__ __attribute__((aligned(16))) float rec[2][PF_TR + PF_TC][PF_REC];
+  // COMPACT: per wave, lane (b, h)'s live-column mask and first record (the epilogue's store table)
+  __shared__ uint2 ptab[COMPACT ? 8 : 1][64];
   auto issue_rec = [&](int r0, int64_t c0, int rb) __attribute__((always_inline)) {
     const int k = 32 * w + (lane >> 1);
     if (w < PF_TR / 32)
@@ -358,19 +360,51 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
         const float se = sab - be * r0v.z + al * cnb[q];
         const float vlo = mu_e * ee - k1 * se * se - k2 * r1v.z * cmag[q];
         const bool lv = ok & (!(vlo > 0.0f) | (eff_hi * eff_hi * CMP >= chi_cut * vlo));
-        const unsigned long long bal = __ballot(lv);
-        n_live += (unsigned)__popcll(bal);
-        const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
-        mine[q] = te == e ? (th ? w1 : w0) : mine[q];
-        // COMPACT: this lane's pair is live; else: a live block (its row r < n_rows: some lane of the half
-        // passed rok) whose column this lane holds
-        st_bits |= ((COMPACT ? lv : (((h ? w1 : w0) != 0u) & cok[q])) ? 1u : 0u) << (2 * e + q);
+        if (COMPACT) {  // this lane's pair is live (the masks come from one bit transpose below)
+          st_bits |= (lv ? 1u : 0u) << (2 * e + q);
+        } else {
+          const unsigned long long bal = __ballot(lv);
+          n_live += (unsigned)__popcll(bal);
+          const unsigned w0 = (unsigned)bal, w1 = (unsigned)(bal >> 32);
+          mine[q] = te == e ? (th ? w1 : w0) : mine[q];
+          // a live block (its row r < n_rows: some lane of the half passed rok) whose column this lane holds
+          st_bits |= ((((h ? w1 : w0) != 0u) & cok[q]) ? 1u : 0u) << (2 * e + q);
+        }
       }
     }
     pstamp(4);
     if (COMPACT) {
-      // one record per live pair: the wave reserves its n_live records with one atomic, then each
-      // (row pair, block) ballot places its pairs in lane order (h = 0 row first, ascending columns)
+      // One record per live pair.  Lane (c, h) holds bit b = 2 e + q of st_bits for column c of element
+      // (e, q); a 32 x 32 bit transpose inside each half-wave (five xor-shuffle rounds) gives lane (b, h)
+      // the live-column mask W of element b's row in half h -- the (row, 32-column block) entry -- in ~25
+      // VALU, where a ballot per element cost ~50 instructions per element (round 4's store phase took
+      // ~5 us of a tile's ~11 us epilogue).  The entries' records are numbered in lane order by a prefix
+      // sum of popc(W) (a block's pairs consecutive, ascending j, as lc_fill reads them), the wave
+      // reserves them with one atomic per PF_CHUNK or more, each lane writes its entry, and each live pair
+      // its record at entry base + rank of its column in W (base and W of the lane's elements read back
+      // from a per-wave LDS table; elements without a live pair in the wave are skipped by a scalar test).
+      unsigned wv = st_bits;
+      constexpr unsigned TMASK[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+      for (int rd = 0; rd < 5; ++rd) {
+        const int s2 = 16 >> rd;
+        const unsigned ml = TMASK[rd];
+        const unsigned y = (unsigned)__shfl_xor((int)wv, s2);
+        wv = (c & s2) ? ((wv & ~ml) | ((y >> s2) & ml)) : ((wv & ml) | ((y & ml) << s2));
+      }
+      // lane (b, h): element b = 2 e + q, row 32 wr + kr(e) + 4 h, 32-column block J
+      const int eb = c >> 1, qb = c & 1;
+      const int trr = r0 + 32 * wr + (eb & 3) + 8 * (eb >> 2) + 4 * h;
+      const int Jb = (int)((c0 + 64 * wc + 32 * qb) / 32);
+      const unsigned cnt = (unsigned)__popc(wv);
+      unsigned incl = cnt;  // inclusive prefix sum over the 64 lanes
+#pragma unroll
+      for (int rd = 0; rd < 6; ++rd) {
+        const int s2 = 1 << rd;
+        const unsigned y = (unsigned)__shfl_up((int)incl, s2);
+        incl += lane >= s2 ? y : 0u;
+      }
+      n_live = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
       unsigned base = 0u;
       if (n_live) {
         if (!LIST) {
@@ -388,31 +422,33 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
           ch_cur += n_live;
         }
       }
+      const unsigned ebase = base + incl - cnt;  // the first record of lane (b, h)'s entry
+      if (wv && trr < a.n_rows && Jb < a.nJ) a.lmask[(int64_t)trr * a.nJ + Jb] = lm_entry(wv, ebase, a.ltag);
       const bool fits = (int64_t)base + n_live <= a.ops_cap;
-      unsigned run = base;
+      // elements with a live pair anywhere in the wave (bit b: either half)
+      const unsigned long long anyb = __ballot(wv != 0u);
+      const unsigned elem_any = (unsigned)anyb | (unsigned)(anyb >> 32);
+      if (n_live) {
+        ptab[w][lane] = make_uint2(wv, ebase);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's table writes are visible to its reads
+        __builtin_amdgcn_wave_barrier();
+      }
       int *const ops = a.ops;
+      const unsigned below = (1u << c) - 1u;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const bool lv = (st_bits >> (2 * e + q)) & 1u;
-          const unsigned long long bal = __ballot(lv);
-          if (bal) {
-            // the first record of each live (row, block) of the ballot: lane 2 e + th writes row th's
-            const unsigned word = th ? (unsigned)(bal >> 32) : (unsigned)bal;
-            const int trr = r0 + 32 * wr + (e & 3) + 8 * (e >> 2) + 4 * th;
-            const int J = (int)((c0 + 64 * wc + 32 * q) / 32);
-            if (te == e && lane < 32 && word && trr < a.n_rows && J < a.nJ)
-              a.lmask[(int64_t)trr * a.nJ + J] = lm_entry(word, run + (th ? (unsigned)__popc((unsigned)bal) : 0u), a.ltag);
-            if (lv && fits) {
-              const unsigned k = run + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+          const int b = 2 * e + q;
+          if ((elem_any >> b) & 1u) {  // wave-uniform
+            if (((st_bits >> b) & 1u) && fits) {
+              const uint2 t = ptab[w][32 * h + b];
+              const unsigned k = t.y + (unsigned)__popc(t.x & below);
               v4i r0v = {acc[q][0][e] >> 1, acc[q][1][e] >> 1, (int)acc4[q][0][e], (int)acc4[q][1][e]};  // exact
               v4i r1v = {(int)acc4[q][2][e], (int)acc4[q][3][e], jq[q], 0};
               *(v4i *)(ops + (int64_t)k * OPS_REC) = r0v;
               *(v4i *)(ops + (int64_t)k * OPS_REC + 4) = r1v;
             }
-            run += (unsigned)__popcll(bal);
           }
         }
       }
@@ -444,7 +480,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       }
     }
     if (a.live_count && lane == 0 && n_live) atomicAdd(a.live_count, (unsigned long long)n_live);
-    if (!LIST && a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
+    if (STAMP && a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
     pstamp(6);
     if (nxt < 0) break;
     r0 = (nxt % x.n_rt) * PF_TR;
@@ -757,9 +793,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
 template __global__ void side_gemm_kernel<2>(SideArgs);
 template __global__ void side_gemm_kernel<3>(SideArgs);
 template __global__ void side_gemm_kernel<4>(SideArgs);
-template __global__ void prefilter_pass_kernel<true, true>(SideArgs);
-template __global__ void prefilter_pass_kernel<false, true>(SideArgs);
-template __global__ void prefilter_pass_kernel<false, false>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, false>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, true>(SideArgs);
+template __global__ void prefilter_pass_kernel<false, false, false>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, true>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, false>(SideArgs);
 template __global__ void prefilter_cov_kernel<2, true>(SideArgs);

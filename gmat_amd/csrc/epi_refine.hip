@@ -813,12 +813,12 @@ __global__ void pair_test_kernel(PairArgs x, int nseg) {
   pair_test(x, p, M);
 }
 
-// (i, j) of every pair of rows[r] (j > i for the triangular kinds, every j for AD), row r's pairs
-// starting at offs[r]
+// (i, j) of every pair of rows[r] (j > i for the triangular kinds, every j for AD; j >= col_lo), row r's
+// pairs starting at offs[r]
 __global__ void all_pairs_kernel(const int64_t *__restrict__ rows, const int64_t *__restrict__ offs, int64_t m, int tri,
-                                 int64_t *__restrict__ pi, int64_t *__restrict__ pj) {
+                                 int64_t col_lo, int64_t *__restrict__ pi, int64_t *__restrict__ pj) {
   const int r = blockIdx.y;
-  const int64_t i = rows[r], j0 = tri ? i + 1 : 0, cnt = m - j0, base = offs[r];
+  const int64_t i = rows[r], j0 = tri ? max(i + 1, col_lo) : col_lo, cnt = m - j0, base = offs[r];
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += (int64_t)gridDim.x * blockDim.x) {
     pi[base + t] = i;
     pj[base + t] = j0 + t;

@@ -107,7 +107,7 @@ struct ScanLaunch {
 // as the triangle's rows shrink); launches without a pair are dropped.  *pairs = the pairs the
 // launches test.
 std::vector<ScanLaunch> fold_launches(const int64_t *rows, int64_t n_rows, int64_t m, int tri, double *pairs,
-                                      int64_t rl = ROWS_PER_LAUNCH) {
+                                      int64_t rl = ROWS_PER_LAUNCH, int64_t col_lo = 0) {
   std::vector<ScanLaunch> plan;
   *pairs = 0;
   const int64_t half = rl / 2, nc = cdiv(n_rows, half);
@@ -117,9 +117,9 @@ std::vector<ScanLaunch> fold_launches(const int64_t *rows, int64_t n_rows, int64
     if (l != k)
       for (int64_t t = l * half; t < std::min(n_rows, (l + 1) * half); ++t) ln.rows.push_back(rows[t]);
     if (ln.rows.empty()) continue;
-    ln.j_lo = tri ? ln.rows[0] + 1 : 0;
-    if (tri && ln.j_lo >= m) continue;
-    for (int64_t r : ln.rows) *pairs += tri ? (double)(m - 1 - r) : (double)m;
+    ln.j_lo = std::max<int64_t>(tri ? ln.rows[0] + 1 : 0, col_lo);
+    if (ln.j_lo >= m) continue;
+    for (int64_t r : ln.rows) *pairs += (double)(m - std::max<int64_t>(tri ? r + 1 : 0, col_lo));
     plan.push_back(std::move(ln));
   }
   return plan;
@@ -261,7 +261,11 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   GMAT_TRY(scan_begin(e, kind, &c));
   const int tri = c.tri;
   // chunks of whole rows of at most `cap` pairs (one row holds at most m)
-  const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : (1 << 24));
+  // (the wide int8 refine keeps R8_S integer partial sums per pair and square of stages: chunks of at
+  // most ~2 GB of them)
+  const int64_t nQ = cdiv(e->n_pad / 64, R8_NC), nseg_w = e->n_pad > 64 * R8_NC ? nQ * (nQ + 1) / 2 : 1;
+  const int64_t dflt = std::min<int64_t>(1 << 24, ((int64_t)1 << 31) / (8 * (1 + R8_S * nseg_w)));
+  const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : dflt);
   if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
   const hipStream_t st = e->s3;
   DBuf di, dj, de, dv, dc, dp, hi, hj, he, hv, hc, hp, cnt, drows, doffs;
@@ -282,7 +286,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
     offs.clear();
     int64_t np = 0, r1 = r0;
     while (r1 < n_rows && r1 - r0 < 65535) {
-      const int64_t c = tri ? m - 1 - rows[r1] : m;
+      const int64_t c = m - std::max<int64_t>(tri ? rows[r1] + 1 : 0, e->col_lo);
       if (np + c > cap) break;
       offs.push_back(np);
       np += c;
@@ -293,10 +297,11 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
     if (np > 0) {
       GMAT_HIP(hipMemcpyAsync(drows.p, rows + r0, nr * 8, hipMemcpyHostToDevice, st));
       GMAT_HIP(hipMemcpyAsync(doffs.p, offs.data(), nr * 8, hipMemcpyHostToDevice, st));
-      const int64_t per_row = tri ? m - 1 - rows[r0] : m;  // the longest row of the chunk (rows increase)
+      // the longest row of the chunk (rows increase)
+      const int64_t per_row = m - std::max<int64_t>(tri ? rows[r0] + 1 : 0, e->col_lo);
       hipLaunchKernelGGL(all_pairs_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(per_row, 256), 64)),
                                                 (unsigned)nr),
-                         dim3(256), 0, st, drows.as<int64_t>(), doffs.as<int64_t>(), m, tri, di.as<int64_t>(),
+                         dim3(256), 0, st, drows.as<int64_t>(), doffs.as<int64_t>(), m, tri, e->col_lo, di.as<int64_t>(),
                          dj.as<int64_t>());
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ev0, st));
@@ -379,7 +384,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     }
   }
   double pairs_tested = 0;
-  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL);
+  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL, e->col_lo);
   // live-pair records per launch: an initial capacity of 1/128 of a launch's pairs (at least 2^20; the
   // configs[2] prefilter keeps 1/250), grown (and the launch rerun) when a launch keeps more
   const int64_t rl_sets = std::max(RL, B.rl);
@@ -586,19 +591,20 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
               if (runs(rt, ct)) tl[run++] = rt + x.n_rt * (int)ct;
       pf_ops_of[li] = (double)run * PF_TR * PF_TC * 16.0 * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
-      if (pf_list) {
-        // persistent grid over the list: one workgroup per CU (a multiple of 8).  (Same-box A/B: 27.6
-        // against 27.7 ms per configs[2] step for as few workgroups as finish in the same number of
-        // tile rounds, and 28.0 against 28.2 for one workgroup per tile, GMAT_PF_NOLIST.)
-        GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
-        x.tile_list = B.tlist[b].as<int>();
-        x.n_list = run;
-        const int g = 8 * (int)std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8));
-        if (run > 0) hipLaunchKernelGGL((prefilter_pass_kernel<true, true>), dim3((unsigned)g), dim3(512), 0, S2, x);
-      } else {
-        if (li == stamp_launch) stamp_grid = x.n_rt * cdiv(ncols, PF_TC);
-        hipLaunchKernelGGL((prefilter_pass_kernel<false, true>), dim3((unsigned)(x.n_rt * cdiv(ncols, PF_TC))), dim3(512),
-                           0, S2, x);
+      // persistent grid over the list: one workgroup per CU (a multiple of 8).  (Same-box A/B: 27.6
+      // against 27.7 ms per configs[2] step for as few workgroups as finish in the same number of
+      // tile rounds, and 28.0 against 28.2 for one workgroup per tile, GMAT_PF_NOLIST: a grid of as many
+      // workgroups as tiles, which the per-tile phase stamps use.)
+      GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
+      x.tile_list = B.tlist[b].as<int>();
+      x.n_list = run;
+      const int g = 8 * (int)(pf_list ? std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8)) : cdiv(run, 8));
+      if (!pf_list && li == stamp_launch) stamp_grid = g;
+      if (run > 0) {
+        if (x.a.pf_stamp)  // the phase-stamped build (GMAT_PF_STAMPS)
+          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true>), dim3((unsigned)g), dim3(512), 0, S2, x);
+        else
+          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false>), dim3((unsigned)g), dim3(512), 0, S2, x);
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
@@ -883,7 +889,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   constexpr int BI = Shape<SCREEN_SHAPE>::BI, MT = Shape<SCREEN_SHAPE>::MT;
   GMAT_CHECK(n_pad % MT == 0, GMAT_E_ARG, "n_pad %lld is not a multiple of the K-block %d", (long long)n_pad, MT);
   double pairs_tested = 0;
-  std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested);
+  std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, ROWS_PER_LAUNCH, e->col_lo);
 
   // Two buffer sets: the side GEMMs of launch L+1 (stream s2) run while the screen of launch
   // L (stream sm) is in flight; each buffer set is rewritten only after the screen that
@@ -963,7 +969,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
     if (!ln.tiles.empty()) return;
     const int Rn = (int)ln.rows.size();
     for (int r0 = 0; r0 < Rn; r0 += BI) {
-      const int64_t jb0 = tri ? (ln.rows[r0] + 1) / BJ : 0;
+      const int64_t jb0 = std::max<int64_t>(tri ? ln.rows[r0] + 1 : 0, ln.j_lo) / BJ;
       for (int64_t J = jb0; J * BJ < m; ++J) {
         ln.tiles.push_back(r0);
         ln.tiles.push_back((int)J);
@@ -1093,7 +1099,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.cs2 = R.p2b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
-        hipLaunchKernelGGL((prefilter_pass_kernel<false, false>), dim3(gp), dim3(512), 0, S2, xp);
+        hipLaunchKernelGGL((prefilter_pass_kernel<false, false, false>), dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
         xp.qimg = e->pf_q.as<uint8_t>();
@@ -1495,22 +1501,30 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
 }  // namespace epi
 }  // namespace gmat
 
-extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+int gmat::epi::scan_dispatch(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
                              int n_slice, int64_t *n_hits) {
-  GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
-  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
-  const int64_t m = e->m, n_pad = e->n_pad;
-  for (int64_t t = 0; t < n_rows; ++t) {
-    GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
-    GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
-  }
-  if (n_slice == GMAT_SCREEN_NONE) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
+  GMAT_CHECK(!e->seg, GMAT_E_ARG, "scan_dispatch: a segmented plan (seg_scan runs its sub-plans)");
+  // no screen asked for, or none available (a plan past EXH_ONLY_NPAD individuals): every pair refined
+  if (n_slice == GMAT_SCREEN_NONE || e->exh_only) return scan_exhaustive(e, kind, rows, n_rows, p_cut, n_hits);
   // the compacted low-rank scan serves the low-rank level (automatic at p_cut <= 1e-4, or forced by
   // n_slice -2); GMAT_LR_BLOCKS=1 keeps the block-granular path below (A/B runs)
   const bool lr_level = e->lr_R > 0 && e->pf_mu > 0.0 && (n_slice == -2 || (n_slice == 0 && p_cut <= 1e-4));
   if (lr_level && pair_screen_fits(e) && !getenv("GMAT_LR_BLOCKS") && !getenv("GMAT_NO_PREFILTER"))
     return scan_lowrank(e, kind, rows, n_rows, p_cut, chi_cut, n_hits);
   return scan_blocks(e, kind, rows, n_rows, p_cut, chi_cut, n_slice, n_hits);
+}
+
+extern "C" int gmat_epi_scan(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, double p_cut, double chi_cut,
+                             int n_slice, int64_t *n_hits) {
+  GMAT_CHECK(e && rows && n_hits, GMAT_E_ARG, "gmat_epi_scan: bad arguments");
+  GMAT_CHECK(kind >= 0 && kind <= 2, GMAT_E_ARG, "gmat_epi_scan: bad kind");
+  const int64_t m = e->m;
+  for (int64_t t = 0; t < n_rows; ++t) {
+    GMAT_CHECK(rows[t] >= 0 && rows[t] < m, GMAT_E_ARG, "row %lld out of range", (long long)rows[t]);
+    GMAT_CHECK(t == 0 || rows[t] > rows[t - 1], GMAT_E_ARG, "rows must be strictly increasing");
+  }
+  if (e->seg) return seg_scan(e, kind, rows, n_rows, p_cut, chi_cut, n_slice, n_hits);
+  return scan_dispatch(e, kind, rows, n_rows, p_cut, chi_cut, n_slice, n_hits);
 }
 
 extern "C" int gmat_epi_hits(gmat_epi *e, int64_t cap, int64_t *i, int64_t *j, double *eff, double *var, double *chi,

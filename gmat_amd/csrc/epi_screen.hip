@@ -825,7 +825,24 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
   const double tot = (h ? lowrank[1] : lowrank[0]) + __shfl_xor(h ? lowrank[0] : lowrank[1], 32);
   const int ri = h ? rr1 : rr0;
   const int64_t i = h ? i1 : i0, j = h ? jc[1] : jc[0];
-  if (ri >= 0 && j >= 0) lrc_test(a, x, (int64_t)(sbase + PB * w + h) * 32 + c, i, j, tot);
+  const bool cand = ri >= 0 && j >= 0 && lrc_cand(a, x, (int64_t)(sbase + PB * w + h) * 32 + c, i, j, tot);
+  // the wave's candidates with one atomic, slot 0's then slot 1's in column order (a slot's candidates
+  // -- one first SNP -- stay adjacent for the pair screen)
+  const unsigned long long bal = __ballot(cand);
+  if (bal) {
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(a.counter, (unsigned long long)__popcll(bal));
+    base = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+    if (cand) {
+      const unsigned long long k =
+          base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+      if ((int64_t)k < a.cap) {
+        a.cand_i[k] = i;
+        a.cand_j[k] = j;
+      }
+    }
+  }
 }
 
 // Left / right test records of a coding (lr_screen_kernel's per-SNP test operands in one 64-byte

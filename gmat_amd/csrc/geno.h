@@ -22,3 +22,8 @@ struct gmat_geno {
   std::vector<int64_t> sum_dose, n_het, n_miss;
   int64_t total_missing = 0;
 };
+
+// A panel of the SNP ranges [lo[r], hi[r]) of g, in that order (device copies of the dosage and
+// heterozygote rows, the per-SNP counts): the sub-panels of a segmented scan plan (epi_seg.hip).  The
+// packed .bed rows are not copied (the scans never read them).
+int geno_subset(const gmat_geno *g, const int64_t *lo, const int64_t *hi, int nr, gmat_geno **out);

@@ -403,6 +403,46 @@ extern "C" int gmat_geno_create(gmat_geno **out, const uint8_t *bed_body, int64_
   return GMAT_OK;
 }
 
+int geno_subset(const gmat_geno *g, const int64_t *lo, const int64_t *hi, int nr, gmat_geno **out) {
+  GMAT_CHECK(g && out && nr >= 1, GMAT_E_ARG, "geno_subset: bad arguments");
+  int64_t m = 0;
+  for (int r = 0; r < nr; ++r) {
+    GMAT_CHECK(lo[r] >= 0 && lo[r] < hi[r] && hi[r] <= g->m, GMAT_E_ARG, "geno_subset: range [%lld, %lld) of %lld SNPs",
+               (long long)lo[r], (long long)hi[r], (long long)g->m);
+    m += hi[r] - lo[r];
+  }
+  auto *s = new gmat_geno();
+  s->n = g->n;
+  s->m = m;
+  s->nb = g->nb;
+  s->n_pad = g->n_pad;
+  if (int rc = s->panels.alloc((size_t)2 * s->n_pad * m)) {
+    delete s;
+    return rc;
+  }
+  int64_t at = 0;
+  for (int r = 0; r < nr; ++r) {
+    const size_t bytes = (size_t)(hi[r] - lo[r]) * g->n_pad;
+    hipError_t e = hipMemcpy(s->dose_ptr() + at * s->n_pad, g->dose_ptr() + lo[r] * g->n_pad, bytes, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(s->het_ptr() + at * s->n_pad, g->het_ptr() + lo[r] * g->n_pad, bytes, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) {
+      set_error("geno_subset: %s", hipGetErrorString(e));
+      delete s;
+      return GMAT_E_HIP;
+    }
+    for (int64_t j = lo[r]; j < hi[r]; ++j) {
+      s->sum_dose.push_back(g->sum_dose[j]);
+      s->n_het.push_back(g->n_het[j]);
+      s->n_miss.push_back(g->n_miss[j]);
+      s->total_missing += g->n_miss[j];
+    }
+    at += hi[r] - lo[r];
+  }
+  *out = s;
+  return GMAT_OK;
+}
+
 extern "C" int gmat_geno_counts(const gmat_geno *g, int64_t *sum_dose, int64_t *n_het, int64_t *n_miss) {
   GMAT_CHECK(g, GMAT_E_ARG, "gmat_geno_counts: null handle");
   if (sum_dose) memcpy(sum_dose, g->sum_dose.data(), g->m * sizeof(int64_t));

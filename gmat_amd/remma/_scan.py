@@ -137,6 +137,13 @@ class EpiPlan:
         N.check(self._lib.gmat_epi_info(self._h, N.ptr(s)), "gmat_epi_info")
         return int(s[0])
 
+    def layout(self):
+        """How the plan holds its panel (gmat_epi_layout): SNP segments (1 = one plan), SNPs per segment,
+        whether the plan is exhaustive-only (no screens past 8,192 individuals), and n_snp."""
+        s = np.zeros(4, np.int64)
+        N.check(self._lib.gmat_epi_layout(self._h, N.ptr(s)), "gmat_epi_layout")
+        return {"segments": int(s[0]), "segment_snps": int(s[1]), "exhaustive_only": bool(s[2]), "n_snp": int(s[3])}
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.gmat_epi_destroy(self._h)

@@ -155,6 +155,11 @@ int gmat_epi_info(const gmat_epi *e, double *out4);
  * done lazily by the first scan of each coding), [6] Cholesky factorisations the certificates ran,
  * [7] covariate directions in the prefilter certificate (null directions of P besides 1) */
 int gmat_epi_setup_stats(const gmat_epi *e, double *out8);
+/* how the plan holds its panel: [0] SNP segments (1: one plan; more when 2 n_snp n_pad would reach
+ * 2^32 bytes, or GMAT_SEG_SNPS asks for them: scans run on sub-plans of one or two segments), [1]
+ * SNPs per segment, [2] 1 when the plan has no screens (n_pad > 8,192: every pair refined exactly),
+ * [3] n_snp */
+int gmat_epi_layout(const gmat_epi *e, int64_t *out4);
 int gmat_epi_destroy(gmat_epi *e);
 
 /* Random-effect prediction of wemai_multi_gmat_pred (uvlmm_varcom.py:147-166) at var_com, as

@@ -23,7 +23,8 @@ BENCH = os.path.join(REPO, "bench.py")
 def _clean_env(**kw):
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR", "GMAT_DIST_BACKEND")}
-    env.update(OMP_NUM_THREADS="1", **kw)
+    env["OMP_NUM_THREADS"] = "1"
+    env.update(**kw)
     return env
 
 

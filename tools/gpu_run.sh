@@ -9,8 +9,23 @@ export TMPDIR=/tmp
 for st in "$@"; do
   case $st in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
       tail -3 $OUT/tests.log ;;
+    newtests)
+      # this round's limit / buffer / launch tests
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_buffers.py tests/test_gpu_limits.py tests/test_launch.py -m gpu -v --timeout 600 --timeout-method thread > $OUT/newtests.log 2>&1 || { tail -60 $OUT/newtests.log; exit 1; }
+      tail -3 $OUT/newtests.log ;;
+    serial)
+      # every kernel's standalone time (launches serialised), summed over 5 timed configs[2] steps
+      AMD_SERIALIZE_KERNEL=3 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/serial -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/serial.json 2> $OUT/serial.log || { tail -20 $OUT/serial.log; exit 1; }
+      cp $(find $OUT/serial -name "*kernel_stats.csv" | head -1) $OUT/serial_kernel_stats.csv
+      head -12 $OUT/serial_kernel_stats.csv | cut -c1-200 ;;
+    timeline)
+      # the overlapped step: kernel trace of 5 timed configs[2] steps, the last step's window
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tl -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/tl.json 2> $OUT/tl.log || { tail -20 $OUT/tl.log; exit 1; }
+      cp $(find $OUT/tl -name "*kernel_stats.csv" | head -1) $OUT/tl_kernel_stats.csv
+      python3 tools/step_timeline.py $(find $OUT/tl -name "*kernel_trace.csv" | head -1) > $OUT/step_timeline.txt
+      head -30 $OUT/step_timeline.txt ;;
     scantests)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_pair_screen.py tests/test_gpu_lr_variants.py tests/test_gpu_parity.py tests/test_gpu_full_triangle.py -x -q --timeout 240 --timeout-method thread > $OUT/scantests.log 2>&1 || { tail -40 $OUT/scantests.log; exit 1; }
       tail -2 $OUT/scantests.log ;;
