@@ -26,6 +26,17 @@ for st in "$@"; do
       cp $(find $OUT/tl -name "*kernel_stats.csv" | head -1) $OUT/tl_kernel_stats.csv
       python3 tools/step_timeline.py $(find $OUT/tl -name "*kernel_trace.csv" | head -1) > $OUT/step_timeline.txt
       head -30 $OUT/step_timeline.txt ;;
+    reml)
+      # configs[1] REML under a kernel trace: per-kernel totals of the REML legs (tools/reml_only.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/reml -o run -- python3 tools/reml_only.py 2000 20000 > $OUT/reml.json 2> $OUT/reml.log || { tail -20 $OUT/reml.log; exit 1; }
+      cp $(find $OUT/reml -name "*kernel_stats.csv" | head -1) $OUT/reml_kernel_stats.csv
+      cat $OUT/reml.json; head -12 $OUT/reml_kernel_stats.csv | cut -c1-160 ;;
+    cfg5probe)
+      # configs[4] REML convergence on full-sib cohorts (tools/cfg5_reml_probe.py), family sizes 5, 10, 20
+      for f in 5 10 20; do
+        timeout -k 10 240 python3 -u tools/cfg5_reml_probe.py $f 200 "0.3,0.1,0.1,0.05,0.05,0.4" "0.3,0.1,0.1,0.1,0.1,0.3" > $OUT/cfg5probe_$f.log 2>&1 || { tail -20 $OUT/cfg5probe_$f.log; exit 1; }
+        cat $OUT/cfg5probe_$f.log | cut -c1-400
+      done ;;
     scantests)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_pair_screen.py tests/test_gpu_lr_variants.py tests/test_gpu_parity.py tests/test_gpu_full_triangle.py -x -q --timeout 240 --timeout-method thread > $OUT/scantests.log 2>&1 || { tail -40 $OUT/scantests.log; exit 1; }
       tail -2 $OUT/scantests.log ;;

@@ -9,7 +9,7 @@ import sys
 
 def short(name):
     name = re.sub(r"\(anonymous namespace\)::", "", name)
-    return re.sub(r"^(void )?(gmat::)?", "", name).split("(")[0][:48]
+    return re.sub(r"^(void )?(gmat::)?(epi::)?", "", name).split("(")[0][:48]
 
 
 def main():
