@@ -135,7 +135,7 @@ def parity_check(plan, rows, exp, p_cut):
 
 
 EXHAUSTIVE_HITS = os.path.join(REPO, "tests", "golden", "cfg3_exhaustive_hits_AA_2000x50000.npz")
-FULL_TRIANGLE_RECORD = "profiles/round4_full_triangle_AA_2000x50000.json"
+FULL_TRIANGLE_RECORD = "profiles/round5_full_triangle_AA_2000x50000.json"
 
 
 def full_triangle_check(g, pvp, py, hits, p_cut, live=None):

@@ -11,6 +11,15 @@
 
 #include "dla.h"
 
+// stage timestamps for tools/chol_micro.hip (defines CHOL_STAMP before including this file)
+#ifndef CHOL_STAMP
+#define CHOL_STAMP(i)
+#endif
+#ifndef CHOL_TASK_BEGIN
+#define CHOL_TASK_BEGIN
+#define CHOL_TASK_END
+#endif
+
 namespace gmat {
 
 namespace {
@@ -27,51 +36,106 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return u.d;
 }
 
-// Factor the kb x kb (kb <= 64) diagonal block at a (lda) in LDS with 4 barrier-separated
-// 16-column panels (instead of one barrier group per column): wave 0 factors a panel with its rows
-// in registers (pivot and the panel's column entries broadcast by readlane, no LDS round trips),
-// then the four waves apply the panel to the trailing lower 16 x 16 blocks on fp64 MFMA.  inv(L)
-// is blocked the same way: the four 16 x 16 diagonal inverses by forward substitution (one thread
-// per column, the column in registers), then the off-diagonal blocks by distance d = i - j as two
-// small MFMA products, X_ij = -X_ii (sum_{j<=k<i} L_ik X_kj).  Rows / columns >= kb are an uncoupled identity.  Writes
-// L back, inv(L) to dinv (kb rows of NB doubles), adds 2 sum(log diag) to *logdet, flags a bad
-// pivot's block in *info.
-__global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv, double *logdet,
-                                                    int *info, int64_t k0) {
-  constexpr int PW = 16, NP = NB / PW;
-  __shared__ double Ls[NB][NB + 1];
-  __shared__ double Xs[NB][NB + 1];
-  __shared__ double Ts[NP - 1][PW][PW + 1];
-  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  {  // the block's 16 values per thread: all loads issued before the first LDS store (a load-store loop
-     // waited for each load in turn: ~16 memory latencies per launch)
-    double v[NB * NB / 256];
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
-      v[u] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
-    }
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
-      Ls[rr][cc] = v[u];
-      Xs[rr][cc] = 0.0;
-    }
+// v's value on lane k (0..15) of each row of 16 lanes (v_mov_b64_dpp row_newbcast; k a constant after
+// unrolling)
+template <int K>
+__device__ __forceinline__ double bcast16_c(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xF, 0xF, true);
+}
+__device__ __forceinline__ double bcast16(double v, int k) {
+  switch (k) {
+    case 0: return bcast16_c<0>(v);
+    case 1: return bcast16_c<1>(v);
+    case 2: return bcast16_c<2>(v);
+    case 3: return bcast16_c<3>(v);
+    case 4: return bcast16_c<4>(v);
+    case 5: return bcast16_c<5>(v);
+    case 6: return bcast16_c<6>(v);
+    case 7: return bcast16_c<7>(v);
+    case 8: return bcast16_c<8>(v);
+    case 9: return bcast16_c<9>(v);
+    case 10: return bcast16_c<10>(v);
+    case 11: return bcast16_c<11>(v);
+    case 12: return bcast16_c<12>(v);
+    case 13: return bcast16_c<13>(v);
+    case 14: return bcast16_c<14>(v);
+    default: return bcast16_c<15>(v);
   }
-  __syncthreads();
-  bool bad = false;
+}
+
+// Row block q of X = inv(L) for the 16 x 16 blocks of the NB x NB factor in Ls (L_qk, k <= q, final;
+// X_kj, j <= k < q, already in Xs), computed by one wave: the diagonal block X_qq by forward substitution
+// in registers -- lane (g = lane / 16, i = lane % 16) row i, columns 4c + g (c = 0..3), which is the
+// v_mfma_f64_16x16x4 A-operand layout of X_qq, rows of X broadcast by row_newbcast -- then, for j = jq
+// < q, X_qj = -X_qq T_j with T_j = sum_{j<=k<q} L_qk X_kj (T_j's accumulator is already the B operand of
+// the second product).  Stores X_qq when diag, X_qj when jq < q.
+__device__ __forceinline__ void x_row_block(const double (*Ls)[NB + 1], double (*Xs)[NB + 1], const double *ipiv, int q,
+                                            int jq, bool diag) {
+  constexpr int PW = 16;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15, o = PW * q;
+  double lo[PW], t[4];
 #pragma unroll
+  for (int m = 0; m < PW; ++m) lo[m] = (m < li) ? Ls[o + li][o + m] : 0.0;  // strictly lower row of L_qq
+  const double id = ipiv[o + li];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t[c] = (li == 4 * c + g) ? 1.0 : 0.0;
+  // row m of X_qq is t / L_mm on lane m once rows < m are subtracted; later rows subtract L_im X_m,c
+  // (rows above m and the diagonal are untouched: lo is strictly lower)
+#pragma unroll
+  for (int m = 0; m < PW; ++m)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[c] = fma(-lo[m], bcast16(t[c] * id, m), t[c]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t[c] *= id;  // X_qq[li][4c + g]
+  if (diag)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Xs[o + li][o + 4 * c + g] = t[c];
+  if (jq < q) {
+    const int j = jq;
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = j; k < q; ++k)
+#pragma unroll
+      for (int s4 = 0; s4 < PW / 4; ++s4) {
+        const double av = Ls[o + li][PW * k + 4 * s4 + g];
+        const double bv = Xs[PW * k + 4 * s4 + g][PW * j + li];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+    v4d x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < PW / 4; ++s4) x = __builtin_amdgcn_mfma_f64_16x16x4f64(t[s4], acc[s4], x, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Xs[o + g + 4 * r][PW * j + li] = -x[r];
+  }
+}
+
+// The factor and its inverse of the NB x NB block in Ls (rows / columns >= kb already an identity), in
+// place: Ls := L (lower; upper zero), Xs := inv(L), piv[j] := L_jj (1 past kb).  Returns whether a pivot
+// within kb was not positive (then replaced by 1).  All 256 threads of the workgroup; ends with a barrier.
+//   4 barrier-separated 16-column panels.  Wave 0 factors the whole 64-row panel in registers: lane l
+//   holds its row of the panel and, in every row of 16 lanes, a copy of the panel's diagonal-block row
+//   l % 16, so each pivot and each L_c0+k,j a rank-1 update needs is one row_newbcast DPP move (no
+//   readlane / SGPR round trips).  Meanwhile waves 1..3 compute row block p - 1 of inv(L)
+//   (x_row_block).  Then the four waves apply the panel to the trailing lower 16 x 16 blocks on fp64
+//   MFMA.  Row block 3 of inv(L) after the last panel.
+__device__ __forceinline__ bool factor_invert_block(double (*Ls)[NB + 1], double (*Xs)[NB + 1], double *piv, int kb) {
+  constexpr int PW = 16, NP = NB / PW;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15;
+  bool bad = false;
+  __shared__ double ipiv[NB];  // 1 / L_jj
+#pragma unroll 1
   for (int p = 0; p < NP; ++p) {
     const int c0 = PW * p;
     if (w == 0) {
-      const int i = lane;
-      double r[PW];
+      double r[PW], dr[PW];
 #pragma unroll
-      for (int q = 0; q < PW; ++q) r[q] = Ls[i][c0 + q];
+      for (int q = 0; q < PW; ++q) {
+        r[q] = Ls[lane][c0 + q];
+        dr[q] = Ls[c0 + li][c0 + q];
+      }
+      double pv = 1.0, ipv = 1.0;
 #pragma unroll
       for (int j = 0; j < PW; ++j) {
-        double d = readlane_d(r[j], c0 + j);
+        double d = bcast16(dr[j], j);
         if (!(d > 0.0)) {
           if (c0 + j < kb) bad = true;
           d = 1.0;
@@ -80,15 +144,28 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
         double inv = __builtin_amdgcn_rsq(d);
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
         inv = inv * fma(-0.5 * d * inv, inv, 1.5);
-        const double ljj = d * inv;
-        if (i == 0) piv[c0 + j] = (c0 + j < kb) ? ljj : 1.0;
-        r[j] = (i > c0 + j) ? r[j] * inv : (i == c0 + j ? ljj : r[j]);
+        if (li == j) {
+          pv = d * inv;
+          ipv = inv;
+        }
+        dr[j] *= inv;
+        r[j] *= inv;
 #pragma unroll
-        for (int k = j + 1; k < PW; ++k) r[k] = fma(-r[j], readlane_d(r[j], c0 + k), r[k]);
+        for (int k = j + 1; k < PW; ++k) {
+          const double t = bcast16(dr[j], k);  // L_c0+k,j
+          dr[k] = fma(-dr[j], t, dr[k]);
+          r[k] = fma(-r[j], t, r[k]);
+        }
       }
-      if (i >= c0)
+      if (lane >= c0)
 #pragma unroll
-        for (int q = 0; q < PW; ++q) Ls[i][c0 + q] = (c0 + q <= i) ? r[q] : 0.0;
+        for (int q = 0; q < PW; ++q) Ls[lane][c0 + q] = (c0 + q <= lane) ? r[q] : 0.0;
+      if (lane < PW) {
+        piv[c0 + lane] = (c0 + lane < kb) ? pv : 1.0;
+        ipiv[c0 + lane] = ipv;
+      }
+    } else if (p > 0) {
+      x_row_block(Ls, Xs, ipiv, p - 1, w - 1, w == 1);
     }
     __syncthreads();
     // trailing lower blocks (bi >= bk > p) -= L_i,p L_k,p' on v_mfma_f64_16x16x4, one wave per block
@@ -111,56 +188,38 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
       }
     }
     __syncthreads();
+    CHOL_STAMP(1 + p);
   }
-  // inv(L): diagonal blocks (thread t < 64: block t / 16, column t % 16)
-  if (tid < NB) {
-    const int o = PW * (tid / PW), c = tid % PW;
-    double x[PW];
+  x_row_block(Ls, Xs, ipiv, NP - 1, w, w == NP - 1);
+  __syncthreads();
+  CHOL_STAMP(5);
+  return bad;
+}
+
+__global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv, double *logdet,
+                                                    int *info, int64_t k0) {
+  constexpr int PW = 16, NP = NB / PW;
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double Xs[NB][NB + 1];
+  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  {  // the block's 16 values per thread: all loads issued before the first LDS store (a load-store loop
+     // waited for each load in turn: ~16 memory latencies per launch)
+    double v[NB * NB / 256];
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      double sacc = 0.0;
-#pragma unroll
-      for (int k = 0; k < q; ++k) sacc = fma(Ls[o + q][o + k], x[k], sacc);
-      const double v = (q == c) ? 1.0 : -sacc;
-      // (a division, not a multiplication by 1 / L_qq: the bits of P = V^-1 .. are pinned by the
-      // recorded exhaustive hit set's cohort fingerprint; the multiplication measured no faster)
-      x[q] = (q >= c) ? v / Ls[o + q][o + q] : 0.0;
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
+      v[u] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
     }
 #pragma unroll
-    for (int q = 0; q < PW; ++q) Xs[o + q][o + c] = x[q];
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
+      Ls[rr][cc] = v[u];
+      Xs[rr][cc] = 0.0;
+    }
   }
   __syncthreads();
-  // off-diagonal blocks by distance d = i - j on v_mfma_f64_16x16x4 (wave j of the level):
-  // T_j = sum_{k=j}^{i-1} L_ik X_kj, then X_ij = -X_ii T_j
-#pragma unroll
-  for (int d = 1; d < NP; ++d) {
-    const int j = w, i = j + d;
-    if (i < NP) {
-      v4d acc = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; ++k)
-#pragma unroll
-        for (int s4 = 0; s4 < PW / 4; ++s4) {
-          const double av = Ls[PW * i + (lane & 15)][PW * k + 4 * s4 + (lane >> 4)];
-          const double bv = Xs[PW * k + 4 * s4 + (lane >> 4)][PW * j + (lane & 15)];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Ts[j][(lane >> 4) + 4 * q][lane & 15] = acc[q];
-    }
-    __syncthreads();
-    if (i < NP) {
-      v4d acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s4 = 0; s4 < PW / 4; ++s4) {
-        const double av = Xs[PW * i + (lane & 15)][PW * i + 4 * s4 + (lane >> 4)];
-        const double bv = Ts[j][4 * s4 + (lane >> 4)][lane & 15];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Xs[PW * i + (lane >> 4) + 4 * q][PW * j + (lane & 15)] = -acc[q];
-    }
-    __syncthreads();
-  }
+  const bool bad = factor_invert_block(Ls, Xs, piv, kb);
   for (int e = tid; e < kb * NB; e += 256) {
     const int r2 = e / NB, c2 = e % NB;
     if (c2 < kb) a[(int64_t)r2 * lda + c2] = Ls[r2][c2];
@@ -176,6 +235,313 @@ __global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t l
   }
 }
 
+// ---- One launch per 64-column step (cholesky_steps): the factorisation, the inverses of its diagonal
+// blocks and optionally X = L^-1 and V^-1 = X'X, without cholesky_inverse()'s chain of small dependent
+// launches (potf2, panel solve, trailing update and the inverse's two products per step, each a few
+// microseconds of work behind its own launch latency).  Launch k (every task independent of the others
+// in it):
+//   D  (block d = k + 1): its last trailing update A_dd - L_dk L_dk', then its factor and inverse in LDS
+//      (factor_invert_block): L_dd into A_dd, inv(L_dd) into dinv, 2 sum log L_jj, the pivot check;
+//      launch -1 factors block 0 as it stands.  Block k + 1's factor is ready when launch k + 1 starts.
+//   T1 (k < j <= i, (i, j) != (k + 1, k + 1)): A_ij -= L_ik L_jk'
+//   T3 (j <= k < i, with X):                   B_ij -= L_ik X_kj     (right-looking L^-1 = X, B = I at first)
+//   W  (the in-place writes of step k - 1, which launch k - 1's readers must not see):
+//      L_i,k-1 = A_i,k-1 inv(L_k-1,k-1)' for i >= k, and X_k-1,j = inv(L_k-1,k-1) B_k-1,j for j <= k - 1.
+//   T5 (with V^-1, row q = k - 2 of X final): V_ab += X_qa' X_qb for b <= a <= q (stored at q = a, the
+//      first term; mirrored into V_ba at q = K - 1, the last).
+// T1 and T3 derive the panel blocks they need, L_ik = A_ik inv(L_kk)' and X_kj = inv(L_kk) B_kj, in the
+// workgroup (the same products as cholesky_inverse's panel solve and inverse step); launches K and K + 1
+// do the last W and T5.  Products are 64 x 64 x 64 on v_mfma_f64_16x16x4f64 from two LDS tiles (two
+// workgroups per CU); a task's global loads are all issued at its start (register-staged tiles); tiles
+// past n are zero (identity on a diagonal block).
+struct StepArgs {
+  int64_t n, lda;
+  int K, k;  // blocks; the step (-1: block 0's factor only; K, K + 1: the last writes only)
+  int nD, nT1, nT3, nWL, nWX, nT5;
+  bool keep_l;  // L into a (else a is scratch: the W_L tasks and D's write of L_dd are skipped)
+  double *a, *linv, *dinv, *logdet, *vinv;
+  int *info;
+};
+
+// acc (+)= A B' for NB x NB operands in LDS (row-major, pitch NB + 1): wave w the 32 x 32 quadrant at rows
+// 32 (w >> 1), columns 32 (w & 1); acc[bi][bj][q] = element (acc_row(bi, q), acc_col(bj))
+__device__ __forceinline__ void mm_abt(const double (*A)[NB + 1], const double (*B)[NB + 1], v4d acc[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = 32 * (w >> 1), c0 = 32 * (w & 1);
+#pragma unroll 4
+  for (int s4 = 0; s4 < NB / 4; ++s4) {
+    const int kk = 4 * s4 + (lane >> 4);
+    const double a0 = A[r0 + (lane & 15)][kk], a1 = A[r0 + 16 + (lane & 15)][kk];
+    const double b0 = B[c0 + (lane & 15)][kk], b1 = B[c0 + 16 + (lane & 15)][kk];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void acc_zero(v4d acc[2][2]) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = v4d{0.0, 0.0, 0.0, 0.0};
+}
+__device__ __forceinline__ int acc_row(int bi, int q) {
+  return 32 * ((threadIdx.x >> 6) >> 1) + 16 * bi + ((threadIdx.x & 63) >> 4) + 4 * q;
+}
+__device__ __forceinline__ int acc_col(int bj) { return 32 * ((threadIdx.x >> 6) & 1) + 16 * bj + (threadIdx.x & 15); }
+
+// an NB x NB tile staged in registers: element e = threadIdx.x + 256 u is (e / NB, e % NB)
+struct TileRegs {
+  double v[NB * NB / 256];
+};
+// the block of src at (r0, c0) (ld), rows < nr and columns < nc; elsewhere 0, or 1 on the diagonal when ident
+__device__ __forceinline__ void tile_load(TileRegs &t, const double *src, int64_t ld, int64_t r0, int64_t c0, int64_t nr,
+                                          int64_t nc, bool ident) {
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u, rr = e / NB, cc = e % NB;
+    t.v[u] = (rr < nr && cc < nc) ? src[(r0 + rr) * ld + c0 + cc] : ((ident && rr == cc) ? 1.0 : 0.0);
+  }
+}
+// S = the tile (transposed when trans)
+__device__ __forceinline__ void tile_to_lds(double (*S)[NB + 1], const TileRegs &t, bool trans) {
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u, rr = e / NB, cc = e % NB;
+    if (trans)
+      S[cc][rr] = t.v[u];
+    else
+      S[rr][cc] = t.v[u];
+  }
+}
+// the block of src at (r0, c0) in the accumulator layout (rows < nr, columns < nc; else 0)
+__device__ __forceinline__ void acc_load(v4d c[2][2], const double *src, int64_t ld, int64_t r0, int64_t c0, int64_t nr,
+                                         int64_t nc) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = acc_row(bi, q), cc = acc_col(bj);
+        c[bi][bj][q] = (r < nr && cc < nc) ? src[(r0 + r) * ld + c0 + cc] : 0.0;
+      }
+}
+// S = acc (transposed when trans); the caller synchronises before and after
+__device__ __forceinline__ void acc_to_lds(double (*S)[NB + 1], const v4d acc[2][2], bool trans) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = acc_row(bi, q), c = acc_col(bj);
+        if (trans)
+          S[c][r] = acc[bi][bj][q];
+        else
+          S[r][c] = acc[bi][bj][q];
+      }
+}
+// the block of dst at (r0, c0) (ld), rows < nr, columns < nc := acc (transposed: dst at (c0, r0) gets
+// element (r, c) at (c, r))
+__device__ __forceinline__ void acc_store(double *dst, int64_t ld, int64_t r0, int64_t c0, int64_t nr, int64_t nc,
+                                          const v4d acc[2][2], bool trans = false) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = acc_row(bi, q), c = acc_col(bj);
+        if (r < nr && c < nc) {
+          if (trans)
+            dst[(c0 + c) * ld + r0 + r] = acc[bi][bj][q];
+          else
+            dst[(r0 + r) * ld + c0 + c] = acc[bi][bj][q];
+        }
+      }
+}
+__device__ __forceinline__ void acc_axpy(v4d y[2][2], double alpha, const v4d x[2][2]) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) y[bi][bj] += alpha * x[bi][bj];
+}
+
+__device__ __forceinline__ void step_tasks(const StepArgs &x, double (*P0)[NB + 1], double (*P1)[NB + 1], double *piv) {
+  const int64_t n = x.n, lda = x.lda;
+  const int k = x.k;
+  const int64_t k0 = (int64_t)k * NB;
+  auto bsize = [n](int b) { return std::min<int64_t>(NB, n - (int64_t)b * NB); };
+  int task = (int)blockIdx.x;
+  TileRegs t0, t1, t2;
+  v4d acc[2][2], acc2[2][2], cc[2][2];
+  if (task < x.nD) {  // D: block d = k + 1
+    const int64_t d0 = k0 + NB, nd = bsize(k + 1);
+    if (k >= 0) {
+      tile_load(t1, x.dinv + k0 * NB, NB, 0, 0, NB, NB, false);  // inv(L_kk), a full block (k + 1 < K)
+      tile_load(t0, x.a, lda, d0, k0, nd, NB, false);            // A_dk
+      acc_load(cc, x.a, lda, d0, d0, nd, nd);                    // A_dd
+      tile_to_lds(P1, t1, false);
+      tile_to_lds(P0, t0, false);
+      __syncthreads();
+      acc_zero(acc);
+      mm_abt(P0, P1, acc);  // L_dk
+      __syncthreads();
+      acc_to_lds(P0, acc, false);
+      __syncthreads();
+      acc_zero(acc);
+      mm_abt(P0, P0, acc);  // L_dk L_dk'
+      __syncthreads();
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int r = acc_row(bi, q), c = acc_col(bj);
+            P0[r][c] = (r < nd && c < nd) ? cc[bi][bj][q] - acc[bi][bj][q] : (r == c ? 1.0 : 0.0);
+          }
+    } else {
+      tile_load(t0, x.a, lda, 0, 0, nd, nd, true);
+      tile_to_lds(P0, t0, false);
+    }
+    for (int e = threadIdx.x; e < NB * NB; e += 256) P1[e / NB][e % NB] = 0.0;
+    __syncthreads();
+    const bool bad = factor_invert_block(P0, P1, piv, (int)nd);
+    for (int e = threadIdx.x; e < nd * NB; e += 256) {
+      const int r2 = e / NB, c2 = e % NB;
+      if (c2 < nd && x.keep_l) x.a[(d0 + r2) * lda + d0 + c2] = P0[r2][c2];
+      x.dinv[(d0 + r2) * NB + c2] = (c2 < nd) ? P1[r2][c2] : 0.0;
+    }
+    if (threadIdx.x < 64) {  // 2 sum log L_jj, one log per lane, fixed shuffle tree
+      double lg = log(piv[threadIdx.x]);
+      for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off);
+      if (threadIdx.x == 0) {
+        *x.logdet += 2.0 * lg;
+        if (bad && *x.info == 0) *x.info = (int)(d0 + 1);
+      }
+    }
+    return;
+  }
+  task -= x.nD;
+  if (task < x.nT1 + x.nT3) {
+    int bi, bj;
+    const bool t1t = task < x.nT1;
+    if (t1t) {  // lower-triangle index t of the trailing blocks, row-major; t = 0 is D's block
+      const int t = task + 1;
+      int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while (i * (i + 1) / 2 > t) --i;
+      while ((i + 1) * (i + 2) / 2 <= t) ++i;
+      bi = k + 1 + i;
+      bj = k + 1 + (t - i * (i + 1) / 2);
+    } else {
+      const int t = task - x.nT1;
+      bi = k + 1 + t / (k + 1);
+      bj = t % (k + 1);
+    }
+    const int64_t i0 = (int64_t)bi * NB, j0 = (int64_t)bj * NB, ni = bsize(bi), nj = bsize(bj);
+    const bool two = !t1t || bj != bi;
+    double *dst = t1t ? x.a : x.linv;
+    const int64_t ldd = t1t ? lda : n;
+    tile_load(t1, x.dinv + k0 * NB, NB, 0, 0, NB, NB, false);  // inv(L_kk) (k < K - 1)
+    tile_load(t0, x.a, lda, i0, k0, ni, NB, false);            // A_ik
+    if (t1t) {
+      if (two) tile_load(t2, x.a, lda, j0, k0, nj, NB, false);  // A_jk
+    } else {
+      tile_load(t2, x.linv, n, k0, j0, NB, nj, false);  // B_kj
+    }
+    acc_load(cc, dst, ldd, i0, j0, ni, nj);  // the tile updated
+    tile_to_lds(P1, t1, false);
+    tile_to_lds(P0, t0, false);
+    __syncthreads();
+    acc_zero(acc);
+    mm_abt(P0, P1, acc);  // L_ik
+    if (two) {
+      __syncthreads();
+      tile_to_lds(P0, t2, !t1t);  // A_jk, or B_kj'
+      __syncthreads();
+      acc_zero(acc2);
+      if (t1t)
+        mm_abt(P0, P1, acc2);  // L_jk = A_jk inv(L_kk)'
+      else
+        mm_abt(P1, P0, acc2);  // X_kj = inv(L_kk) B_kj
+    }
+    __syncthreads();
+    acc_to_lds(P0, acc, false);
+    if (two) acc_to_lds(P1, acc2, !t1t);  // L_jk, or X_kj'
+    __syncthreads();
+    acc_zero(acc);
+    mm_abt(P0, two ? P1 : P0, acc);
+    acc_axpy(cc, -1.0, acc);
+    acc_store(dst, ldd, i0, j0, ni, nj, cc);
+    return;
+  }
+  task -= x.nT1 + x.nT3;
+  if (task < x.nWL + x.nWX) {  // W: block k - 1's panel column and row of X
+    const int64_t p0 = k0 - NB, np = bsize(k - 1);
+    tile_load(t1, x.dinv + p0 * NB, NB, 0, 0, np, np, false);  // inv(L_k-1,k-1)
+    acc_zero(acc);
+    if (task < x.nWL) {  // L_i,k-1 = A_i,k-1 inv(L_k-1,k-1)', i = k + task
+      const int64_t i0 = (int64_t)(k + task) * NB, ni = bsize(k + task);
+      tile_load(t0, x.a, lda, i0, p0, ni, NB, false);
+      tile_to_lds(P1, t1, false);
+      tile_to_lds(P0, t0, false);
+      __syncthreads();
+      mm_abt(P0, P1, acc);
+      acc_store(x.a, lda, i0, p0, ni, NB, acc);
+    } else {  // X_k-1,j = inv(L_k-1,k-1) B_k-1,j
+      const int j = task - x.nWL;
+      const int64_t j0 = (int64_t)j * NB, nj = bsize(j);
+      tile_load(t0, x.linv, n, p0, j0, np, nj, false);
+      tile_to_lds(P1, t1, false);
+      tile_to_lds(P0, t0, true);
+      __syncthreads();
+      mm_abt(P1, P0, acc);
+      acc_store(x.linv, n, p0, j0, np, nj, acc);
+    }
+    return;
+  }
+  task -= x.nWL + x.nWX;
+  {  // T5: V_ab += X_qa' X_qb, q = k - 2, lower-triangle index (a, b) over blocks <= q
+    const int q = k - 2, K = x.K;
+    int a = (int)((sqrt(8.0 * task + 1.0) - 1.0) * 0.5);
+    while (a * (a + 1) / 2 > task) --a;
+    while ((a + 1) * (a + 2) / 2 <= task) ++a;
+    const int b = task - a * (a + 1) / 2;
+    const int64_t q0 = (int64_t)q * NB, a0 = (int64_t)a * NB, b0 = (int64_t)b * NB;
+    const int64_t nq = bsize(q), na = bsize(a), nb = bsize(b);
+    tile_load(t0, x.linv, n, q0, a0, nq, na, false);
+    tile_load(t1, x.linv, n, q0, b0, nq, nb, false);
+    if (q > a)
+      acc_load(cc, x.vinv, n, a0, b0, na, nb);
+    else
+      acc_zero(cc);
+    tile_to_lds(P0, t0, true);
+    tile_to_lds(P1, t1, true);
+    __syncthreads();
+    acc_zero(acc);
+    mm_abt(P0, P1, acc);
+    acc_axpy(cc, 1.0, acc);
+    acc_store(x.vinv, n, a0, b0, na, nb, cc);
+    if (q == K - 1 && a != b) acc_store(x.vinv, n, a0, b0, na, nb, cc, true);
+  }
+}
+
+__global__ __launch_bounds__(256) void chol_step_kernel(StepArgs x) {
+  __shared__ double P0[NB][NB + 1];
+  __shared__ double P1[NB][NB + 1];
+  __shared__ double piv[NB];
+  CHOL_TASK_BEGIN;
+  step_tasks(x, P0, P1, piv);
+  CHOL_TASK_END;
+}
+
+__global__ void identity_kernel(double *p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * n) p[i] = (i / n == i % n) ? 1.0 : 0.0;
+}
+
 __global__ void zero_kernel(double *p, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0.0;
@@ -185,9 +551,56 @@ __global__ void copy_block_kernel(int kb, const double *src, double *dst, int64_
   int r = blockIdx.x, c = threadIdx.x;
   if (r < kb && c < kb) dst[r * ldd + c] = src[r * NB + c];
 }
+
 }  // namespace
 
+// The factorisation, X = L^-1 into linv (n x n) when given and V^-1 = X'X into vinv (n x n, full; needs
+// linv) when given, as K + 2 (+ 1 with vinv) chol_step_kernel launches.
+int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
+                   double *linv, bool keep_l, double *vinv) {
+  GMAT_CHECK(!vinv || linv, GMAT_E_ARG, "cholesky_steps: V^-1 needs L^-1");
+  GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
+  GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
+  if (linv) {
+    hipLaunchKernelGGL(identity_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s, linv, n);
+    GMAT_HIP(hipGetLastError());
+  }
+  const int K = (int)cdiv(n, NB);
+  GMAT_CHECK((int64_t)K * (K + 1) / 2 < (1ll << 31), GMAT_E_ARG, "cholesky_steps: n = %lld", (long long)n);
+  for (int k = -1; k <= K + (vinv ? 1 : 0); ++k) {
+    StepArgs x{};
+    x.n = n;
+    x.lda = lda;
+    x.K = K;
+    x.k = k;
+    x.a = a;
+    x.linv = linv;
+    x.dinv = dinv;
+    x.logdet = logdet_dev;
+    x.info = info_dev;
+    x.vinv = vinv;
+    x.keep_l = keep_l;
+    const int r = K - 1 - k;  // trailing blocks below block k
+    if (k >= 0 && k < K) {
+      x.nT1 = r >= 1 ? r * (r + 1) / 2 - 1 : 0;
+      x.nT3 = linv ? r * (k + 1) : 0;
+    }
+    x.nD = k + 1 < K ? 1 : 0;
+    x.nWL = (k >= 1 && k <= K && keep_l) ? K - k : 0;
+    x.nWX = (k >= 1 && k <= K && linv) ? k : 0;
+    const int q = k - 2;
+    x.nT5 = (vinv && q >= 0 && q < K) ? (q + 1) * (q + 2) / 2 : 0;
+    const int64_t grid = (int64_t)x.nD + x.nT1 + x.nT3 + x.nWL + x.nWX + x.nT5;
+    if (grid == 0) continue;
+    hipLaunchKernelGGL(chol_step_kernel, dim3((unsigned)grid), dim3(256), 0, s, x);
+    GMAT_HIP(hipGetLastError());
+  }
+  return GMAT_OK;
+}
+
 int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev) {
+  static const bool dgemm_path = getenv("GMAT_CHOL_DGEMM") != nullptr;  // the former path, for comparison
+  if (!dgemm_path) return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, nullptr, true, nullptr);
   GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
   GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
   for (int64_t k0 = 0; k0 < n; k0 += NB) {
@@ -208,48 +621,35 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
   return GMAT_OK;
 }
 
-// cholesky() and chol_lower_inverse() overlapped: block row i of L^-1 needs only panel i of L (its
-// diagonal block's inverse and the panel below it, final once the panel solve of step i is done), so
-// the inverse's step i runs on a second stream as soon as that panel is out, beside the factorisation's
-// trailing update and later panels.  Both chains are dozens of small dependent launches that leave most
-// CUs idle; side by side they take about the time of the longer one.  The inverse is computed even if
-// a pivot fails (the caller checks *info_dev).
+// The factorisation and L^-1 (linv, n x n, lower): cholesky_steps; GMAT_CHOL_DGEMM=1 runs the former
+// path for comparison -- cholesky() with the inverse's block steps (chol_lower_inverse) on a second stream,
+// each step as soon as its panel is solved.  The inverse is computed even if a pivot fails (the caller
+// checks *info_dev).
 int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
-                     double *linv) {
-  // Optional look-ahead (GMAT_CHOL_LOOKAHEAD): after panel k is solved, the main stream updates only
-  // block column k + 1 of the trailing matrix ("narrow") and goes on to factor it, while the rest of the trailing update
-  // (block columns k + 2 ..) runs on a third stream; the narrow update of step k + 1 waits for that
-  // rest (both write block column k + 2).  The factorisation's critical path per step becomes potf2 +
-  // panel solve + the narrow update instead of potf2 + panel solve + the whole trailing update.
+                     double *linv, double *vinv) {
+  static const bool dgemm_path = getenv("GMAT_CHOL_DGEMM") != nullptr;
+  if (!dgemm_path) return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, linv, false, vinv);
   static std::mutex mu;
-  static hipStream_t side[64] = {nullptr}, rest_s[64] = {nullptr};
+  static hipStream_t side[64] = {nullptr};
   static std::vector<hipEvent_t> evs[64];
   int dev = 0;
   GMAT_HIP(hipGetDevice(&dev));
   GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_ARG, "cholesky_inverse: device %d", dev);
   std::lock_guard<std::mutex> lock(mu);
   if (!side[dev]) GMAT_HIP(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
-  if (!rest_s[dev]) GMAT_HIP(hipStreamCreateWithFlags(&rest_s[dev], hipStreamNonBlocking));
-  const hipStream_t s2 = side[dev], s3 = rest_s[dev];
+  const hipStream_t s2 = side[dev];
   const int64_t nb = cdiv(n, NB);
-  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done, ev[nb + 2 + i]: rest update i done,
-  // ev[2 nb + 2]: all rest updates done
-  while ((int64_t)evs[dev].size() < 2 * nb + 3) {
+  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done
+  while ((int64_t)evs[dev].size() < nb + 2) {
     hipEvent_t e;
     GMAT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     evs[dev].push_back(e);
   }
   hipEvent_t *ev = evs[dev].data();
-  hipEvent_t *ev_rest = ev + nb + 2;
-  // (one-box A/B at n = 2,000: 2.77 ms per REML iteration with the look-ahead against 2.33 without --
-  // the narrow update is as latency-bound as the whole one and the cross-stream waits add their own;
-  // kept behind GMAT_CHOL_LOOKAHEAD)
-  const bool lookahead = getenv("GMAT_CHOL_LOOKAHEAD") != nullptr;
   GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
   GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
   GMAT_HIP(hipEventRecord(ev[0], s));
   GMAT_HIP(hipStreamWaitEvent(s2, ev[0], 0));  // after the caller's earlier work on s
-  GMAT_HIP(hipStreamWaitEvent(s3, ev[0], 0));
   hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s2, linv, n * n);
   GMAT_HIP(hipGetLastError());
   for (int64_t k0 = 0, i = 0; k0 < n; k0 += NB, ++i) {
@@ -271,28 +671,17 @@ int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *d
     if (rem > 0) {
       GMAT_TRY(dgemm(s2, rem, k0 + kb, kb, -1.0, DView{a + (k0 + kb) * lda + k0, lda, 0}, DView{xi, n, 0}, 1.0,
                      linv + (k0 + kb) * n, n));
-      double *a22 = a + (k0 + kb) * lda + (k0 + kb);
-      const int64_t kb1 = std::min<int64_t>(NB, rem), rest = rem - kb1;
-      if (!lookahead || rest <= 0) {  // A22 -= L21 L21'  (lower tiles), all on the main stream
-        if (i > 0 && lookahead) GMAT_HIP(hipStreamWaitEvent(s, ev_rest[i - 1], 0));
-        GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
-      } else {
-        // rest: block columns k + 2 .. (rows k + 2 ..) on the third stream, after panel k
-        GMAT_HIP(hipStreamWaitEvent(s3, ev[1 + i], 0));
-        GMAT_TRY(dgemm(s3, rest, rest, kb, -1.0, DView{panel + kb1 * lda, lda, 0}, DView{panel + kb1 * lda, lda, 1}, 1.0,
-                       a22 + kb1 * lda + kb1, lda, 1));
-        GMAT_HIP(hipEventRecord(ev_rest[i], s3));
-        // narrow: block column k + 1 (rows k + 1 ..) on the main stream, after the previous rest (which
-        // wrote this block column)
-        if (i > 0) GMAT_HIP(hipStreamWaitEvent(s, ev_rest[i - 1], 0));
-        GMAT_TRY(dgemm(s, rem, kb1, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda));
-      }
+      // A22 -= L21 L21'  (lower tiles)
+      GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a + (k0 + kb) * lda + k0 + kb,
+                     lda, 1));
     }
   }
-  GMAT_HIP(hipEventRecord(ev[2 * nb + 2], s3));
-  GMAT_HIP(hipStreamWaitEvent(s, ev[2 * nb + 2], 0));
   GMAT_HIP(hipEventRecord(ev[nb + 1], s2));
   GMAT_HIP(hipStreamWaitEvent(s, ev[nb + 1], 0));
+  if (vinv) {  // V^-1 = L^-T L^-1 (lower tiles, then mirrored)
+    GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{linv, n, 1}, DView{linv, n, 0}, 0.0, vinv, n, 2));
+    GMAT_TRY(fill_sym_upper(s, n, vinv, n));
+  }
   return GMAT_OK;
 }
 

@@ -35,11 +35,17 @@ int dgemm_i8b(hipStream_t s, int64_t M, int64_t N, int64_t K, double alpha, DVie
 // the diagonal blocks are written to dinv (n x 64 doubles).  *logdet_dev (device double)
 // receives sum(log(diag(L)))*2; *info_dev (device int) > 0 marks a non-positive pivot.
 int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev);
-// cholesky() followed by chol_lower_inverse(l = a) into linv, the inverse's block steps overlapped
-// with the factorisation on a second stream (ordered after the caller's earlier work on s; s waits
-// for both on return).
+// cholesky() and, when linv is given, L^-1 (n x n, lower; upper zero) as one launch per 64-column step
+// (chol.hip chol_step_kernel).  keep_l: L into a's lower triangle (upper unspecified), else a is scratch.
+// vinv (needs linv): V^-1 = L^-T L^-1, n x n, both triangles.
+int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
+                   double *linv, bool keep_l = true, double *vinv = nullptr);
+// L^-1 into linv, optionally A^-1 into vinv (both triangles), log|A| and the pivot check, a used as
+// scratch: cholesky_steps (GMAT_CHOL_DGEMM=1:
+// cholesky() with chol_lower_inverse's block steps on a second stream, L left in a); ordered after the
+// caller's earlier work on s.
 int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
-                     double *linv);
+                     double *linv, double *vinv = nullptr);
 // linv = L^-1 (n x n, lower triangle; the upper triangle is zeroed) from the factor and its
 // diagonal-block inverses.
 int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *linv);

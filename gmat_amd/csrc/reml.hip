@@ -163,8 +163,8 @@ struct Model {
     GMAT_HIP(hipGetLastError());
     double *dl = small.as<double>();
     int *info = reinterpret_cast<int *>(small.as<double>() + 1);
-    // V = LL' with L^-1 built beside the factorisation (work), then V^-1 = L^-T L^-1
-    GMAT_TRY(cholesky_inverse(s, n, v.as<double>(), n, dinv.as<double>(), dl, info, work.as<double>()));
+    // V = LL' with L^-1 (work) and V^-1 = L^-T L^-1 (vi) built beside the factorisation
+    GMAT_TRY(cholesky_inverse(s, n, v.as<double>(), n, dinv.as<double>(), dl, info, work.as<double>(), vi.as<double>()));
     double hdl[2];
     GMAT_HIP(hipMemcpyAsync(hdl, small.p, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
     GMAT_HIP(hipStreamSynchronize(s));
@@ -172,9 +172,6 @@ struct Model {
     memcpy(&hinfo, &hdl[1], sizeof(int));
     GMAT_CHECK(hinfo == 0, GMAT_E_NOTPD, "V is not positive definite (pivot %d)", hinfo);
     if (ll_v) *ll_v = hdl[0];
-    GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{work.as<double>(), n, 1}, DView{work.as<double>(), n, 0}, 0.0, vi.as<double>(), n,
-                   2));
-    GMAT_TRY(fill_sym_upper(s, n, vi.as<double>(), n));
     // VX = V^-1 X ; XVX = X' VX
     GMAT_TRY(dgemm(s, n, p, n, 1.0, DView{vi.as<double>(), n, 0}, DView{x.as<double>(), p, 0}, 0.0, vx.as<double>(), p));
     double *dxvx = small.as<double>() + 8;
@@ -446,14 +443,14 @@ extern "C" int gmat_spd_inverse(int64_t n, const double *a, double *ainv, double
   GMAT_TRY(sm.alloc(2 * sizeof(double)));
   GMAT_HIP(hipMemcpy(da.p, a, n * n * sizeof(double), hipMemcpyHostToDevice));
   int *info = reinterpret_cast<int *>(sm.as<double>() + 1);
-  GMAT_TRY(cholesky(0, n, da.as<double>(), n, dinv.as<double>(), sm.as<double>(), info));
+  GMAT_TRY(cholesky_inverse(0, n, da.as<double>(), n, dinv.as<double>(), sm.as<double>(), info, work.as<double>(),
+                            out.as<double>()));
   double h[2];
   GMAT_HIP(hipMemcpy(h, sm.p, 2 * sizeof(double), hipMemcpyDeviceToHost));
   int hinfo;
   memcpy(&hinfo, &h[1], sizeof(int));
   GMAT_CHECK(hinfo == 0, GMAT_E_NOTPD, "matrix is not positive definite (pivot %d)", hinfo);
   if (logdet) *logdet = h[0];
-  GMAT_TRY(spd_inverse_from_chol(0, n, da.as<double>(), n, dinv.as<double>(), work.as<double>(), out.as<double>()));
   GMAT_HIP(hipMemcpy(ainv, out.p, n * n * sizeof(double), hipMemcpyDeviceToHost));
   return GMAT_OK;
 }
