@@ -412,11 +412,12 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
     scans at p_cut, rows sharded over the ranks like configs[3] (GRM and REML on rank 0).  Each scan:
     one untimed full scan (codings and buffers at the timed size), then `reps` timed scans, median
     reported.  Returns the record on rank 0.
-    The REML does not meet the reference's stopping rule here (gradient norm < 1e-6): on this cohort
-    the likelihood's maximum lies on the boundary (AxA -> 0), so every iteration needs an EM weight
-    > 0 and the gradient norm stalls near 3 even after 3,000 iterations
-    (profiles/round4_cfg5_reml_probe.txt); the reference's loop returns its 200th iterate then, and so
-    does this one (its iterates match the oracle's: tests/test_gpu_cfg5.py)."""
+    The REML does not meet the reference's stopping rule here (gradient norm < 1e-6): the epistatic
+    kernels are near-collinear at this size (asymptotic standard errors 10-48x the simulated AxA / AxD /
+    DxD variances, tools/cfg5_identifiability.py), so the pure AI step leaves the positive orthant and
+    nearly every iteration needs an EM weight > 0; 0 of 48 phenotype draws converge within 200
+    iterations (profiles/round5_cfg5_reml_probe.txt).  The reference's loop returns its 200th iterate
+    then, and so does this one (its iterates match the oracle's: tests/test_gpu_cfg5.py)."""
     import ctypes
     from gmat_amd import dist, synth
     from gmat_amd import _native as N

@@ -2,7 +2,8 @@
 converge on bench.py's cfg5 cohort, and after how many iterations?  For each simulated variance
 vector: iterations, convergence, the estimate, and the gradient / update norms and EM weights along
 the way (gmat_reml_trace).
-    python tools/cfg5_reml_probe.py FAMILY_SIZE MAXITER "0.3,0.1,0.1,0.05,0.05,0.4" ["..."]"""
+    python tools/cfg5_reml_probe.py FAMILY_SIZE MAXITER "0.3,0.1,0.1,0.05,0.05,0.4[@SEEDS]" ["..."]
+SEEDS (e.g. "2-17"): phenotype draws (the bench's is seed + 1 = 2), one REML each."""
 import ctypes
 import json
 import sys
@@ -33,19 +34,26 @@ g.close()
 a, d = mats
 gl = [a, d, a * a, a * d, d * d]
 print("cohort + GRMs %.1f s" % (time.time() - t0), flush=True)
+chol = [np.linalg.cholesky(k + 1e-3 * np.eye(n)) for k in gl]
+print("factors %.1f s" % (time.time() - t0), flush=True)
+runs = []
 for spec in sys.argv[3:]:
-    var = np.array([float(v) for v in spec.split(",")])
-    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    vs, _, seeds = spec.partition("@")
+    lo_hi = [int(v) for v in (seeds or str(seed + 1)).split("-")]
+    for ps in range(lo_hi[0], lo_hi[-1] + 1):
+        runs.append((np.array([float(v) for v in vs.split(",")]), ps))
+for var, ps in runs:
+    rng = np.random.Generator(np.random.PCG64(ps))
     y = np.ones(n)
-    for k, s_ in zip(gl, var[:5]):
-        y += np.sqrt(s_) * (np.linalg.cholesky(k + 1e-3 * np.eye(n)) @ rng.standard_normal(n))
+    for L, s_ in zip(chol, var[:5]):
+        y += np.sqrt(s_) * (L @ rng.standard_normal(n))
     y += np.sqrt(var[5]) * rng.standard_normal(n)
     t1 = time.perf_counter()
     est = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), gl, maxiter=maxiter)
     tr = _wemai_multi_gmat.last_trace
     it = tr.shape[1]
     marks = [k for k in (1, 10, 50, 100, 200, 500, 1000, 2000, 5000) if k <= it] + [it]
-    print(json.dumps({"family_size": fam, "simulated": var.tolist(), "iters": it, "converged": it < maxiter,
+    print(json.dumps({"family_size": fam, "pheno_seed": ps, "simulated": var.tolist(), "iters": it, "converged": it < maxiter,
                       "wall_s": time.perf_counter() - t1, "var": np.round(est, 5).tolist(),
                       "grad_norm_at": {k: float(tr[0, k - 1]) for k in marks},
                       "update_norm_at": {k: float(tr[1, k - 1]) for k in marks},
