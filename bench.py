@@ -370,27 +370,28 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed, geno=None, cpu_budget=10.0):
             "cpu_baseline": cpu}
 
 
-def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), reps=2):
+def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), reps=5):
     """configs[3] rehearsed on one GPU: each part of the multi-GPU split (dist.rank_rows: part k of
     the reference's folded parallel=[N,k] rows, remma_epiAA.py:125-139) timed serially on this GPU
-    -- what one rank of an N-GPU run computes between its barriers.  Reports per-part ms, the
-    max / mean imbalance and the projected N-GPU step (slowest part; the hit gather is a few
-    hundred KB), and checks that the parts' hits add up to the 1-GPU step's."""
+    -- what one rank of an N-GPU run computes between its barriers.  A part is timed as the step is:
+    one untimed scan, then `reps` scans back to back between two device synchronisations, the mean
+    (round 4 took the best of two single scans).  Reports per-part ms, the max / mean imbalance and
+    the projected N-GPU step (slowest part; the hit gather is a few hundred KB), and checks that the
+    parts' hits add up to the 1-GPU step's."""
     from gmat_amd import dist
     out = {}
     for N in ways:
         ms, hits, pairs = [], 0, []
         for k in range(N):
             rows = dist.rank_rows("AA", m, k, N)
-            best = None
+            plan.scan("AA", rows, p_cut)
+            lib.gmat_device_synchronize()
+            t0 = time.perf_counter()
             for _ in range(reps):
-                lib.gmat_device_synchronize()
-                t0 = time.perf_counter()
                 res = plan.scan("AA", rows, p_cut)
-                lib.gmat_device_synchronize()
-                dt = (time.perf_counter() - t0) * 1e3
-                best = dt if best is None else min(best, dt)
-            ms.append(best)
+                plan.stats()  # the step's per-scan bookkeeping
+            lib.gmat_device_synchronize()
+            ms.append((time.perf_counter() - t0) * 1e3 / reps)
             hits += int(res[0].size)
             pairs.append(float(np.sum(m - 1 - rows)))
         mean = float(np.mean(ms))
@@ -654,12 +655,12 @@ def main():
     screen_s = launches = ops = cands = hits = side_s = ref_s = 0.0
     ks, kx = {}, {}
     n_slice = 0
-    for _ in range(args.steps):
+    for it in range(args.steps):
         res = step()
-        for name, v in plan.kernel_stats_ext().items():
-            acc = kx.setdefault(name, {"s": 0.0, "launches": 0.0, "pairs": 0.0})
-            for key in acc:
-                acc[key] += v[key]
+        if it == args.steps - 1:  # the candidate kernels' HIP-event times of the last step (reading them
+            # every step was ~60 us of host time per step; they are scaled to the steps below)
+            for name, v in plan.kernel_stats_ext().items():
+                kx[name] = {key: v[key] * args.steps for key in ("s", "launches", "pairs")}
         st = plan.stats()
         screen_s += st["screen_s"]
         launches += st["launches"]

@@ -248,7 +248,9 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 13 * 1024, PF_NS = 5, PF_NQ = 13;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
 constexpr int PF_CHUNK = 128;  // live-pair records a persistent prefilter wave reserves at a time
-constexpr int PF_NSTAMP = 7;  // GMAT_PF_STAMPS: start, prologue, main loop, column records, tests, stores, end
+constexpr int PF_NSTAMP = 9;  // GMAT_PF_STAMPS: start, prologue, main loop, column records, tests, stores, end
+                               // (s_memrealtime), then s_memtime (shader clock) at start and end
+constexpr int PF_NPHASE = 7;
 // fp4 codes of c^2 from those of c in {0, 1, 2} (0x0, 0x2, 0x4 -> 0x0, 0x2, 0x6): nibble bit 2 -> bit 1
 __device__ __forceinline__ v8i_ sq4(v4i x) {
   v8i_ r = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -926,7 +928,8 @@ struct gmat_epi {
   // scan state
   DBuf cand_i, cand_j, counter, ceff, cvar, cchi, cp;
   DBuf cand2_i, cand2_j, counter2, ps_side;  // pair screen survivors; its per-pair side terms
-  DBuf cpack;                                 // refined candidates packed for the read-back
+  DBuf cpack;                                 // the refined candidates' hits packed for the read-back
+  DBuf hcount;                                // their count (hit_pack_kernel)
   DBuf ps_mpart;                              // pair_mxr_kernel's segment partials
   int64_t cand_cap = 0;
   std::vector<int64_t> hit_i, hit_j;
@@ -1132,8 +1135,8 @@ __global__ void audit_kernel(int64_t n, int64_t n_pad, int R, int ncov, const in
                                                       const double *U, double pf_mu, double pf_tau, double pf_eps,
                                                       double pf_ku, double lr_lam, double lr_tau, double lr_eps,
                                                       double *out);
-__global__ void cand_pack_kernel(int64_t n, const int64_t *ci, const int64_t *cj, const double *eff, const double *var,
-                                 const double *chi, const double *p, double *out);
+__global__ void hit_pack_kernel(int64_t n, const int64_t *ci, const int64_t *cj, const double *eff, const double *var,
+                                const double *chi, const double *p, double p_cut, double *out, unsigned long long *count);
 
 constexpr int AUD_T = 256;  // audit_kernel workgroup (the low-rank rank it serves at most)
 

@@ -119,8 +119,11 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   int r0 = (tile % x.n_rt) * PF_TR;
   int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PF_TC;
   auto pstamp = [&](int k) __attribute__((always_inline)) {  // the workgroup's first tile only
-    if (STAMP && a.pf_stamp && threadIdx.x == 0)
+    if (STAMP && a.pf_stamp && threadIdx.x == 0) {
       a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+      if (k == 0 || k == PF_NPHASE - 1)
+        a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + PF_NPHASE + (k ? 1 : 0)] = __builtin_amdgcn_s_memtime();
+    }
   };
   pstamp(0);
   // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
@@ -515,8 +518,11 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     return t;
   };
   auto pstamp = [&](int st_) __attribute__((always_inline)) {  // GMAT_PF_STAMPS (one tile per workgroup)
-    if (!LIST && a.pf_stamp && threadIdx.x == 0)
+    if (!LIST && a.pf_stamp && threadIdx.x == 0) {
       a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + st_] = __builtin_amdgcn_s_memrealtime();
+      if (st_ == 0 || st_ == PF_NPHASE - 1)
+        a.pf_stamp[PF_NSTAMP * (int64_t)blockIdx.x + PF_NPHASE + (st_ ? 1 : 0)] = __builtin_amdgcn_s_memtime();
+    }
   };
   pstamp(0);
   int tile = tile_at(0);

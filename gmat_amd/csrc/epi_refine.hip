@@ -855,16 +855,27 @@ __global__ __launch_bounds__(256) void hit_compact_kernel(int64_t np, const int6
 // fp64 refine of the survivors, and the hits p < p_cut appended to the plan's lists.  Candidates
 // below hi are free afterwards.
 // [i | j | eff | var | chi | p] of n refined candidates in one buffer (one read-back copy)
-__global__ void cand_pack_kernel(int64_t n, const int64_t *ci, const int64_t *cj, const double *eff, const double *var,
-                                 const double *chi, const double *p, double *out) {
+// the refined candidates with p < p_cut (NaN never passes, as in the reference's res[res[4] < p_cut]) as
+// 48-byte records (i, j, eff, var, chi, p) in any order (the caller sorts by (i, j)); one atomic per wave
+__global__ void hit_pack_kernel(int64_t n, const int64_t *ci, const int64_t *cj, const double *eff, const double *var,
+                                const double *chi, const double *p, double p_cut, double *out,
+                                unsigned long long *count) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n) return;
-  ((int64_t *)out)[k] = ci[k];
-  ((int64_t *)out)[n + k] = cj[k];
-  out[2 * n + k] = eff[k];
-  out[3 * n + k] = var[k];
-  out[4 * n + k] = chi[k];
-  out[5 * n + k] = p[k];
+  const bool hit = k < n && p[k] < p_cut;
+  const unsigned long long bal = __ballot(hit);
+  if (!bal) return;
+  unsigned long long base = 0;
+  if ((threadIdx.x & 63) == __builtin_ctzll(bal)) base = atomicAdd(count, (unsigned long long)__popcll(bal));
+  base = __shfl(base, __builtin_ctzll(bal));
+  if (!hit) return;
+  const unsigned long long r = base + __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+  double *o = out + r * 6;
+  ((int64_t *)o)[0] = ci[k];
+  ((int64_t *)o)[1] = cj[k];
+  o[2] = eff[k];
+  o[3] = var[k];
+  o[4] = chi[k];
+  o[5] = p[k];
 }
 
 

@@ -177,36 +177,44 @@ int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, 
   if (nf > 0) {
     GMAT_TRY(refine(e, st, *c.L, *c.R, c.lp, c.rp, fi, fj, nf, e->ceff.as<double>(), e->cvar.as<double>(),
                     e->cchi.as<double>(), e->cp.as<double>()));
-    GMAT_TRY(pin.reserve((size_t)nf * 48));
-    int64_t *ci = pin.as<int64_t>(), *cj = ci + nf;
-    double *ce = (double *)(cj + nf), *cv = ce + nf, *cc = cv + nf, *cq = cc + nf;
-    // the six candidate arrays packed on the device and read back in one copy (six copies cost ~0.1 ms
-    // of a step: each is a round trip)
+    // the hits (p < p_cut) compacted on the device and read back: their count, then their 48-byte records
+    // (round 4 read back all refined candidates, ~12 MB per configs[2] step, and filtered on the host:
+    // ~0.5 ms of the step between its last kernel and the next scan's first)
     if (e->cpack.bytes < (size_t)nf * 48) {
       GMAT_HIP(hipStreamSynchronize(st));
       GMAT_TRY(e->cpack.alloc((size_t)std::max<int64_t>(nf, 1 << 16) * 48));
     }
-    hipLaunchKernelGGL(cand_pack_kernel, dim3((unsigned)cdiv(nf, 256)), dim3(256), 0, st, nf, fi, fj, e->ceff.as<double>(),
-                       e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>(), e->cpack.as<double>());
+    if (!e->hcount.p) GMAT_TRY(e->hcount.alloc(8));
+    GMAT_TRY(pin.reserve(4096));
+    GMAT_HIP(hipMemsetAsync(e->hcount.p, 0, 8, st));
+    hipLaunchKernelGGL(hit_pack_kernel, dim3((unsigned)cdiv(nf, 256)), dim3(256), 0, st, nf, fi, fj, e->ceff.as<double>(),
+                       e->cvar.as<double>(), e->cchi.as<double>(), e->cp.as<double>(), p_cut, e->cpack.as<double>(),
+                       e->hcount.as<unsigned long long>());
     GMAT_HIP(hipGetLastError());
-    GMAT_HIP(hipMemcpyAsync(ci, e->cpack.p, (size_t)nf * 48, hipMemcpyDeviceToHost, st));
+    GMAT_HIP(hipMemcpyAsync(pin.p, e->hcount.p, 8, hipMemcpyDeviceToHost, st));
     GMAT_HIP(hipEventRecord(end, st));
     GMAT_HIP(hipStreamSynchronize(st));
-    // one bulk copy out of the pinned staging block (element-wise reads of it cost ~50 ns each)
-    std::vector<double> hb((size_t)nf * 6);
-    std::memcpy(hb.data(), ci, (size_t)nf * 48);
-    const int64_t *hi_ = (const int64_t *)hb.data(), *hj_ = hi_ + nf;
-    const double *he_ = hb.data() + 2 * nf, *hv_ = he_ + nf, *hc_ = hv_ + nf, *hq_ = hc_ + nf;
-    (void)ce, (void)cv, (void)cc, (void)cq;
-    for (int64_t k = 0; k < nf; ++k)
-      if (hq_[k] < p_cut) {  // NaN never passes, as in the reference's res[res[4] < p_cut]
-        e->hit_i.push_back(hi_[k]);
-        e->hit_j.push_back(hj_[k]);
-        e->hit_eff.push_back(he_[k]);
-        e->hit_var.push_back(hv_[k]);
-        e->hit_chi.push_back(hc_[k]);
-        e->hit_p.push_back(hq_[k]);
+    const int64_t nh = (int64_t)*pin.as<unsigned long long>();
+    if (nh > 0) {
+      GMAT_TRY(pin.reserve((size_t)nh * 48));
+      GMAT_HIP(hipMemcpyAsync(pin.p, e->cpack.p, (size_t)nh * 48, hipMemcpyDeviceToHost, st));
+      GMAT_HIP(hipStreamSynchronize(st));
+      std::vector<double> hb((size_t)nh * 6);  // one bulk copy out of the pinned block
+      std::memcpy(hb.data(), pin.p, (size_t)nh * 48);
+      const size_t h0 = e->hit_i.size();
+      for (auto *v : {&e->hit_eff, &e->hit_var, &e->hit_chi, &e->hit_p}) v->resize(h0 + nh);
+      e->hit_i.resize(h0 + nh);
+      e->hit_j.resize(h0 + nh);
+      for (int64_t k = 0; k < nh; ++k) {
+        const double *r = &hb[(size_t)k * 6];
+        std::memcpy(&e->hit_i[h0 + k], &r[0], 8);
+        std::memcpy(&e->hit_j[h0 + k], &r[1], 8);
+        e->hit_eff[h0 + k] = r[2];
+        e->hit_var[h0 + k] = r[3];
+        e->hit_chi[h0 + k] = r[4];
+        e->hit_p[h0 + k] = r[5];
       }
+    }
   } else {
     GMAT_HIP(hipEventRecord(end, st));
     GMAT_HIP(hipStreamSynchronize(st));
@@ -217,16 +225,46 @@ int refine_collect(gmat_epi *e, const ScanSide &c, hipStream_t st, bool use_ps, 
   return GMAT_OK;
 }
 
-// hits in (i, j) order, as the reference's row loop emits them
+// hits in (i, j) order, as the reference's row loop emits them: an LSD radix sort (11-bit digits, passes
+// whose digit is the same for every hit skipped) of the keys i m + j with the hits' positions, then the
+// six arrays permuted through a reused scratch block (the comparison sort of the positions took ~0.4 ms
+// of host time per configs[2] step)
 int64_t sort_hits(gmat_epi *e) {
-  std::vector<int64_t> ord(e->hit_i.size());
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
-    return e->hit_i[x] != e->hit_i[y] ? e->hit_i[x] < e->hit_i[y] : e->hit_j[x] < e->hit_j[y];
-  });
+  const size_t n = e->hit_i.size();
+  if (n < 2) return (int64_t)n;
+  thread_local std::vector<uint64_t> key, key2, tmp;
+  thread_local std::vector<uint32_t> pos, pos2;
+  key.resize(n);
+  key2.resize(n);
+  pos.resize(n);
+  pos2.resize(n);
+  tmp.resize(n);
+  const uint64_t mm = (uint64_t)e->m;
+  uint64_t kmax = 0;
+  for (size_t k = 0; k < n; ++k) {
+    key[k] = (uint64_t)e->hit_i[k] * mm + (uint64_t)e->hit_j[k];
+    pos[k] = (uint32_t)k;
+    kmax = std::max(kmax, key[k]);
+  }
+  constexpr int DB = 11, ND = 1 << DB;
+  std::vector<uint32_t> cnt(ND + 1);
+  for (int sh = 0; sh < 64 && (kmax >> sh) != 0; sh += DB) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    for (size_t k = 0; k < n; ++k) ++cnt[((key[k] >> sh) & (ND - 1)) + 1];
+    if (cnt[((key[0] >> sh) & (ND - 1)) + 1] == n) continue;  // one digit value: the pass keeps the order
+    for (int d = 0; d < ND; ++d) cnt[d + 1] += cnt[d];
+    for (size_t k = 0; k < n; ++k) {
+      const uint32_t q = cnt[(key[k] >> sh) & (ND - 1)]++;
+      key2[q] = key[k];
+      pos2[q] = pos[k];
+    }
+    key.swap(key2);
+    pos.swap(pos2);
+  }
   auto apply = [&](auto &v) {
-    auto c2 = v;
-    for (size_t k = 0; k < ord.size(); ++k) v[k] = c2[ord[k]];
+    static_assert(sizeof(v[0]) == 8, "64-bit hit fields");
+    for (size_t k = 0; k < n; ++k) std::memcpy(&tmp[k], &v[pos[k]], 8);
+    std::memcpy(v.data(), tmp.data(), n * 8);
   };
   apply(e->hit_i);
   apply(e->hit_j);
@@ -234,7 +272,7 @@ int64_t sort_hits(gmat_epi *e) {
   apply(e->hit_var);
   apply(e->hit_chi);
   apply(e->hit_p);
-  return (int64_t)e->hit_i.size();
+  return (int64_t)n;
 }
 
 // owner of the events a scan creates
@@ -712,7 +750,9 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // (one-box A/Bs with the 7/8 prefilter grid: 18.25 against 18.41 ms per configs[2] step one launch
   // ahead against two; 3.12 against 3.14-3.19 ms for rank 0's part of an 8-way split)
   const size_t ahead = 1;
+  const double t_setup = now();
   for (size_t li = 0; li < std::min<size_t>(ahead, plan.size()); ++li) GMAT_TRY(enqueue_side(li, (int)li));
+  const double t_enq0 = now();
   for (size_t li = 0; li < plan.size(); ++li) {
     const int b = (int)(li % NBUF);
     const ScanLaunch &ln = plan[li];
@@ -790,6 +830,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     }
   }
   GMAT_HIP(hipStreamSynchronize(sm));
+  const double t_loop = now();
   if (!plan.empty()) {
     const int lb = (int)((plan.size() - 1) % NBUF);
     float ms;
@@ -797,7 +838,12 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     t_screen += ms * 1e-3;
     GMAT_TRY(flush(read_count(lb)));
   }
+  const double t_flush = now();
   *n_hits = sort_hits(e);
+  if (getenv("GMAT_HOST_T"))  // host-side phases of the scan (diagnostics)
+    fprintf(stderr, "scan host: setup %.1f us, first enqueue %.1f, launches %.1f, flush %.1f, sort %.1f (%lld hits)\n",
+            (t_setup - t_start) * 1e6, (t_enq0 - t_setup) * 1e6, (t_loop - t_enq0) * 1e6, (t_flush - t_loop) * 1e6,
+            (now() - t_flush) * 1e6, (long long)*n_hits);
   e->stats[0] = pairs_tested;
   e->stats[1] = tally.n_cand;
   e->stats[2] = ops;
@@ -819,22 +865,24 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   if (pf_st.p && stamp_grid > 0 && stamp_grid <= (1 << 20)) {  // phase times of the stamped launch
     std::vector<unsigned long long> hs((size_t)PF_NSTAMP * stamp_grid);
     GMAT_HIP(hipMemcpy(hs.data(), pf_st.p, hs.size() * 8, hipMemcpyDeviceToHost));
-    double d[PF_NSTAMP - 1] = {0, 0, 0, 0, 0, 0};
+    double d[PF_NPHASE - 1] = {0, 0, 0, 0, 0, 0}, clk = 0.0;
     unsigned long long t_min = ~0ull, t_max = 0;
     int64_t nw = 0;
     for (int64_t g = 0; g < stamp_grid; ++g) {
       const unsigned long long *q = &hs[PF_NSTAMP * g];
-      if (!q[0] || !q[PF_NSTAMP - 1]) continue;  // tiles that exit at once
+      if (!q[0] || !q[PF_NPHASE - 1]) continue;  // tiles that exit at once
       ++nw;
-      for (int k = 0; k + 1 < PF_NSTAMP; ++k) d[k] += (double)(q[k + 1] - q[k]) * 0.01;  // 100 MHz ticks -> us
+      for (int k = 0; k + 1 < PF_NPHASE; ++k) d[k] += (double)(q[k + 1] - q[k]) * 0.01;  // 100 MHz ticks -> us
+      // the shader clock over the tile: s_memtime ticks per s_memrealtime tick (100 MHz)
+      clk += (double)(q[PF_NPHASE + 1] - q[PF_NPHASE]) / (double)std::max<unsigned long long>(q[PF_NPHASE - 1] - q[0], 1) * 0.1;
       t_min = std::min(t_min, q[0]);
-      t_max = std::max(t_max, q[PF_NSTAMP - 1]);
+      t_max = std::max(t_max, q[PF_NPHASE - 1]);
     }
     const double nn = (double)std::max<int64_t>(nw, 1);
     fprintf(stderr, "prefilter launch %zu: %lld tiles run, per tile: prologue %.2f us, main loop %.2f us, epilogue "
-            "%.2f us (column records %.2f, tests %.2f, stores %.2f, masks %.2f); launch span %.1f us\n", stamp_launch,
-            (long long)nw, d[0] / nn, d[1] / nn, (d[2] + d[3] + d[4] + d[5]) / nn, d[2] / nn, d[3] / nn, d[4] / nn,
-            d[5] / nn, (double)(t_max - t_min) * 0.01);
+            "%.2f us (column records %.2f, tests %.2f, stores %.2f, masks %.2f); launch span %.1f us; s_memtime "
+            "clock %.3f GHz\n", stamp_launch, (long long)nw, d[0] / nn, d[1] / nn, (d[2] + d[3] + d[4] + d[5]) / nn,
+            d[2] / nn, d[3] / nn, d[4] / nn, d[5] / nn, (double)(t_max - t_min) * 0.01, clk / nn);
   }
   if (live_cnt.p) {
     unsigned long long lcnt = 0;

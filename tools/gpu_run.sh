@@ -46,6 +46,17 @@ for st in "$@"; do
     quick)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/quick.json 2> $OUT/quick.log || { tail -30 $OUT/quick.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/quick.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
+    hostt)
+      # host-side phases of each scan (GMAT_HOST_T) and the Python time around the calls
+      GMAT_HOST_T=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/hostt.json 2> $OUT/hostt.log || { tail -30 $OUT/hostt.log; exit 1; }
+      grep "scan host" $OUT/hostt.log | tail -4 ;;
+    stamps)
+      # per-tile phase times of one prefilter launch (GMAT_PF_STAMPS: one workgroup per tile, first tile)
+      GMAT_PF_STAMPS=1 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/stamps.json 2> $OUT/stamps.log || { tail -30 $OUT/stamps.log; exit 1; }
+      grep "prefilter launch" $OUT/stamps.log | tail -2
+      # the same launch with every kernel serialised (no co-running screens): clock and phases alone
+      AMD_SERIALIZE_KERNEL=3 GMAT_PF_STAMPS=1 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/stamps_serial.json 2> $OUT/stamps_serial.log || { tail -30 $OUT/stamps_serial.log; exit 1; }
+      grep "prefilter launch" $OUT/stamps_serial.log | tail -1 ;;
     pmc)
       # counter passes of the six scan kernels (one rocprofv3 run per counter group) and their traffic
       # records keyed by the epi stage files' sha256 (bench.py attaches them to roofline.kernels)
