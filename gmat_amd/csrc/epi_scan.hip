@@ -403,13 +403,14 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const int64_t nJ = cdiv(m, BJ);
   auto &B = e->lrc;
   constexpr int NBUF = 3;  // buffer sets: launch L uses set L % 3
-  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least GMAT_LRC_MIN_LAUNCHES (4) launches down to
-  // 512 rows (a rank's part of a multi-GPU split keeps the prefilter-ahead pipeline filled), and no more
+  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least GMAT_LRC_MIN_LAUNCHES (6) launches down to
+  // 512 rows (a rank's part of a multi-GPU split keeps the prefilter-ahead pipeline filled: rank 0's
+  // 8-way part 2.62 ms at 1,024 rows per launch against 2.75 at 1,536, 2.72 at 768, 2.82 at 512), and no more
   // than the three sets' live masks and record bases (8 bytes per (row, 32-column block)) fit in an
   // eighth of the free HBM; GMAT_LRC_ROWS forces it for A/B runs (a multiple of 128, at most 4096)
   int64_t RL = 0;
   {
-    const int64_t min_launches = getenv("GMAT_LRC_MIN_LAUNCHES") ? std::max(1, atoi(getenv("GMAT_LRC_MIN_LAUNCHES"))) : 4;
+    const int64_t min_launches = getenv("GMAT_LRC_MIN_LAUNCHES") ? std::max(1, atoi(getenv("GMAT_LRC_MIN_LAUNCHES"))) : 6;
     RL = getenv("GMAT_LRC_ROWS")
              ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
              : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / min_launches / 128 * 128));

@@ -57,6 +57,10 @@ for st in "$@"; do
       # the same launch with every kernel serialised (no co-running screens): clock and phases alone
       AMD_SERIALIZE_KERNEL=3 GMAT_PF_STAMPS=1 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/stamps_serial.json 2> $OUT/stamps_serial.log || { tail -30 $OUT/stamps_serial.log; exit 1; }
       grep "prefilter launch" $OUT/stamps_serial.log | tail -1 ;;
+    covstamps)
+      # per-tile phase times of one covariate prefilter launch (GMAT_PF_STAMPS, one workgroup per tile)
+      GMAT_PF_STAMPS=1 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --covariates --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/covstamps.json 2> $OUT/covstamps.log || { tail -30 $OUT/covstamps.log; exit 1; }
+      grep "prefilter launch" $OUT/covstamps.log | tail -1 ;;
     pmc)
       # counter passes of the six scan kernels (one rocprofv3 run per counter group) and their traffic
       # records keyed by the epi stage files' sha256 (bench.py attaches them to roofline.kernels)
