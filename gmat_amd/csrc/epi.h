@@ -995,7 +995,7 @@ namespace epi {
 // ---- kernels (defined in the stage files)
 template <int PASS>
 __global__ void side_gemm_kernel(SideArgs x);
-template <bool LIST, bool COMPACT, bool STAMP>
+template <bool LIST, bool COMPACT, bool STAMP, int TR, int NS>
 __global__ void prefilter_pass_kernel(SideArgs x);
 template <int NC, bool LIST>
 __global__ void prefilter_cov_kernel(SideArgs x);

@@ -90,8 +90,18 @@ __global__ __launch_bounds__(256, 2) void side_gemm_kernel(SideArgs x) {
 
 // COMPACT: the compacted low-rank path's output (live masks + one record per live pair at a.ops); else
 // the block-granular path's (flags + E3 and code products of every pair of a live block, dense)
-template <bool LIST, bool COMPACT, bool STAMP>
-__global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
+// TR = 64: 64 x 256 tiles, 8 waves (2 row x 4 column waves), one workgroup per CU; TR = 32: 32 x 256
+// tiles, 4 waves (1 x 4), two workgroups per CU (each SIMD then holds one wave of each of two
+// independent workgroups, whose stage barriers and epilogues fall at different times)
+template <bool LIST, bool COMPACT, bool STAMP, int TR, int NS>
+__global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kernel(SideArgs x) {
+  static_assert(NS == 5 || NS == 6, "prefilter ring depth");
+  static_assert(TR == 64 || TR == 32, "prefilter tile rows");
+  constexpr int NW = TR / 8;  // waves
+  // stage image: int8 L3 slices 0, 1 (TR rows x 64 B each), the rows' 2-bit codes (TR x 16 B, in a
+  // whole 1 KB DMA), the columns' 2-bit codes (256 x 16 B)
+  constexpr int O_R8 = 0, O_R8S = TR * 64, O_R4 = 2 * TR * 64, O_C4 = O_R4 + 1024, ST = O_C4 + PF_TC * 16;
+  static_assert(TR != 64 || (ST == PF_ST && O_C4 == 9216), "prefilter stage image");
   const ScreenArgs &a = x.a;
   // The workgroup's tiles.  With a tile list (the launch's running tiles), XCD x (workgroup b runs on
   // XCD b mod 8) takes the list's x-th eighth and its G workgroups stride through it: a persistent
@@ -108,7 +118,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     if (i > 0) return -1;
     const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8;
     const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + kw;
-    const int tr0 = (t % x.n_rt) * PF_TR;
+    const int tr0 = (t % x.n_rt) * TR;
     const int64_t tc0 = (a.j_lo / 32) * 32 + (int64_t)(t / x.n_rt) * PF_TC;
     if (tr0 >= a.n_rows || tc0 >= a.m) return -1;
     if (a.tri && tc0 + PF_TC - 1 <= a.rows[tr0]) return -1;  // rows ascend within a launch
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
   };
   int it = 0, tile = tile_at(0);
   if (tile < 0) return;
-  int r0 = (tile % x.n_rt) * PF_TR;
+  int r0 = (tile % x.n_rt) * TR;
   int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PF_TC;
   auto pstamp = [&](int k) __attribute__((always_inline)) {  // the workgroup's first tile only
     if (STAMP && a.pf_stamp && threadIdx.x == 0) {
@@ -126,84 +136,92 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
   };
   pstamp(0);
-  // 8 waves: wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
+  // wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wr = w >> 2, wc = w & 3;  // wave-uniform (SGPR)
-  constexpr int O_R8 = 0, O_R8S = 4096, O_R4 = 8192, O_C4 = 9216;
-  static_assert(O_C4 + PF_TC * 16 == PF_ST && PF_ST == 1024 * PF_NQ, "prefilter stage image");
-  const int nq = w + 8 < PF_NQ ? 2 : 1;  // stage DMAs of this wave (q = w, w + 8)
-  __shared__ __attribute__((aligned(16))) uint8_t ring[PF_NS][PF_ST];
+  // stage DMAs of this wave: TR = 64: q = w, w + 8 (waves 0-4 two, 5-7 one; q 8 the rows' codes);
+  // TR = 32: the L3 piece w, the columns 64 w .., and wave 0 the rows' codes
+  const int nq = TR == 64 ? (w + 8 < PF_NQ ? 2 : 1) : (w == 0 ? 3 : 2);
+  __shared__ __attribute__((aligned(16))) uint8_t ring[NS][ST];
   // stage-blocked panels: a stage's 64-byte / 16-byte pieces of consecutive SNPs are contiguous, so
   // an instruction's 1 KB comes from 8 whole 128-byte lines (int8 pieces in the even / odd
   // individual order of i8x2_of_fp4_eo).  Sources: a wave-uniform base per instruction (the panel's
   // stage st, SGPRs) + a 32-bit lane offset
   constexpr int64_t rstride = SG_K, cstride = SG_K / 4;
-  const uint8_t *sbase0 = (const uint8_t *)x.rs[w >> 2];           // q = w: L3 slice w / 4
-  const uint8_t *sbase1 = w == 0 ? x.rs2 : x.cs2;                  // q = w + 8: codes
+  constexpr int RQ = TR / 16;                                      // L3 DMAs per slice
+  const uint8_t *sbase0 = (const uint8_t *)x.rs[w / RQ];           // q = w: L3 slice w / RQ
+  const uint8_t *sbase1 = (TR == 64 && w == 0) ? x.rs2 : x.cs2;    // TR = 64, q = w + 8: codes
   const int64_t sstep0 = a.m * SG_K, sstep1 = a.m * cstride;
-  unsigned voff[2];
+  unsigned voff[3];
   auto set_src = [&](int r0, int64_t c0) __attribute__((always_inline)) {
-    {  // int8 L3 slices: 16 rows x 4 chunks per instruction (q 0..3 slice 0, 4..7 slice 1)
-      const int row = (w & 3) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
+    {  // int8 L3 slices: 16 rows x 4 chunks per instruction
+      const int row = (w % RQ) * 16 + (lane >> 2), lg = (lane & 3) ^ ((row >> 2) & 3);
       voff[0] = (unsigned)(a.rows[min(r0 + row, a.n_rows - 1)] * rstride + 16 * lg);
     }
-    if (w == 0)  // q 8: 2-bit codes of the 64 rows, one per lane
-      voff[1] = (unsigned)(a.rows[min(r0 + lane, a.n_rows - 1)] * cstride);
-    else  // q 9..12: 2-bit codes of 64 columns per instruction
-      voff[1] = (unsigned)(min(c0 + 64 * (w - 1) + lane, a.m - 1) * cstride);
+    if (TR == 64) {
+      if (w == 0)  // q 8: 2-bit codes of the 64 rows, one per lane
+        voff[1] = (unsigned)(a.rows[min(r0 + lane, a.n_rows - 1)] * cstride);
+      else  // q 9..12: 2-bit codes of 64 columns per instruction
+        voff[1] = (unsigned)(min(c0 + 64 * (w - 1) + lane, a.m - 1) * cstride);
+    } else {
+      voff[1] = (unsigned)(min(c0 + 64 * w + lane, a.m - 1) * cstride);
+      if (w == 0)  // the 32 rows' codes, twice (lanes 32-63 fill the unused half of the 1 KB)
+        voff[2] = (unsigned)(a.rows[min(r0 + (lane & 31), a.n_rows - 1)] * cstride);
+    }
   };
   set_src(r0, c0);
   typedef __attribute__((address_space(3))) const void *lds_ct;
-  const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
-  // stage st into ring slot `slot` (= st % PF_NS, kept by the caller)
+  const unsigned ring_b = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]);
+  const unsigned ring_m0 = ring_b + w * 1024;
+  // stage st into ring slot `slot` (= st % NS, kept by the caller)
   auto issue = [&](int st, int slot) __attribute__((always_inline)) {
-    lds_dma16_sv(voff[0], sbase0 + st * sstep0, ring_m0 + slot * PF_ST);
-    if (nq == 2) lds_dma16_sv(voff[1], sbase1 + st * sstep1, ring_m0 + slot * PF_ST + 8 * 1024);
+    lds_dma16_sv(voff[0], sbase0 + st * sstep0, ring_m0 + slot * ST);
+    if (TR == 64) {
+      if (nq == 2) lds_dma16_sv(voff[1], sbase1 + st * sstep1, ring_m0 + slot * ST + 8 * 1024);
+    } else {
+      lds_dma16_sv(voff[1], x.cs2 + st * sstep1, ring_b + slot * ST + O_C4 + w * 1024);
+      if (w == 0) lds_dma16_sv(voff[2], x.rs2 + st * sstep1, ring_b + slot * ST + O_R4);
+    }
   };
   // wait until stage `st` has landed given the stages issued up to `last` (nq DMAs per stage), then
   // the workgroup barrier, in ONE asm statement: the compiler does not know that the DMA asm writes
   // LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist the next
   // stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations retire in order
   // (they do on gfx9 for loads).  (The record DMAs are older than any stage.)
-  static_assert(PF_NS == 5, "wait_for's vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
-    const int ahead = last - st;
-    if (nq == 2) {
-      if (ahead >= 3)
-        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (ahead == 2)
-        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (ahead == 1)
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      if (ahead >= 3)
-        asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (ahead == 2)
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (ahead == 1)
-        asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int ahead = min(last - st, NS - 2);
+    switch (nq * ahead) {
+      case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
     }
   };
   v16i acc[2][E3_PF];
   v16f_ acc4[2][4];  // per column block: a.b, a^2.b, a.b^2, a^2.b^2
   const int S = (int)(x.n_pad / SG_K);
-  const int pre = min(S, PF_NS - 1);
+  const int pre = min(S, NS - 1);
   // the epilogue's test records (32 B per row / column) by LDS-DMA ahead of the stages: wave w the
   // 32 columns 32 w .., waves 0 and 1 also the 32 rows 32 w ..; lane l half l & 1 of record l / 2.
   // They retire before stage 0 (in-order vmcnt), so the stage waits cover them.
   // Two record buffers: the next tile's land while the current tile's epilogue reads its own.
-  __shared__ __attribute__((aligned(16))) float rec[2][PF_TR + PF_TC][PF_REC];
+  __shared__ __attribute__((aligned(16))) float rec[2][TR + PF_TC][PF_REC];
   // COMPACT: per wave, lane (b, h)'s live-column mask and first record (the epilogue's store table)
-  __shared__ uint2 ptab[COMPACT ? 8 : 1][64];
+  __shared__ uint2 ptab[COMPACT ? NW : 1][64];
   auto issue_rec = [&](int r0, int64_t c0, int rb) __attribute__((always_inline)) {
     const int k = 32 * w + (lane >> 1);
-    if (w < PF_TR / 32)
+    if (w < TR / 32)
       lds_dma16(x.recL + a.rows[min(r0 + k, a.n_rows - 1)] * PF_REC + 4 * (lane & 1), &rec[rb][32 * w][0]);
-    lds_dma16(x.recR + min(c0 + k, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[rb][PF_TR + 32 * w][0]);
+#pragma unroll
+    for (int u = 0; u < PF_TC / 32 / NW; ++u) {  // wave w: the columns 32 (w + NW u) ..
+      const int kc = 32 * (w + NW * u) + (lane >> 1);
+      lds_dma16(x.recR + min(c0 + kc, a.m - 1) * PF_REC + 4 * (lane & 1), &rec[rb][TR + 32 * (w + NW * u)][0]);
+    }
   };
   issue_rec(r0, c0, 0);
   for (int st = 0; st < pre; ++st) issue(st, st);
@@ -238,13 +256,13 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     }
     // (two stages per barrier, a six-slot ring, measured slower: 11.7 against 11.0 ms of prefilter per
     // configs[2] step, serialised)
-    int slot = 0, slot_ahead = PF_NS - 1;  // ring slots of stage st and of stage st + 4
+    int slot = 0, slot_ahead = NS - 1;  // ring slots of stage st and of stage st + NS - 1
     for (int st = 0; st < S; ++st) {
       const uint8_t *bf = ring[slot];
       // slot (st + 4) % 5 was read in stage st - 1, which every wave has left (barrier)
-      if (st + PF_NS - 1 < S) issue(st + PF_NS - 1, slot_ahead);
-      slot = slot == PF_NS - 1 ? 0 : slot + 1;
-      slot_ahead = slot_ahead == PF_NS - 1 ? 0 : slot_ahead + 1;
+      if (st + NS - 1 < S) issue(st + NS - 1, slot_ahead);
+      slot = slot == NS - 1 ? 0 : slot + 1;
+      slot_ahead = slot_ahead == NS - 1 ? 0 : slot_ahead + 1;
       // lane (c, h) holds the fp4 codes of individuals 32h .. 32h + 31 of the stage; the int8 E3
       // product kk sums individuals 32h + 16kk .. + 15 (A side: logical int8 chunk 2h + kk)
       v4i rb4[2];
@@ -279,14 +297,14 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
             acc4[q][p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[q][p], 4, 4, 0, 127, 0, 127);
         }
       }
-      wait_for(st + 1, min(st + PF_NS - 1, S - 1));
+      wait_for(st + 1, min(st + NS - 1, S - 1));
     }
     pstamp(2);
     // every wave has passed the last stage's barrier (its vmcnt(0) wait): the ring is free, so the
     // next tile's records and first stages go out now and land while this tile's epilogue runs
     const int nxt = tile_at(it + 1);
     if (nxt >= 0) {
-      const int nr0 = (nxt % x.n_rt) * PF_TR;
+      const int nr0 = (nxt % x.n_rt) * TR;
       const int64_t nc0 = (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PF_TC;
       set_src(nr0, nc0);
       issue_rec(nr0, nc0, rb ^ 1);
@@ -321,7 +339,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
       const int cl = 64 * wc + 32 * q + c;
       jq[q] = (int)(c0 + cl);
       // beta, csum, C1n, n beta - csum | beta spy - sb, sum_k (b + beta)^2, monomorphic
-      const float4 cv0 = rv[2 * (PF_TR + cl)], cv1 = rv[2 * (PF_TR + cl) + 1];
+      const float4 cv0 = rv[2 * (TR + cl)], cv1 = rv[2 * (TR + cl) + 1];
       cbe[q] = cv0.x;
       ccb[q] = cv0.y;
       cC1n[q] = cv0.z;
@@ -486,7 +504,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_pass_kernel(SideArgs x) {
     if (STAMP && a.pf_stamp) __syncthreads();  // the phase stamps time the slowest wave
     pstamp(6);
     if (nxt < 0) break;
-    r0 = (nxt % x.n_rt) * PF_TR;
+    r0 = (nxt % x.n_rt) * TR;
     c0 = (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PF_TC;
     set_src(r0, c0);  // again: the source addresses stay out of the epilogue's registers
   }
@@ -799,9 +817,11 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
 template __global__ void side_gemm_kernel<2>(SideArgs);
 template __global__ void side_gemm_kernel<3>(SideArgs);
 template __global__ void side_gemm_kernel<4>(SideArgs);
-template __global__ void prefilter_pass_kernel<true, true, false>(SideArgs);
-template __global__ void prefilter_pass_kernel<true, true, true>(SideArgs);
-template __global__ void prefilter_pass_kernel<false, false, false>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, false, 64, PF_NS>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, true, 64, PF_NS>(SideArgs);
+template __global__ void prefilter_pass_kernel<false, false, false, 64, PF_NS>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, false, 32, 5>(SideArgs);
+template __global__ void prefilter_pass_kernel<true, true, true, 32, 5>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, true>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, false>(SideArgs);
 template __global__ void prefilter_cov_kernel<2, true>(SideArgs);

@@ -484,7 +484,14 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // by default 7/8 of the CUs (28 of an XCD's 32): the slot lists and the low-rank screens of the
   // launches before run on the rest instead of waiting for a whole prefilter launch (one-box A/Bs,
   // configs[2]: 18.4 against 19.2 ms per step at 224 against 256 workgroups; 240 and 232 were slower)
-  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : std::max(8, e->n_cu * 7 / 8);
+  // 32 x 256 tiles of four waves, two workgroups on every CU (GMAT_PF_TR=64: 64 x 256 tiles of eight
+  // waves on 7/8 of the CUs, one per CU; configs[2] one-box A/B: 16.7-16.9 against 17.7 ms per step,
+  // and 17.0-17.4 ms for the 32-row tiles on 7/8 of the CUs, 16.6-17.1 on 480 workgroups)
+  const int pf_tr = getenv("GMAT_PF_TR") && atoi(getenv("GMAT_PF_TR")) == 64 ? 64 : 32;
+  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG")))
+                                         : std::max(8, pf_tr == 32 ? 2 * e->n_cu : e->n_cu * 7 / 8);
+  // (a six-slot ring for the 32-row tiles measured 16.9-17.0 against 16.8 ms per step)
+  const int pf_rg = getenv("GMAT_PF_RG") ? std::max(1, atoi(getenv("GMAT_PF_RG"))) : 4 * PF_TR / pf_tr;
   if (getenv("GMAT_PF_STAMPS")) {
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
@@ -608,7 +615,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       for (int t = 0; t < E3_PF; ++t) x.rs[t] = (const int8_t *)L.L3b.as<uint8_t>() + t * ss;
       x.rs2 = L.p2b.as<uint8_t>();
       x.cs2 = R.p2b.as<uint8_t>();
-      x.n_rt = (int)cdiv(Rn, PF_TR);
+      x.n_rt = (int)cdiv(Rn, pf_tr);
       // the tiles that run (a tile entirely left of the diagonal has no pair), in tile order
       // rt + n_rt ct; MFMA work per pair: 4 fp4 code products + 2 int8 E3 slices over n_pad
       // individuals = 16 n_pad fp4-equivalent ops
@@ -617,18 +624,19 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       const int64_t n_ct = cdiv(ncols, PF_TC);
       auto runs = [&](int rt, int64_t ct) {
         const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PF_TC;
-        return c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * PF_TR]);
+        return c0 < m && !(tri && c0 + PF_TC - 1 <= ln.rows[rt * pf_tr]);
       };
       // blocks of 4 row tiles x 8 column tiles (the 32 workgroups of an XCD run one block at a time:
       // 4 row and 8 column panels per stage instead of 32 + 1), blocks of a row group consecutive
       // (its rows stay in L2 while the columns stream), row groups dealt to the XCDs in eighths
       // (round 3 A/B: 23.8 against 24.2 ms per configs[2] step for the column-tile-major list)
-      for (int rg = 0; rg < x.n_rt; rg += 4)
+      const int rgs = pf_rg;  // row tiles per block (default 256 rows)
+      for (int rg = 0; rg < x.n_rt; rg += rgs)
         for (int64_t cg = 0; cg < n_ct; cg += 8)
           for (int64_t ct = cg; ct < std::min(n_ct, cg + 8); ++ct)
-            for (int rt = rg; rt < std::min(x.n_rt, rg + 4); ++rt)
+            for (int rt = rg; rt < std::min(x.n_rt, rg + rgs); ++rt)
               if (runs(rt, ct)) tl[run++] = rt + x.n_rt * (int)ct;
-      pf_ops_of[li] = (double)run * PF_TR * PF_TC * 16.0 * (double)n_pad;
+      pf_ops_of[li] = (double)run * pf_tr * PF_TC * 16.0 * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
       // persistent grid over the list: one workgroup per CU (a multiple of 8).  (Same-box A/B: 27.6
       // against 27.7 ms per configs[2] step for as few workgroups as finish in the same number of
@@ -640,10 +648,17 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       const int g = 8 * (int)(pf_list ? std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8)) : cdiv(run, 8));
       if (!pf_list && li == stamp_launch) stamp_grid = g;
       if (run > 0) {
-        if (x.a.pf_stamp)  // the phase-stamped build (GMAT_PF_STAMPS)
-          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true>), dim3((unsigned)g), dim3(512), 0, S2, x);
-        else
-          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false>), dim3((unsigned)g), dim3(512), 0, S2, x);
+        if (pf_tr == 32) {
+          if (x.a.pf_stamp)  // the phase-stamped build (GMAT_PF_STAMPS)
+            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
+          else
+            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
+        } else {
+          if (x.a.pf_stamp)
+            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true, 64, PF_NS>), dim3((unsigned)g), dim3(512), 0, S2, x);
+          else
+            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false, 64, PF_NS>), dim3((unsigned)g), dim3(512), 0, S2, x);
+        }
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
@@ -1148,7 +1163,7 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.cs2 = R.p2b.as<uint8_t>();
         xp.n_rt = (int)cdiv(Rn, PF_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PF_TC));
-        hipLaunchKernelGGL((prefilter_pass_kernel<false, false, false>), dim3(gp), dim3(512), 0, S2, xp);
+        hipLaunchKernelGGL((prefilter_pass_kernel<false, false, false, PF_TR, PF_NS>), dim3(gp), dim3(512), 0, S2, xp);
       } else {  // covariate designs: 64 x 128 tiles with the direction products
         SideArgs xp = x;
         xp.qimg = e->pf_q.as<uint8_t>();
