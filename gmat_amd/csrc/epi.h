@@ -244,7 +244,9 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 // fp4 codes (fp4_of_code2: two VALU per dword), their squares (sq4) and the int8 b of the E3 products
 // (i8x2_of_fp4_eo) come from them in registers.  The int8 16-byte chunks XOR-swizzled through the
 // DMA source address (chunk ^ (row >> 2) & 3); the image holds DMA instruction q (1 KB) at q KB, wave w
-// issuing q = w + 8u (u < 2; waves 0-4 two, 5-7 one).
+// issuing q = w + 8u (u < 2; waves 0-4 two, 5-7 one).  Round 5: by default 32 x 256 tiles of four
+// waves (1 row x 4 column waves, a 9 KB stage), two workgroups per CU (prefilter_pass_kernel<.., 32, 5>);
+// the constants below are the 64-row shape's (GMAT_PF_TR=64, the block-granular path).
 constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 13 * 1024, PF_NS = 5, PF_NQ = 13;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
 constexpr int PF_CHUNK = 128;  // live-pair records a persistent prefilter wave reserves at a time
@@ -321,12 +323,15 @@ __device__ __forceinline__ void lds_dma16_m0(const void *g, unsigned m0) {
 // while stage s multiplies.  Eight-slot ring: stage s + 7 streams while stage s multiplies (stages up
 // to s + 2 have landed at its closing barrier, five more in flight: the loop is bound by the latency of
 // the LDS-DMA stream as much as by its rate).
+// Round 5: by default 32 x 128 tiles of four waves, two workgroups per CU (TC = 128: b's codes at q 5-6,
+// the q slices at q 7; a seven-slot ring), as the intercept-only prefilter's 32-row tiles.
 constexpr int PC_TR = 32, PC_TC = 256, PC_NS = 8, PF_NCOV_MAX = 4;
-template <int NC>
+template <int NC, int TC = PC_TC>
 struct PcShape {
-  static constexpr int O_A2 = 4096, O_B2 = 5120, O_Q = 9216;
-  static constexpr int QT = 10;                        // DMA instructions per stage
-  static constexpr int ST = 10240;                     // slot bytes
+  static constexpr int O_A2 = 4096, O_B2 = 5120, O_Q = O_B2 + TC * 16;
+  static constexpr int QT = 6 + TC / 64;               // DMA instructions per stage
+  static constexpr int ST = O_Q + 1024;                // slot bytes
+  static constexpr int NS = TC == PC_TC ? PC_NS : 7;   // ring slots
 };
 // s_waitcnt vmcnt(n) lgkmcnt(0) + s_barrier as ONE asm statement (see prefilter_pass_kernel)
 __device__ __forceinline__ void vm_wait_barrier(int n) {
@@ -997,7 +1002,7 @@ template <int PASS>
 __global__ void side_gemm_kernel(SideArgs x);
 template <bool LIST, bool COMPACT, bool STAMP, int TR, int NS>
 __global__ void prefilter_pass_kernel(SideArgs x);
-template <int NC, bool LIST>
+template <int NC, bool LIST, int TC>
 __global__ void prefilter_cov_kernel(SideArgs x);
 template <int SH>
 __global__ void screen_kernel(ScreenArgs a);

@@ -188,11 +188,26 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
   // LDS, and the barrier builtin is no memory fence, so a separate builtin would let it hoist the next
   // stage's ds_reads above the barrier.  The counted vmcnt assumes that VMEM operations retire in order
   // (they do on gfx9 for loads).  (The record DMAs are older than any stage.)
+  // The steady state (NS - 2 stages younger than st in flight) tests one wave-uniform condition; the
+  // generic chain of cases (a dozen scalar compares and branches per stage) only runs at a tile's end.
+  static_assert(NS == 5, "wait_for's steady-state vmcnt values");
   auto wait_for = [&](int st, int last) __attribute__((always_inline)) {
     const int ahead = min(last - st, NS - 2);
+    if (ahead == NS - 2) {
+      if (nq == (TR == 64 ? 2 : 3)) {
+        if (TR == 64)
+          asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        if (TR == 64)
+          asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      return;
+    }
     switch (nq * ahead) {
-      case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-      case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
       case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
       case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
       case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
@@ -513,10 +528,11 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
 // LIST: a persistent grid over the launch's tile list (as prefilter_pass_kernel<true>: XCD x takes the
 // list's x-th eighth, its workgroups stride through it, and the next tile's first stages stream into
 // the ring while this tile's epilogue runs); else one workgroup per tile of the XCD-aware remap.
-template <int NC, bool LIST>
-__global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
-  using SH = PcShape<NC>;
-  constexpr int NW = 8;
+template <int NC, bool LIST, int TC>
+__global__ __launch_bounds__(TC * 2, TC == PC_TC ? 1 : 2) void prefilter_cov_kernel(SideArgs x) {
+  static_assert(TC == 256 || TC == 128, "covariate prefilter tile columns");
+  using SH = PcShape<NC, TC>;
+  constexpr int NW = TC / 32, NS = SH::NS, NCQ = 5 + TC / 64;  // waves, ring slots, first q-slice DMA
   const ScreenArgs &a = x.a;
   const int xcd = (int)blockIdx.x % 8, kw = (int)blockIdx.x / 8, G = (int)gridDim.x / 8;
   const int l_lo = LIST ? (int)(((int64_t)x.n_list * xcd) / 8) : 0;
@@ -530,9 +546,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     const int nwg = (int)gridDim.x, xq = nwg / 8, xr = nwg % 8;
     const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + kw;
     const int r0_ = (t % x.n_rt) * PC_TR;
-    const int64_t c0_ = (a.j_lo / 32) * 32 + (int64_t)(t / x.n_rt) * PC_TC;
+    const int64_t c0_ = (a.j_lo / 32) * 32 + (int64_t)(t / x.n_rt) * TC;
     if (r0_ >= a.n_rows || c0_ >= a.m) return -1;
-    if (a.tri && c0_ + PC_TC - 1 <= a.rows[r0_]) return -1;  // rows ascend within a launch
+    if (a.tri && c0_ + TC - 1 <= a.rows[r0_]) return -1;  // rows ascend within a launch
     return t;
   };
   auto pstamp = [&](int st_) __attribute__((always_inline)) {  // GMAT_PF_STAMPS (one tile per workgroup)
@@ -545,19 +561,19 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   pstamp(0);
   int tile = tile_at(0);
   if (tile < 0) return;
-  // 8 waves at two per SIMD: wave w = the tile's 32 rows x columns 32 w .. +32
+  // NW waves (two per SIMD: one workgroup of 8 or two of 4): wave w = the tile's 32 rows x columns 32 w .. +32
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
             c = lane & 31;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[PC_NS][SH::ST];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[NS][SH::ST];
   __shared__ __attribute__((aligned(16))) uint8_t img[2][NC][2048];  // direction images, stages s % 2
-  // DMA instruction q = w + 8u (u < 2): a wave-uniform base per instruction (the panel at stage st,
+  // DMA instruction q = w + NW u (u < 2): a wave-uniform base per instruction (the panel at stage st,
   // SGPRs) + a 32-bit lane offset
   const int nq = (w + NW < SH::QT) ? 2 : 1;  // DMA instructions this wave issues per stage
   auto base_of = [&](int q) __attribute__((always_inline)) -> const uint8_t * {
-    return q < 4 ? (const uint8_t *)x.rs[q >> 1] : q == 4 ? x.rs2 : q < 9 ? x.cs2 : x.qimg;
+    return q < 4 ? (const uint8_t *)x.rs[q >> 1] : q == 4 ? x.rs2 : q < NCQ ? x.cs2 : x.qimg;
   };
   auto step_of = [&](int q) __attribute__((always_inline)) -> int64_t {
-    return q < 4 ? (int64_t)SG_K * a.m : q < 9 ? (int64_t)(SG_K / 4) * a.m : (int64_t)SG_K;
+    return q < 4 ? (int64_t)SG_K * a.m : q < NCQ ? (int64_t)(SG_K / 4) * a.m : (int64_t)SG_K;
   };
   const uint8_t *sbase0 = base_of(w), *sbase1 = base_of(w + NW);
   const int64_t sstep0 = step_of(w), sstep1 = step_of(w + NW);
@@ -571,7 +587,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
         voff[u] = (unsigned)(a.rows[min(r0 + row, a.n_rows - 1)] * SG_K + 16 * lg);
       } else if (q == 4) {  // 2-bit codes of the 32 rows (lanes 32-63: a copy)
         voff[u] = (unsigned)(a.rows[min(r0 + (lane & 31), a.n_rows - 1)] * (SG_K / 4));
-      } else if (q < 9) {  // 2-bit codes of 64 columns per instruction
+      } else if (q < NCQ) {  // 2-bit codes of 64 columns per instruction
         voff[u] = (unsigned)(min(c0 + 64 * (q - 5) + lane, a.m - 1) * (SG_K / 4));
       } else {  // the q slices: lane l = direction min(l / 4, NC - 1), chunk l % 4
         voff[u] = (unsigned)(min(lane >> 2, NC - 1) * x.n_pad + 16 * (lane & 3));
@@ -581,16 +597,17 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   typedef __attribute__((address_space(3))) const void *lds_ct;
   const unsigned ring_m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0][0]) + w * 1024;
   auto issue = [&](int st) __attribute__((always_inline)) {
-    const unsigned m0 = ring_m0 + (st % PC_NS) * SH::ST;
+    const unsigned m0 = ring_m0 + (st % NS) * SH::ST;
     lds_dma16_sv(voff[0], sbase0 + st * sstep0, m0);
     if (nq == 2) lds_dma16_sv(voff[1], sbase1 + st * sstep1, m0 + NW * 1024);
   };
   // the direction images of stage st (its codes and q slices have landed): thread t < 128 NC forms
   // direction t / 128, row (t / 4) % 32, 16-individual chunk t % 4
   auto image = [&](int st) __attribute__((always_inline)) {
-    if (tid < 128 * NC) {
-      uint8_t *sl = ring[st % PC_NS];
-      const int k = tid >> 7, row = (tid >> 2) & 31, ch = tid & 3;
+#pragma unroll
+    for (int t = tid; t < 128 * NC; t += 64 * NW) {
+      uint8_t *sl = ring[st % NS];
+      const int k = t >> 7, row = (t >> 2) & 31, ch = t & 3;
       const unsigned cw = *(const unsigned *)(sl + SH::O_A2 + row * 16 + 4 * ch);  // 16 individuals, 2 bits each
       const v4i qv = *(const v4i *)(sl + SH::O_Q + 64 * k + 16 * ch);
       *(v4i *)(&img[st & 1][k][row * 64 + 16 * (ch ^ ((row >> 2) & 3))]) =
@@ -598,9 +615,9 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
     }
   };
   const int S = (int)(x.n_pad / SG_K);
-  const int pre = min(S, PC_NS - 1);
+  const int pre = min(S, NS - 1);
   int r0 = (tile % x.n_rt) * PC_TR;
-  int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PC_TC;
+  int64_t c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * TC;
   set_src(r0, c0);
   for (int st = 0; st < pre; ++st) issue(st);
   unsigned ch_cur = 0u, ch_end = 0u;  // LIST: record chunks (prefilter_pass_kernel)
@@ -626,8 +643,8 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   const int rrow = c;
   const int crow = 32 * w + c;
   for (int st = 0; st < S; ++st) {
-    const uint8_t *bf = ring[st % PC_NS];
-    if (st + PC_NS - 1 < S) issue(st + PC_NS - 1);
+    const uint8_t *bf = ring[st % NS];
+    if (st + NS - 1 < S) issue(st + NS - 1);
     if (st + 1 < S) image(st + 1);
     const v4i rb4 = fp4_of_code2(*(const v2i_ *)&bf[SH::O_B2 + crow * 16 + 8 * h]);
 #pragma unroll
@@ -651,7 +668,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
         acc4[p] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[p & 1], fb[p >> 1], acc4[p], 4, 4, 0, 127, 0, 127);
     }
     // stages up to st + 2 have landed (the image of st + 2 is formed in the next iteration)
-    vm_wait_barrier(nq * max(0, min(st + PC_NS - 1, S - 1) - (st + 2)));
+    vm_wait_barrier(nq * max(0, min(st + NS - 1, S - 1) - (st + 2)));
   }
   pstamp(2);
   // epilogue as prefilter_pass_kernel's (fp32 with its certified slack, straight-line tests), plus the
@@ -715,7 +732,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   // per-column loads have been consumed: the compiler's waits for those count the DMAs as well.)
   const int nxt = tile_at(it + 1);
   if (nxt >= 0) {
-    set_src((nxt % x.n_rt) * PC_TR, (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * PC_TC);
+    set_src((nxt % x.n_rt) * PC_TR, (a.j_lo / 32) * 32 + (int64_t)(nxt / x.n_rt) * TC);
     asm volatile("" ::"v"(cbe), "v"(ccb), "v"(cC1n), "v"(cnb), "v"(cbsb), "v"(cmag), "v"(cub[0]), "v"((int)cmono));
     for (int st = 0; st < pre; ++st) issue(st);
   }
@@ -809,7 +826,7 @@ __global__ __launch_bounds__(512, 1) void prefilter_cov_kernel(SideArgs x) {
   if (nxt < 0) break;
   tile = nxt;
   r0 = (tile % x.n_rt) * PC_TR;
-  c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * PC_TC;
+  c0 = (a.j_lo / 32) * 32 + (int64_t)(tile / x.n_rt) * TC;
   }  // tile loop
 }
 
@@ -822,14 +839,22 @@ template __global__ void prefilter_pass_kernel<true, true, true, 64, PF_NS>(Side
 template __global__ void prefilter_pass_kernel<false, false, false, 64, PF_NS>(SideArgs);
 template __global__ void prefilter_pass_kernel<true, true, false, 32, 5>(SideArgs);
 template __global__ void prefilter_pass_kernel<true, true, true, 32, 5>(SideArgs);
-template __global__ void prefilter_cov_kernel<1, true>(SideArgs);
-template __global__ void prefilter_cov_kernel<1, false>(SideArgs);
-template __global__ void prefilter_cov_kernel<2, true>(SideArgs);
-template __global__ void prefilter_cov_kernel<2, false>(SideArgs);
-template __global__ void prefilter_cov_kernel<3, true>(SideArgs);
-template __global__ void prefilter_cov_kernel<3, false>(SideArgs);
-template __global__ void prefilter_cov_kernel<4, true>(SideArgs);
-template __global__ void prefilter_cov_kernel<4, false>(SideArgs);
+template __global__ void prefilter_cov_kernel<1, true, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<1, false, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<2, true, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<2, false, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<3, true, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<3, false, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<4, true, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<4, false, 256>(SideArgs);
+template __global__ void prefilter_cov_kernel<1, true, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<1, false, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<2, true, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<2, false, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<3, true, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<3, false, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<4, true, 128>(SideArgs);
+template __global__ void prefilter_cov_kernel<4, false, 128>(SideArgs);
 
 }  // namespace epi
 }  // namespace gmat

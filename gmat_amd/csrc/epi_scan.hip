@@ -446,8 +446,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_TRY(B.cnt[b].alloc(rl * sizeof(int)));
       GMAT_TRY(B.soff[b].alloc(rl * sizeof(int)));
       GMAT_TRY(B.info[b].alloc(4 * sizeof(int)));
-      GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(rl, PC_TR) * (cdiv(m, PC_TC) + 1) * sizeof(int)));  // PC tiles: the most
-      GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(rl, PC_TR) * (cdiv(m, PC_TC) + 1) * sizeof(int)));
+      GMAT_TRY(B.tlist[b].alloc((size_t)cdiv(rl, PC_TR) * (cdiv(m, 128) + 1) * sizeof(int)));  // PC tiles: the most
+      GMAT_TRY(e->pins.tl[b].reserve((size_t)cdiv(rl, PC_TR) * (cdiv(m, 128) + 1) * sizeof(int)));
       GMAT_TRY(e->pins.rows[b].reserve(rl * 8));
       GMAT_TRY(e->pins.cnt[b].reserve(8));
       GMAT_TRY(e->pins.t2[b].reserve(32));
@@ -491,6 +491,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG")))
                                          : std::max(8, pf_tr == 32 ? 2 * e->n_cu : e->n_cu * 7 / 8);
   // (a six-slot ring for the 32-row tiles measured 16.9-17.0 against 16.8 ms per step)
+  // covariate designs: 32 x 128 tiles of four waves, two workgroups on every CU (GMAT_PC_TC=256: 32 x 256
+  // tiles of eight waves on 7/8 of the CUs)
+  const int pc_tc = getenv("GMAT_PC_TC") && atoi(getenv("GMAT_PC_TC")) == 256 ? 256 : 128;
+  const int pc_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG")))
+                                         : std::max(8, pc_tc == 128 ? 2 * e->n_cu : e->n_cu * 7 / 8);
   const int pf_rg = getenv("GMAT_PF_RG") ? std::max(1, atoi(getenv("GMAT_PF_RG"))) : 4 * PF_TR / pf_tr;
   if (getenv("GMAT_PF_STAMPS")) {
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
@@ -666,20 +671,20 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       x.rs2 = L.p2b.as<uint8_t>();
       x.cs2 = R.p2b.as<uint8_t>();
       x.n_rt = (int)cdiv(Rn, PC_TR);
-      // the running 64 x 128 tiles in blocks of 4 row x 8 column tiles (as the intercept-only prefilter's
-      // list), a persistent grid of one workgroup per CU over them (GMAT_PF_NOLIST: one per tile)
+      // the running 32 x pc_tc tiles in blocks of 8 row x (2048 / pc_tc) column tiles (256 x 2,048, as the
+      // intercept-only prefilter's list), a persistent grid over them (GMAT_PF_NOLIST: one per tile)
       int *tl = e->pins.tl[b].as<int>();
       int run = 0;
-      const int64_t n_ct = cdiv(ncols, PC_TC);
-      for (int rg = 0; rg < x.n_rt; rg += 4)
-        for (int64_t cg = 0; cg < n_ct; cg += 8)
-          for (int64_t ct = cg; ct < std::min(n_ct, cg + 8); ++ct)
-            for (int rt = rg; rt < std::min(x.n_rt, rg + 4); ++rt) {
-              const int64_t c0 = (ln.j_lo / 32) * 32 + ct * PC_TC;
-              if (c0 < m && !(tri && c0 + PC_TC - 1 <= ln.rows[rt * PC_TR])) tl[run++] = rt + x.n_rt * (int)ct;
+      const int64_t n_ct = cdiv(ncols, pc_tc), cgs = 2048 / pc_tc;
+      for (int rg = 0; rg < x.n_rt; rg += 8)
+        for (int64_t cg = 0; cg < n_ct; cg += cgs)
+          for (int64_t ct = cg; ct < std::min(n_ct, cg + cgs); ++ct)
+            for (int rt = rg; rt < std::min(x.n_rt, rg + 8); ++rt) {
+              const int64_t c0 = (ln.j_lo / 32) * 32 + ct * pc_tc;
+              if (c0 < m && !(tri && c0 + pc_tc - 1 <= ln.rows[rt * PC_TR])) tl[run++] = rt + x.n_rt * (int)ct;
             }
       // MFMA work per pair: 4 fp4 code products + (2 + K0) int8 products over n_pad individuals
-      pf_ops_of[li] = (double)run * PC_TR * PC_TC * (8.0 + 4.0 * (2 + e->pf_ncov)) * (double)n_pad;
+      pf_ops_of[li] = (double)run * PC_TR * pc_tc * (8.0 + 4.0 * (2 + e->pf_ncov)) * (double)n_pad;
       GMAT_HIP(hipEventRecord(pf_beg[b], S2));
       // persistent (one-box A/B, covariate configs[2] step: 35.8 against 41.9 ms for one workgroup per
       // tile, GMAT_PF_NOLIST; the persistent variant spills a few registers at three or four directions)
@@ -687,22 +692,30 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         GMAT_HIP(hipMemcpyAsync(B.tlist[b].p, tl, (size_t)run * sizeof(int), hipMemcpyHostToDevice, S2));
         x.tile_list = B.tlist[b].as<int>();
         x.n_list = run;
-        const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8))));
+        const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pc_wg, 8), cdiv(run, 8))));
+        const dim3 bd((unsigned)(2 * pc_tc));
+#define PC_LAUNCH(NC_, L_)                                                           \
+  if (pc_tc == 128)                                                                  \
+    hipLaunchKernelGGL((prefilter_cov_kernel<NC_, L_, 128>), gp, bd, 0, S2, x);      \
+  else                                                                               \
+    hipLaunchKernelGGL((prefilter_cov_kernel<NC_, L_, 256>), gp, bd, 0, S2, x)
         switch (e->pf_ncov) {
-          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, true>), gp, dim3(512), 0, S2, x); break;
-          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, true>), gp, dim3(512), 0, S2, x); break;
-          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, true>), gp, dim3(512), 0, S2, x); break;
-          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, true>), gp, dim3(512), 0, S2, x); break;
+          case 1: PC_LAUNCH(1, true); break;
+          case 2: PC_LAUNCH(2, true); break;
+          case 3: PC_LAUNCH(3, true); break;
+          default: PC_LAUNCH(4, true); break;
         }
       } else if (run > 0) {
         const dim3 gp((unsigned)(x.n_rt * n_ct));
+        const dim3 bd((unsigned)(2 * pc_tc));
         if (li == stamp_launch) stamp_grid = x.n_rt * n_ct;
         switch (e->pf_ncov) {
-          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false>), gp, dim3(512), 0, S2, x); break;
-          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false>), gp, dim3(512), 0, S2, x); break;
-          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, false>), gp, dim3(512), 0, S2, x); break;
-          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, false>), gp, dim3(512), 0, S2, x); break;
+          case 1: PC_LAUNCH(1, false); break;
+          case 2: PC_LAUNCH(2, false); break;
+          case 3: PC_LAUNCH(3, false); break;
+          default: PC_LAUNCH(4, false); break;
         }
+#undef PC_LAUNCH
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
@@ -1173,10 +1186,10 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
         xp.n_rt = (int)cdiv(Rn, PC_TR);
         const unsigned gp = (unsigned)(xp.n_rt * cdiv(ncols, PC_TC));
         switch (e->pf_ncov) {
-          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false>), dim3(gp), dim3(512), 0, S2, xp); break;
-          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false>), dim3(gp), dim3(512), 0, S2, xp); break;
-          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, false>), dim3(gp), dim3(512), 0, S2, xp); break;
-          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, false>), dim3(gp), dim3(512), 0, S2, xp); break;
+          case 1: hipLaunchKernelGGL((prefilter_cov_kernel<1, false, PC_TC>), dim3(gp), dim3(512), 0, S2, xp); break;
+          case 2: hipLaunchKernelGGL((prefilter_cov_kernel<2, false, PC_TC>), dim3(gp), dim3(512), 0, S2, xp); break;
+          case 3: hipLaunchKernelGGL((prefilter_cov_kernel<3, false, PC_TC>), dim3(gp), dim3(512), 0, S2, xp); break;
+          default: hipLaunchKernelGGL((prefilter_cov_kernel<4, false, PC_TC>), dim3(gp), dim3(512), 0, S2, xp); break;
         }
       }
       GMAT_HIP(hipGetLastError());
