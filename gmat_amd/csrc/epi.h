@@ -623,6 +623,7 @@ typedef int v2i__ __attribute__((ext_vector_type(2)));
 // LDS-DMA ring (six in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
 // folds the row block).
 constexpr int R8_S = 7, R8_TB = 2048, R8_TILE = R8_S * R8_TB, R8_NC = 32, R8_PP = 128;
+constexpr int R8_NT = 4;  // O(n) sums per pair stored by refine8_side_kernel for refine8_fin_kernel
 __host__ __device__ inline int64_t r8_toff(int64_t kb, int64_t NS) {  // tiles of the row blocks before kb
   const int64_t h = kb >> 1;
   return kb * NS - ((kb & 1) ? h * h : h * (h - 1));
@@ -975,6 +976,9 @@ struct gmat_epi {
   } pins;
   hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;  // scan pipeline: screen / side terms / refine
   hipStream_t s4 = nullptr;  // the compacted scan's second prefilter stream (odd launches)
+  hipStream_t s5 = nullptr;  // the int8 refine's O(n) terms beside refine8_kernel
+  hipEvent_t r8ev[2] = {nullptr, nullptr};  // refine(): fork / join of that stream
+  DBuf r8_terms;                            // refine8_side_kernel's terms [R8_NT][np]
   struct LrcBuffers {  // three sets: the prefilters of launches L + 1 and L + 2 are queued while L screens
     DBuf drows[3], lmask[3], ops[3], opc[3], slot_ops[3], slot_row[3], slot_j[3], cnt[3], soff[3], info[3], tlist[3];
     int64_t rl = 0, ops_cap = 0, slot_cap = 0;  // the sets' rows per launch, record and slot capacities
@@ -990,6 +994,9 @@ struct gmat_epi {
     stream_release(s2);
     stream_release(s3);
     stream_release(s4);
+    stream_release(s5);
+    for (auto ev : r8ev)
+      if (ev) (void)hipEventDestroy(ev);
   }
 };
 
@@ -1040,11 +1047,14 @@ __global__ void refine8_side_kernel(int64_t n_pad, const int8_t *__restrict__ sl
                                                            const double *soff_l, const double *soff_r, const double *off_l,
                                                            const double *off_r, const double *qa, const double *ra,
                                                            const double *qb, const double *rb, double zz,
-                                                           const uint8_t *mono_l, const uint8_t *mono_r,
                                                            const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
-                                                           int64_t np, const double *varw, int nseg, const double *tpart,
-                                                           double unit, double *eff, double *var, double *chi,
-                                                           double *pv);
+                                                           int64_t np, double *__restrict__ terms);
+__global__ void refine8_fin_kernel(int64_t np, const double *__restrict__ terms, const double *soff_l,
+                                   const double *soff_r, const double *qa, const double *ra, const double *qb,
+                                   const double *rb, double zz, const uint8_t *mono_l, const uint8_t *mono_r,
+                                   const int64_t *__restrict__ pi, const int64_t *__restrict__ pj, const double *varw,
+                                   int nseg, const double *tpart, double unit, double *eff, double *var, double *chi,
+                                   double *pv);
 __global__ void pair_side_kernel(PairArgs x);
 __global__ void pair_mxr_kernel(PairArgs x);
 __global__ void pair_mxw_kernel(PairArgs x);

@@ -236,7 +236,29 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
     double *tpart = e->r8_varw.as<double>() + np;
     const int li = (int)(&L - e->code), ri = (int)(&R - e->code);
     const int8_t *sl = screen_panel(e, li), *sr = screen_panel(e, ri);
+    // the O(n) terms on a second stream beside refine8_kernel (round 5: 0.27 ms less at the end of a
+    // configs[2] step, where refine8_side_kernel ran alone after it), joined before refine8_fin_kernel
+    if (e->r8_terms.bytes < (size_t)R8_NT * np * sizeof(double)) {
+      GMAT_HIP(hipStreamSynchronize(st));
+      if (e->s5) GMAT_HIP(hipStreamSynchronize(e->s5));
+      GMAT_TRY(e->r8_terms.alloc((size_t)R8_NT * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
+    }
+    if (!e->s5) GMAT_TRY(stream_acquire(&e->s5));
+    for (auto &ev : e->r8ev)
+      if (!ev) GMAT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipStream_t s5 = e->s5;
+    GMAT_HIP(hipEventRecord(e->r8ev[0], st));  // the pair list is ready
+    GMAT_HIP(hipStreamWaitEvent(s5, e->r8ev[0], 0));
     size_t kt0;
+    GMAT_TRY(kt_begin(e, s5, &kt0));
+    hipLaunchKernelGGL(refine8_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, s5, e->n_pad, sl, sr,
+                       L.U.as<double>(), R.U.as<double>(), e->z.as<double>(), e->dg.as<double>(), e->py.as<double>(), lp,
+                       rp, L.soff.as<double>(), R.soff.as<double>(), L.off.as<double>(), R.off.as<double>(),
+                       L.qa.as<double>(), L.ra.as<double>(), R.qb.as<double>(), R.rb.as<double>(), e->zz, pi, pj, np,
+                       e->r8_terms.as<double>());
+    GMAT_HIP(hipGetLastError());
+    GMAT_TRY(kt_end(e, s5, KT_REFINE_SIDE, kt0, (double)np));
+    GMAT_HIP(hipEventRecord(e->r8ev[1], s5));
     GMAT_TRY(kt_begin(e, st, &kt0));
     if (wide)
       hipLaunchKernelGGL(refine8w_kernel, dim3((unsigned)wgs, (unsigned)nseg), dim3(512), 0, st, e->n_pad,
@@ -246,17 +268,13 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
                          e->r8_tiles.as<int8_t>(), sl, sr, pi, pj, np, e->r8_unit, e->r8_varw.as<double>(), tpart);
     GMAT_HIP(hipGetLastError());
     GMAT_TRY(kt_end(e, st, KT_REFINE, kt0, (double)np));
-    GMAT_TRY(kt_begin(e, st, &kt0));
-    // the O(n) terms, the segments' combination and the p-values in one launch (as three launches they
-    // were two more dependent steps at the end of every scan)
-    hipLaunchKernelGGL(refine8_side_kernel, dim3((unsigned)cdiv(np, 4)), dim3(256), 0, st, e->n_pad, sl, sr,
-                       L.U.as<double>(), R.U.as<double>(), e->z.as<double>(), e->dg.as<double>(), e->py.as<double>(), lp,
-                       rp, L.soff.as<double>(), R.soff.as<double>(), L.off.as<double>(), R.off.as<double>(),
-                       L.qa.as<double>(), L.ra.as<double>(), R.qb.as<double>(), R.rb.as<double>(), e->zz,
-                       L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj, np, e->r8_varw.as<double>(), nseg, tpart,
-                       e->r8_unit, eff, var, chi, p);
+    // the segments' combination, the O(n) terms and the p-values in one launch
+    GMAT_HIP(hipStreamWaitEvent(st, e->r8ev[1], 0));
+    hipLaunchKernelGGL(refine8_fin_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, st, np, e->r8_terms.as<double>(),
+                       L.soff.as<double>(), R.soff.as<double>(), L.qa.as<double>(), L.ra.as<double>(),
+                       R.qb.as<double>(), R.rb.as<double>(), e->zz, L.mono.as<uint8_t>(), R.mono.as<uint8_t>(), pi, pj,
+                       e->r8_varw.as<double>(), nseg, tpart, e->r8_unit, eff, var, chi, p);
     GMAT_HIP(hipGetLastError());
-    GMAT_TRY(kt_end(e, st, KT_REFINE_SIDE, kt0, (double)np));
     return GMAT_OK;
   }
   // a fixed number of segments per pair tile (not one chosen from np: a pair's numbers must not

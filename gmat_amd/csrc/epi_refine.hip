@@ -423,7 +423,9 @@ __global__ __launch_bounds__(512, 1) void refine8w_kernel(int64_t n_pad, const i
 }
 
 // The O(n) terms of e'Pe in fp64 (refine8_kernel's expansion) and eff = e'Py from the reference
-// codes; one wave per pair, lanes over individuals, lane partials added in a fixed tree.
+// codes; one wave per pair, lanes over individuals, lane partials added in a fixed tree.  Round 5: it
+// runs on a second stream beside refine8_kernel (whose 2 waves per SIMD leave room for a third) and
+// stores its terms; refine8_fin_kernel adds them to w'P_off w in the order one kernel used (same bits).
 __global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const int8_t *__restrict__ sl,
                                                            const int8_t *__restrict__ sr, const double *__restrict__ Ua,
                                                            const double *__restrict__ Ub, const double *__restrict__ z,
@@ -432,11 +434,8 @@ __global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const 
                                                            const double *soff_l, const double *soff_r, const double *off_l,
                                                            const double *off_r, const double *qa, const double *ra,
                                                            const double *qb, const double *rb, double zz,
-                                                           const uint8_t *mono_l, const uint8_t *mono_r,
                                                            const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
-                                                           int64_t np, const double *varw, int nseg, const double *tpart,
-                                                           double unit, double *eff, double *var, double *chi,
-                                                           double *pv) {
+                                                           int64_t np, double *__restrict__ terms) {
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= np) return;
@@ -460,6 +459,25 @@ __global__ __launch_bounds__(256) void refine8_side_kernel(int64_t n_pad, const 
     ef += __shfl_xor(ef, off);
   }
   if (lane) return;
+  const double tv[R8_NT] = {s1, s2, s3, ef};
+#pragma unroll
+  for (int k = 0; k < R8_NT; ++k) terms[(int64_t)k * np + p] = tv[k];
+}
+
+// var = w'P_off w + the O(n) terms (refine8_side_kernel's, added in its former order), chi, p
+__global__ __launch_bounds__(256) void refine8_fin_kernel(int64_t np, const double *__restrict__ terms,
+                                                          const double *soff_l, const double *soff_r, const double *qa,
+                                                          const double *ra, const double *qb, const double *rb, double zz,
+                                                          const uint8_t *mono_l, const uint8_t *mono_r,
+                                                          const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
+                                                          const double *varw, int nseg, const double *tpart, double unit,
+                                                          double *eff, double *var, double *chi, double *pv) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const int64_t i = pi[p], j = pj[p];
+  const double al = soff_l[i], be = soff_r[j], ab = al * be;
+  const double s1 = terms[p], s2 = terms[np + p], s3 = terms[2 * np + p], ef = terms[3 * np + p];
+  // (the expressions of the single kernel, so that the compiler forms the same products and sums)
   const double t3 = be * be * qa[i], t5 = al * al * qb[j], t7 = ab * ab * zz, t8 = 2.0 * ab * s2, t4 = -2.0 * ab * be * ra[i],
                t6 = -2.0 * ab * al * rb[j];
   // w'P_off w: refine8_kernel's value, or its segments' integer sums added exactly in fp64 (integers

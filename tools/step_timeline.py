@@ -16,7 +16,9 @@ def main():
     path = sys.argv[1]
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]))
                 for r in csv.DictReader(open(path)))
-    rf = [k for k, e in enumerate(ev) if e[2].startswith(("refine_kernel", "refine8_side_kernel"))]
+    rf = [k for k, e in enumerate(ev) if e[2].startswith(("refine_kernel", "refine8_side_kernel", "refine8_fin_kernel"))]
+    if any(ev[k][2].startswith("refine8_fin_kernel") for k in rf):  # round 5: the finish kernel ends a scan
+        rf = [k for k in rf if ev[k][2].startswith("refine8_fin_kernel")]
     pf = [k for k, e in enumerate(ev) if e[2].startswith(("prefilter_pass", "prefilter_cov"))]
     if len(sys.argv) > 2:
         pf = pf[-int(sys.argv[2]):]
