@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 #include "common.h"
 
@@ -172,6 +173,34 @@ int stream_acquire(hipStream_t *out) {
     }
   }
   GMAT_HIP(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+  return GMAT_OK;
+}
+
+// The scan pipeline's streams, one fixed set per device shared by every plan (round 5).  HIP maps a
+// process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues as they are created, and streams that
+// share a queue wait for each other's kernels; the pipeline was tuned on the set a first plan creates
+// (the screen stream, then the even / odd prefilter streams, the pair-screen / refine stream and the
+// refine's side stream).  Taken from a pool, later plans got those roles on other queues: the
+// covariate leg of the bench ran 38.5 instead of 32.0 ms per step with the intercept plan alive.  The
+// set is created once, in that order, on the first request; plans do not release it.
+int pipeline_stream(int role, hipStream_t *out) {
+  constexpr int NR = 5;
+  static std::mutex mu;
+  static std::map<int, std::vector<hipStream_t>> sets;
+  if (role < 0 || role >= NR) {
+    set_error("pipeline_stream: role %d", role);
+    return GMAT_E_ARG;
+  }
+  int dev = 0;
+  GMAT_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  std::vector<hipStream_t> &v = sets[dev];
+  while ((int)v.size() < NR) {
+    hipStream_t s = nullptr;
+    GMAT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    v.push_back(s);
+  }
+  *out = v[role];
   return GMAT_OK;
 }
 

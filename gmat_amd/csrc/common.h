@@ -31,6 +31,10 @@ void pinned_free(void *p, size_t bytes);
 // non-blocking HIP streams from a process-wide cache (stream creation / destruction cost milliseconds);
 // stream_release synchronises the stream and keeps it for the next stream_acquire on its device
 int stream_acquire(hipStream_t *out);
+// the scan pipeline's fixed streams per device, in creation order: 0 the screen (and plan setup), 1 the
+// even launches' prefilter, 2 pair screen and refine, 3 the odd launches' prefilter, 4 the refine's side
+// terms -- shared by every plan, never released (capi.cpp)
+int pipeline_stream(int role, hipStream_t *out);
 void stream_release(hipStream_t s);
 
 #define GMAT_HIP(x)                                                                        \

@@ -990,11 +990,8 @@ struct gmat_epi {
     gmat::epi::seg_free(seg);
     for (auto ev : kev) (void)hipEventDestroy(ev);
     for (auto ev : sev) (void)hipEventDestroy(ev);
-    stream_release(s1);
-    stream_release(s2);
-    stream_release(s3);
-    stream_release(s4);
-    stream_release(s5);
+    for (hipStream_t st : {s1, s2, s3, s4, s5})  // the device's pipeline streams (shared): drained, kept
+      if (st) (void)hipStreamSynchronize(st);
     for (auto ev : r8ev)
       if (ev) (void)hipEventDestroy(ev);
   }

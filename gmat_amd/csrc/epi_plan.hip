@@ -243,7 +243,7 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
       if (e->s5) GMAT_HIP(hipStreamSynchronize(e->s5));
       GMAT_TRY(e->r8_terms.alloc((size_t)R8_NT * std::max<int64_t>(np, 1 << 16) * sizeof(double)));
     }
-    if (!e->s5) GMAT_TRY(stream_acquire(&e->s5));
+    if (!e->s5) GMAT_TRY(pipeline_stream(4, &e->s5));
     for (auto &ev : e->r8ev)
       if (!ev) GMAT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const hipStream_t s5 = e->s5;
@@ -786,10 +786,10 @@ int gmat::epi::epi_create_impl(gmat_epi **out, gmat_geno *g, const double *pvp, 
       (rc = rabs.alloc(n_pad * sizeof(double))))
     return fail(rc);
   hipStream_t sx = nullptr;
-  if ((rc = stream_acquire(&sx)) != GMAT_OK) return fail(rc);
-  struct StreamGuard {
+  if ((rc = pipeline_stream(0, &sx)) != GMAT_OK) return fail(rc);
+  struct StreamGuard {  // the squarings are done before the plan is (or fails)
     hipStream_t s;
-    ~StreamGuard() { stream_release(s); }
+    ~StreamGuard() { (void)hipStreamSynchronize(s); }
   } sx_guard{sx};
   (void)hipDeviceSynchronize();  // P, the slices and z / dg are ready for both streams
   const double os = qmax > 0 ? 15.0 / qmax : 1.0;

@@ -304,7 +304,7 @@ int scan_exhaustive(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, 
   const int64_t nQ = cdiv(e->n_pad / 64, R8_NC), nseg_w = e->n_pad > 64 * R8_NC ? nQ * (nQ + 1) / 2 : 1;
   const int64_t dflt = std::min<int64_t>(1 << 24, ((int64_t)1 << 31) / (8 * (1 + R8_S * nseg_w)));
   const int64_t cap = std::max<int64_t>(m, getenv("GMAT_EXH_CHUNK") ? atoll(getenv("GMAT_EXH_CHUNK")) : dflt);
-  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
+  if (!e->s3) GMAT_TRY(pipeline_stream(2, &e->s3));
   const hipStream_t st = e->s3;
   DBuf di, dj, de, dv, dc, dp, hi, hj, he, hv, hc, hp, cnt, drows, doffs;
   for (DBuf *b : {&di, &dj, &de, &dv, &dc, &dp, &hi, &hj, &he, &hv, &hc, &hp}) GMAT_TRY(b->alloc((size_t)cap * 8));
@@ -501,10 +501,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
   }
-  if (!e->s1) GMAT_TRY(stream_acquire(&e->s1));
-  if (!e->s2) GMAT_TRY(stream_acquire(&e->s2));
-  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
-  if (!e->s4) GMAT_TRY(stream_acquire(&e->s4));
+  if (!e->s1) GMAT_TRY(pipeline_stream(0, &e->s1));
+  if (!e->s2) GMAT_TRY(pipeline_stream(1, &e->s2));
+  if (!e->s3) GMAT_TRY(pipeline_stream(2, &e->s3));
+  if (!e->s4) GMAT_TRY(pipeline_stream(3, &e->s4));
   // the prefilter passes of even / odd launches on two streams: launch L + 1 (other buffer set) can
   // start on the CUs that the tail of launch L leaves idle (a launch's ~800 equal tiles fill its last
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
@@ -1013,9 +1013,9 @@ int scan_blocks(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, doub
   // pair screen + refine on S3; ordered after the coding setup by a device synchronisation
   // (Refining launch by launch beside the screens was measured 2.7x slower overall: refine waves
   // occupy CUs that a screen workgroup, which needs a whole CU, then waits for.)
-  if (!e->s1) GMAT_TRY(stream_acquire(&e->s1));
-  if (!e->s2) GMAT_TRY(stream_acquire(&e->s2));
-  if (!e->s3) GMAT_TRY(stream_acquire(&e->s3));
+  if (!e->s1) GMAT_TRY(pipeline_stream(0, &e->s1));
+  if (!e->s2) GMAT_TRY(pipeline_stream(1, &e->s2));
+  if (!e->s3) GMAT_TRY(pipeline_stream(2, &e->s3));
   const hipStream_t sm = e->s1, S2 = e->s2, S3 = e->s3;
   GMAT_HIP(hipDeviceSynchronize());
   ScanEvents evs{e};
