@@ -195,10 +195,23 @@ int pipeline_stream(int role, hipStream_t *out) {
   GMAT_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
   std::vector<hipStream_t> &v = sets[dev];
-  while ((int)v.size() < NR) {
-    hipStream_t s = nullptr;
-    GMAT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    v.push_back(s);
+  if (v.empty()) {
+    // GMAT_STREAM_ORDER (diagnostics): the roles in creation order, e.g. "0,1,3,2,4"
+    int order[NR] = {0, 1, 2, 3, 4};
+    if (const char *o = getenv("GMAT_STREAM_ORDER")) {
+      int k = 0, seen = 0;
+      for (const char *c = o; *c && k < NR; ++c)
+        if (*c >= '0' && *c < '0' + NR && !(seen >> (*c - '0') & 1)) {
+          order[k++] = *c - '0';
+          seen |= 1 << (*c - '0');
+        }
+      if (k != NR) {
+        set_error("GMAT_STREAM_ORDER=%s: a permutation of 0..%d", o, NR - 1);
+        return GMAT_E_ARG;
+      }
+    }
+    v.assign(NR, nullptr);
+    for (int k = 0; k < NR; ++k) GMAT_HIP(hipStreamCreateWithFlags(&v[order[k]], hipStreamNonBlocking));
   }
   *out = v[role];
   return GMAT_OK;
