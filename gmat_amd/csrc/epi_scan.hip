@@ -510,6 +510,11 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, e->s4};
+  // the slot lists on the screen stream for scans of ten or more launches, else on the prefilter's
+  // stream (one-box A/Bs: configs[2], 13 launches, 16.1-16.2 against 16.6-16.8 ms per step -- a launch's
+  // lists no longer hold back the prefilter two launches later on the same stream --; rank 0's 8-way
+  // part, 7 launches, 2.82-2.88 against 2.67-2.75 ms; the pair-screen stream 16.9-17.1 / 2.93-2.96 ms)
+  const int lists_on = getenv("GMAT_LISTS_STREAM") ? atoi(getenv("GMAT_LISTS_STREAM")) : plan.size() >= 10 ? 2 : 0;
   GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
@@ -720,17 +725,21 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
     GMAT_HIP(hipGetLastError());
-    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
+    // the slot lists on SL (GMAT_LISTS_STREAM: 0 the prefilter's stream, 1 the pair-screen stream, 2 the
+    // screen stream), after the prefilter
+    const hipStream_t SL = lists_on == 1 ? S3 : lists_on == 2 ? sm : S2;
+    if (SL != S2) GMAT_HIP(hipStreamWaitEvent(SL, pf_end[b], 0));
+    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
                        B.cnt[b].as<int>());
-    hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, S2, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
+    hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, SL, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
                        B.info[b].as<int>(), B.slot_row[b].as<int>(), B.slot_cap);
-    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, S2, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
+    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
                        B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>(),
                        B.ops[b].as<int>(), B.ops_cap, B.slot_ops[b].as<int>(), B.slot_cap);
     GMAT_HIP(hipGetLastError());
-    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].p, B.info[b].p, 4 * sizeof(int), hipMemcpyDeviceToHost, S2));
-    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].as<int>() + 4, B.opc[b].p, sizeof(int), hipMemcpyDeviceToHost, S2));
-    GMAT_HIP(hipEventRecord(side_end[b], S2));
+    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].p, B.info[b].p, 4 * sizeof(int), hipMemcpyDeviceToHost, SL));
+    GMAT_HIP(hipMemcpyAsync(e->pins.t2[b].as<int>() + 4, B.opc[b].p, sizeof(int), hipMemcpyDeviceToHost, SL));
+    GMAT_HIP(hipEventRecord(side_end[b], SL));
     return GMAT_OK;
   };
   // (Refining each pair-screen chunk's survivors beside the later launches instead of all of them at
