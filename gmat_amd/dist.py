@@ -146,8 +146,21 @@ def init(backend=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not tdist.is_initialized():
             tdist.init_process_group("gloo")
+            # tear the gloo group down before interpreter shutdown: left to the destructors, its
+            # worker threads can be destroyed while joinable (std::terminate, exit status -6)
+            import atexit
+            atexit.register(_destroy_gloo)
     _state["backend"] = backend
     return backend
+
+
+def _destroy_gloo():
+    import torch.distributed as tdist
+    if tdist.is_initialized():
+        try:
+            tdist.barrier()
+        finally:
+            tdist.destroy_process_group()
 
 
 def _require():
