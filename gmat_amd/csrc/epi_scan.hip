@@ -423,7 +423,23 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
     }
   }
   double pairs_tested = 0;
-  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, RL, e->col_lo);
+  // Scans of fewer than ten launches (a rank's part of a multi-GPU split) fold into the same number of
+  // launches of equal rows (an even number of equal chunks, none left alone) instead of RL-row launches
+  // plus a short lone middle chunk.  One-box A/Bs (bench split rehearsal, twice): 2 / 4 / 8-way parts
+  // 8.62-8.69 / 4.29-4.34 / 2.42-2.48 ms against 8.78-8.85 / 4.42-4.60 / 2.47-2.52; the configs[2] step
+  // (13 launches) keeps the RL-row launches and its half-size last launch (16.05-16.14 against
+  // 16.35-16.43 ms).  GMAT_FOLD_EVEN forces it: 0 off, 1 on, 2 an odd number of equal chunks (the last
+  // launch one lone chunk: no better than off)
+  int64_t fold_rl = RL;
+  int fold_even = getenv("GMAT_FOLD_EVEN") ? atoi(getenv("GMAT_FOLD_EVEN")) : -1;
+  if (fold_even < 0) fold_even = cdiv(n_rows, RL) < 10 ? 1 : 0;
+  if (fold_even == 1 && n_rows > RL) fold_rl = 2 * cdiv(n_rows, 2 * cdiv(n_rows, RL));
+  if (fold_even == 2 && n_rows > RL) {
+    int64_t nl = cdiv(n_rows, RL);
+    while (2 * cdiv(n_rows, 2 * nl - 1) > RL) ++nl;
+    fold_rl = 2 * cdiv(n_rows, 2 * nl - 1);
+  }
+  const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, fold_rl, e->col_lo);
   // live-pair records per launch: an initial capacity of 1/128 of a launch's pairs (at least 2^20; the
   // configs[2] prefilter keeps 1/250), grown (and the launch rerun) when a launch keeps more
   const int64_t rl_sets = std::max(RL, B.rl);
