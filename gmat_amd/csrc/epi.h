@@ -47,7 +47,7 @@ constexpr int LK = 64;   // inner (individual) depth per LDS stage
 constexpr int AP = 80;   // LDS pitch of a 64-byte row (conflict-free ds_read_b128)
 constexpr int BJ = 32;   // second-SNP columns per screen tile
 constexpr int ROWS_PER_LAUNCH = 512;       // first SNPs per launch of the block-granular scan
-constexpr int LRC_ROWS_PER_LAUNCH = 4096;  // ... and of the compacted low-rank scan
+constexpr int LRC_ROWS_PER_LAUNCH = 7168;  // ... and of the compacted low-rank scan
 constexpr int SIDE_T = 3;        // int8 slices of the O(n)-per-pair side vectors (21 bits)
 constexpr int E3_PF = 2;         // L3 slices of the prefilter pass (eff to ~2^-14: enough to screen)
 constexpr int SIDE_P = 3;        // left side-vector parts per band row: L', L3, Ld

@@ -403,16 +403,18 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   const int64_t nJ = cdiv(m, BJ);
   auto &B = e->lrc;
   constexpr int NBUF = 3;  // buffer sets: launch L uses set L % 3
-  // first SNPs per launch: LRC_ROWS_PER_LAUNCH, but at least GMAT_LRC_MIN_LAUNCHES (6) launches down to
+  // first SNPs per launch: LRC_ROWS_PER_LAUNCH (7,168: configs[2] in 7 launches, 15.57-15.81 ms per step
+  // against 15.99-16.12 at 4,096 in 13, 15.78-15.81 at 6,144, 15.65-16.02 at 8,192 on one box; each launch
+  // costs its pipeline turn), but at least GMAT_LRC_MIN_LAUNCHES (6) launches down to
   // 512 rows (a rank's part of a multi-GPU split keeps the prefilter-ahead pipeline filled: rank 0's
   // 8-way part 2.62 ms at 1,024 rows per launch against 2.75 at 1,536, 2.72 at 768, 2.82 at 512), and no more
   // than the three sets' live masks and record bases (8 bytes per (row, 32-column block)) fit in an
-  // eighth of the free HBM; GMAT_LRC_ROWS forces it for A/B runs (a multiple of 128, at most 4096)
+  // eighth of the free HBM; GMAT_LRC_ROWS forces it for A/B runs (a multiple of 128, at most 8192)
   int64_t RL = 0;
   {
     const int64_t min_launches = getenv("GMAT_LRC_MIN_LAUNCHES") ? std::max(1, atoi(getenv("GMAT_LRC_MIN_LAUNCHES"))) : 6;
     RL = getenv("GMAT_LRC_ROWS")
-             ? std::min<int64_t>(4096, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
+             ? std::min<int64_t>(8192, std::max<int64_t>(128, atoll(getenv("GMAT_LRC_ROWS")) / 128 * 128))
              : std::min<int64_t>(LRC_ROWS_PER_LAUNCH, std::max<int64_t>(512, n_rows / min_launches / 128 * 128));
     if (RL > B.rl) {  // buffers sized for fewer rows than this scan wants: is there room?
       size_t free_b = 0, total_b = 0;
@@ -526,11 +528,15 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, e->s4};
-  // the slot lists on the screen stream for scans of ten or more launches, else on the prefilter's
-  // stream (one-box A/Bs: configs[2], 13 launches, 16.1-16.2 against 16.6-16.8 ms per step -- a launch's
+  // the slot lists on the screen stream for long launches, else on the prefilter's stream (round-5
+  // one-box A/Bs at 4,096-row launches: configs[2], 13 launches, 16.1-16.2 against 16.6-16.8 ms per step -- a launch's
   // lists no longer hold back the prefilter two launches later on the same stream --; rank 0's 8-way
   // part, 7 launches, 2.82-2.88 against 2.67-2.75 ms; the pair-screen stream 16.9-17.1 / 2.93-2.96 ms)
-  const int lists_on = getenv("GMAT_LISTS_STREAM") ? atoi(getenv("GMAT_LISTS_STREAM")) : plan.size() >= 10 ? 2 : 0;
+  // (round 5, 7,168-row launches: lists on the screen stream for launches of 4,096 rows or more -- configs[2]
+  // 15.75-15.81 against 16.04-16.07 ms per step on the prefilter stream; the 2-way part 8.55-8.60 against
+  // 8.63-8.64 ms --, on the prefilter stream for shorter ones: the 4 / 8-way parts 4.37 / 2.47-2.50 against
+  // 4.56-4.61 / 2.59 ms)
+  const int lists_on = getenv("GMAT_LISTS_STREAM") ? atoi(getenv("GMAT_LISTS_STREAM")) : RL >= 4096 ? 2 : 0;
   GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
