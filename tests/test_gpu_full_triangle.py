@@ -3,7 +3,7 @@
 hits of the exhaustive scan (level GMAT_SCREEN_NONE: every pair refined, the reference's
 computation remma_epiAA.py:71-82 / remma_epiAD.py:68-80 / remma_epiDD.py:68-79), with
 byte-identical eff / var / chi / p.  The exhaustive scan itself is checked against the oracle on
-a few rows.  tools/full_triangle.py runs the same audit on the full configs[2] cohort.
+a few rows, on up to 20,000 of its hits all over the triangle and on a random sample of its non-hits.  tools/full_triangle.py runs the same audit on the full configs[2] cohort.
 """
 import ctypes
 
@@ -114,6 +114,19 @@ def test_full_triangle_aa(aa_cohort):
     sel = np.isin(exh[0], rows)
     np.testing.assert_array_equal(np.column_stack([exh[0][sel], exh[1][sel]]), exp[:, :2].astype(np.int64))
     np.testing.assert_allclose(np.column_stack([exh[2][sel], exh[4][sel], exh[5][sel]]), exp[:, 2:], rtol=1e-8)
+    # the exhaustive level's hits all over the triangle (up to 20,000 of them) against the oracle's pair
+    # formula (remma_epiAA_pair.py:79-84), and a random sample of the other pairs: none of them a hit
+    hits = np.column_stack([exh[0], exh[1]])
+    pick = np.sort(np.random.default_rng(7).permutation(hits.shape[0])[:20000])
+    eff_o, var_o, chi_o, p_o = O.epi_pair("AA", snp, pvp, py.reshape(-1, 1), hits[pick])
+    assert np.all(p_o < 1e-3)
+    np.testing.assert_allclose(np.column_stack([exh[2][pick], exh[3][pick], exh[4][pick], exh[5][pick]]),
+                               np.column_stack([eff_o, var_o, chi_o, p_o]), rtol=1e-8)
+    sample = np.column_stack([i, j])[i < j]
+    sample = sample[~np.isin(sample[:, 0] * g.m + sample[:, 1], hits[:, 0] * g.m + hits[:, 1])]
+    p_s = O.epi_pair("AA", snp, pvp, py.reshape(-1, 1), sample)[3]
+    # (a monomorphic SNP gives var 0 and a NaN p, as in the reference: not a hit either)
+    assert sample.shape[0] > 3000 and not np.any(p_s < 1e-3), (sample.shape[0], float(np.nanmin(p_s)))
 
 
 @pytest.mark.parametrize("kind", ["AD", "DD"])
