@@ -60,11 +60,22 @@ def build_inputs(n, m, seed, var, rank, ws, covariates=False):
     body = dist.allgather_packed(local, m, nb)
     geno = shard if ws == 1 else None
     log("cohort %d x %d: shard [%d, %d) generated, panel all-gathered in %.1f s" % (n, m, lo, hi, time.time() - t0))
-    import ctypes
     from gmat_amd.plink import Geno
     g = Geno(body=body, n_id=n, n_snp=m)
     pvp = py = ka = y = None
     if rank == 0:
+        pvp, py, ka, y = _rank0_inputs(g, n, seed, var, covariates)
+    pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
+    py = dist.broadcast_array(py, 0, shape=(n,))
+    return geno, g, pvp, py, ka, y
+
+
+def _rank0_inputs(g, n, seed, var, covariates):
+    """GRM, simulated phenotype and P / Py of the cohort (rank 0: the drop-in API as one process)."""
+    import ctypes
+    from gmat_amd import dist
+    from gmat_amd import _native as N
+    with dist.local():
         lib = N.ensure_device()
         ka = np.empty((n, n))
         sc = ctypes.c_double()
@@ -80,9 +91,7 @@ def build_inputs(n, m, seed, var, rank, ws, covariates=False):
         if covariates:
             x, y = covariate_design(n, seed, y)
         pvp, py = projection(y, x, identity(n, format="csr"), [ka, ka * ka], var)
-    pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
-    py = dist.broadcast_array(py, 0, shape=(n,))
-    return geno, g, pvp, py, ka, y
+    return pvp, py, ka, y
 
 
 def cpu_baseline(geno, pvp, py, budget_s):
@@ -419,12 +428,9 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
     nearly every iteration needs an EM weight > 0; 0 of 48 phenotype draws converge within 200
     iterations (profiles/round5_cfg5_reml_probe.txt).  The reference's loop returns its 200th iterate
     then, and so does this one (its iterates match the oracle's: tests/test_gpu_cfg5.py)."""
-    import ctypes
     from gmat_amd import dist, synth
     from gmat_amd import _native as N
     from gmat_amd.plink import Geno
-    from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat, projection
-    from scipy.sparse import identity
     lib = N.ensure_device()
     nb = (n + 3) // 4
     t0 = time.time()
@@ -445,6 +451,53 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
            "cohort_s": t_cohort}
     pvp = py = None
     if rank == 0:
+        pvp, py = _cfg5_rank0(g, n, m, seed, var, reml_iters, out)
+    pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
+    py = dist.broadcast_array(py, 0, shape=(n,))
+    t1 = time.perf_counter()
+    plan = dist.shared_plan(g, pvp, py)  # spectral state computed on rank 0, imported by the others
+    out["plan_create_s"] = time.perf_counter() - t1
+    out["setup"] = plan.setup_stats()
+    out["lowrank_rank"] = plan.lowrank_rank()
+    total = t_all = 0.0
+    for kind in ("DD", "AD"):
+        rows = dist.rank_rows(kind, m, rank, ws)
+        t1 = time.perf_counter()
+        plan.scan(kind, rows, p_cut)  # codings (side vectors) and scan buffers at the timed size, untimed
+        lib.gmat_device_synchronize()
+        t_first = time.perf_counter() - t1
+        times = []
+        for _ in range(reps):
+            dist.barrier()
+            t1 = time.perf_counter()
+            res = plan.scan(kind, rows, p_cut)
+            lib.gmat_device_synchronize()
+            dist.barrier()
+            times.append(dist.allreduce_max(time.perf_counter() - t1))
+        dt = float(np.median(times))
+        pairs = float(m) * (m - 1) / 2 if kind == "DD" else float(m) * m
+        st = plan.stats()
+        out["epi" + kind] = {"pairs": pairs, "s": dt, "s_all": times, "first_scan_s": t_first, "pairs_per_s": pairs / dt,
+                             "hits": int(dist.allreduce_sum(res[0].size)),
+                             "candidates": int(dist.allreduce_sum(st["candidates"])), "screen_level": int(st["n_slice"])}
+        total += pairs
+        t_all += dt
+    out["pairs_per_s"] = total / t_all
+    plan.close()
+    g.close()
+    return out if rank == 0 else None
+
+
+def _cfg5_rank0(g, n, m, seed, var, reml_iters, out):
+    """configs[4] on rank 0 (the drop-in API as one process): A and D GRMs, the 5-GRM REML and P / Py
+    from its estimate; fills out["grm"], out["reml"], out["projection_s"]."""
+    import ctypes
+    from gmat_amd import dist
+    from gmat_amd import _native as N
+    from gmat_amd.uvlmm.uvlmm_varcom import _wemai_multi_gmat, projection
+    from scipy.sparse import identity
+    lib = N.ensure_device()
+    with dist.local():
         mats, grm = [], {}
         for kind, name in ((0, "A"), (1, "D")):
             k = np.empty((n, n))
@@ -484,40 +537,7 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
         t1 = time.perf_counter()
         pvp, py = projection(y, np.ones((n, 1)), identity(n, format="csr"), gl, np.asarray(est, dtype=float))
         out["projection_s"] = time.perf_counter() - t1
-    pvp = dist.broadcast_array(pvp, 0, shape=(n, n))
-    py = dist.broadcast_array(py, 0, shape=(n,))
-    t1 = time.perf_counter()
-    plan = dist.shared_plan(g, pvp, py)  # spectral state computed on rank 0, imported by the others
-    out["plan_create_s"] = time.perf_counter() - t1
-    out["setup"] = plan.setup_stats()
-    out["lowrank_rank"] = plan.lowrank_rank()
-    total = t_all = 0.0
-    for kind in ("DD", "AD"):
-        rows = dist.rank_rows(kind, m, rank, ws)
-        t1 = time.perf_counter()
-        plan.scan(kind, rows, p_cut)  # codings (side vectors) and scan buffers at the timed size, untimed
-        lib.gmat_device_synchronize()
-        t_first = time.perf_counter() - t1
-        times = []
-        for _ in range(reps):
-            dist.barrier()
-            t1 = time.perf_counter()
-            res = plan.scan(kind, rows, p_cut)
-            lib.gmat_device_synchronize()
-            dist.barrier()
-            times.append(dist.allreduce_max(time.perf_counter() - t1))
-        dt = float(np.median(times))
-        pairs = float(m) * (m - 1) / 2 if kind == "DD" else float(m) * m
-        st = plan.stats()
-        out["epi" + kind] = {"pairs": pairs, "s": dt, "s_all": times, "first_scan_s": t_first, "pairs_per_s": pairs / dt,
-                             "hits": int(dist.allreduce_sum(res[0].size)),
-                             "candidates": int(dist.allreduce_sum(st["candidates"])), "screen_level": int(st["n_slice"])}
-        total += pairs
-        t_all += dt
-    out["pairs_per_s"] = total / t_all
-    plan.close()
-    g.close()
-    return out if rank == 0 else None
+    return pvp, py
 
 
 def cfg5_main(args):
@@ -789,11 +809,12 @@ def main():
         parity = parity_check(plan, used_rows, exp_hits, args.p_cut)
     grm = reml = None
     if rank == 0 and not args.no_grm:
-        log("configs[1] GRM")
-        grm = grm_bench(n, 20000, args.seed)
-        if not args.no_reml:
-            log("configs[1] REML")
-            reml = reml_bench(grm_bench.last_k, args.seed)
+        with dist.local():
+            log("configs[1] GRM")
+            grm = grm_bench(n, 20000, args.seed)
+            if not args.no_reml:
+                log("configs[1] REML")
+                reml = reml_bench(grm_bench.last_k, args.seed)
     split = None
     if rank == 0 and ws == 1 and not args.no_split:
         log("multi-GPU split rehearsed part by part")

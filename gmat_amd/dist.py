@@ -25,14 +25,18 @@ raises (the launcher then stops the job) -- there is no silent per-rank fallback
 ranks on different backends.  ``gloo`` (torch.distributed on CPU) is the test harness of
 tests/test_dist_cpu.py, chosen only when no GPU is visible or GMAT_DIST_BACKEND=gloo says so.
 """
+import contextlib
 import ctypes
+import functools
 import os
+import pickle
+import sys
 import tempfile
 import time
 
 import numpy as np
 
-_state = {"backend": None, "comm": None}
+_state = {"backend": None, "comm": None, "root_depth": 0, "failed": False}
 
 
 def world():
@@ -150,17 +154,38 @@ def init(backend=None):
             # worker threads can be destroyed while joinable (std::terminate, exit status -6)
             import atexit
             atexit.register(_destroy_gloo)
+            global _prev_hook
+            if sys.excepthook is not _note_failure:
+                _prev_hook, sys.excepthook = sys.excepthook, _note_failure
     _state["backend"] = backend
     return backend
 
 
+def _note_failure(exc_type, exc, tb):
+    """sys.excepthook: a rank dying on an exception skips the exit barrier (its peers wait in another
+    collective, or are gone: the barrier would hold the failing rank for gloo's 30-minute timeout)."""
+    _state["failed"] = True
+    _prev_hook(exc_type, exc, tb)
+
+
+_prev_hook = sys.__excepthook__
+
+
 def _destroy_gloo():
     import torch.distributed as tdist
-    if tdist.is_initialized():
-        try:
-            tdist.barrier()
-        finally:
-            tdist.destroy_process_group()
+    if not tdist.is_initialized():
+        return
+    try:
+        if not _state.get("failed"):
+            # clean exit: wait for the peers (a rank leaving first tears its sockets down under a peer's
+            # last collective), bounded so that a peer that died without an exception cannot hold us
+            import datetime
+            try:
+                tdist.monitored_barrier(timeout=datetime.timedelta(seconds=60))
+            except Exception:
+                pass
+    finally:
+        tdist.destroy_process_group()
 
 
 def _require():
@@ -300,31 +325,8 @@ def gather_hits(local, root=0):
     rank, ws, _ = world()
     if b is None or ws == 1:
         return merge_hits([local])
-    if b == "rccl":
-        N, lib = _lib()
-        send = _pack_hits(local)
-        sizes = np.zeros(ws)
-        sizes[rank] = send.nbytes
-        N.check(lib.gmat_comm_allreduce_f64(_state["comm"], N.ptr(sizes), ws, 0), "gmat_comm_allreduce_f64")
-        total = int(sizes.sum())
-        recv = np.zeros(total // _HIT.itemsize if rank == root else 0, dtype=_HIT)
-        counts = np.zeros(ws, np.int64)
-        need = ctypes.c_int64()
-        N.check(lib.gmat_comm_gatherv(_state["comm"], N.ptr(send) if send.size else None, send.nbytes, root,
-                                      N.ptr(counts), N.ptr(recv) if recv.size else None, recv.nbytes,
-                                      ctypes.byref(need)), "gmat_comm_gatherv")
-        if rank != root:
-            return None
-        parts, off = [], 0
-        for r in range(ws):
-            k = int(counts[r]) // _HIT.itemsize
-            parts.append(_unpack_hits(recv[off:off + k]))
-            off += k
-        return merge_hits(parts)
-    import torch.distributed as tdist
-    gathered = [None] * ws if rank == root else None
-    tdist.gather_object(None if local is None else tuple(np.asarray(a) for a in local), gathered, dst=root)
-    return merge_hits(gathered) if rank == root else None
+    rec = gather_records(_pack_hits(local), root)
+    return merge_hits([_unpack_hits(rec)]) if rank == root else None
 
 
 def shared_plan(geno, pvp, py, **kw):
@@ -332,9 +334,8 @@ def shared_plan(geno, pvp, py, **kw):
     searches, the plan setup's dominant cost) computed once on rank 0 and broadcast: the other
     ranks import it (gmat_epi_create_with), so the certificates are identical on every rank."""
     from .remma._scan import EpiPlan
-    b = _require()
-    rank, ws, _ = world()
-    if b is None or ws == 1:
+    rank, ws = job()
+    if ws == 1:
         return EpiPlan(geno, pvp, py, **kw)
     if rank == 0:
         plan = EpiPlan(geno, pvp, py, **kw)
@@ -355,3 +356,202 @@ def distributed_scan(scan_fn, kind, num_snp, p_cut, rows=None):
     mine = rank_rows(kind, num_snp, rank, ws, rows)
     local = scan_fn(kind, mine, p_cut) if mine.size else None
     return gather_hits(local)
+
+
+# ---------------------------------------------------------------- the drop-in API as one multi-rank job
+#
+# A user script run as N ranks (torchrun, ``python -m gmat_amd.launch --gpus N script.py`` or
+# GMAT_NUM_GPUS=N) executes every line on every rank.  The reference's functions then behave as one job:
+# * the exhaustive scans, the pair lists and the effect screens shard their work over the ranks and
+#   rank 0 alone writes the output files (remma/_scan.py, remma/_eff.py);
+# * everything single-GPU (GRM, REML, projections, single-SNP tests, annotation, random pairs) runs on
+#   rank 0 only and its result is broadcast (root_call): the files exist before any rank returns, and
+#   the other ranks get the same return value;
+# * the global np.random state is rank 0's on every rank after each such call, as if every rank had
+#   made it (imputation of missing calls and the unseeded random pairs draw from it).
+
+
+def job():
+    """(rank, world_size) of the drop-in API: the process group is set up on first use when
+    WORLD_SIZE > 1.  Inside a rank-0-only section (root_call) this is (0, 1): a nested call runs as a
+    single process."""
+    rank, ws, _ = world()
+    if ws <= 1 or _state["root_depth"] > 0:
+        return 0, 1
+    init()
+    return rank, ws
+
+
+@contextlib.contextmanager
+def local():
+    """Inside: the drop-in API runs as a single process on this rank (no collectives), e.g. bench.py's
+    rank-0-only legs."""
+    _state["root_depth"] += 1
+    try:
+        yield
+    finally:
+        _state["root_depth"] -= 1
+
+
+def broadcast_bytes(data, src=0):
+    """A byte string from `src` to every rank (others pass None)."""
+    rank, ws = job()
+    if ws == 1:
+        return data
+    size = np.array([len(data) if rank == src else 0], dtype=np.int64)
+    size = broadcast_array(size, src, shape=(1,), dtype=np.int64)
+    n = int(size[0])
+    if n == 0:
+        return b""
+    buf = np.frombuffer(data, dtype=np.uint8) if rank == src else None
+    return broadcast_array(buf, src, shape=(n,), dtype=np.uint8).tobytes()
+
+
+def broadcast_object(obj, src=0):
+    """A Python object of this process's own making (never a file's content) from `src`."""
+    rank, ws = job()
+    if ws == 1:
+        return obj
+    data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL) if rank == src else None
+    return pickle.loads(broadcast_bytes(data, src))
+
+
+def sync_rng(src=0):
+    """The global np.random state of `src` on every rank."""
+    rank, ws = job()
+    if ws > 1:
+        np.random.set_state(broadcast_object(np.random.get_state() if rank == src else None, src))
+
+
+def root_call(fn, *args, **kw):
+    """fn(*args, **kw) on rank 0 only; every rank returns its result (or raises its exception) and
+    leaves with rank 0's np.random state.  A single process just calls fn."""
+    rank, ws = job()
+    if ws == 1:
+        return fn(*args, **kw)
+    payload = None
+    if rank == 0:
+        _state["root_depth"] += 1
+        try:
+            payload = ("ok", fn(*args, **kw))
+        except BaseException as exc:  # noqa: B902 -- re-raised below on every rank
+            try:
+                pickle.dumps(exc)
+                payload = ("err", exc)
+            except Exception:
+                payload = ("err", RuntimeError("rank 0: %s: %s" % (type(exc).__name__, exc)))
+        finally:
+            _state["root_depth"] -= 1
+        payload = payload + (np.random.get_state(),)
+    status, value, state = broadcast_object(payload)
+    np.random.set_state(state)
+    if status == "err":
+        raise value
+    return value
+
+
+def on_root(fn):
+    """Decorator: the function runs as root_call(fn, ...)."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kw):
+        return root_call(fn, *args, **kw)
+    wrapper.__wrapped_root__ = fn
+    return wrapper
+
+
+def split_weighted(weights, ws):
+    """Contiguous bounds b[0] = 0 <= ... <= b[ws] = len(weights) splitting `weights` (pairs per row)
+    into ws runs of about equal sum (list order kept: concatenating the runs gives the list back)."""
+    w = np.asarray(weights, dtype=np.float64)
+    if w.size == 0:
+        return np.zeros(ws + 1, dtype=np.int64)
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    targets = cum[-1] * np.arange(ws + 1) / ws
+    b = np.searchsorted(cum, targets, side="left").astype(np.int64)
+    b[0], b[-1] = 0, w.size
+    return np.maximum.accumulate(b)
+
+
+def row_pairs(kind, num_snp, rows):
+    """Pairs a scan of first SNP i tests: m - 1 - i (AA / DD, j > i), m (AD, every j)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    return np.full(rows.size, num_snp, np.int64) if kind == "AD" else num_snp - 1 - rows
+
+
+def shard_rows(kind, num_snp, rows, rank, ws):
+    """This rank's share of the sorted unique first-SNP rows of a scan: the reference's folded split
+    (rank_rows) when the rows are the whole triangle, else a contiguous run of about 1/ws of the pairs."""
+    rows = np.asarray(rows, dtype=np.int64)
+    if ws == 1:
+        return rows
+    hi = num_snp if kind == "AD" else num_snp - 1
+    if rows.size == hi and (hi == 0 or (rows[0] == 0 and rows[-1] == hi - 1)):
+        return rank_rows(kind, num_snp, rank, ws)
+    b = split_weighted(row_pairs(kind, num_snp, rows), ws)
+    return rows[b[rank]:b[rank + 1]]
+
+
+def read_bed_rows(bed_file, lo, hi):
+    """Packed .bed rows [lo, hi) (uint8, (hi - lo) x nb) read from their offset, the magic and the
+    whole file's size checked as plink.read_bed_body does; returns (rows, n_id, n_snp)."""
+    from .plink import BED_MAGIC, count_lines
+    n = count_lines(bed_file + ".fam")
+    m = count_lines(bed_file + ".bim")
+    nb = (n + 3) // 4
+    with open(bed_file + ".bed", "rb") as f:
+        magic = f.read(3)
+        if magic != BED_MAGIC:
+            raise ValueError("%s.bed is not a SNP-major PLINK .bed (magic %r)" % (bed_file, magic))
+        size = os.fstat(f.fileno()).st_size - 3
+        if size < nb * m:
+            raise ValueError("%s.bed has %d data bytes; %d SNPs x %d individuals need %d"
+                             % (bed_file, size, m, n, nb * m))
+        f.seek(3 + lo * nb)
+        rows = np.frombuffer(f.read((hi - lo) * nb), dtype=np.uint8).reshape(hi - lo, nb)
+    return rows, n, m
+
+
+def load_geno(bed_file):
+    """The device genotype panel of a .bed fileset on every rank: each rank reads its SNP shard and
+    the packed shards are all-gathered (RCCL over xGMI); missing calls are imputed on the whole panel
+    with the (synchronised) global np.random state, so every rank holds the same panel, the one a
+    single process would impute (process_plink.py:12-25)."""
+    from .plink import Geno
+    rank, ws = job()
+    if ws == 1:
+        return Geno(bed_file)
+    from .plink import count_lines
+    m = count_lines(bed_file + ".bim")
+    lo, hi = snp_shard(m, rank, ws)
+    local, n, m = read_bed_rows(bed_file, lo, hi)
+    body = allgather_packed(local, m, (n + 3) // 4)
+    sync_rng()
+    return Geno(body=body, n_id=n, n_snp=m)
+
+
+def gather_records(rec, root=0):
+    """A structured numpy array from every rank, concatenated in rank order on `root` (None
+    elsewhere)."""
+    b = _require()
+    rank, ws, _ = world()
+    if b is None or ws == 1:
+        return rec
+    if b == "rccl":
+        N, lib = _lib()
+        send = np.ascontiguousarray(rec)
+        recv_n = None
+        sizes = np.zeros(ws)
+        sizes[rank] = send.nbytes
+        N.check(lib.gmat_comm_allreduce_f64(_state["comm"], N.ptr(sizes), ws, 0), "gmat_comm_allreduce_f64")
+        recv_n = int(sizes.sum()) // rec.dtype.itemsize
+        recv = np.zeros(recv_n if rank == root else 0, dtype=rec.dtype)
+        counts = np.zeros(ws, np.int64)
+        need = ctypes.c_int64()
+        N.check(lib.gmat_comm_gatherv(_state["comm"], N.ptr(send) if send.size else None, send.nbytes, root,
+                                      N.ptr(counts), N.ptr(recv) if recv.size else None, recv.nbytes,
+                                      ctypes.byref(need)), "gmat_comm_gatherv")
+        return recv if rank == root else None
+    import torch.distributed as tdist
+    gathered = [None] * ws if rank == root else None
+    tdist.gather_object(np.ascontiguousarray(rec), gathered, dst=root)
+    return np.concatenate(gathered) if rank == root else None

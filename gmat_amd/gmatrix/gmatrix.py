@@ -11,6 +11,7 @@ import time
 import numpy as np
 
 from .. import _native as N
+from .. import dist
 from ..plink import Geno, read_fam_ids
 
 
@@ -24,6 +25,7 @@ def _fam_ids_as_pandas(bed_file):
         return np.array(iid, dtype=object)
 
 
+@dist.on_root
 def output_mat(mat, id, out_file, out_fmt):
     """Output of gmatrix.py:10-31: 'mat' (np.savetxt '%.18e', suffix 0), 'row_col_val' (1-based
     lower triangle, suffix 1), 'id_id_val' (suffix 2), byte-identical to the reference's
@@ -63,6 +65,7 @@ def _grm(bed_file, kind, inv, small_val, out_fmt, suffix, inv_suffix):
     return kin, kin_inv
 
 
+@dist.on_root
 def spd_inverse(a):
     """Inverse of a symmetric positive-definite matrix on the device (Cholesky)."""
     lib = N.ensure_device()
@@ -73,12 +76,14 @@ def spd_inverse(a):
     return out
 
 
+@dist.on_root
 def agmat(bed_file, inv=False, small_val=0.001, out_fmt="mat"):
     """Additive genomic relationship matrix (gmatrix.py:34-94).  Writes
     ``bed_file + '.agrm{0,1,2}'`` (and ``.agiv*`` when inv) and returns (kin, kin_inv)."""
     return _grm(bed_file, N.GMAT_GRM_ADD, inv, small_val, out_fmt, ".agrm", ".agiv")
 
 
+@dist.on_root
 def dgmat_as(bed_file, inv=False, small_val=0.001, out_fmt="mat"):
     """Dominance genomic relationship matrix (gmatrix.py:97-159).  Writes
     ``bed_file + '.dgrm_as*'`` (and ``.dgiv_as*``) and returns (kin, kin_inv)."""

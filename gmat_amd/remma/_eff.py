@@ -19,6 +19,7 @@ import pandas as pd
 from scipy.stats import chi2
 
 from .. import _native as N
+from .. import dist
 from ..plink import Geno, count_lines
 from ..uvlmm.design_matrix import design_matrix_wemai_multi_gmat
 from ..uvlmm.uvlmm_varcom import projection
@@ -30,10 +31,10 @@ _SYM_MAF = {"AA": "remma_epiAA_maf_eff_cpu", "AD": "remma_epiAD_maf_eff_cpu", "D
 
 
 def _py(y, xmat, zmat, gmat_lst, var_com):
-    """Z'Py (remma_epiAA_eff.py:36-51); P stays on the device side of gmat_projection."""
+    """Z'Py (remma_epiAA_eff.py:36-51); P stays on the device side of gmat_projection.  Computed on
+    rank 0 of a multi-rank job and broadcast."""
     logging.info("Calculate the phenotypic covariance matrix and inversion")
-    _, py = projection(y, xmat, zmat, gmat_lst, var_com)
-    return N.f64(py)
+    return N.f64(dist.root_call(lambda: projection(y, xmat, zmat, gmat_lst, var_com)[1]))
 
 
 def _rows(kind, num_snp, snp_lst_0):
@@ -68,6 +69,36 @@ def _screen(sym, args, temp_file):
     logging.info("Running time: Clock time, {:.5f} sec. {}".format(time.perf_counter() - t0, eff_stats()))
 
 
+def _screen_parts(kind, sym, make_args, num_snp, rows, temp_file):
+    """The effect screen over `rows` into temp_file.  As a multi-rank job: the row list is cut into
+    contiguous runs of about equal pair counts, rank r screens run r into temp_file.part<r>, and rank 0
+    joins the parts in rank order (one header) -- the file a single process writes, byte for byte."""
+    rank, ws = dist.job()
+    if ws == 1:
+        _screen(sym, make_args(rows, temp_file), temp_file)
+        return
+    b = dist.split_weighted(dist.row_pairs(kind, num_snp, rows), ws)
+    mine = np.ascontiguousarray(rows[b[rank]:b[rank + 1]])
+    part = "%s.part%d" % (temp_file, rank)
+    _screen(sym, make_args(mine, part), part)
+    dist.barrier()
+    if rank == 0:
+        with open(temp_file, "wb") as fout:
+            for r in range(ws):
+                name = "%s.part%d" % (temp_file, r)
+                with open(name, "rb") as fin:
+                    head = fin.readline()
+                    if r == 0:
+                        fout.write(head)
+                    while True:
+                        blk = fin.read(1 << 22)
+                        if not blk:
+                            break
+                        fout.write(blk)
+                os.remove(name)
+    dist.barrier()
+
+
 def _append_p(temp_file, out_file, deno):
     """The reference's post-processing loop (remma_epiAA_eff.py:85-96): each screened line gets
     chi_app = eff^2 / deno and p_app = chi2.sf(chi_app, 1), with eff re-read from the %g text.
@@ -99,9 +130,9 @@ def run_eff(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0=None, va
     eff_cut = np.sqrt(chi_cut * var_app)
     temp_file = out_file + ".temp"
     logging.info("Test")
-    _screen(_SYM[kind], (_enc(bed_file), num_id, num_snp, N.ptr(rows), rows.size, N.ptr(py), float(eff_cut),
-                         _enc(temp_file)), temp_file)
-    _append_p(temp_file, out_file, lambda i, j: var_app)
+    _screen_parts(kind, _SYM[kind], lambda r, tf: (_enc(bed_file), num_id, num_snp, N.ptr(r), r.size, N.ptr(py),
+                                                   float(eff_cut), _enc(tf)), num_snp, rows, temp_file)
+    dist.root_call(_append_p, temp_file, out_file, lambda i, j: var_app)
     return 0
 
 
@@ -124,18 +155,20 @@ def run_maf_eff(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0=None
     chi_cut = chi2.isf(p_cut, 1)
     eff_cut = np.ascontiguousarray(np.sqrt(chi_cut * np.asarray(freq_deno, dtype=float)))
     if kind != "AD":
-        np.savetxt("eff_cut", eff_cut)  # remma_epiAA_maf_eff.py:79 (written to the working directory)
+        # remma_epiAA_maf_eff.py:79 (written to the working directory)
+        dist.root_call(np.savetxt, "eff_cut", eff_cut)
     temp_file = out_file + ".temp"
     logging.info("Test")
-    if kind == "AD":
-        args = (_enc(bed_file), num_id, num_snp, N.ptr(rows), rows.size, N.ptr(py), N.ptr(freq_i), N.ptr(freq_j),
-                N.ptr(eff_cut), _enc(temp_file))
-    else:
-        args = (_enc(bed_file), num_id, num_snp, N.ptr(rows), rows.size, N.ptr(py), N.ptr(freq_i), N.ptr(eff_cut),
-                _enc(temp_file))
-    _screen(_SYM_MAF[kind], args, temp_file)
+
+    def make_args(r, tf):
+        if kind == "AD":
+            return (_enc(bed_file), num_id, num_snp, N.ptr(r), r.size, N.ptr(py), N.ptr(freq_i), N.ptr(freq_j),
+                    N.ptr(eff_cut), _enc(tf))
+        return (_enc(bed_file), num_id, num_snp, N.ptr(r), r.size, N.ptr(py), N.ptr(freq_i), N.ptr(eff_cut), _enc(tf))
+
+    _screen_parts(kind, _SYM_MAF[kind], make_args, num_snp, rows, temp_file)
     deno = np.asarray(freq_deno, dtype=float)
-    _append_p(temp_file, out_file, lambda i, j: deno[freq_i[i] * 10 + freq_j[j]])
+    dist.root_call(_append_p, temp_file, out_file, lambda i, j: deno[freq_i[i] * 10 + freq_j[j]])
     return 0
 
 
@@ -167,11 +200,13 @@ def _pheno_pairs(kind, pheno_file, bed_file, gmat_lst, var_com, pair_file, out_f
     return run_pairs(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, pair_file, 50000, 1, out_file)
 
 
+@dist.on_root
 def _random(kind, num_snp, out_file, num_pair, seed):
     fn = random_pairAD if kind == "AD" else random_pair
     return fn(num_snp, out_file=out_file, num_pair=num_pair, seed=seed)
 
 
+@dist.on_root
 def _merge(approx_file, exact_file, out_file):
     """remma_epiAA_approx.py:40-53: insert p_app before the exact p of every exact_p line."""
     logging.info("\n\n#####Merge the results#####")
@@ -189,6 +224,16 @@ def _merge(approx_file, exact_file, out_file):
     os.remove(exact_file)
 
 
+@dist.on_root
+def _median_var(random_file, pair_file):
+    """Median exact variance of the random pairs (remma_epiAA_approx.py:24-27); both files removed."""
+    res_df = pd.read_csv(random_file, header=0, sep=r"\s+")
+    var_median = np.median(res_df["var"])
+    os.remove(pair_file)
+    os.remove(random_file)
+    return var_median
+
+
 def run_approx(kind, pheno_file, bed_file, gmat_lst, var_com, p_cut=1.0e-5, num_random_pair=100000,
                out_file="epiAA_approx", parallel=None, seed=None):
     """remma_epiXX_approx (remma_epiAA_approx.py:10-53) and its _parallel form (:56-101):
@@ -200,10 +245,7 @@ def run_approx(kind, pheno_file, bed_file, gmat_lst, var_com, p_cut=1.0e-5, num_
     rp = out_file + ".random_pair" + sfx
     _random(kind, num_snp, rp, num_random_pair, seed)
     _pheno_pairs(kind, pheno_file, bed_file, gmat_lst, var_com, rp, out_file + ".random" + sfx)
-    res_df = pd.read_csv(out_file + ".random" + sfx, header=0, sep=r"\s+")
-    var_median = np.median(res_df["var"])
-    os.remove(rp)
-    os.remove(out_file + ".random" + sfx)
+    var_median = _median_var(out_file + ".random" + sfx, rp)
     logging.info("\n\n#####Screen the epistatic effects and select top SNP pairs based on approximate test#####")
     y, xmat, zmat = design_matrix_wemai_multi_gmat(pheno_file, bed_file)
     if parallel is None:
@@ -221,6 +263,7 @@ def run_approx(kind, pheno_file, bed_file, gmat_lst, var_com, p_cut=1.0e-5, num_
     return 0
 
 
+@dist.on_root
 def _freq_classes(kind, bed_file, out_file, sfx):
     """Frequency classes of remma_epiAA_maf_approx.py:32-41 (AA: minor allele frequency),
     remma_epiDD_maf_approx.py:33-44 (DD: heterozygosity) and remma_epiAD_maf_approx.py:33-50
@@ -251,6 +294,7 @@ def _freq_classes(kind, bed_file, out_file, sfx):
     return np.array(freq_a * 20, dtype=np.longlong), np.array(freq_d * 20, dtype=np.longlong)
 
 
+@dist.on_root
 def _class_denominators(kind, random_file, freq_i, freq_j, deno_file):
     """Mean exact variance per (class_i, class_j) of the random pairs, both orientations for
     AA / DD (remma_epiAA_maf_approx.py:43-71), (A class of snp_0, D class of snp_1) for AD
@@ -295,7 +339,7 @@ def run_maf_approx(kind, pheno_file, bed_file, gmat_lst, var_com, p_cut=1.0e-5, 
     rp = out_file + (".random_pairAD" if (kind == "AD" and parallel is None) else ".random_pair") + sfx
     _random(kind, num_snp, rp, num_random_pair, seed)
     _pheno_pairs(kind, pheno_file, bed_file, gmat_lst, var_com, rp, out_file + ".random" + sfx)
-    os.remove(rp)
+    dist.root_call(os.remove, rp)
     logging.info("\n\n#####Calcualte the approximate denominator for Wald chi-square test#####")
     freq_i, freq_j = _freq_classes(kind, bed_file, out_file, sfx)
     freq_deno = _class_denominators(kind, out_file + ".random" + sfx, freq_i, freq_j,

@@ -15,7 +15,8 @@ import numpy as np
 from scipy.stats import chi2
 
 from .. import _native as N
-from ..plink import Geno, count_lines
+from .. import dist
+from ..plink import count_lines
 from ..uvlmm.uvlmm_varcom import projection
 
 KINDS = {"AA": N.GMAT_AA, "AD": N.GMAT_AD, "DD": N.GMAT_DD}
@@ -169,18 +170,22 @@ LAST_PHASES = {}
 
 
 def open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file, phases=None):
-    """P / Py on the device (remma_epiAA.py:33-49), genotype panel decoded on the device."""
+    """P / Py on the device (remma_epiAA.py:33-49), genotype panel decoded on the device.
+    As a rank of a multi-rank job (dist.job): P / Py computed on rank 0 and broadcast, the panel read
+    shard by shard and all-gathered, the plan's spectral state computed on rank 0 and imported by the
+    other ranks (dist.shared_plan)."""
     phases = {} if phases is None else phases
     logging.info("Calculate the phenotypic covariance matrix and inversion")
     t0 = time.perf_counter()
-    pvp, py = projection(y, xmat, zmat, gmat_lst, var_com)
+    pvp, py = dist.root_call(projection, y, xmat, zmat, gmat_lst, var_com)
     t1 = time.perf_counter()
-    geno = Geno(bed_file)
+    geno = dist.load_geno(bed_file)
     t2 = time.perf_counter()
     phases["projection"], phases["decode"] = t1 - t0, t2 - t1
     if geno.n != pvp.shape[0]:
+        geno.close()
         raise ValueError("Z has %d individuals, the .fam has %d" % (pvp.shape[0], geno.n))
-    plan = EpiPlan(geno, pvp, py)
+    plan = dist.shared_plan(geno, pvp, py)
     phases["plan"] = time.perf_counter() - t2
     return plan
 
@@ -216,19 +221,29 @@ def resolve_rows(kind, num_snp, snp_lst_0):
     return rows
 
 
+def _no_hits():
+    return (np.zeros(0, np.int64), np.zeros(0, np.int64)) + tuple(np.zeros(0) for _ in range(4))
+
+
 def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut, out_file):
     """_remma_epiXX: header, then the hits of each row of snp_lst_0 in list order (the
-    reference appends each row's hits with j ascending)."""
-    with open(out_file, "w") as f:
-        f.write(SCAN_HEADER + "\n")
+    reference appends each row's hits with j ascending).
+    As a multi-rank job (dist.job): the rows are sharded over the ranks (the folded split of the
+    whole triangle, dist.rank_rows, or equal pair counts of a given list), the hits are merged on
+    rank 0 and rank 0 alone writes out_file -- the bytes a single process writes."""
+    rank, ws = dist.job()
+    if rank == 0:
+        with open(out_file, "w") as f:
+            f.write(SCAN_HEADER + "\n")
     num_snp = count_lines(bed_file + ".bim")
     rows = resolve_rows(kind, num_snp, snp_lst_0)
     phases = {}
     plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file, phases)
     try:
         uniq = np.unique(rows)
+        mine = dist.shard_rows(kind, num_snp, uniq, rank, ws)
         t0 = time.perf_counter()
-        hi, hj, eff, var, chi, p = plan.scan(kind, uniq, p_cut)
+        local = plan.scan(kind, mine, p_cut) if mine.size else _no_hits()
         phases["scan"] = time.perf_counter() - t0
         logging.info("Running time: Clock time, {:.5f} sec.".format(phases["scan"]))
         logging.info("scan stats: %s" % plan.stats())
@@ -237,16 +252,24 @@ def run_scan(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_lst_0, p_cut,
         plan.close()
         plan.geno.close()
         phases["release"] = time.perf_counter() - t0
-    if rows.size == uniq.size and np.all(np.diff(rows) > 0):
-        order = np.arange(hi.size)
-    else:  # replay the caller's row order (and duplicates) like the reference's loop
-        starts = np.searchsorted(hi, uniq, side="left")
-        ends = np.searchsorted(hi, uniq, side="right")
-        pos = np.searchsorted(uniq, rows)
-        order = np.concatenate([np.arange(starts[k], ends[k]) for k in pos]) if rows.size else np.zeros(0, int)
-    t0 = time.perf_counter()
-    append_rows(out_file, [hi[order], hj[order], eff[order], chi[order], p[order]], 3)
-    phases["write"] = time.perf_counter() - t0
+    if ws > 1:
+        t0 = time.perf_counter()
+        local = dist.gather_hits(local)
+        phases["gather"] = time.perf_counter() - t0
+    if rank == 0:
+        hi, hj, eff, var, chi, p = local
+        if rows.size == uniq.size and np.all(np.diff(rows) > 0):
+            order = np.arange(hi.size)
+        else:  # replay the caller's row order (and duplicates) like the reference's loop
+            starts = np.searchsorted(hi, uniq, side="left")
+            ends = np.searchsorted(hi, uniq, side="right")
+            pos = np.searchsorted(uniq, rows)
+            order = np.concatenate([np.arange(starts[k], ends[k]) for k in pos]) if rows.size else np.zeros(0, int)
+        t0 = time.perf_counter()
+        append_rows(out_file, [hi[order], hj[order], eff[order], chi[order], p[order]], 3)
+        phases["write"] = time.perf_counter() - t0
+    if ws > 1:
+        dist.barrier()  # out_file is complete when any rank returns
     LAST_PHASES.clear()
     LAST_PHASES.update(phases)
     return 0
@@ -284,24 +307,55 @@ def read_pair_file(snp_pair_file):
     return np.array(out, dtype=np.int64).reshape(-1, 2)
 
 
+_PAIR_REC = np.dtype([("eff", "<f8"), ("var", "<f8"), ("chi", "<f8"), ("p", "<f8")])
+
+
 def run_pairs(kind, y, xmat, zmat, gmat_lst, var_com, bed_file, snp_pair_file, max_test_pair, p_cut, out_file):
     """_remma_epiXX_pair (remma_epiAA_pair.py:16-92): exact statistics of the listed pairs,
-    rows with p < p_cut in file order, columns snp_0 snp_1 eff var chi p."""
+    rows with p < p_cut in file order, columns snp_0 snp_1 eff var chi p.  The reference tests
+    max_test_pair pairs at a time and stops at the first chunk holding an out-of-range SNP (the
+    earlier chunks' rows are written, then ValueError).
+    As a multi-rank job: the valid prefix of the list is cut into contiguous equal runs, one per rank
+    (each tested max_test_pair at a time), the statistics are gathered in list order on rank 0, and
+    rank 0 alone writes out_file."""
+    rank, ws = dist.job()
     pairs = read_pair_file(snp_pair_file)
     num_snp = count_lines(bed_file + ".bim")
+    step = max(1, int(max_test_pair))
+    n_ok = pairs.shape[0]
+    for t0 in range(0, pairs.shape[0], step):
+        chunk = pairs[t0:t0 + step]
+        if chunk.size and (chunk.max() > num_snp - 1 or chunk.min() < 0):
+            n_ok = t0
+            break
     plan = open_plan(y, xmat, zmat, gmat_lst, var_com, bed_file)
-    with open(out_file, "w") as f:
-        f.write(PAIR_HEADER + "\n")
+    if rank == 0:
+        with open(out_file, "w") as f:
+            f.write(PAIR_HEADER + "\n")
     try:
-        for t0 in range(0, pairs.shape[0], max(1, int(max_test_pair))):
-            chunk = pairs[t0:t0 + int(max_test_pair)]
-            if chunk.size and (chunk.max() > num_snp - 1 or chunk.min() < 0):
-                logging.error("snp_pair is out of range!")
-                raise ValueError("snp_pair is out of range!")
-            eff, var, chi, p = plan.pairs(kind, chunk)
-            keep = p < p_cut
-            append_rows(out_file, [chunk[keep, 0], chunk[keep, 1], eff[keep], var[keep], chi[keep], p[keep]], 4)
+        b = dist.split_weighted(np.ones(n_ok), ws)
+        mine = pairs[b[rank]:b[rank + 1]]
+        rec = np.zeros(mine.shape[0], dtype=_PAIR_REC)
+        for t0 in range(0, mine.shape[0], step):
+            res = plan.pairs(kind, mine[t0:t0 + step])
+            for name, col in zip(_PAIR_REC.names, res):
+                rec[name][t0:t0 + step] = col
+            if ws == 1:  # a single process writes chunk by chunk, as the reference
+                keep = rec["p"][t0:t0 + step] < p_cut
+                sub = mine[t0:t0 + step]
+                append_rows(out_file, [sub[keep, 0], sub[keep, 1]] +
+                            [rec[nm][t0:t0 + step][keep] for nm in _PAIR_REC.names], 4)
     finally:
         plan.close()
         plan.geno.close()
+    if ws > 1:
+        rec = dist.gather_records(rec)
+        if rank == 0:
+            keep = rec["p"] < p_cut
+            sub = pairs[:n_ok]
+            append_rows(out_file, [sub[keep, 0], sub[keep, 1]] + [rec[nm][keep] for nm in _PAIR_REC.names], 4)
+        dist.barrier()
+    if n_ok < pairs.shape[0]:
+        logging.error("snp_pair is out of range!")
+        raise ValueError("snp_pair is out of range!")
     return 0

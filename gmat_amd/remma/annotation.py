@@ -1,6 +1,8 @@
 """Hit annotation -- drop-in for gmat.remma.annotation.annotation_snp_pos (annotation.py:22-73)."""
+from .. import dist
 
 
+@dist.on_root
 def annotation_snp_pos(res_file, bed_file, p_cut=1, dis=0, ld_file=None, r2=0.2):
     """Rewrite res_file's header with .bim columns and keep rows with p <= p_cut whose SNPs
     are on different chromosomes or more than `dis` bp apart; writes res_file + '.anno'

@@ -4,6 +4,8 @@ import logging
 
 import numpy as np
 
+from .. import dist
+
 
 def _draw(num_snp, out_file, num_pair, num_each_pair, accept, seed):
     rng = np.random.default_rng(seed) if seed is not None else np.random
@@ -23,6 +25,7 @@ def _draw(num_snp, out_file, num_pair, num_each_pair, accept, seed):
     return res
 
 
+@dist.on_root
 def random_pair(num_snp, out_file="random_pair", num_pair=100000, num_each_pair=5000, seed=None):
     """Unique random pairs i < j (AA / DD); writes out_file and returns the (num_pair, 2) array."""
     if num_pair > num_snp * (num_snp - 1) / 2:
@@ -32,6 +35,7 @@ def random_pair(num_snp, out_file="random_pair", num_pair=100000, num_each_pair=
     return _draw(num_snp, out_file, num_pair, num_each_pair, lambda a: a[:, 0] < a[:, 1], seed)
 
 
+@dist.on_root
 def random_pairAD(num_snp, out_file="random_pair", num_pair=100000, num_each_pair=5000, seed=None):
     """Unique random ordered pairs i != j (AD)."""
     if num_pair > num_snp * (num_snp - 1):

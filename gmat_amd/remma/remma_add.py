@@ -10,6 +10,7 @@ import pandas as pd
 from scipy.stats import chi2
 
 from .. import _native as N
+from .. import dist
 from ..plink import Geno
 from ..uvlmm.design_matrix import design_matrix_wemai_multi_gmat
 from ..uvlmm.uvlmm_varcom import projection
@@ -51,6 +52,7 @@ def single_snp_table(bed_file, xpy, xpx, scale, sigma):
     return res_df
 
 
+@dist.on_root
 def _remma_add(y, xmat, zmat, gmat_lst, var_com, bed_file, out_file='remma_add'):
     """Writes out_file ('chro snp_ID pos allele1 allele2 eff_val chi_val eff_val_to_fixed p_val')
     and returns the DataFrame.  var_com[0] is the additive variance."""

@@ -4,11 +4,13 @@ s = 2p(1-p), and var_com[1] as the dominance variance.  Device work as in remma_
 import logging
 
 from .. import _native as N
+from .. import dist
 from ..uvlmm.design_matrix import design_matrix_wemai_multi_gmat
 from ..uvlmm.uvlmm_varcom import projection
 from .remma_add import single_snp_table, snp_products
 
 
+@dist.on_root
 def _remma_dom(y, xmat, zmat, gmat_lst, var_com, bed_file, out_file='remma_dom'):
     logging.info("Calculate the phenotypic covariance matrix and inversion")
     pvp, py = projection(y, xmat, zmat, gmat_lst, var_com)

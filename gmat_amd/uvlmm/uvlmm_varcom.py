@@ -10,6 +10,7 @@ import logging
 import numpy as np
 
 from .. import _native as N
+from .. import dist
 from .design_matrix import design_matrix_wemai_multi_gmat, design_matrix_wemai_multi_gmat_pred, z_columns
 
 
@@ -22,6 +23,7 @@ def _gmat_ptrs(gmat_lst, n_id):
     return mats, arr
 
 
+@dist.on_root
 def _wemai_multi_gmat(y, xmat, zmat, gmat_lst, init=None, maxiter=200, cc_par=1.0e-8, cc_gra=1.0e-6):
     """Estimate the variance components (residual last).  Same arguments and result as
     uvlmm_varcom.py:8."""
@@ -54,6 +56,7 @@ def _wemai_multi_gmat(y, xmat, zmat, gmat_lst, init=None, maxiter=200, cc_par=1.
     return var
 
 
+@dist.on_root
 def wemai_multi_gmat(pheno_file, bed_file, gmat_lst, init=None, maxiter=200, cc_par=1.0e-8, cc_gra=1.0e-6,
                      out_file="wemai_multi_gmat.var"):
     """uvlmm_varcom.py:107-126: design matrices, REML, np.savetxt(out_file, var_com)."""
@@ -63,6 +66,7 @@ def wemai_multi_gmat(pheno_file, bed_file, gmat_lst, init=None, maxiter=200, cc_
     return var_com
 
 
+@dist.on_root
 def predict_random(y, xmat, zmat, gmat_lst, var_com):
     """rand_eff (n_id x len(gmat_lst)) of wemai_multi_gmat_pred (uvlmm_varcom.py:147-165), on the
     device (gmat_blup), with the reference's formula as written there."""
@@ -81,6 +85,7 @@ def predict_random(y, xmat, zmat, gmat_lst, var_com):
     return out
 
 
+@dist.on_root
 def wemai_multi_gmat_pred(pheno_file, bed_file, gmat_lst, init=None, maxiter=200, cc_par=1.0e-8, cc_gra=1.0e-6,
                           out_file='wemai_multi_gmat_pred'):
     """uvlmm_varcom.py:129-167: REML with genotyped-but-unphenotyped ids kept in Z, then the
@@ -94,6 +99,7 @@ def wemai_multi_gmat_pred(pheno_file, bed_file, gmat_lst, init=None, maxiter=200
     return var_com
 
 
+@dist.on_root
 def projection(y, xmat, zmat, gmat_lst, var_com):
     """(Z'PZ, Z'Py) of the scans' setup (remma_epiAA.py:33-49), computed on the device."""
     lib = N.ensure_device()
