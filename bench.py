@@ -771,15 +771,19 @@ def main():
                     "issued_ops_per_launch": kr["ops_per_launch"], "kernels": kern_rec,
                     "fp64_equiv_tflops": total_pairs * (2.0 * n * n + 5 * n) / (t_max / args.steps) / 1e12}
         if dom == "prefilter_pass_kernel":
-            # the prefilter's other roof: every tile streams 18 KB per 64-individual stage (+ 10 KB of
+            # the prefilter's other roof: every tile streams its stage image per 64 individuals (+ its
             # test records) from L2 / MALL into LDS by LDS-DMA, and the chip moves ~6.4 TB/s of
-            # LDS-DMA with every CU streaming (MI355X_MICROARCH.md, ldsdma-fill)
-            n_pad_ = -(-n // 256) * 256  # the panel padding (geno.hip: round_up(n_id, 256))
-            tiles_per_launch = kr["ops_per_launch"] / (16.0 * n_pad_) / (64 * 256)
-            dma_bytes = tiles_per_launch * (n_pad_ / 64 * 18432 + 10240)
+            # LDS-DMA with every CU streaming (MI355X_MICROARCH.md, ldsdma-fill); the tile shape and
+            # bytes are the plan's (gmat_epi_info)
+            pi = plan.info()
+            n_pad_ = pi["n_pad"]
+            tiles_per_launch = kr["ops_per_launch"] / (16.0 * n_pad_) / (pi["pf_tile_rows"] * pi["pf_tile_cols"])
+            dma_bytes = tiles_per_launch * (n_pad_ / 64 * pi["pf_stage_dma_bytes"] + pi["pf_tile_record_bytes"])
             dma_tbps = dma_bytes / (kr["avg_launch_ms"] * 1e-3) / 1e12
             roofline["lds_dma"] = {"bytes_per_launch": dma_bytes, "achieved_TBps": dma_tbps, "peak_TBps": LDS_DMA_PEAK_TBPS,
-                                   "frac": dma_tbps / LDS_DMA_PEAK_TBPS, "tiles_per_launch": tiles_per_launch}
+                                   "frac": dma_tbps / LDS_DMA_PEAK_TBPS, "tiles_per_launch": tiles_per_launch,
+                                   "tile": [pi["pf_tile_rows"], pi["pf_tile_cols"]],
+                                   "stage_bytes": pi["pf_stage_dma_bytes"], "record_bytes": pi["pf_tile_record_bytes"]}
     else:  # a level without per-kernel accounting (int8 / MX screens): the screen kernel's own stats
         avg_launch_s = screen_s / max(launches, 1)
         achieved = ops / max(launches, 1) / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0

@@ -196,22 +196,18 @@ int pipeline_stream(int role, hipStream_t *out) {
   std::lock_guard<std::mutex> lk(mu);
   std::vector<hipStream_t> &v = sets[dev];
   if (v.empty()) {
-    // GMAT_STREAM_ORDER (diagnostics): the roles in creation order, e.g. "0,1,3,2,4"
-    int order[NR] = {0, 1, 2, 3, 4};
-    if (const char *o = getenv("GMAT_STREAM_ORDER")) {
-      int k = 0, seen = 0;
-      for (const char *c = o; *c && k < NR; ++c)
-        if (*c >= '0' && *c < '0' + NR && !(seen >> (*c - '0') & 1)) {
-          order[k++] = *c - '0';
-          seen |= 1 << (*c - '0');
-        }
-      if (k != NR) {
-        set_error("GMAT_STREAM_ORDER=%s: a permutation of 0..%d", o, NR - 1);
-        return GMAT_E_ARG;
+    // created into a local set, committed only when all five exist (a partial set would hand later
+    // plans the null stream for the missing roles)
+    hipStream_t made[NR] = {};
+    for (int k = 0; k < NR; ++k) {
+      const hipError_t err = hipStreamCreateWithFlags(&made[k], hipStreamNonBlocking);
+      if (err != hipSuccess) {
+        for (int q = 0; q < k; ++q) (void)hipStreamDestroy(made[q]);
+        set_error("pipeline_stream: hipStreamCreateWithFlags: %s", hipGetErrorString(err));
+        return GMAT_E_HIP;
       }
     }
-    v.assign(NR, nullptr);
-    for (int k = 0; k < NR; ++k) GMAT_HIP(hipStreamCreateWithFlags(&v[order[k]], hipStreamNonBlocking));
+    v.assign(made, made + NR);
   }
   *out = v[role];
   return GMAT_OK;

@@ -196,45 +196,6 @@ __device__ __forceinline__ bool factor_invert_block(double (*Ls)[NB + 1], double
   return bad;
 }
 
-__global__ __launch_bounds__(256) void potf2_kernel(int kb, double *a, int64_t lda, double *dinv, double *logdet,
-                                                    int *info, int64_t k0) {
-  constexpr int PW = 16, NP = NB / PW;
-  __shared__ double Ls[NB][NB + 1];
-  __shared__ double Xs[NB][NB + 1];
-  __shared__ double piv[NB];  // L_jj (log-determinant summed at the end, off the pivot chain)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  {  // the block's 16 values per thread: all loads issued before the first LDS store (a load-store loop
-     // waited for each load in turn: ~16 memory latencies per launch)
-    double v[NB * NB / 256];
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
-      v[u] = (rr < kb && cc < kb) ? a[(int64_t)rr * lda + cc] : (rr == cc ? 1.0 : 0.0);
-    }
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int e = tid + 256 * u, rr = e / NB, cc = e % NB;
-      Ls[rr][cc] = v[u];
-      Xs[rr][cc] = 0.0;
-    }
-  }
-  __syncthreads();
-  const bool bad = factor_invert_block(Ls, Xs, piv, kb);
-  for (int e = tid; e < kb * NB; e += 256) {
-    const int r2 = e / NB, c2 = e % NB;
-    if (c2 < kb) a[(int64_t)r2 * lda + c2] = Ls[r2][c2];
-    dinv[r2 * NB + c2] = (c2 < kb) ? Xs[r2][c2] : 0.0;
-  }
-  if (w == 0) {  // sum of log L_jj over the block, one log per lane, fixed shuffle tree
-    double lg = log(piv[lane]);
-    for (int off = 32; off > 0; off >>= 1) lg += __shfl_xor(lg, off);
-    if (lane == 0) {
-      *logdet += 2.0 * lg;
-      if (bad && *info == 0) *info = (int)(k0 + 1);
-    }
-  }
-}
-
 // ---- One launch per 64-column step (cholesky_steps): the factorisation, the inverses of its diagonal
 // blocks and optionally X = L^-1 and V^-1 = X'X, without cholesky_inverse()'s chain of small dependent
 // launches (potf2, panel solve, trailing update and the inverse's two products per step, each a few
@@ -599,90 +560,14 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
 }
 
 int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev) {
-  static const bool dgemm_path = getenv("GMAT_CHOL_DGEMM") != nullptr;  // the former path, for comparison
-  if (!dgemm_path) return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, nullptr, true, nullptr);
-  GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
-  GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
-  for (int64_t k0 = 0; k0 < n; k0 += NB) {
-    const int kb = (int)std::min<int64_t>(NB, n - k0);
-    double *akk = a + k0 * lda + k0;
-    hipLaunchKernelGGL(potf2_kernel, dim3(1), dim3(256), 0, s, kb, akk, lda, dinv + k0 * NB, logdet_dev, info_dev,
-                       k0);
-    GMAT_HIP(hipGetLastError());
-    const int64_t rem = n - k0 - kb;
-    if (rem <= 0) continue;
-    double *panel = a + (k0 + kb) * lda + k0;
-    // L21 = A21 * inv(L11)'   (in place: one 64-wide column tile per row block)
-    GMAT_TRY(dgemm(s, rem, kb, kb, 1.0, DView{panel, lda, 0}, DView{dinv + k0 * NB, NB, 1}, 0.0, panel, lda));
-    // A22 -= L21 L21'  (lower tiles)
-    double *a22 = a + (k0 + kb) * lda + (k0 + kb);
-    GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a22, lda, 1));
-  }
-  return GMAT_OK;
+  return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, nullptr, true, nullptr);
 }
 
-// The factorisation and L^-1 (linv, n x n, lower): cholesky_steps; GMAT_CHOL_DGEMM=1 runs the former
-// path for comparison -- cholesky() with the inverse's block steps (chol_lower_inverse) on a second stream,
-// each step as soon as its panel is solved.  The inverse is computed even if a pivot fails (the caller
-// checks *info_dev).
+// The factorisation and L^-1 (linv, n x n, lower) by cholesky_steps; a is scratch.  The inverse is computed
+// even if a pivot fails (the caller checks *info_dev).
 int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
                      double *linv, double *vinv) {
-  static const bool dgemm_path = getenv("GMAT_CHOL_DGEMM") != nullptr;
-  if (!dgemm_path) return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, linv, false, vinv);
-  static std::mutex mu;
-  static hipStream_t side[64] = {nullptr};
-  static std::vector<hipEvent_t> evs[64];
-  int dev = 0;
-  GMAT_HIP(hipGetDevice(&dev));
-  GMAT_CHECK(dev >= 0 && dev < 64, GMAT_E_ARG, "cholesky_inverse: device %d", dev);
-  std::lock_guard<std::mutex> lock(mu);
-  if (!side[dev]) GMAT_HIP(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
-  const hipStream_t s2 = side[dev];
-  const int64_t nb = cdiv(n, NB);
-  // ev[0]: start, ev[1 + i]: panel i solved, ev[nb + 1]: inverse done
-  while ((int64_t)evs[dev].size() < nb + 2) {
-    hipEvent_t e;
-    GMAT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    evs[dev].push_back(e);
-  }
-  hipEvent_t *ev = evs[dev].data();
-  GMAT_HIP(hipMemsetAsync(logdet_dev, 0, sizeof(double), s));
-  GMAT_HIP(hipMemsetAsync(info_dev, 0, sizeof(int), s));
-  GMAT_HIP(hipEventRecord(ev[0], s));
-  GMAT_HIP(hipStreamWaitEvent(s2, ev[0], 0));  // after the caller's earlier work on s
-  hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(n * n, 256)), dim3(256), 0, s2, linv, n * n);
-  GMAT_HIP(hipGetLastError());
-  for (int64_t k0 = 0, i = 0; k0 < n; k0 += NB, ++i) {
-    const int kb = (int)std::min<int64_t>(NB, n - k0);
-    double *akk = a + k0 * lda + k0;
-    hipLaunchKernelGGL(potf2_kernel, dim3(1), dim3(256), 0, s, kb, akk, lda, dinv + k0 * NB, logdet_dev, info_dev, k0);
-    GMAT_HIP(hipGetLastError());
-    const int64_t rem = n - k0 - kb;
-    double *panel = a + (k0 + kb) * lda + k0;
-    if (rem > 0)  // L21 = A21 * inv(L11)'
-      GMAT_TRY(dgemm(s, rem, kb, kb, 1.0, DView{panel, lda, 0}, DView{dinv + k0 * NB, NB, 1}, 0.0, panel, lda));
-    GMAT_HIP(hipEventRecord(ev[1 + i], s));
-    // inverse step i on the side stream (chol_lower_inverse's loop body)
-    GMAT_HIP(hipStreamWaitEvent(s2, ev[1 + i], 0));
-    double *xi = linv + k0 * n;
-    if (k0 > 0) GMAT_TRY(dgemm(s2, kb, k0, kb, 1.0, DView{dinv + k0 * NB, NB, 0}, DView{xi, n, 0}, 0.0, xi, n));
-    hipLaunchKernelGGL(copy_block_kernel, dim3(kb), dim3(NB), 0, s2, kb, dinv + k0 * NB, xi + k0, n);
-    GMAT_HIP(hipGetLastError());
-    if (rem > 0) {
-      GMAT_TRY(dgemm(s2, rem, k0 + kb, kb, -1.0, DView{a + (k0 + kb) * lda + k0, lda, 0}, DView{xi, n, 0}, 1.0,
-                     linv + (k0 + kb) * n, n));
-      // A22 -= L21 L21'  (lower tiles)
-      GMAT_TRY(dgemm(s, rem, rem, kb, -1.0, DView{panel, lda, 0}, DView{panel, lda, 1}, 1.0, a + (k0 + kb) * lda + k0 + kb,
-                     lda, 1));
-    }
-  }
-  GMAT_HIP(hipEventRecord(ev[nb + 1], s2));
-  GMAT_HIP(hipStreamWaitEvent(s, ev[nb + 1], 0));
-  if (vinv) {  // V^-1 = L^-T L^-1 (lower tiles, then mirrored)
-    GMAT_TRY(dgemm(s, n, n, n, 1.0, DView{linv, n, 1}, DView{linv, n, 0}, 0.0, vinv, n, 2));
-    GMAT_TRY(fill_sym_upper(s, n, vinv, n));
-  }
-  return GMAT_OK;
+  return cholesky_steps(s, n, a, lda, dinv, logdet_dev, info_dev, linv, false, vinv);
 }
 
 int chol_lower_inverse(hipStream_t s, int64_t n, const double *l, int64_t ldl, const double *dinv, double *linv) {

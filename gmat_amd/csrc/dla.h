@@ -41,9 +41,7 @@ int cholesky(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, dou
 int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
                    double *linv, bool keep_l = true, double *vinv = nullptr);
 // L^-1 into linv, optionally A^-1 into vinv (both triangles), log|A| and the pivot check, a used as
-// scratch: cholesky_steps (GMAT_CHOL_DGEMM=1:
-// cholesky() with chol_lower_inverse's block steps on a second stream, L left in a); ordered after the
-// caller's earlier work on s.
+// scratch (cholesky_steps); ordered after the caller's earlier work on s.
 int cholesky_inverse(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
                      double *linv, double *vinv = nullptr);
 // linv = L^-1 (n x n, lower triangle; the upper triangle is zeroed) from the factor and its

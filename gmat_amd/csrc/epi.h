@@ -246,7 +246,7 @@ __device__ __forceinline__ void lds_dma16(const void *g, const void *lds) {
 // DMA source address (chunk ^ (row >> 2) & 3); the image holds DMA instruction q (1 KB) at q KB, wave w
 // issuing q = w + 8u (u < 2; waves 0-4 two, 5-7 one).  Round 5: by default 32 x 256 tiles of four
 // waves (1 row x 4 column waves, a 9 KB stage), two workgroups per CU (prefilter_pass_kernel<.., 32, 5>);
-// the constants below are the 64-row shape's (GMAT_PF_TR=64, the block-granular path).
+// the constants below are the 64-row shape's (eight waves: the block-granular path).
 constexpr int PF_TR = 64, PF_TC = 256, PF_ST = 13 * 1024, PF_NS = 5, PF_NQ = 13;
 constexpr int PF_REC = 8;  // floats per prefilter test record (pf_rec_kernel)
 constexpr int PF_CHUNK = 128;  // live-pair records a persistent prefilter wave reserves at a time

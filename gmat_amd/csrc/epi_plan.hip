@@ -1049,13 +1049,20 @@ extern "C" int gmat_epi_setup_stats(const gmat_epi *e, double *out8) {
   return GMAT_OK;
 }
 
-extern "C" int gmat_epi_info(const gmat_epi *e, double *out4) {
-  GMAT_CHECK(e && out4, GMAT_E_ARG, "gmat_epi_info: bad arguments");
-  if (e->seg) return gmat_epi_info(seg_base(e), out4);
-  out4[0] = e->lr_R;
-  out4[1] = e->lr_lam;
-  out4[2] = e->pf_mu;
-  out4[3] = (double)e->n_pad;
+extern "C" int gmat_epi_info(const gmat_epi *e, double *out8) {
+  GMAT_CHECK(e && out8, GMAT_E_ARG, "gmat_epi_info: bad arguments");
+  if (e->seg) return gmat_epi_info(seg_base(e), out8);
+  out8[0] = e->lr_R;
+  out8[1] = e->lr_lam;
+  out8[2] = e->pf_mu;
+  out8[3] = (double)e->n_pad;
+  // prefilter_pass_kernel<.., 32, 5> (epi_prefilter.hip): per stage four 1 KB DMAs of the two int8 L3
+  // slices, four of the 256 columns' 2-bit codes and one of the 32 rows' codes (twice); per tile the
+  // 32-byte test records of its 32 rows and 256 columns
+  out8[4] = 32;
+  out8[5] = PF_TC;
+  out8[6] = 9 * 1024;
+  out8[7] = (32 + PF_TC) * PF_REC * sizeof(float);
   return GMAT_OK;
 }
 

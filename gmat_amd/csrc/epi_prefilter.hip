@@ -834,18 +834,12 @@ __global__ __launch_bounds__(TC * 2, TC == PC_TC ? 1 : 2) void prefilter_cov_ker
 template __global__ void side_gemm_kernel<2>(SideArgs);
 template __global__ void side_gemm_kernel<3>(SideArgs);
 template __global__ void side_gemm_kernel<4>(SideArgs);
-template __global__ void prefilter_pass_kernel<true, true, false, 64, PF_NS>(SideArgs);
-template __global__ void prefilter_pass_kernel<true, true, true, 64, PF_NS>(SideArgs);
 template __global__ void prefilter_pass_kernel<false, false, false, 64, PF_NS>(SideArgs);
 template __global__ void prefilter_pass_kernel<true, true, false, 32, 5>(SideArgs);
 template __global__ void prefilter_pass_kernel<true, true, true, 32, 5>(SideArgs);
-template __global__ void prefilter_cov_kernel<1, true, 256>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, false, 256>(SideArgs);
-template __global__ void prefilter_cov_kernel<2, true, 256>(SideArgs);
 template __global__ void prefilter_cov_kernel<2, false, 256>(SideArgs);
-template __global__ void prefilter_cov_kernel<3, true, 256>(SideArgs);
 template __global__ void prefilter_cov_kernel<3, false, 256>(SideArgs);
-template __global__ void prefilter_cov_kernel<4, true, 256>(SideArgs);
 template __global__ void prefilter_cov_kernel<4, false, 256>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, true, 128>(SideArgs);
 template __global__ void prefilter_cov_kernel<1, false, 128>(SideArgs);

@@ -430,17 +430,9 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // plus a short lone middle chunk.  One-box A/Bs (bench split rehearsal, twice): 2 / 4 / 8-way parts
   // 8.62-8.69 / 4.29-4.34 / 2.42-2.48 ms against 8.78-8.85 / 4.42-4.60 / 2.47-2.52; the configs[2] step
   // (13 launches) keeps the RL-row launches and its half-size last launch (16.05-16.14 against
-  // 16.35-16.43 ms).  GMAT_FOLD_EVEN forces it: 0 off, 1 on, 2 an odd number of equal chunks (the last
-  // launch one lone chunk: no better than off)
+  // 16.35-16.43 ms; an odd number of equal chunks, the last launch one lone chunk, was no better)
   int64_t fold_rl = RL;
-  int fold_even = getenv("GMAT_FOLD_EVEN") ? atoi(getenv("GMAT_FOLD_EVEN")) : -1;
-  if (fold_even < 0) fold_even = cdiv(n_rows, RL) < 10 ? 1 : 0;
-  if (fold_even == 1 && n_rows > RL) fold_rl = 2 * cdiv(n_rows, 2 * cdiv(n_rows, RL));
-  if (fold_even == 2 && n_rows > RL) {
-    int64_t nl = cdiv(n_rows, RL);
-    while (2 * cdiv(n_rows, 2 * nl - 1) > RL) ++nl;
-    fold_rl = 2 * cdiv(n_rows, 2 * nl - 1);
-  }
+  if (cdiv(n_rows, RL) < 10 && n_rows > RL) fold_rl = 2 * cdiv(n_rows, 2 * cdiv(n_rows, RL));
   const std::vector<ScanLaunch> plan = fold_launches(rows, n_rows, m, tri, &pairs_tested, fold_rl, e->col_lo);
   // live-pair records per launch: an initial capacity of 1/128 of a launch's pairs (at least 2^20; the
   // configs[2] prefilter keeps 1/250), grown (and the launch rerun) when a launch keeps more
@@ -502,19 +494,16 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // by default 7/8 of the CUs (28 of an XCD's 32): the slot lists and the low-rank screens of the
   // launches before run on the rest instead of waiting for a whole prefilter launch (one-box A/Bs,
   // configs[2]: 18.4 against 19.2 ms per step at 224 against 256 workgroups; 240 and 232 were slower)
-  // 32 x 256 tiles of four waves, two workgroups on every CU (GMAT_PF_TR=64: 64 x 256 tiles of eight
-  // waves on 7/8 of the CUs, one per CU; configs[2] one-box A/B: 16.7-16.9 against 17.7 ms per step,
-  // and 17.0-17.4 ms for the 32-row tiles on 7/8 of the CUs, 16.6-17.1 on 480 workgroups)
-  const int pf_tr = getenv("GMAT_PF_TR") && atoi(getenv("GMAT_PF_TR")) == 64 ? 64 : 32;
-  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG")))
-                                         : std::max(8, pf_tr == 32 ? 2 * e->n_cu : e->n_cu * 7 / 8);
-  // (a six-slot ring for the 32-row tiles measured 16.9-17.0 against 16.8 ms per step)
-  // covariate designs: 32 x 128 tiles of four waves, two workgroups on every CU (GMAT_PC_TC=256: 32 x 256
-  // tiles of eight waves on 7/8 of the CUs)
-  const int pc_tc = getenv("GMAT_PC_TC") && atoi(getenv("GMAT_PC_TC")) == 256 ? 256 : 128;
-  const int pc_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG")))
-                                         : std::max(8, pc_tc == 128 ? 2 * e->n_cu : e->n_cu * 7 / 8);
-  const int pf_rg = getenv("GMAT_PF_RG") ? std::max(1, atoi(getenv("GMAT_PF_RG"))) : 4 * PF_TR / pf_tr;
+  // 32 x 256 tiles of four waves, two workgroups on every CU (round 5; configs[2] one-box A/B: 16.7-16.9
+  // against 17.7 ms per step for the former 64 x 256 tiles of eight waves on 7/8 of the CUs, 17.0-17.4 ms
+  // for the 32-row tiles on 7/8 of the CUs, 16.6-17.1 on 480 workgroups; a six-slot ring 16.9-17.0 ms)
+  constexpr int pf_tr = 32;
+  const int pf_wg = getenv("GMAT_PF_WG") ? std::max(8, atoi(getenv("GMAT_PF_WG"))) : std::max(8, 2 * e->n_cu);
+  // covariate designs: 32 x 128 tiles of four waves, two workgroups on every CU (covariate configs[2]
+  // 32.0 against 33.5 ms per step for 32 x 256 tiles of eight waves on 7/8 of the CUs)
+  constexpr int pc_tc = 128;
+  const int pc_wg = pf_wg;
+  constexpr int pf_rg = 8;  // row tiles per tile-list block (256 rows)
   if (getenv("GMAT_PF_STAMPS")) {
     GMAT_TRY(pf_st.alloc((size_t)PF_NSTAMP * 8 * 1 << 20));
     GMAT_HIP(hipMemset(pf_st.p, 0, (size_t)PF_NSTAMP * 8 * 1 << 20));
@@ -536,7 +525,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // 15.75-15.81 against 16.04-16.07 ms per step on the prefilter stream; the 2-way part 8.55-8.60 against
   // 8.63-8.64 ms --, on the prefilter stream for shorter ones: the 4 / 8-way parts 4.37 / 2.47-2.50 against
   // 4.56-4.61 / 2.59 ms)
-  const int lists_on = getenv("GMAT_LISTS_STREAM") ? atoi(getenv("GMAT_LISTS_STREAM")) : RL >= 4096 ? 2 : 0;
+  const bool lists_on_screen = RL >= 4096;
   GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
@@ -680,17 +669,10 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       const int g = 8 * (int)(pf_list ? std::min<int64_t>(cdiv(pf_wg, 8), cdiv(run, 8)) : cdiv(run, 8));
       if (!pf_list && li == stamp_launch) stamp_grid = g;
       if (run > 0) {
-        if (pf_tr == 32) {
-          if (x.a.pf_stamp)  // the phase-stamped build (GMAT_PF_STAMPS)
-            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
-          else
-            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
-        } else {
-          if (x.a.pf_stamp)
-            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true, 64, PF_NS>), dim3((unsigned)g), dim3(512), 0, S2, x);
-          else
-            hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false, 64, PF_NS>), dim3((unsigned)g), dim3(512), 0, S2, x);
-        }
+        if (x.a.pf_stamp)  // the phase-stamped build (GMAT_PF_STAMPS)
+          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, true, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
+        else
+          hipLaunchKernelGGL((prefilter_pass_kernel<true, true, false, 32, 5>), dim3((unsigned)g), dim3(256), 0, S2, x);
       }
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     } else {
@@ -721,11 +703,7 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
         x.n_list = run;
         const dim3 gp((unsigned)(8 * (int)std::min<int64_t>(cdiv(pc_wg, 8), cdiv(run, 8))));
         const dim3 bd((unsigned)(2 * pc_tc));
-#define PC_LAUNCH(NC_, L_)                                                           \
-  if (pc_tc == 128)                                                                  \
-    hipLaunchKernelGGL((prefilter_cov_kernel<NC_, L_, 128>), gp, bd, 0, S2, x);      \
-  else                                                                               \
-    hipLaunchKernelGGL((prefilter_cov_kernel<NC_, L_, 256>), gp, bd, 0, S2, x)
+#define PC_LAUNCH(NC_, L_) hipLaunchKernelGGL((prefilter_cov_kernel<NC_, L_, pc_tc>), gp, bd, 0, S2, x)
         switch (e->pf_ncov) {
           case 1: PC_LAUNCH(1, true); break;
           case 2: PC_LAUNCH(2, true); break;
@@ -747,9 +725,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
     GMAT_HIP(hipGetLastError());
-    // the slot lists on SL (GMAT_LISTS_STREAM: 0 the prefilter's stream, 1 the pair-screen stream, 2 the
-    // screen stream), after the prefilter
-    const hipStream_t SL = lists_on == 1 ? S3 : lists_on == 2 ? sm : S2;
+    // the slot lists after the prefilter, on the screen stream for long launches, else on the prefilter's
+    const hipStream_t SL = lists_on_screen ? sm : S2;
     if (SL != S2) GMAT_HIP(hipStreamWaitEvent(SL, pf_end[b], 0));
     hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
                        B.cnt[b].as<int>());

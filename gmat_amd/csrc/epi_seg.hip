@@ -47,8 +47,10 @@ int64_t seg_snps(const gmat_geno *g) {
   // the largest segment of which two fit one plan: 2 (2 s) n_pad < 2^32
   const int64_t s_max = ((((int64_t)1 << 31) - 1) / g->n_pad - 1) / 2;
   int64_t s = s_max;
-  if (const char *v = getenv("GMAT_SEG_SNPS")) s = std::min(s_max, std::max<int64_t>(64, atoll(v)));
-  if (g->m <= s && 2 * g->m * g->n_pad < ((int64_t)1 << 32)) return 0;  // one plan holds the panel
+  const char *v = getenv("GMAT_SEG_SNPS");
+  if (v) s = std::min(s_max, std::max<int64_t>(64, atoll(v)));
+  // one plan holds the panel: segments only past 2 m n_pad >= 2^32, or at a forced size (tests)
+  if (2 * g->m * g->n_pad < ((int64_t)1 << 32) && (!v || g->m <= s)) return 0;
   const int64_t k = cdiv(g->m, s);
   return cdiv(g->m, k);  // equal segments
 }

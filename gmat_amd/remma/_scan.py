@@ -134,9 +134,15 @@ class EpiPlan:
 
     def lowrank_rank(self):
         """Rank of the plan's low-rank spectral screen (0: scans use the fp6 quadratic form)."""
-        s = np.zeros(4)
+        return int(self.info()["lowrank_rank"])
+
+    def info(self):
+        """Screen certificates and the prefilter's tile shape (gmat_epi_info)."""
+        s = np.zeros(8)
         N.check(self._lib.gmat_epi_info(self._h, N.ptr(s)), "gmat_epi_info")
-        return int(s[0])
+        keys = ("lowrank_rank", "lowrank_lam", "prefilter_mu", "n_pad", "pf_tile_rows", "pf_tile_cols",
+                "pf_stage_dma_bytes", "pf_tile_record_bytes")
+        return dict(zip(keys, s.tolist()))
 
     def layout(self):
         """How the plan holds its panel (gmat_epi_layout): SNP segments (1 = one plan), SNPs per segment,

@@ -147,9 +147,11 @@ int gmat_epi_kernel_stats_ext(const gmat_epi *e, double *out, int cap, int *coun
  * such screen).  Compared with the exact e'Pe of gmat_epi_pairs, every ratio must be >= 1. */
 int gmat_epi_audit(gmat_epi *e, int kind, const int64_t *pairs, int64_t n_pairs, double *out5);
 /* screen certificates of the plan: [0] rank of the low-rank spectral screen (padded to 128; 0 =
- * none, scans use the fp6 quadratic form), [1] its lam, [2] the prefilter's mu, [3] n_pad.  In
+ * none, scans use the fp6 quadratic form), [1] its lam, [2] the prefilter's mu, [3] n_pad; the
+ * compacted scan's prefilter (prefilter_pass_kernel): [4] tile rows, [5] tile columns, [6] bytes one
+ * tile streams into LDS by LDS-DMA per 64-individual stage, [7] bytes of a tile's test records.  In
  * gmat_epi_stats, [8] = -1 marks a scan screened by the low-rank bound. */
-int gmat_epi_info(const gmat_epi *e, double *out4);
+int gmat_epi_info(const gmat_epi *e, double *out8);
 /* plan setup seconds: [0] gmat_epi_create total, [1] prefilter certificate, [2] eigendecomposition
  * of P, [3] low-rank certificate, [4] slices and residual bounds, [5] coding builds (side vectors;
  * done lazily by the first scan of each coding), [6] Cholesky factorisations the certificates ran,

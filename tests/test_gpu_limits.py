@@ -178,6 +178,34 @@ def test_segments_identical_cfg3_rows():
     assert ref["AA", 1e-3][0].size > 200
 
 
+def test_one_plan_below_the_limit():
+    """2,000 individuals x 600,000 SNPs (2 m n_pad = 2.46e9 < 2^32): one plan holds the panel (no
+    segments), and a row in its last tenth has the oracle's hits on the repeated base cohort."""
+    from gmat_amd import synth
+    from gmat_amd.plink import Geno
+    from gmat_amd.remma._scan import EpiPlan
+    from oracle import gmat_oracle as O
+    n, m0, reps, p_cut = 2000, 50000, 12, 1e-4
+    base = synth.simulate_genotypes(n, m0, seed=81)
+    snp0 = np.ascontiguousarray(base.T, dtype=np.float64)
+    pvp, py = _projection(snp0, 81)
+    body0 = np.frombuffer(synth.pack_bed(base)[3:], dtype=np.uint8).reshape(m0, (n + 3) // 4)
+    body = np.tile(body0, (reps, 1)).ravel()
+    m = m0 * reps
+    i = 11 * m0 + 777
+    with Geno(body=body, n_id=n, n_snp=m) as g, EpiPlan(g, pvp, py) as plan:
+        lay = plan.layout()
+        assert lay["segments"] == 1 and not lay["exhaustive_only"], lay
+        hi, hj, eff, var, chi, p = plan.scan("AA", np.array([i], dtype=np.int64), p_cut)
+    st = O.epi_pair("AA", snp0, pvp, py.reshape(-1, 1), np.column_stack([np.full(m0, i % m0), np.arange(m0)]))
+    j = np.arange(i + 1, m, dtype=np.int64)
+    j = j[st[3][j % m0] < p_cut]
+    assert j.size > 5
+    np.testing.assert_array_equal(hj, j)
+    np.testing.assert_allclose(np.column_stack([eff, chi, p]),
+                               np.column_stack([st[0][j % m0], st[2][j % m0], st[3][j % m0]]), rtol=1e-8, atol=1e-300)
+
+
 def test_real_snp_limit_tiled_cohort():
     """2,000 individuals x 1.1 M SNPs: past 2 m n_pad < 2^32, so the plan is cut into segments (three).
     Rows in every segment, AA and AD, checked against the oracle on the 50,000-SNP base cohort the
