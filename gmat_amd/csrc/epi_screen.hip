@@ -729,8 +729,17 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
     const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
     return v8i_{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
-  auto compute = [&](int b, bool first) __attribute__((always_inline)) {
-    const v16f_ z = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // the accumulators are zeroed at each chunk's start (a branch taken once per nK stages: selecting a zero
+  // C operand for a chunk's first stage compiled to 128 v_cndmask in EVERY stage)
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int t = 0; t < PB; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][t][e] = 0.f;
+  };
+  auto compute = [&](int b) __attribute__((always_inline)) {
     v8i_ fa = afrag(b, 0, 0);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -755,7 +764,7 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
         const v8i_ fn = last ? fa : afrag(b, r < RB - 1 ? kk : 1, (r + 1) % RB);
 #pragma unroll
         for (int t = 0; t < PB; ++t)  // x2 (scale 128): the fp4 codes hold w/2
-          acc[r][t] = mfma_mx(fa, fb[t], (first && kk == 0) ? z : acc[r][t], fa[6], 128);
+          acc[r][t] = mfma_mx(fa, fb[t], acc[r][t], fa[6], 128);
         fa = fn;
       }
     }
@@ -812,12 +821,16 @@ __global__ __launch_bounds__(512, 1) void lrc_screen_kernel(ScreenArgs a, LrcArg
   // leaves the younger stages' DMAs in flight (VMEM operations retire in order)
   const int P = nC * nK;
   for (int q = 0; q < LA && q < P; ++q) load(q % NSL, q);
+  zero_acc();
   vm_wait_barrier(NL * (min(LA, P) - 1));
   for (int q = 0; q < P; ++q) {
     if (q + LA < P) load((q + LA) % NSL, q + LA);  // its slot was read in stage q - 1 (barrier passed)
     const int kc = q % nK;
-    compute(q % NSL, kc == 0);
-    if (kc == nK - 1) epilogue(q / nK);
+    compute(q % NSL);
+    if (kc == nK - 1) {
+      epilogue(q / nK);
+      zero_acc();
+    }
     const int ahead = min(q + LA, P - 1) - (q + 1);  // stages issued beyond q + 1
     vm_wait_barrier(q + 1 < P ? NL * ahead : 0);
   }
