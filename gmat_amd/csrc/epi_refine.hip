@@ -252,6 +252,10 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   int v = 0;
   for (int kb = kb_lo; kb < kb_hi; ++kb) {
     const int c0 = kb >> 1;
+    // the row block's sums start at zero (its first tile is cs = NS - 1; a zero C operand selected per
+    // tile compiled to a v_cndmask per accumulator register in every tile)
+#pragma unroll
+    for (int s = 0; s < R8_S; ++s) acc[s][0] = acc[s][1] = zv;
 #pragma unroll
     for (int cs = R8_NC - 1; cs >= 0; --cs) {
       int cq = c0;  // opaque per unrolled copy (see pair_mxr_kernel)
@@ -265,13 +269,12 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
           asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue_next();
         const int8_t *tb = sA[v % NSL];
-        const bool first = cs == NS - 1;
 #pragma unroll
         for (int s = 0; s < R8_S; ++s)
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) {
             const v4i fa = *(const v4i *)(tb + s * R8_TB + (rt * 16 + c) * 64 + swz);
-            acc[s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[cs], first ? zv : acc[s][rt], 0, 0, 0);
+            acc[s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[cs], acc[s][rt], 0, 0, 0);
           }
         if (cs == cq) {  // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile
 #pragma unroll
@@ -377,6 +380,8 @@ __global__ __launch_bounds__(512, 1) void refine8w_kernel(int64_t n_pad, const i
     asm volatile("" : "+s"(lo));  // opaque per unrolled copy (see pair_mxr_kernel)
     if (lo > C1 - 1) continue;
 #pragma unroll
+    for (int s2 = 0; s2 < R8_S; ++s2) acc[s2][0] = acc[s2][1] = zv;  // (as refine8_kernel)
+#pragma unroll
     for (int kc = R8_NC - 1; kc >= 0; --kc) {
       if (C0 + kc < C1 && C0 + kc >= lo) {
         static_assert(LA == 6, "vmcnt values");
@@ -386,13 +391,12 @@ __global__ __launch_bounds__(512, 1) void refine8w_kernel(int64_t n_pad, const i
           asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue_next();
         const int8_t *tb = sA[v % NSL];
-        const bool first = C0 + kc == C1 - 1;
 #pragma unroll
         for (int s2 = 0; s2 < R8_S; ++s2)
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) {
             const v4i fa = *(const v4i *)(tb + s2 * R8_TB + (rt * 16 + c) * 64 + swz);
-            acc[s2][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[kc], first ? zv : acc[s2][rt], 0, 0, 0);
+            acc[s2][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[kc], acc[s2][rt], 0, 0, 0);
           }
         ++v;
       }
@@ -653,6 +657,8 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
   int v = 0;
   for (int kb = kb_lo; kb < kb_hi; ++kb) {
 #pragma unroll
+    for (int r = 0; r < MX_RB; ++r) acc[r] = zv;  // the row block's first tile is cs = nK - 1 (as refine8_kernel)
+#pragma unroll
     for (int cs = PXR_NK - 1; cs >= 0; --cs) {
       // an opaque copy of kb per unrolled copy: with kb itself the compiler turns the copies' kb == cs
       // tests into one switch and merges the fold copies into one block that indexes wf dynamically
@@ -664,7 +670,6 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
         issue_next();
         const uint8_t *tb = sA[v % NSL];
         const int bs = cs == kb ? 128 : 129;  // off-diagonal tiles count twice
-        const bool first = cs == nK - 1;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const v4i wb = wf[2 * cs + kk];
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(512, 1) void pair_mxr_kernel(PairArgs x) {
             const uint8_t *ar = tb + (2 * kk + h) * 4096 + (32 * r + c) * 32;
             const v4i lo = *(const v4i *)(ar + sw16), hi = *(const v4i *)(ar + (16 - sw16));
             const v8i_ fa = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            acc[r] = mfma_mx(fa, fb, (first && kk == 0) ? zv : acc[r], hi[2], bs);
+            acc[r] = mfma_mx(fa, fb, acc[r], hi[2], bs);
           }
         }
         if (cs == kq) {  // row block kb complete: sum_rows w[row] acc[row] (register e <-> slot 16 h + e)
@@ -771,13 +776,14 @@ __global__ __launch_bounds__(512, 1) void pair_mxw_kernel(PairArgs x) {
     int lo = max(C0, kb);
     asm volatile("" : "+s"(lo));  // opaque per unrolled copy (see pair_mxr_kernel)
 #pragma unroll
+    for (int r = 0; r < MX_RB; ++r) acc[r] = zv;  // (as pair_mxr_kernel)
+#pragma unroll
     for (int cl = PXR_NK - 1; cl >= 0; --cl) {
       if (C0 + cl < C1 && C0 + cl >= lo) {
         vm_wait_barrier(2 * min(LA - 1, N - 1 - v));  // tile v has landed (younger DMAs may be in flight)
         issue_next();
         const uint8_t *tb = sA[v % NSL];
         const int bs = C0 + cl == kb ? 128 : 129;  // off-diagonal tiles count twice
-        const bool first = C0 + cl == C1 - 1;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const v4i wb = wf[2 * cl + kk];
@@ -787,7 +793,7 @@ __global__ __launch_bounds__(512, 1) void pair_mxw_kernel(PairArgs x) {
             const uint8_t *ar = tb + (2 * kk + h) * 4096 + (32 * r + c) * 32;
             const v4i lo4 = *(const v4i *)(ar + sw16), hi4 = *(const v4i *)(ar + (16 - sw16));
             const v8i_ fa = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-            acc[r] = mfma_mx(fa, fb, (first && kk == 0) ? zv : acc[r], hi4[2], bs);
+            acc[r] = mfma_mx(fa, fb, acc[r], hi4[2], bs);
           }
         }
         ++v;
