@@ -623,6 +623,7 @@ typedef int v2i__ __attribute__((ext_vector_type(2)));
 // LDS-DMA ring (six in flight) in the order kb, then cs from the last stage down to kb / 2 (whose visit
 // folds the row block).
 constexpr int R8_S = 7, R8_TB = 2048, R8_TILE = R8_S * R8_TB, R8_NC = 32, R8_PP = 128;
+constexpr int R8_PP2 = 256;  // pairs per workgroup of refine8_kernel (w held as 2-bit codes; refine8w_kernel: R8_PP)
 constexpr int R8_NT = 4;  // O(n) sums per pair stored by refine8_side_kernel for refine8_fin_kernel
 __host__ __device__ inline int64_t r8_toff(int64_t kb, int64_t NS) {  // tiles of the row blocks before kb
   const int64_t h = kb >> 1;

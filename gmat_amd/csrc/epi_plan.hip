@@ -224,8 +224,8 @@ int refine(gmat_epi *e, hipStream_t st, const Coding &L, const Coding &R, const 
       GMAT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       e->n_cu = std::max(cus, 8);
     }
-    const int64_t wgs = cdiv(np, R8_PP);
     const bool wide = e->n_pad > 64 * R8_NC;  // w by squares of stages (refine8w_kernel)
+    const int64_t wgs = cdiv(np, wide ? R8_PP : R8_PP2);
     const int nQ = (int)cdiv(e->n_pad / 64, R8_NC);
     const int nseg = wide ? nQ * (nQ + 1) / 2 : (int)std::max<int64_t>(1, std::min<int64_t>(seg_max(), e->n_cu / wgs));
     const size_t need = (size_t)np * sizeof(double) * (nseg > 1 ? 1 + R8_S * nseg : 1);

@@ -186,6 +186,29 @@ __global__ void r8_image_kernel(int64_t n_pad, const double *__restrict__ Ps, do
   (void)NB;
 }
 
+// w = a o b of 16 individuals (4 dwords of int8 values 0 / 1 / 2 / 4) as 16 2-bit codes {0, 1, 2, 3}
+__device__ __forceinline__ unsigned r8_pack_w(v4i v) {
+  unsigned d = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned x = (unsigned)v[k], c = x - ((x >> 2) & 0x01010101u);  // 4 -> 3
+    d |= ((c | (c >> 6) | (c >> 12) | (c >> 18)) & 0xffu) << (8 * k);
+  }
+  return d;
+}
+// the 4 int8 w of codes 4 k .. 4 k + 3 of a packed dword (byte j: code j of byte k of d, through {0, 1, 2, 4})
+__device__ __forceinline__ int r8_w4(unsigned d, int k) {
+  const unsigned x = (d >> (8 * k)) & 0xffu;
+  const unsigned y = (x << 6) | x;
+  const unsigned sel = ((y << 12) | y) & 0x03030303u;
+  return (int)__builtin_amdgcn_perm(0u, 0x04020100u, sel);
+}
+__device__ __forceinline__ v4i r8_unpack_w(unsigned d) { return v4i{r8_w4(d, 0), r8_w4(d, 1), r8_w4(d, 2), r8_w4(d, 3)}; }
+
+// 256 pairs per workgroup (R8_PP2): a wave holds w of two 16-pair groups as 2-bit codes (one dword per
+// 64-individual chunk and lane instead of four int8 dwords), expanded into the MFMA's B fragments per tile
+// (five VALU per dword), so every slice tile streamed into LDS serves twice the pairs of the int8-register
+// layout: the kernel is bound by that L2 -> LDS stream (14.7 MB per workgroup at n_pad 2,048).
 __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const int8_t *__restrict__ tiles,
                                                          const int8_t *__restrict__ sl, const int8_t *__restrict__ sr,
                                                          const int64_t *__restrict__ pi, const int64_t *__restrict__ pj,
@@ -206,22 +229,26 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   kb_hi = kb_lo;
   while (kb_hi < NB && r8_toff(kb_hi, NS) * nseg < N_all * (seg + 1)) ++kb_hi;
   const int N = (int)(r8_toff(kb_hi, NS) - r8_toff(kb_lo, NS));
-  const int64_t p = (int64_t)blockIdx.x * R8_PP + 16 * w + c;
-  const bool valid = p < np;
-  // w = a o b (screen codes 0 / 1 / 2): chunk kc holds individuals 64 kc + 16 g .. + 15 of pair c
-  v4i wf[R8_NC];
-  {
-    const int8_t *ra = sl + (valid ? pi[p] : 0) * n_pad, *rb = sr + (valid ? pj[p] : 0) * n_pad;
+  // pair group u of the wave: pairs 32 w + 16 u + c; chunk kc of w (screen codes 0 / 1 / 2 multiplied)
+  // holds individuals 64 kc + 16 g .. + 15 as 2-bit codes
+  int64_t p[2];
+  bool valid[2];
+  unsigned wf[2][R8_NC];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    p[u] = (int64_t)blockIdx.x * R8_PP2 + 32 * w + 16 * u + c;
+    valid[u] = p[u] < np;
+    const int8_t *ra = sl + (valid[u] ? pi[p[u]] : 0) * n_pad, *rb = sr + (valid[u] ? pj[p[u]] : 0) * n_pad;
 #pragma unroll
     for (int kc = 0; kc < R8_NC; ++kc) {
       v4i v = {0, 0, 0, 0};
-      if (valid && kc < NS) {
+      if (valid[u] && kc < NS) {
         const v4i va = *(const v4i *)(ra + 64 * kc + 16 * g), vb = *(const v4i *)(rb + 64 * kc + 16 * g);
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           v[d] = (int)__builtin_amdgcn_perm(T_HI, T_LO, to_offset((unsigned)va[d]) + (unsigned)vb[d]);
       }
-      wf[kc] = v;
+      wf[u][kc] = r8_pack_w(v);
     }
   }
   // tile ring: visit v reads slot v % NSL; tile v + LA goes out at visit v into the slot of visit v - 1.
@@ -244,18 +271,25 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
   };
   for (int q = 0; q < LA; ++q) issue_next();
   const v4i zv = {0, 0, 0, 0};
-  v4i acc[R8_S][2];
-  double T[R8_S];
+  v4i acc[2][R8_S][2];
+  // per-lane slice sums in int32: |acc| <= 127 * 4 * n_pad = 2^20 (n_pad <= 2,048), a fold of four rows
+  // <= 2^24, at most 64 row blocks per lane <= 2^30; the lanes' sums are added in fp64
+  int T[2][R8_S];
 #pragma unroll
-  for (int s = 0; s < R8_S; ++s) T[s] = 0.0;
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < R8_S; ++s) T[u][s] = 0;
   const int swz = 16 * (g ^ r8_swz(c));
   int v = 0;
+  unsigned wlast[2] = {0u, 0u};
   for (int kb = kb_lo; kb < kb_hi; ++kb) {
     const int c0 = kb >> 1;
     // the row block's sums start at zero (its first tile is cs = NS - 1; a zero C operand selected per
     // tile compiled to a v_cndmask per accumulator register in every tile)
 #pragma unroll
-    for (int s = 0; s < R8_S; ++s) acc[s][0] = acc[s][1] = zv;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < R8_S; ++s) acc[u][s][0] = acc[u][s][1] = zv;
 #pragma unroll
     for (int cs = R8_NC - 1; cs >= 0; --cs) {
       int cq = c0;  // opaque per unrolled copy (see pair_mxr_kernel)
@@ -269,48 +303,67 @@ __global__ __launch_bounds__(512, 1) void refine8_kernel(int64_t n_pad, const in
           asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue_next();
         const int8_t *tb = sA[v % NSL];
+        unsigned wc[2] = {wf[0][cs], wf[1][cs]};
+        // opaque per visit: else the expansion of every chunk is hoisted out of the row-block loop (256
+        // registers of B fragments, spilled)
+        asm volatile("" : "+v"(wc[0]), "+v"(wc[1]));
+        const v4i wb0 = r8_unpack_w(wc[0]), wb1 = r8_unpack_w(wc[1]);
 #pragma unroll
         for (int s = 0; s < R8_S; ++s)
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) {
             const v4i fa = *(const v4i *)(tb + s * R8_TB + (rt * 16 + c) * 64 + swz);
-            acc[s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wf[cs], acc[s][rt], 0, 0, 0);
+            acc[0][s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wb0, acc[0][s][rt], 0, 0, 0);
+            acc[1][s][rt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa, wb1, acc[1][s][rt], 0, 0, 0);
           }
-        if (cs == cq) {  // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile
-#pragma unroll
-          for (int rt = 0; rt < 2; ++rt) {
-            const int sl_ = c + 16 * (2 * (kb & 1) + rt);  // the lanes holding the row tile's w
-            const v4i src = wf[cs];
-            const int d0 = __shfl(src[0], sl_), d1 = __shfl(src[1], sl_), d2 = __shfl(src[2], sl_),
-                      d3 = __shfl(src[3], sl_);
-            const unsigned wd = (unsigned)(g == 0 ? d0 : g == 1 ? d1 : g == 2 ? d2 : d3);
-            const int w0 = (int)(wd & 0xff), w1 = (int)((wd >> 8) & 0xff), w2 = (int)((wd >> 16) & 0xff),
-                      w3 = (int)(wd >> 24);
-#pragma unroll
-            for (int s = 0; s < R8_S; ++s)
-              T[s] += (double)(w0 * acc[s][rt][0] + w1 * acc[s][rt][1] + w2 * acc[s][rt][2] + w3 * acc[s][rt][3]);
-          }
+        if (cs == cq) {  // the row block's last tile: its w is the fold's
+          wlast[0] = wc[0];
+          wlast[1] = wc[1];
         }
         ++v;
       }
     }
+    // rows of block kb done: fold with w at the lane's rows 4 g .. 4 g + 3 of each row tile (after the
+    // unrolled visits, which stay small enough to unroll fully: a fold inside each copy put wf in scratch)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        // row tile rt of block kb is individuals 64 cs + 16 (2 (kb & 1) + rt) + .. of chunk cs = kb / 2: group
+        // 2 (kb & 1) + rt, held by lane c + 16 (2 (kb & 1) + rt); this lane's rows 4 g .. + 3 are its byte g
+        const unsigned wd = (unsigned)__shfl((int)wlast[u], c + 16 * (2 * (kb & 1) + rt));
+        const unsigned w4 = (unsigned)r8_w4(wd, g);
+        const int w0 = (int)(w4 & 0xff), w1 = (int)((w4 >> 8) & 0xff), w2 = (int)((w4 >> 16) & 0xff), w3 = (int)(w4 >> 24);
+#pragma unroll
+        for (int s = 0; s < R8_S; ++s)  // |acc| < 2^21: 24-bit multiplies are exact
+          T[u][s] += __mul24(w0, acc[u][s][rt][0]) + __mul24(w1, acc[u][s][rt][1]) + __mul24(w2, acc[u][s][rt][2]) +
+                     __mul24(w3, acc[u][s][rt][3]);
+      }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the workgroup ends
+  double Td[2][R8_S];
 #pragma unroll
-  for (int s = 0; s < R8_S; ++s) {
-    T[s] += __shfl_xor(T[s], 16);
-    T[s] += __shfl_xor(T[s], 32);
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < R8_S; ++s) {
+      Td[u][s] = (double)T[u][s];
+      Td[u][s] += __shfl_xor(Td[u][s], 16);
+      Td[u][s] += __shfl_xor(Td[u][s], 32);
+    }
+  if (g) return;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!valid[u]) continue;
+    if (nseg > 1) {
+#pragma unroll
+      for (int s = 0; s < R8_S; ++s) tpart[((int64_t)seg * R8_S + s) * np + p[u]] = Td[u][s];
+      continue;
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + Td[u][s];
+    varw[p[u]] = unit * sum;
   }
-  if (g || !valid) return;
-  if (nseg > 1) {
-#pragma unroll
-    for (int s = 0; s < R8_S; ++s) tpart[((int64_t)seg * R8_S + s) * np + p] = T[s];
-    return;
-  }
-  double sum = 0.0;
-#pragma unroll
-  for (int s = R8_S - 1; s >= 0; --s) sum = sum * (1.0 / 128.0) + T[s];
-  varw[p] = unit * sum;
 }
 
 // refine8_kernel for n_pad > 64 R8_NC (configs[4]: 80 stages), where one wave cannot hold every chunk of
