@@ -1121,12 +1121,12 @@ __global__ void tl_fill_kernel(const uint8_t *__restrict__ flags, int Rn, int nJ
                                                       const int *__restrict__ cnt4, const int *__restrict__ H,
                                                       const int *__restrict__ info, int *__restrict__ mxt,
                                                       int *__restrict__ mxr);
-__global__ void lc_count_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
+__global__ void lc_count_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ, int Rn,
                                                         int *__restrict__ cnt);
 __global__ void lc_scan_kernel(const int *__restrict__ cnt, int Rn, int *__restrict__ soff,
                                                        int *__restrict__ info, int *__restrict__ slot_row,
                                                        int64_t slot_cap);
-__global__ void lc_fill_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
+__global__ void lc_fill_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ, int Rn,
                                                        const int *__restrict__ cnt, const int *__restrict__ soff,
                                                        int *__restrict__ slot_row, int *__restrict__ slot_j,
                                                        const int *__restrict__ ops, int64_t ops_cap,

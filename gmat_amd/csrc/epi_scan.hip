@@ -517,15 +517,8 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
   // round of 256 CUs only partly; on one stream the next launch would wait for the whole tail)
   const hipStream_t sm = e->s1, S3 = e->s3;
   const hipStream_t S2b[2] = {e->s2, e->s4};
-  // the slot lists on the screen stream for long launches, else on the prefilter's stream (round-5
-  // one-box A/Bs at 4,096-row launches: configs[2], 13 launches, 16.1-16.2 against 16.6-16.8 ms per step -- a launch's
-  // lists no longer hold back the prefilter two launches later on the same stream --; rank 0's 8-way
-  // part, 7 launches, 2.82-2.88 against 2.67-2.75 ms; the pair-screen stream 16.9-17.1 / 2.93-2.96 ms)
-  // (round 5, 7,168-row launches: lists on the screen stream for launches of 4,096 rows or more -- configs[2]
-  // 15.75-15.81 against 16.04-16.07 ms per step on the prefilter stream; the 2-way part 8.55-8.60 against
-  // 8.63-8.64 ms --, on the prefilter stream for shorter ones: the 4 / 8-way parts 4.37 / 2.47-2.50 against
-  // 4.56-4.61 / 2.59 ms)
-  const bool lists_on_screen = RL >= 4096;
+  // (the slot lists: after each prefilter on its stream, below; round 5 put those of launches of 4,096 rows or
+  // more on the screen stream, where the former workgroup-per-row list kernels measured faster)
   GMAT_HIP(hipStreamSynchronize(e->s));  // the codings were built on the plan's stream
   ScanEvents evs{e};
   hipEvent_t side_beg[NBUF], side_end[NBUF], scr_beg[NBUF], scr_end[NBUF], pf_beg[NBUF], pf_end[NBUF], ref_beg, ref_end;
@@ -725,14 +718,17 @@ int scan_lowrank(gmat_epi *e, int kind, const int64_t *rows, int64_t n_rows, dou
       GMAT_HIP(hipEventRecord(pf_end[b], S2));
     }
     GMAT_HIP(hipGetLastError());
-    // the slot lists after the prefilter, on the screen stream for long launches, else on the prefilter's
-    const hipStream_t SL = lists_on_screen ? sm : S2;
-    if (SL != S2) GMAT_HIP(hipStreamWaitEvent(SL, pf_end[b], 0));
-    hipLaunchKernelGGL(lc_count_kernel, dim3(Rn), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
+    // the slot lists after the prefilter on its stream (round 6, with the one-wave-per-row list kernels:
+    // configs[2] 14.95-14.96 against 15.00-15.01 ms per step on the screen stream, one box; a prefilter
+    // also waiting for the screen two launches back: 18.5 ms)
+    const hipStream_t SL = S2;
+    hipLaunchKernelGGL(lc_count_kernel, dim3((unsigned)cdiv(Rn, LC_T / 64)), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag,
+                       (int)nJ, Rn,
                        B.cnt[b].as<int>());
     hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, SL, B.cnt[b].as<int>(), Rn, B.soff[b].as<int>(),
                        B.info[b].as<int>(), B.slot_row[b].as<int>(), B.slot_cap);
-    hipLaunchKernelGGL(lc_fill_kernel, dim3(Rn), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag, (int)nJ,
+    hipLaunchKernelGGL(lc_fill_kernel, dim3((unsigned)cdiv(Rn, LC_T / 64)), dim3(LC_T), 0, SL, B.lmask[b].as<uint64_t>(), tag,
+                       (int)nJ, Rn,
                        B.cnt[b].as<int>(), B.soff[b].as<int>(), B.slot_row[b].as<int>(), B.slot_j[b].as<int>(),
                        B.ops[b].as<int>(), B.ops_cap, B.slot_ops[b].as<int>(), B.slot_cap);
     GMAT_HIP(hipGetLastError());

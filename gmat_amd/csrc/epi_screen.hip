@@ -963,79 +963,89 @@ __global__ __launch_bounds__(1024) void tl_fill_kernel(const uint8_t *__restrict
   }
 }
 
-__global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
+// The slot lists of a launch (the compacted low-rank screen's input) from the prefilter's tagged live-block
+// entries: lc_count (live pairs per band row), lc_scan (slots per row -> the rows' first slots), lc_fill
+// (each row's live second SNPs in ascending order into its slots, with their records).  One wave per row,
+// LC_T / 64 rows per workgroup: the row's entries are read 64 at a time (coalesced) and placed with a
+// wave shuffle scan (round 5: a workgroup per row, contiguous per-thread ranges and a 16-barrier LDS scan).
+__global__ __launch_bounds__(LC_T) void lc_count_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ, int Rn,
                                                         int *__restrict__ cnt) {
-  __shared__ int part[LC_T / 64];
-  const int r = blockIdx.x, tid = threadIdx.x;
+  const int r = (int)blockIdx.x * (LC_T / 64) + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= Rn) return;
+  const uint64_t *mk = lmask + (int64_t)r * nJ;
   int c = 0;
-  for (int J = tid; J < nJ; J += LC_T) c += __popc(lm_mask(lmask[(int64_t)r * nJ + J], tag));
+  for (int J = lane; J < nJ; J += 64) c += __popc(lm_mask(mk[J], tag));
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((tid & 63) == 0) part[tid >> 6] = c;
-  __syncthreads();
-  if (tid == 0) cnt[r] = (part[0] + part[1]) + (part[2] + part[3]);
+  if (lane == 0) cnt[r] = c;
+}
+
+// wave-inclusive prefix sum of v over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  return v;
 }
 
 // one workgroup: exclusive scan of the rows' slot counts (soff), info = {slots, tiles}, the padding
-// slots of the last tile
+// slots of the last tile; 1,024 rows per pass (coalesced), wave shuffle scans and one LDS step
 __global__ __launch_bounds__(1024) void lc_scan_kernel(const int *__restrict__ cnt, int Rn, int *__restrict__ soff,
                                                        int *__restrict__ info, int *__restrict__ slot_row,
                                                        int64_t slot_cap) {
-  __shared__ int part[1024];
-  const int t = threadIdx.x, per = (Rn + 1023) / 1024, r0 = t * per, r1 = min(Rn, r0 + per);
-  int sum = 0;
-  for (int r = r0; r < r1; ++r) sum += (cnt[r] + 31) / 32;
-  part[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  __shared__ int wsum[2][16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int run = 0, par = 0;  // slots of the passes before (uniform)
+  for (int base = 0; base < Rn; base += 1024, par ^= 1) {
+    const int r = base + t;
+    const int sl = r < Rn ? (cnt[r] + 31) / 32 : 0;
+    const int inc = wave_incl_scan(sl, lane);
+    if (lane == 63) wsum[par][wv] = inc;
+    __syncthreads();  // (the two buffers: a pass's totals are not overwritten while the previous one reads)
+    int wpre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int v = wsum[par][k];
+      wpre += k < wv ? v : 0;
+      tot += v;
+    }
+    if (r < Rn) soff[r] = run + wpre + inc - sl;
+    run += tot;
   }
-  int run = part[t] - sum;
-  for (int r = r0; r < r1; ++r) {
-    soff[r] = run;
-    run += (cnt[r] + 31) / 32;
-  }
+  const int slots = run, tiles = (slots + LC_SLOTS - 1) / LC_SLOTS;
   if (t == 0) {
-    const int slots = part[1023], tiles = (slots + LC_SLOTS - 1) / LC_SLOTS;
     info[0] = slots;
     info[1] = tiles;
-    for (int q = slots; q < tiles * LC_SLOTS && q < slot_cap; ++q) slot_row[q] = -1;
   }
+  const int q = slots + t;
+  if (q < tiles * LC_SLOTS && q < slot_cap) slot_row[q] = -1;
 }
 
-// lc_fill: band row r's live second SNPs in ascending order into its slots (one workgroup per row;
-// each thread takes a contiguous range of column blocks, a block-wide scan places its pairs), and
-// each live pair's record (the prefilter's, at its block's first record + its rank in the block) copied to
-// its slot position in slot_ops
-__global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ,
+// lc_fill: band row r's live second SNPs in ascending order into its slots, and each live pair's record
+// (the prefilter's, at its block's first record + its rank in the block) copied to its slot position in
+// slot_ops.  One wave per row: 64 entries per step, the next step's entries loaded ahead.
+__global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint64_t *__restrict__ lmask, unsigned tag, int nJ, int Rn,
                                                        const int *__restrict__ cnt, const int *__restrict__ soff,
                                                        int *__restrict__ slot_row, int *__restrict__ slot_j,
                                                        const int *__restrict__ ops, int64_t ops_cap,
                                                        int *__restrict__ slot_ops, int64_t slot_cap) {
-  __shared__ int part[LC_T];
-  const int r = blockIdx.x, tid = threadIdx.x;
-  const int per = (nJ + LC_T - 1) / LC_T, J0 = min(nJ, tid * per), J1 = min(nJ, J0 + per);
+  const int r = (int)blockIdx.x * (LC_T / 64) + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= Rn) return;
   const uint64_t *mk = lmask + (int64_t)r * nJ;
-  int c = 0;
-  for (int J = J0; J < J1; ++J) c += __popc(lm_mask(mk[J], tag));
-  part[tid] = c;
-  __syncthreads();
-  for (int off = 1; off < LC_T; off <<= 1) {
-    const int v = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
   const int base = soff[r] * 32, n_live = cnt[r], n_slots = (n_live + 31) / 32;
   if ((int64_t)soff[r] + n_slots > slot_cap) return;  // records overflowed: the host reruns the launch
-  int k = part[tid] - c;
-  for (int J = J0; J < J1; ++J) {
-    const uint64_t ent = mk[J];
+  int k0 = 0;  // pairs placed by the earlier steps
+  uint64_t nxt = lane < nJ ? mk[lane] : 0ull;
+  for (int J0 = 0; J0 < nJ; J0 += 64) {
+    const uint64_t ent = nxt;
+    nxt = J0 + 64 + lane < nJ ? mk[J0 + 64 + lane] : 0ull;
     uint32_t w = lm_mask(ent, tag);
-    if (!w) continue;
+    const int c = __popc(w);
+    const int inc = wave_incl_scan(c, lane);
+    int k = k0 + inc - c;
     uint32_t src = lm_base(ent);
+    const int J = J0 + lane;
     while (w) {
       const int b = __ffs(w) - 1;
       w &= w - 1;
@@ -1048,9 +1058,10 @@ __global__ __launch_bounds__(LC_T) void lc_fill_kernel(const uint64_t *__restric
       ++src;
       slot_j[base + k++] = 32 * J + b;
     }
+    k0 += __shfl(inc, 63);
   }
-  for (int q = n_live + tid; q < n_slots * 32; q += LC_T) slot_j[base + q] = -1;
-  for (int q = tid; q < n_slots; q += LC_T) slot_row[soff[r] + q] = r;
+  for (int q = n_live + lane; q < n_slots * 32; q += 64) slot_j[base + q] = -1;
+  for (int q = lane; q < n_slots; q += 64) slot_row[soff[r] + q] = r;
 }
 
 // the instantiations the host code launches
