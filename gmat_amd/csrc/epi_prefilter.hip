@@ -136,9 +136,6 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
     }
   };
   pstamp(0);
-#if defined(PF_PRIO) && PF_PRIO == 3
-  if (TR == 32 && (blockIdx.x & 8)) __builtin_amdgcn_s_setprio(1);
-#endif
   // wave w = rows 32 (w >> 2) .. +32 x columns 64 (w & 3) .. +64 (two 32-column blocks)
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wr = w >> 2, wc = w & 3;  // wave-uniform (SGPR)
@@ -261,11 +258,6 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     pstamp(1);
-#if defined(PF_PRIO) && PF_PRIO == 1
-    if (TR == 32) __builtin_amdgcn_s_setprio(1);
-#elif defined(PF_PRIO) && PF_PRIO == 2
-    if (TR == 32) __builtin_amdgcn_s_setprio(0);
-#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -323,11 +315,6 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
       wait_for(st + 1, min(st + NS - 1, S - 1));
     }
     pstamp(2);
-#if defined(PF_PRIO) && PF_PRIO == 1
-    if (TR == 32) __builtin_amdgcn_s_setprio(0);
-#elif defined(PF_PRIO) && PF_PRIO == 2
-    if (TR == 32) __builtin_amdgcn_s_setprio(1);
-#endif
     // every wave has passed the last stage's barrier (its vmcnt(0) wait): the ring is free, so the
     // next tile's records and first stages go out now and land while this tile's epilogue runs
     const int nxt = tile_at(it + 1);
