@@ -379,7 +379,7 @@ def eff_bench(g, pvp, py, plan, n, m, p_cut, seed, geno=None, cpu_budget=10.0):
             "cpu_baseline": cpu}
 
 
-def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), reps=5):
+def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), reps=5, kind="AA"):
     """configs[3] rehearsed on one GPU: each part of the multi-GPU split (dist.rank_rows: part k of
     the reference's folded parallel=[N,k] rows, remma_epiAA.py:125-139) timed serially on this GPU
     -- what one rank of an N-GPU run computes between its barriers.  A part is timed as the step is:
@@ -392,17 +392,17 @@ def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), rep
     for N in ways:
         ms, hits, pairs = [], 0, []
         for k in range(N):
-            rows = dist.rank_rows("AA", m, k, N)
-            plan.scan("AA", rows, p_cut)
+            rows = dist.rank_rows(kind, m, k, N)
+            plan.scan(kind, rows, p_cut)
             lib.gmat_device_synchronize()
             t0 = time.perf_counter()
             for _ in range(reps):
-                res = plan.scan("AA", rows, p_cut)
+                res = plan.scan(kind, rows, p_cut)
                 plan.stats()  # the step's per-scan bookkeeping
             lib.gmat_device_synchronize()
             ms.append((time.perf_counter() - t0) * 1e3 / reps)
             hits += int(res[0].size)
-            pairs.append(float(np.sum(m - 1 - rows)))
+            pairs.append(float(rows.size * m) if kind == "AD" else float(np.sum(m - 1 - rows)))
         mean = float(np.mean(ms))
         out["%d" % N] = {"part_ms": [round(x, 3) for x in ms], "max_over_mean": max(ms) / mean,
                          "pairs_max_over_mean": max(pairs) / float(np.mean(pairs)),
@@ -412,7 +412,7 @@ def split_emulation(plan, m, p_cut, step_ms, hits_step, lib, ways=(2, 4, 8), rep
     return out
 
 
-def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None, reps=3):
+def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None, reps=3, split=True):
     """BASELINE configs[4]: synthetic related 5,000 x 100,000 cohort (60 founders, 6
     generations of random mating; `family_size`: the last generation in full-sib families instead),
     5-GRM model [A, D, AxA, AxD, DxD]: GRMs (agmat / dgmat_as products), weighted EM-AI REML
@@ -421,7 +421,9 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
     workflow), then the exhaustive epiDD (j > i) and epiAD (every ordered pair, i == j included)
     scans at p_cut, rows sharded over the ranks like configs[3] (GRM and REML on rank 0).  Each scan:
     one untimed full scan (codings and buffers at the timed size), then `reps` timed scans, median
-    reported.  Returns the record on rank 0.
+    reported.  On one GPU (`split`), each kind's 2 / 4 / 8-way split (dist.rank_rows: the reference's
+    folded parallel=[N, k] rows, remma_epiDD.py / remma_epiAD.py:134-140) is rehearsed part by part, as
+    configs[3]'s.  Returns the record on rank 0.
     The REML does not meet the reference's stopping rule here (gradient norm < 1e-6): the epistatic
     kernels are near-collinear at this size (asymptotic standard errors 10-48x the simulated AxA / AxD /
     DxD variances, tools/cfg5_identifiability.py), so the pure AI step leaves the positive orthant and
@@ -483,6 +485,11 @@ def cfg5_leg(n, m, p_cut, seed, reml_iters, rank, ws, backend, family_size=None,
         total += pairs
         t_all += dt
     out["pairs_per_s"] = total / t_all
+    if split and ws == 1:
+        log("configs[4] split rehearsed part by part")
+        out["split_rehearsal"] = {kind: split_emulation(plan, m, p_cut, out["epi" + kind]["s"] * 1e3,
+                                                        out["epi" + kind]["hits"], lib, reps=1, kind=kind)
+                                  for kind in ("DD", "AD")}
     plan.close()
     g.close()
     return out if rank == 0 else None
@@ -740,10 +747,15 @@ def main():
         kern_rec[kname] = {"kernel_s_per_step": v["s"] / args.steps, "launches_per_step": v["launches"] / args.steps,
                            "pairs_per_step": v["pairs"] / args.steps, "avg_launch_ms": v["s"] / v["launches"] * 1e3,
                            "achieved": rate, "unit": unit, "peak": peak, "frac": rate / peak, "ops_note": what,
-                           "work_per_pair": per_pair}
+                           "work_per_pair": per_pair,
+                           "stats_source": "HIP events of the last timed step, scaled to the %d steps" % args.steps}
     screens = [k for k in ("prefilter_pass_kernel", "lrc_screen_kernel") if k in kern_rec]
     if screens:
-        dom = max(screens, key=lambda k: kern_rec[k]["kernel_s_per_step"])
+        # the dominant kernel: the most work per step at its roof (issued ops / peak), not the longest
+        # event span -- the candidate kernels' spans stretch while they share the CUs with the next
+        # launch's prefilter, whose work per step is ~14x theirs
+        dom = max(screens, key=lambda k: kern_rec[k]["ops_per_launch"] * kern_rec[k]["kernel_s_per_step"]
+                  / kern_rec[k]["avg_launch_ms"])
         kr = kern_rec[dom]
         # fabric bytes per launch of this kernel from the PMC passes of tools/pmc.sh (FETCH_SIZE x 2 +
         # WRITE_SIZE); used only when recorded on the same kernel source (sha256 of the epi stage files), kernel,

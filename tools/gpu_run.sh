@@ -43,6 +43,15 @@ for st in "$@"; do
     bench)
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.log || { tail -30 $OUT/bench.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/bench.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
+    benchprof)
+      # rocprofv3 kernel trace + stats of the driver's default bench command (the roofline's launch times
+      # must agree with the stats of the same command)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bp -o run -- python3 bench.py > $OUT/benchprof.json 2> $OUT/benchprof.log || { tail -30 $OUT/benchprof.log; exit 1; }
+      cp $(find $OUT/bp -name "*kernel_stats.csv" | head -1) $OUT/bench_kernel_stats.csv
+      python3 tools/bench_trace_summary.py $(find $OUT/bp -name "*kernel_trace.csv" | head -1) $OUT/benchprof.json > $OUT/bench_rocprof_summary.txt || exit 1
+      cat $OUT/bench_rocprof_summary.txt
+      rm -rf $OUT/bp
+      head -8 $OUT/bench_kernel_stats.csv | cut -c1-160 ;;
     quick)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-grm --no-eff --no-e2e --no-cov --no-split --no-cfg5 > $OUT/quick.json 2> $OUT/quick.log || { tail -30 $OUT/quick.log; exit 1; }
       python -c "import json; d=json.load(open('$OUT/quick.json')); print('value %.4g ms %.2f frac %.3f' % (d['value'], d['ms_per_step'], d['roofline']['frac']))" ;;
