@@ -83,7 +83,9 @@ for st in "$@"; do
       # one rank's part of the 8-way split (rank 0), traced: the timeline of a multi-GPU step
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/part -o run -- python3 tools/split_part.py 0 8 5 > $OUT/part.log 2>&1 || { tail -30 $OUT/part.log; exit 1; }
       grep "part 0" $OUT/part.log | tail -3
-      python3 tools/step_timeline.py $(find $OUT/part -name "*kernel_trace.csv" | head -1) | tee $OUT/part_timeline.txt ;;
+      python3 tools/step_timeline.py $(find $OUT/part -name "*kernel_trace.csv" | head -1) | tee $OUT/part_timeline.txt
+      python3 tools/step_gantt.py $(find $OUT/part -name "*kernel_trace.csv" | head -1) > $OUT/part_gantt.txt
+      rm -rf $OUT/part ;;
     parthost)
       # host API trace of rank 0's part (which HIP calls sit between the steps' kernels)
       timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --output-format csv -d $OUT/parthost -o run -- python3 tools/split_part.py 0 8 5 > $OUT/parthost.log 2>&1 || { tail -30 $OUT/parthost.log; exit 1; }
@@ -94,6 +96,9 @@ for st in "$@"; do
     covtests)
       timeout -k 10 500 python -u -m pytest tests/test_gpu_scale.py tests/test_gpu_parity.py tests/test_gpu_workflow.py -x -q --timeout 300 --timeout-method thread > $OUT/covtests.log 2>&1 || { tail -40 $OUT/covtests.log; exit 1; }
       tail -2 $OUT/covtests.log ;;
+    cfg5split)
+      timeout -k 10 600 python -u bench.py --config cfg5 --cfg5-reps 1 > $OUT/cfg5split.json 2> $OUT/cfg5split.log || { tail -30 $OUT/cfg5split.log; exit 1; }
+      python -c "import json; d=json.load(open('$OUT/cfg5split.json')); print('cfg5 value %.3g' % d['value'], {k: {n: (round(v['projected_efficiency'], 3), v['hits_match_step']) for n, v in r.items()} for k, r in d['split_rehearsal'].items()})" ;;
     cfg5|cfg5f0|cfg5f2|cfg5f10)
       FS=5; case $st in cfg5f0) FS=0;; cfg5f2) FS=2;; cfg5f10) FS=10;; esac
       timeout -k 10 600 python -u bench.py --config cfg5 --family-size $FS --cfg5-reps ${CFG5_REPS:-3} > $OUT/$st.json 2> $OUT/$st.log || { tail -30 $OUT/$st.log; exit 1; }
