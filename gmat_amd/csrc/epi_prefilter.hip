@@ -258,6 +258,10 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     pstamp(1);
+    // the main loop at issue priority 1, the epilogue at 0: on a SIMD, one workgroup's MFMA stages take the
+    // issue slots before the other workgroup's epilogue VALU work (round 6: 1,347 -> 1,322 us per launch
+    // serialised, 1.446 -> 1.385 ms in the configs[2] step, step time unchanged)
+    if (TR == 32) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
 #pragma unroll
@@ -315,6 +319,7 @@ __global__ __launch_bounds__(TR * 8, TR == 64 ? 1 : 2) void prefilter_pass_kerne
       wait_for(st + 1, min(st + NS - 1, S - 1));
     }
     pstamp(2);
+    if (TR == 32) __builtin_amdgcn_s_setprio(0);
     // every wave has passed the last stage's barrier (its vmcnt(0) wait): the ring is free, so the
     // next tile's records and first stages go out now and land while this tile's epilogue runs
     const int nxt = tile_at(it + 1);
