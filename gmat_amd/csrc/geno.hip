@@ -59,42 +59,32 @@ __global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__
   }
 }
 
-// ---- GRM: int8 MFMA SYRK straight from the packed .bed rows.
+// ---- GRM: SYRK of the 0/1/2 codes on the block-scaled fp4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4).
 //
-// Work: the lower-triangular 256 x 256 tiles of GG' (G: individuals x SNPs codes), each a K loop
-// over 64-SNP stages.  The (tile, stage) iterations are laid out tile-major and dealt to a grid of
-// one workgroup (8 waves, each a 128 x 64 block) per CU in equal contiguous ranges (stream-K), so
-// a 2,000-individual panel (36 tiles) still fills 256 CUs; every range writes its int32 partial tile
-// to a slot and
-// grm_epilogue_kernel sums a tile's slots in a fixed order (exact integers: deterministic).
+// The codes are exact in fp4 e2m1 as halves (0, 0.5 = 0001, 1.0 = 0010: the 2-bit dosage itself in
+// the nibble's low bits), so with an e8m0 scale of 2 on each operand every product is the integer
+// g_a g_b and the fp32 accumulators hold exact integers (a sum is at most 4m <= 8e6 < 2^24).  fp4 runs
+// the 32x32 MFMA at K = 64 in the cycles the int8 form needs for K = 32.
 //
-// Staging: each thread loads 4 SNP rows x 4 bytes (16 individuals x 4 SNPs, 2 bits each) of the
-// packed rows, decodes the 2-bit codes in place (SWAR), gathers the 4 rows' bytes per byte position
-// with v_perm and writes each individual's 4 SNP codes as one dword of the LDS tile [row][k]
-// (pitch 80 B: conflict-free ds_read_b128 fragments, at most 2-way on the stores).  The code of individual 4p+f sits at bits
-// 2f of byte p; fields 0-2 are masked in place (values scaled by 1, 4, 16) and field 3 shifted by 4
-// (scale 4), so one AND (two for f = 3) yields int8 values <= 32; the product picks up the exact
-// factor s(f_a) s(f_b) <= 256, divided out in the epilogue.  LDS row of tile individual i (i =
-// 64h + 16d + x, x = 4b + f): 64h + 8(x >> 1) + 2d + (x & 1), so a wave's 64 x 64 quadrant of the
-// tile holds 64 contiguous individuals on each side, and the 32 lanes of a store group (four dword
-// positions d on rows 2 apart = 8 banks apart at the 80-byte pitch, eight SNP quads) hit 32
-// distinct banks.
-constexpr int GT = 256, GS = 64, GP = 80, GD = 4;  // GD: stages of packed rows in flight per thread
+// Image (grm_image_kernel, once per call): the panel transposed into 2-bit fragment images, one
+// 1 KB image per (32-individual row block rb, 128-SNP stage s) at ((rb S + s) 64 + L) 16: lane L
+// holds individual 32 rb + (L & 31); its dword k (< 4) the 16 codes of SNPs 128 s + 64 (k >> 1) +
+// 32 (L >> 5) + 16 (k & 1) + [0, 16), code t at bits 2t.  A wave expands dwords 2kk, 2kk + 1 into
+// the fp4 fragment of chunk kk with two masks (x & 0x33.., (x >> 2) & 0x33..: the codes of even and
+// odd t in the nibbles' low bits; the K order inside a fragment is the same for both operands).
+// Individuals past n and SNPs past m are zeros.  The image has the packed panel's size, so the
+// stages stream half the bytes fp4 images would (the LDS-DMA fabric, not the MFMA, bounds this loop).
+//
+// SYRK (grm_partial_kernel): the lower-triangular 256 x 256 tiles of GG', each a K loop over 128-SNP
+// stages (two 64-SNP chunks); the (tile, stage) iterations are laid out tile-major and dealt to one
+// workgroup (8 waves, each a 128 x 64 block) per CU in equal contiguous ranges (stream-K), so a
+// 2,000-individual panel (36 tiles) still fills 256 CUs; every range writes its partial tile (exact
+// integers) to a slot and grm_epilogue_kernel sums a tile's slots (exact: order-free).  A stage's
+// 16 images (8 KB per operand) stream into a six-stage LDS ring by LDS-DMA (2 per wave), the waves
+// read them with conflict-free ds_read_b128 (lane-contiguous images).
+constexpr int GT = 256, GS = 128, GNS = 6;
+constexpr int GSTAGE = 2 * (GT / 32) * 1024;  // bytes per ring stage: A and B tiles, 16 KB
 constexpr int GNT = 512;                            // threads: 8 waves, 2 x 4 wave tiles of 128 x 64
-
-// i = 64h + 16d + x  ->  row = 64h + 8(x >> 1) + 2d + (x & 1)
-__device__ __host__ inline int grm_row_of(int i) {
-  const int x = i & 15, d = (i >> 4) & 3;
-  return (i & ~63) + 8 * (x >> 1) + 2 * d + (x & 1);
-}
-__device__ __host__ inline int grm_ind_of(int row) {
-  const int r = row & 63;
-  return (row & ~63) + 16 * ((r >> 1) & 3) + 2 * (r >> 3) + (r & 1);
-}
-__device__ __host__ inline int grm_scale_of_row(int row) {
-  const int f = ((row >> 2) & 2) | (row & 1);  // field of the individual = its index mod 4
-  return f == 0 ? 1 : (f == 2 ? 16 : 4);
-}
 
 // 2-bit codes of an imputed panel (no 01) to dosages 00 -> 0, 10 -> 1, 11 -> 2 (c - c/2, no borrow
 // between fields) or to the heterozygote indicator (10 -> 1)
@@ -172,6 +162,36 @@ __global__ __launch_bounds__(256) void pad_rows_kernel(const uint8_t *__restrict
   if (j < m && b < nb4) dst[j * nb4 + b] = b < nb ? src[j * nb + b] : 0;
 }
 
+// the images of one (dword position dp = 16 individuals, stage s, lane half h): 64 row dwords decoded,
+// each individual's 4 dwords written as its lane's 16 bytes (16 consecutive lanes: 256 B contiguous)
+template <int KIND>
+__global__ __launch_bounds__(64) void grm_image_kernel(const uint8_t *__restrict__ packed, int64_t nbs, int64_t m,
+                                                       int64_t nd, int64_t S, uint8_t *__restrict__ img) {
+  const int64_t dp = (int64_t)blockIdx.x * 64 + threadIdx.x, s = blockIdx.y >> 1, h = blockIdx.y & 1;
+  if (dp >= nd) return;
+  uint32_t d[64];  // row (SNP) 128 s + 64 (k >> 1) + 32 h + 16 (k & 1) + t at d[16 k + t]
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int64_t j = 128 * s + 64 * (k >> 1) + 32 * h + 16 * (k & 1) + t;
+      d[16 * k + t] = (j < m && 4 * dp < nbs) ? grm_decode<KIND>(*(const uint32_t *)(packed + j * nbs + 4 * dp)) : 0u;
+    }
+#pragma unroll
+  for (int x = 0; x < 16; ++x) {
+    const int64_t ind = 16 * dp + x, rb = ind >> 5, L = (ind & 31) + 32 * h;
+    v4i o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) v |= ((d[16 * k + t] >> (2 * x)) & 3u) << (2 * t);
+      o[k] = (int)v;
+    }
+    *(v4i *)(img + ((rb * S + s) * 64 + L) * 16) = o;
+  }
+}
+
 struct GrmWork {
   const int *seg0;   // [W + 1]: the segments of workgroup w are [seg0[w], seg0[w+1])
   const int *stile;  // per segment: tile, first and end stage (the segment's slot = its index)
@@ -179,103 +199,87 @@ struct GrmWork {
   const int *ta, *tb;  // per tile: row / column tile
 };
 
-template <int KIND, bool ALIGNED>
-__global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restrict__ packed, int64_t nb, int64_t m,
-                                                          GrmWork wk, int *__restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) int8_t sm[2][2][GT * GP];  // [buffer][operand]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+typedef int v8i_g __attribute__((ext_vector_type(8)));
+typedef float v16f_g __attribute__((ext_vector_type(16)));
+
+// LDS-DMA of one 1 KB image per wave (lane i's 16 bytes land at m0 + 16 i), issued through inline asm
+// so that the kernel, not the compiler, counts vmcnt (the builtin makes every ds_read wait for it)
+__device__ __forceinline__ void grm_dma(unsigned voff, const void *sbase, unsigned m0) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+}
+
+// the fp4 fragment (dwords 2kk, 2kk + 1 of a lane's image bytes): codes of even / odd t per nibble
+__device__ __forceinline__ v8i_g grm_expand(int x0, int x1) {
+  const unsigned a = (unsigned)x0, b = (unsigned)x1;
+  return v8i_g{(int)(a & 0x33333333u), (int)((a >> 2) & 0x33333333u), (int)(b & 0x33333333u),
+               (int)((b >> 2) & 0x33333333u), 0, 0, 0, 0};
+}
+
+__global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restrict__ img, int S, GrmWork wk,
+                                                          int *__restrict__ partial) {
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[GNS * GSTAGE];  // 96 KB
+  typedef __attribute__((address_space(3))) const void *lds_ct;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;  // wave block: rows 128 wr .. +128, columns 64 wc .. +64
-  // loader (waves 0-3: row tile, 4-7: column tile): a store group of 32 lanes covers four dword
-  // positions (rows 2 apart) x eight SNP quads; each lane loads its dword of four stage rows
-  const int op = w >> 2, wv = w & 3;
-  const int dpos = (lane & 3) + 4 * (lane >> 5) + 8 * (wv & 1), qd = (wv >> 1) * 8 + ((lane >> 2) & 7);
+  // DMA role: waves 0-3 the row tile's images, 4-7 the column tile's; wave w moves the images of
+  // row blocks 2 (w & 3) + u (u < 2) of its operand
+  const int op = w >> 2, q0 = 2 * (w & 3);
+  const unsigned ring_b = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ct)&ring[0]);
   // XCD-aware: workgroup b runs on XCD b mod 8, so the work ranges are dealt in 8 contiguous
   // groups -- the workgroups of one XCD stream neighbouring tiles (shared row panels) in its L2
   const int nx = gridDim.x % 8 == 0 ? 8 : 1, bl = (blockIdx.x % nx) * (gridDim.x / nx) + blockIdx.x / nx;
   const int s0 = wk.seg0[bl], s1 = wk.seg0[bl + 1];
-  const __amdgpu_buffer_rsrc_t rs = grm_rsrc(packed, m * nb + 256);  // + the zeroed tail of the panel
+  const unsigned voff = 16u * lane;
   for (int sg = s0; sg < s1; ++sg) {
     const int t = wk.stile[sg], it0 = wk.sit0[sg], it1 = wk.sit1[sg];
-    // byte offsets of this thread's dword in its four rows of a stage; the stage adds it * GS * nb
-    // as the scalar offset, and rows past the panel read the zeroed tail or 0 (buffer range)
-    const int boff = (op ? wk.tb[t] : wk.ta[t]) * (GT / 4) + 4 * dpos;
-    int vo[4];
+    const int64_t rb0 = (int64_t)(op ? wk.tb[t] : wk.ta[t]) * (GT / 32);
+    const uint8_t *src[2];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) vo[q] = (4 * qd + q) * (int)nb + boff;
-    uint32_t raw[GD][4];  // register ring: stages in flight
-    auto load = [&](int it, uint32_t (&rw)[4]) {  // unconditional (past the segment: ignored or zeros),
-      const int so = it * GS * (int)nb;
+    for (int u = 0; u < 2; ++u) src[u] = img + (rb0 + q0 + u) * S * 1024;
+    // stage st of the ring (stages past the end re-read the last one: fixed DMA counts)
+    auto issue = [&](int st) __attribute__((always_inline)) {
+      const int sc = min(st, S - 1);
+      const unsigned m0 = ring_b + (unsigned)(st % GNS) * GSTAGE + op * (GSTAGE / 2) + q0 * 1024;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (ALIGNED) {
-          rw[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo[q], so, 0);
-        } else {
-          uint32_t v = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, vo[q] + k, so, 0) << (8 * k);
-          rw[q] = v;
-        }
-      }
+      for (int u = 0; u < 2; ++u) grm_dma(voff, src[u] + (int64_t)sc * 1024, m0 + u * 1024);
     };
-    auto unpack = [&](int buf, const uint32_t (&rw)[4]) {
-      const uint32_t d0 = grm_decode<KIND>(rw[0]), d1 = grm_decode<KIND>(rw[1]), d2 = grm_decode<KIND>(rw[2]),
-                     d3 = grm_decode<KIND>(rw[3]);
-      // X_b = [d0.b, d1.b, d2.b, d3.b]: byte position b of the four SNP rows
-      const uint32_t t01l = __builtin_amdgcn_perm(d1, d0, 0x05010400u), t23l = __builtin_amdgcn_perm(d3, d2, 0x05010400u);
-      const uint32_t t01h = __builtin_amdgcn_perm(d1, d0, 0x07030602u), t23h = __builtin_amdgcn_perm(d3, d2, 0x07030602u);
-      uint32_t X[4];
-      X[0] = __builtin_amdgcn_perm(t23l, t01l, 0x05040100u);
-      X[1] = __builtin_amdgcn_perm(t23l, t01l, 0x07060302u);
-      X[2] = __builtin_amdgcn_perm(t23h, t01h, 0x05040100u);
-      X[3] = __builtin_amdgcn_perm(t23h, t01h, 0x07060302u);
-      int8_t *dst = sm[buf][op] + 4 * qd;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int i0 = 16 * dpos + 4 * b;  // individuals i0 .. i0+3 (fields 0..3)
-        *(uint32_t *)(dst + grm_row_of(i0 + 0) * GP) = X[b] & 0x03030303u;
-        *(uint32_t *)(dst + grm_row_of(i0 + 1) * GP) = X[b] & 0x0c0c0c0cu;
-        *(uint32_t *)(dst + grm_row_of(i0 + 2) * GP) = X[b] & 0x30303030u;
-        *(uint32_t *)(dst + grm_row_of(i0 + 3) * GP) = (X[b] >> 4) & 0x0c0c0c0cu;
-      }
-    };
-    v16i acc[4][2];
+    v16f_g acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
-    // ring slot u holds stage it0 + u (mod GD); stage it0 is unpacked before the loop
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 #pragma unroll
-    for (int u = 0; u < GD; ++u) load(it0 + u, raw[u]);
-    unpack(0, raw[0]);
-    __syncthreads();
-    for (int base = it0; base < it1; base += GD) {  // segments hold whole multiples of GD stages
+    for (int u = 0; u < GNS - 1; ++u) issue(it0 + u);
+    for (int st = it0; st < it1; ++st) {
+      // stage st has landed for this wave (the later GNS - 2 stages may be in flight) and, after the
+      // barrier, for every wave; every wave is past stage st - 1, so its slot takes stage st + GNS - 1
+      static_assert(GNS == 6, "vmcnt: the later GNS - 2 stages' 2 DMAs per wave");
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      issue(st + GNS - 1);
+      const uint8_t *A = ring + (st % GNS) * GSTAGE, *B = A + GSTAGE / 2;
+      v4i xa[4], xb[2];
 #pragma unroll
-      for (int u = 0; u < GD; ++u) {
-        const int it = base + u;
-        const int cur = (it - it0) & 1;
-        load(it + GD, raw[u]);  // slot u's stage (it) is already in LDS
-        const int8_t *A = sm[cur][0], *B = sm[cur][1];
+      for (int tt = 0; tt < 4; ++tt) xa[tt] = *(const v4i *)&A[(wr * 4 + tt) * 1024 + 16 * lane];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          v4i fa[4], fb[2];
+      for (int tt = 0; tt < 2; ++tt) xb[tt] = *(const v4i *)&B[(wc * 2 + tt) * 1024 + 16 * lane];
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt)
-            fa[tt] = *(const v4i *)&A[(wr * 128 + tt * 32 + (lane & 31)) * GP + kk * 32 + (lane >> 5) * 16];
+      for (int kk = 0; kk < 2; ++kk) {
+        v8i_g fa[4], fb[2];
 #pragma unroll
-          for (int tt = 0; tt < 2; ++tt)
-            fb[tt] = *(const v4i *)&B[(wc * 64 + tt * 32 + (lane & 31)) * GP + kk * 32 + (lane >> 5) * 16];
+        for (int tt = 0; tt < 4; ++tt) fa[tt] = grm_expand(xa[tt][2 * kk], xa[tt][2 * kk + 1]);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int tt = 0; tt < 2; ++tt) fb[tt] = grm_expand(xb[tt][2 * kk], xb[tt][2 * kk + 1]);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        }
-        if (it + 1 < it1) unpack(cur ^ 1, raw[(u + 1) % GD]);
-        __syncthreads();
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[i], fb[j], acc[i][j], 4, 4, 0, 128, 0, 128);
       }
     }
+    // the ring's last (re-read) stages land before the next segment's prologue refills it
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     int *dst = partial + (int64_t)sg * GT * GT;
     // slot layout [wave][i][j][e4][lane][4]: every store instruction writes 1 KB contiguous
 #pragma unroll
@@ -285,19 +289,17 @@ __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restr
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           v4i v;
-          v[0] = acc[i][j][4 * e4];
-          v[1] = acc[i][j][4 * e4 + 1];
-          v[2] = acc[i][j][4 * e4 + 2];
-          v[3] = acc[i][j][4 * e4 + 3];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = (int)acc[i][j][4 * e4 + k];
           ((v4i *)dst)[(((w * 8 + i * 2 + j) * 4 + e4) * 64) + lane] = v;
         }
   }
 }
 
-// One workgroup per (tile, 128 x 64 wave block, 64-row half): sum the block's partial slots (fixed
-// order), undo the field scales, centre and scale in fp64 (v = (g - r_a - r_b + c'c) / scale,
-// diagonal times (1 + small_val)) and write it and its mirror with coalesced rows through an LDS
-// copy.
+// One workgroup per (tile, 128 x 64 wave block, 64-row half): sum the block's partial slots, centre
+// and scale in fp64 (v = (g - r_a - r_b + c'c) / scale, diagonal times (1 + small_val)) and write it
+// and its mirror with coalesced rows through an LDS copy.  Accumulator element (i, j, e, lane) of a
+// wave is row 32 i + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), column 32 j + (lane & 31) of its block.
 __global__ __launch_bounds__(256) void grm_epilogue_kernel(const int *__restrict__ partial, const int *__restrict__ slot0,
                                                            const int *__restrict__ ta_, const int *__restrict__ tb_,
                                                            int64_t n, const double *__restrict__ r, double cc,
@@ -322,19 +324,16 @@ __global__ __launch_bounds__(256) void grm_epilogue_kernel(const int *__restrict
     const int v4 = h * 1024 + tid + k * 256;
     const int lane = v4 & 63, e0 = ((v4 >> 6) & 3) * 4, ij = v4 >> 8;
     const int i = ij >> 1, j = ij & 1;
-    const int col = wc * 64 + j * 32 + (lane & 31);
-    const int bi = grm_ind_of(col) - wc * 64, sb = grm_scale_of_row(col);
+    const int bi = j * 32 + (lane & 31);
     const int64_t b = b0 + bi;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int e = e0 + q;
-      const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-      const int ai = grm_ind_of(row) - wr * 128 - h * 64, sa = grm_scale_of_row(row);
+      const int ai = (i & 1) * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);  // i in {2h, 2h + 1}
       const int64_t a = a0 + ai;
       double v = 0.0;
       if (a < n && b < n) {
-        const int g = s[k][q] / (sa * sb);  // exact: every product carries the factor sa * sb
-        v = ((double)g - r[a] - r[b] + cc) / scale;
+        v = ((double)s[k][q] - r[a] - r[b] + cc) / scale;
         if (a == b) v = v + v * small_val;
       }
       sk[ai][bi] = v;
@@ -470,8 +469,7 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   GMAT_CHECK(g->total_missing == 0, GMAT_E_ARG, "gmat_grm: panel has %lld missing genotypes (impute first)",
              (long long)g->total_missing);
   const int64_t n = g->n, m = g->m, nb = g->nb;
-  GMAT_CHECK(m <= 2000000 && (m + 2 * GS * GD) * round_up(nb, 4) + 256 < (1LL << 31), GMAT_E_ARG,
-             "gmat_grm: at most 2,000,000 SNPs and 2 GB of packed codes (int32 accumulation, 32-bit offsets)");
+  GMAT_CHECK(m <= 2000000, GMAT_E_ARG, "gmat_grm: at most 2,000,000 SNPs (exact fp32 / int32 accumulation)");
   // centring vector and scale exactly as gmatrix.py:53-57 (additive) / :116-120 (dominance)
   std::vector<double> c(m);
   double scale = 0.0, cc = 0.0;
@@ -490,14 +488,13 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   if (scale_out) *scale_out = scale;
   // stream-K work list: tiles (ta >= tb) x stages, tile-major, dealt in equal ranges
   const int nt = (int)cdiv(n, GT), ntile = nt * (nt + 1) / 2;
-  const int64_t S = round_up(cdiv(m, GS), GD), L = (int64_t)ntile * S;  // stages past m read zeros
+  const int64_t S = cdiv(m, GS), L = (int64_t)ntile * S;  // image SNPs past m are zeros
   int cus = 256;
   {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   }
-  const char *wenv = getenv("GMAT_GRM_WG_PER_CU");
-  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(L / GD, (int64_t)cus * (wenv ? std::max(1, atoi(wenv)) : 1)));
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(L, cus));  // one workgroup per CU (128 KB ring)
   std::vector<int> ta(ntile), tb(ntile), seg0(W + 1), st, s0, s1, slot0(ntile + 1, 0);
   for (int a = 0, t = 0; a < nt; ++a)
     for (int b = 0; b <= a; ++b, ++t) {
@@ -506,7 +503,7 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
     }
   for (int w = 0; w < W; ++w) {
     seg0[w] = (int)st.size();
-    const int64_t i0 = L / GD * w / W * GD, i1 = L / GD * (w + 1) / W * GD;
+    const int64_t i0 = L * w / W, i1 = L * (w + 1) / W;
     for (int64_t it = i0; it < i1;) {
       const int64_t t = it / S, e = std::min(i1, (t + 1) * S);
       st.push_back((int)t);
@@ -521,7 +518,8 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   for (int t = 0; t < ntile; ++t) slot0[t + 1] = std::max(slot0[t + 1], slot0[t]);
   std::vector<int> tabl;
   for (auto *v : {&seg0, &st, &s0, &s1, &ta, &tb, &slot0}) tabl.insert(tabl.end(), v->begin(), v->end());
-  DBuf dc, dr, dpart, dk, dtab, dpar;
+  DBuf dc, dr, dpart, dk, dtab, dpar, dimg;
+  const int64_t nd_img = (int64_t)nt * GT / 16;  // image dword positions: every tile row
   const int64_t nd = cdiv(nb, 4);
   const int nch = (int)cdiv(m, GR);
   GMAT_TRY(dc.alloc(m * sizeof(double)));
@@ -529,6 +527,7 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   GMAT_TRY(dpar.alloc((size_t)nch * 16 * nd * sizeof(double)));
   GMAT_TRY(dpart.alloc((size_t)nseg * GT * GT * sizeof(int)));
   GMAT_TRY(dk.alloc(n * n * sizeof(double)));
+  GMAT_TRY(dimg.alloc((size_t)nt * (GT / 32) * S * 1024));
   GMAT_TRY(dtab.alloc(tabl.size() * sizeof(int)));
   GMAT_HIP(hipMemcpy(dc.p, c.data(), m * sizeof(double), hipMemcpyHostToDevice));
   GMAT_HIP(hipMemcpy(dtab.p, tabl.data(), tabl.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -566,9 +565,12 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
                      nch, dr.as<double>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[1], 0));
-  auto kern = kind == GMAT_GRM_ADD ? (al ? grm_partial_kernel<GMAT_GRM_ADD, true> : grm_partial_kernel<GMAT_GRM_ADD, false>)
-                                   : (al ? grm_partial_kernel<GMAT_GRM_DOM, true> : grm_partial_kernel<GMAT_GRM_DOM, false>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)W), dim3(GNT), 0, 0, pk, nbs, m, wk, dpart.as<int>());
+  hipLaunchKernelGGL(kind == GMAT_GRM_ADD ? grm_image_kernel<GMAT_GRM_ADD> : grm_image_kernel<GMAT_GRM_DOM>,
+                     dim3((unsigned)cdiv(nd_img, 64), (unsigned)(2 * S)), dim3(64), 0, 0, pk, nbs, m, nd_img, S,
+                     dimg.as<uint8_t>());
+  GMAT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(grm_partial_kernel, dim3((unsigned)W), dim3(GNT), 0, 0, dimg.as<uint8_t>(), (int)S, wk,
+                     dpart.as<int>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[2], 0));
   hipLaunchKernelGGL(grm_epilogue_kernel, dim3((unsigned)ntile, 8, 2), dim3(256), 0, 0, dpart.as<int>(), dslot0, wk.ta, wk.tb, n,
@@ -580,8 +582,8 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   GMAT_HIP(hipEventElapsedTime(&ms_gemm, ev[1], ev[2]));
   GMAT_HIP(hipEventElapsedTime(&ms_all, ev[0], ev[3]));
   for (auto &x : ev) (void)hipEventDestroy(x);
-  g_grm_stats[0] = ms_gemm * 1e-3;                                   // grm_partial_kernel (the int8 SYRK)
-  g_grm_stats[1] = (double)ntile * 2.0 * GT * GT * (double)(cdiv(m, GS) * GS);  // int8 ops of the lower tiles
+  g_grm_stats[0] = ms_gemm * 1e-3;                                   // image + the fp4 SYRK
+  g_grm_stats[1] = (double)ntile * 2.0 * GT * GT * (double)(S * GS);  // fp4 MFMA ops of the lower tiles
   g_grm_stats[2] = 2.0 * (double)n * n * m;                           // dense-equivalent flop 2n^2m
   g_grm_stats[3] = ms_all * 1e-3;                                     // row sums + SYRK + epilogue
   GMAT_HIP(hipMemcpy(kin, dk.p, n * n * sizeof(double), hipMemcpyDeviceToHost));

@@ -64,8 +64,9 @@ int gmat_geno_destroy(gmat_geno *g);
  * dominance GRM of dgmat_as (gmatrix.py:115-130) for GMAT_GRM_DOM, diagonal scaled by
  * (1 + small_val).  *scale_out receives the scale factor. */
 int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, double *scale_out);
-/* last gmat_grm call: [0] seconds of the int8 MFMA product+epilogue kernel, [1] int8 ops it
- * issued, [2] dense-equivalent flop 2 n^2 m, [3] reserved */
+/* last gmat_grm call: [0] seconds of the product (fp4 fragment images + the block-scaled fp4 MFMA
+ * SYRK), [1] fp4 MFMA ops it issued, [2] dense-equivalent flop 2 n^2 m, [3] seconds of every kernel
+ * of the call (row sums, product, centring epilogue) */
 int gmat_grm_stats(double *out4);
 
 /* ainv = a^-1 for a symmetric positive-definite n x n matrix (scipy.linalg.inv at
