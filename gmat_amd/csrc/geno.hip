@@ -169,26 +169,43 @@ __global__ __launch_bounds__(64) void grm_image_kernel(const uint8_t *__restrict
                                                        int64_t nd, int64_t S, uint8_t *__restrict__ img) {
   const int64_t dp = (int64_t)blockIdx.x * 64 + threadIdx.x, s = blockIdx.y >> 1, h = blockIdx.y & 1;
   if (dp >= nd) return;
+  // the stage's rows through a buffer resource: rows past m read 0 (range check), no branches
+  const int64_t rows = std::min<int64_t>(128, m - 128 * s);
+  const __amdgpu_buffer_rsrc_t rs = grm_rsrc(packed + 128 * s * nbs, rows * nbs);
+  // dword positions past the row (individuals past n) read out of range too: zeros, no branches
+  const int vo = 4 * dp < nbs ? (int)(4 * dp) : 0x40000000;
   uint32_t d[64];  // row (SNP) 128 s + 64 (k >> 1) + 32 h + 16 (k & 1) + t at d[16 k + t]
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      const int64_t j = 128 * s + 64 * (k >> 1) + 32 * h + 16 * (k & 1) + t;
-      d[16 * k + t] = (j < m && 4 * dp < nbs) ? grm_decode<KIND>(*(const uint32_t *)(packed + j * nbs + 4 * dp)) : 0u;
+      const int r = 64 * (k >> 1) + 32 * (int)h + 16 * (k & 1) + t;
+      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, r * (int)nbs, 0);
+      d[16 * k + t] = grm_decode<KIND>(v);  // zero codes decode to zero
     }
+  // each k block: the 16 x 16 matrix of 2-bit codes (row t = SNP, field x = individual) transposed in
+  // place by delta swaps (blocks of 8, 4, 2, 1 fields): afterwards d[16 k + x] holds individual x's
+  // 16 codes, SNP t at bits 2t
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t *q = d + 16 * k;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 8 >> jj;
+      const uint32_t msk = jj == 0 ? 0x0000ffffu : jj == 1 ? 0x00ff00ffu : jj == 2 ? 0x0f0f0f0fu : 0x33333333u;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r & j) continue;
+        const uint32_t t = ((q[r] >> (2 * j)) ^ q[r + j]) & msk;
+        q[r + j] ^= t;
+        q[r] ^= t << (2 * j);
+      }
+    }
+  }
 #pragma unroll
   for (int x = 0; x < 16; ++x) {
     const int64_t ind = 16 * dp + x, rb = ind >> 5, L = (ind & 31) + 32 * h;
-    v4i o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) v |= ((d[16 * k + t] >> (2 * x)) & 3u) << (2 * t);
-      o[k] = (int)v;
-    }
-    *(v4i *)(img + ((rb * S + s) * 64 + L) * 16) = o;
+    *(v4i *)(img + ((rb * S + s) * 64 + L) * 16) = v4i{(int)d[x], (int)d[16 + x], (int)d[32 + x], (int)d[48 + x]};
   }
 }
 
@@ -215,6 +232,9 @@ __device__ __forceinline__ v8i_g grm_expand(int x0, int x1) {
                (int)((b >> 2) & 0x33333333u), 0, 0, 0, 0};
 }
 
+// SHORT: slots of 16-bit counts (a segment of at most 127 stages sums at most 4 x 128 x 127 < 2^16
+// per entry): half the slot bytes written here and read by the epilogue
+template <bool SHORT>
 __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restrict__ img, int S, GrmWork wk,
                                                           int *__restrict__ partial) {
   __shared__ __attribute__((aligned(1024))) uint8_t ring[GNS * GSTAGE];  // 96 KB
@@ -280,18 +300,22 @@ __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restr
     }
     // the ring's last (re-read) stages land before the next segment's prologue refills it
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    int *dst = partial + (int64_t)sg * GT * GT;
-    // slot layout [wave][i][j][e4][lane][4]: every store instruction writes 1 KB contiguous
+    // slot layout [wave][i][j][e4][lane][4 counts]: every store instruction writes 1 KB (512 B
+    // SHORT) contiguous
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
-          v4i v;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = (int)acc[i][j][4 * e4 + k];
-          ((v4i *)dst)[(((w * 8 + i * 2 + j) * 4 + e4) * 64) + lane] = v;
+          const int64_t at = (int64_t)sg * (GT * GT / 4) + (((w * 8 + i * 2 + j) * 4 + e4) * 64) + lane;
+          const float a[4] = {acc[i][j][4 * e4], acc[i][j][4 * e4 + 1], acc[i][j][4 * e4 + 2], acc[i][j][4 * e4 + 3]};
+          if (SHORT) {
+            typedef int v2i_g __attribute__((ext_vector_type(2)));
+            ((v2i_g *)partial)[at] = v2i_g{(int)a[0] | ((int)a[1] << 16), (int)a[2] | ((int)a[3] << 16)};
+          } else {
+            ((v4i *)partial)[at] = v4i{(int)a[0], (int)a[1], (int)a[2], (int)a[3]};
+          }
         }
   }
 }
@@ -300,6 +324,7 @@ __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restr
 // and scale in fp64 (v = (g - r_a - r_b + c'c) / scale, diagonal times (1 + small_val)) and write it
 // and its mirror with coalesced rows through an LDS copy.  Accumulator element (i, j, e, lane) of a
 // wave is row 32 i + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), column 32 j + (lane & 31) of its block.
+template <bool SHORT>
 __global__ __launch_bounds__(256) void grm_epilogue_kernel(const int *__restrict__ partial, const int *__restrict__ slot0,
                                                            const int *__restrict__ ta_, const int *__restrict__ tb_,
                                                            int64_t n, const double *__restrict__ r, double cc,
@@ -313,11 +338,19 @@ __global__ __launch_bounds__(256) void grm_epilogue_kernel(const int *__restrict
   v4i s[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) s[k] = v4i{0, 0, 0, 0};
-  const v4i *base = (const v4i *)partial + (size_t)w * 2048 + h * 1024 + tid;
+  const size_t base = (size_t)w * 2048 + h * 1024 + tid;
   for (int sl = sbeg; sl < send; ++sl) {
-    const v4i *src = base + (size_t)sl * (GT * GT / 4);
+    const size_t at = base + (size_t)sl * (GT * GT / 4);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s[k] += src[k * 256];
+    for (int k = 0; k < 4; ++k) {
+      if (SHORT) {
+        typedef unsigned v2u_g __attribute__((ext_vector_type(2)));
+        const v2u_g x = ((const v2u_g *)partial)[at + k * 256];
+        s[k] += v4i{(int)(x[0] & 0xffffu), (int)(x[0] >> 16), (int)(x[1] & 0xffffu), (int)(x[1] >> 16)};
+      } else {
+        s[k] += ((const v4i *)partial)[at + k * 256];
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -514,6 +547,9 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   }
   seg0[W] = (int)st.size();
   const int nseg = (int)st.size();
+  int longest = 0;
+  for (int sg = 0; sg < nseg; ++sg) longest = std::max(longest, s1[sg] - s0[sg]);
+  const bool shorts = longest * GS * 4 < 65536;  // 16-bit slots hold every segment's counts
   for (int sg = 0; sg < nseg; ++sg) slot0[st[sg] + 1] = sg + 1;  // segments are in tile order
   for (int t = 0; t < ntile; ++t) slot0[t + 1] = std::max(slot0[t + 1], slot0[t]);
   std::vector<int> tabl;
@@ -569,11 +605,12 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
                      dim3((unsigned)cdiv(nd_img, 64), (unsigned)(2 * S)), dim3(64), 0, 0, pk, nbs, m, nd_img, S,
                      dimg.as<uint8_t>());
   GMAT_HIP(hipGetLastError());
-  hipLaunchKernelGGL(grm_partial_kernel, dim3((unsigned)W), dim3(GNT), 0, 0, dimg.as<uint8_t>(), (int)S, wk,
-                     dpart.as<int>());
+  hipLaunchKernelGGL(shorts ? grm_partial_kernel<true> : grm_partial_kernel<false>, dim3((unsigned)W), dim3(GNT), 0, 0,
+                     dimg.as<uint8_t>(), (int)S, wk, dpart.as<int>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[2], 0));
-  hipLaunchKernelGGL(grm_epilogue_kernel, dim3((unsigned)ntile, 8, 2), dim3(256), 0, 0, dpart.as<int>(), dslot0, wk.ta, wk.tb, n,
+  hipLaunchKernelGGL(shorts ? grm_epilogue_kernel<true> : grm_epilogue_kernel<false>, dim3((unsigned)ntile, 8, 2), dim3(256),
+                     0, 0, dpart.as<int>(), dslot0, wk.ta, wk.tb, n,
                      dr.as<double>(), cc, scale, small_val, dk.as<double>());
   GMAT_HIP(hipGetLastError());
   GMAT_HIP(hipEventRecord(ev[3], 0));
