@@ -115,21 +115,23 @@ __global__ __launch_bounds__(64) void grm_rowdot_kernel(const uint8_t *__restric
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.0;
   const int64_t j0 = ch * GR, j1 = std::min<int64_t>(m, j0 + GR);
+  // the chunk's rows through a buffer resource (rows past m read 0): the loads go out together
+  const __amdgpu_buffer_rsrc_t rs = grm_rsrc(packed + j0 * nb, (j1 - j0) * nb);
   for (int64_t jb = j0; jb < j1; jb += 16) {
     uint32_t raw[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int64_t j = jb + u;
-      uint32_t v = 0;
-      if (j < j1) {
-        const uint8_t *src = packed + j * nb + 4 * dp;
-        if (ALIGNED)
-          v = *(const uint32_t *)src;
-        else
-          v = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
+      const int so = (int)((jb + u - j0) * nb);
+      if (ALIGNED) {
+        raw[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * dp), so, 0);
+      } else {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(4 * dp) + k, so, 0) << (8 * k);
+        raw[u] = v;
       }
-      raw[u] = v;
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       if (jb + u >= j1) break;
@@ -180,9 +182,13 @@ __global__ __launch_bounds__(64) void grm_image_kernel(const uint8_t *__restrict
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int r = 64 * (k >> 1) + 32 * (int)h + 16 * (k & 1) + t;
-      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, r * (int)nbs, 0);
-      d[16 * k + t] = grm_decode<KIND>(v);  // zero codes decode to zero
+      d[16 * k + t] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, r * (int)nbs, 0);
     }
+  // every load issued before the first decode (otherwise the scheduler can put each decode, and so a
+  // vmcnt(0) wait, right behind its load: 64 serial round trips)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < 64; ++t) d[t] = grm_decode<KIND>(d[t]);  // zero codes decode to zero
   // each k block: the 16 x 16 matrix of 2-bit codes (row t = SNP, field x = individual) transposed in
   // place by delta swaps (blocks of 8, 4, 2, 1 fields): afterwards d[16 k + x] holds individual x's
   // 16 codes, SNP t at bits 2t
