@@ -170,12 +170,13 @@ template <int KIND>
 __global__ __launch_bounds__(64) void grm_image_kernel(const uint8_t *__restrict__ packed, int64_t nbs, int64_t m,
                                                        int64_t nd, int64_t S, uint8_t *__restrict__ img) {
   const int64_t dp = (int64_t)blockIdx.x * 64 + threadIdx.x, s = blockIdx.y >> 1, h = blockIdx.y & 1;
-  if (dp >= nd) return;
+  // threads past nd (when nd is not a multiple of 64) load zeros and store nothing (the LDS pass below
+  // needs every thread of the block)
   // the stage's rows through a buffer resource: rows past m read 0 (range check), no branches
   const int64_t rows = std::min<int64_t>(128, m - 128 * s);
   const __amdgpu_buffer_rsrc_t rs = grm_rsrc(packed + 128 * s * nbs, rows * nbs);
   // dword positions past the row (individuals past n) read out of range too: zeros, no branches
-  const int vo = 4 * dp < nbs ? (int)(4 * dp) : 0x40000000;
+  const int vo = (dp < nd && 4 * dp < nbs) ? (int)(4 * dp) : 0x40000000;
   uint32_t d[64];  // row (SNP) 128 s + 64 (k >> 1) + 32 h + 16 (k & 1) + t at d[16 k + t]
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -208,10 +209,20 @@ __global__ __launch_bounds__(64) void grm_image_kernel(const uint8_t *__restrict
       }
     }
   }
+  // through LDS, so that every store instruction writes two whole 512-byte lane-half runs: thread t's
+  // individual x (block-local 16 t + x) at LDS slot 17 t + x (conflict-free 16-byte writes), then lane
+  // l of pass p stores individual 32 (2 p + (l >> 5)) + (l & 31) of the block
+  __shared__ v4i stg[64 * 17];
+  const int tl = threadIdx.x;
 #pragma unroll
-  for (int x = 0; x < 16; ++x) {
-    const int64_t ind = 16 * dp + x, rb = ind >> 5, L = (ind & 31) + 32 * h;
-    *(v4i *)(img + ((rb * S + s) * 64 + L) * 16) = v4i{(int)d[x], (int)d[16 + x], (int)d[32 + x], (int)d[48 + x]};
+  for (int x = 0; x < 16; ++x) stg[17 * tl + x] = v4i{(int)d[x], (int)d[16 + x], (int)d[32 + x], (int)d[48 + x]};
+  __syncthreads();
+  const int64_t nrb = nd / 2;  // row blocks of the image (32 individuals = 2 dword positions each)
+#pragma unroll 4
+  for (int p = 0; p < 16; ++p) {
+    const int il = 32 * (2 * p + (tl >> 5)) + (tl & 31);
+    const int64_t rb = ((int64_t)blockIdx.x * 1024 + il) >> 5;
+    if (rb < nrb) *(v4i *)(img + ((rb * S + s) * 64 + (il & 31) + 32 * h) * 16) = stg[17 * (il >> 4) + (il & 15)];
   }
 }
 
