@@ -6,6 +6,7 @@
 // Right-looking, 64-wide panels: a one-workgroup kernel factors the diagonal block (16-wide
 // sub-panels in registers) and inverts its factor; the panel solve and the trailing update are
 // MFMA dgemm calls.
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -17,7 +18,7 @@
 #endif
 #ifndef CHOL_TASK_BEGIN
 #define CHOL_TASK_BEGIN
-#define CHOL_TASK_END
+#define CHOL_TASK_END(task)
 #endif
 
 namespace gmat {
@@ -329,15 +330,15 @@ __device__ __forceinline__ void acc_axpy(v4d y[2][2], double alpha, const v4d x[
     for (int bj = 0; bj < 2; ++bj) y[bi][bj] += alpha * x[bi][bj];
 }
 
-__device__ __forceinline__ void step_tasks(const StepArgs &x, double (*P0)[NB + 1], double (*P1)[NB + 1], double *piv) {
+// the D task of launch k (block d = k + 1)
+__device__ __forceinline__ void step_d(const StepArgs &x, double (*P0)[NB + 1], double (*P1)[NB + 1], double *piv) {
   const int64_t n = x.n, lda = x.lda;
   const int k = x.k;
   const int64_t k0 = (int64_t)k * NB;
   auto bsize = [n](int b) { return std::min<int64_t>(NB, n - (int64_t)b * NB); };
-  int task = (int)blockIdx.x;
-  TileRegs t0, t1, t2;
-  v4d acc[2][2], acc2[2][2], cc[2][2];
-  if (task < x.nD) {  // D: block d = k + 1
+  TileRegs t0, t1;
+  v4d acc[2][2], cc[2][2];
+  {  // D: block d = k + 1
     const int64_t d0 = k0 + NB, nd = bsize(k + 1);
     if (k >= 0) {
       tile_load(t1, x.dinv + k0 * NB, NB, 0, 0, NB, NB, false);  // inv(L_kk), a full block (k + 1 < K)
@@ -383,9 +384,17 @@ __device__ __forceinline__ void step_tasks(const StepArgs &x, double (*P0)[NB + 
         if (bad && *x.info == 0) *x.info = (int)(d0 + 1);
       }
     }
-    return;
   }
-  task -= x.nD;
+}
+
+// the other tasks of launch k (T1, T3, W, T5)
+__device__ __forceinline__ void step_t(const StepArgs &x, double (*P0)[NB + 1], double (*P1)[NB + 1], int task) {
+  const int64_t n = x.n, lda = x.lda;
+  const int k = x.k;
+  const int64_t k0 = (int64_t)k * NB;
+  auto bsize = [n](int b) { return std::min<int64_t>(NB, n - (int64_t)b * NB); };
+  TileRegs t0, t1, t2;
+  v4d acc[2][2], acc2[2][2], cc[2][2];
   if (task < x.nT1 + x.nT3) {
     int bi, bj;
     const bool t1t = task < x.nT1;
@@ -489,13 +498,22 @@ __device__ __forceinline__ void step_tasks(const StepArgs &x, double (*P0)[NB + 
   }
 }
 
-__global__ __launch_bounds__(256) void chol_step_kernel(StepArgs x) {
+// ROLE 0: the D task alone (one workgroup; the 64 x 64 factor takes ~340 registers); ROLE 1: the
+// product tasks alone, two workgroups per CU (188 registers); ROLE 2: both in one launch (task 0 the D
+// task), one workgroup per CU.  cholesky_steps runs 0 and 1 side by side on two streams for the steps
+// with many product tasks, 2 for the others.
+template <int ROLE>
+__global__ __launch_bounds__(256, ROLE == 1 ? 2 : 1) void chol_step_kernel(StepArgs x) {
   __shared__ double P0[NB][NB + 1];
   __shared__ double P1[NB][NB + 1];
   __shared__ double piv[NB];
   CHOL_TASK_BEGIN;
-  step_tasks(x, P0, P1, piv);
-  CHOL_TASK_END;
+  const int task = ROLE == 1 ? x.nD + (int)blockIdx.x : (int)blockIdx.x;
+  if (ROLE == 0 || (ROLE == 2 && task < x.nD))
+    step_d(x, P0, P1, piv);
+  else
+    step_t(x, P0, P1, task - x.nD);
+  CHOL_TASK_END(task);
 }
 
 __global__ void identity_kernel(double *p, int64_t n) {
@@ -516,7 +534,40 @@ __global__ void copy_block_kernel(int kb, const double *src, double *dst, int64_
 }  // namespace
 
 // The factorisation, X = L^-1 into linv (n x n) when given and V^-1 = X'X into vinv (n x n, full; needs
-// linv) when given, as K + 2 (+ 1 with vinv) chol_step_kernel launches.
+// linv) when given.  Step k's D task and product tasks touch disjoint blocks; D(k) needs T(k - 1) (its
+// block's last updates) and T(k) needs D(k - 1) (inv(L_kk)).  A step with at least CHOL_SPLIT product
+// tasks runs D (chol_step_kernel<0>) on a side stream beside them (chol_step_kernel<1>, two workgroups
+// per CU), two events carrying those edges; the others run as one launch (<2>, or <1> without a D
+// task) on s: a cross-stream edge costs ~10 us per step, which only a long product launch repays
+// (REML at n = 5,000: 11.7 -> 10.3 ms per iteration split at every step, n = 2,000: 1.33 -> 1.72).
+constexpr int CHOL_SPLIT = 768;
+namespace {
+// the D stream: one per device, created on first use and kept (a pooled stream would be synchronised
+// by the host on release, after the whole factorisation)
+int chol_side_stream(hipStream_t *out) {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> side;
+  int dev = 0;
+  GMAT_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = side.find(dev);
+  if (it == side.end()) {
+    hipStream_t st = nullptr;
+    GMAT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    it = side.emplace(dev, st).first;
+  }
+  *out = it->second;
+  return GMAT_OK;
+}
+struct StepEvents {  // the two events of one call (per call: concurrent callers share the D stream)
+  hipEvent_t ed = nullptr, et = nullptr;
+  ~StepEvents() {
+    if (ed) (void)hipEventDestroy(ed);
+    if (et) (void)hipEventDestroy(et);
+  }
+};
+}  // namespace
+
 int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *dinv, double *logdet_dev, int *info_dev,
                    double *linv, bool keep_l, double *vinv) {
   GMAT_CHECK(!vinv || linv, GMAT_E_ARG, "cholesky_steps: V^-1 needs L^-1");
@@ -528,6 +579,11 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
   }
   const int K = (int)cdiv(n, NB);
   GMAT_CHECK((int64_t)K * (K + 1) / 2 < (1ll << 31), GMAT_E_ARG, "cholesky_steps: n = %lld", (long long)n);
+  struct {
+    hipStream_t s2 = nullptr;
+    StepEvents ev;
+  } ss;
+  bool d_pending = false;              // ed holds a D launch that s has not waited for
   for (int k = -1; k <= K + (vinv ? 1 : 0); ++k) {
     StepArgs x{};
     x.n = n;
@@ -551,11 +607,35 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
     x.nWX = (k >= 1 && k <= K && linv) ? k : 0;
     const int q = k - 2;
     x.nT5 = (vinv && q >= 0 && q < K) ? (q + 1) * (q + 2) / 2 : 0;
-    const int64_t grid = (int64_t)x.nD + x.nT1 + x.nT3 + x.nWL + x.nWX + x.nT5;
-    if (grid == 0) continue;
-    hipLaunchKernelGGL(chol_step_kernel, dim3((unsigned)grid), dim3(256), 0, s, x);
-    GMAT_HIP(hipGetLastError());
+    const int64_t grid = (int64_t)x.nT1 + x.nT3 + x.nWL + x.nWX + x.nT5;
+    if (x.nD && grid >= CHOL_SPLIT) {
+      // D(k) after T(k - 1) (et: everything queued on s so far) on the side stream, T(k) after D(k - 1)
+      // (ed) on s; the stream and events are set up at the first split step (none at small n)
+      if (!ss.s2) {
+        GMAT_TRY(chol_side_stream(&ss.s2));
+        GMAT_HIP(hipEventCreateWithFlags(&ss.ev.ed, hipEventDisableTiming));
+        GMAT_HIP(hipEventCreateWithFlags(&ss.ev.et, hipEventDisableTiming));
+      }
+      GMAT_HIP(hipEventRecord(ss.ev.et, s));
+      GMAT_HIP(hipStreamWaitEvent(ss.s2, ss.ev.et, 0));
+      hipLaunchKernelGGL(chol_step_kernel<0>, dim3(1), dim3(256), 0, ss.s2, x);
+      GMAT_HIP(hipGetLastError());
+      if (d_pending) GMAT_HIP(hipStreamWaitEvent(s, ss.ev.ed, 0));
+      hipLaunchKernelGGL(chol_step_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, x);
+      GMAT_HIP(hipGetLastError());
+      GMAT_HIP(hipEventRecord(ss.ev.ed, ss.s2));
+      d_pending = true;
+    } else if (x.nD + grid > 0) {  // one launch on s
+      if (d_pending) GMAT_HIP(hipStreamWaitEvent(s, ss.ev.ed, 0));
+      d_pending = false;
+      if (x.nD)
+        hipLaunchKernelGGL(chol_step_kernel<2>, dim3((unsigned)(x.nD + grid)), dim3(256), 0, s, x);
+      else
+        hipLaunchKernelGGL(chol_step_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, x);
+      GMAT_HIP(hipGetLastError());
+    }
   }
+  if (d_pending) GMAT_HIP(hipStreamWaitEvent(s, ss.ev.ed, 0));  // the last D before s's later work
   return GMAT_OK;
 }
 

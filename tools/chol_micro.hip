@@ -8,10 +8,10 @@ __device__ long long g_stamp[8];
 __device__ long long *g_task;
 constexpr int MAXT = 4096;
 #define CHOL_TASK_BEGIN const long long t_begin_ = wall_clock64();
-#define CHOL_TASK_END                                                              \
-  if (threadIdx.x == 0 && g_task && blockIdx.x < MAXT) {                           \
-    g_task[((int64_t)(x.k + 1) * MAXT + blockIdx.x) * 2] = t_begin_;               \
-    g_task[((int64_t)(x.k + 1) * MAXT + blockIdx.x) * 2 + 1] = wall_clock64();     \
+#define CHOL_TASK_END(task)                                                        \
+  if (threadIdx.x == 0 && g_task && (task) < MAXT) {                               \
+    g_task[((int64_t)(x.k + 1) * MAXT + (task)) * 2] = t_begin_;                   \
+    g_task[((int64_t)(x.k + 1) * MAXT + (task)) * 2 + 1] = wall_clock64();         \
   }
 #include "../gmat_amd/csrc/chol.hip"
 
