@@ -223,6 +223,10 @@ struct StepArgs {
   bool keep_l;  // L into a (else a is scratch: the W_L tasks and D's write of L_dd are skipped)
   double *a, *linv, *dinv, *logdet, *vinv;
   int *info;
+  // split steps: the panel L_ik (i > k) and X_kj (j <= k) of step k precomputed by chol_step_kernel<3>
+  // into 64 x 64 tiles (tile b at b NB^2, row-major), so that a product task does one product, not three
+  double *lp, *xr;
+  int nPL, nPX;
 };
 
 // acc (+)= A B' for NB x NB operands in LDS (row-major, pitch NB + 1): wave w the 32 x 32 quadrant at rows
@@ -414,6 +418,23 @@ __device__ __forceinline__ void step_t(const StepArgs &x, double (*P0)[NB + 1], 
     const bool two = !t1t || bj != bi;
     double *dst = t1t ? x.a : x.linv;
     const int64_t ldd = t1t ? lda : n;
+    if (x.lp) {  // the panel tiles precomputed: one product
+      tile_load(t0, x.lp + (int64_t)bi * NB * NB, NB, 0, 0, ni, NB, false);  // L_ik
+      if (t1t) {
+        if (two) tile_load(t2, x.lp + (int64_t)bj * NB * NB, NB, 0, 0, nj, NB, false);  // L_jk
+      } else {
+        tile_load(t2, x.xr + (int64_t)bj * NB * NB, NB, 0, 0, NB, nj, false);  // X_kj
+      }
+      acc_load(cc, dst, ldd, i0, j0, ni, nj);
+      tile_to_lds(P0, t0, false);
+      if (two) tile_to_lds(P1, t2, !t1t);  // L_jk, or X_kj'
+      __syncthreads();
+      acc_zero(acc);
+      mm_abt(P0, two ? P1 : P0, acc);
+      acc_axpy(cc, -1.0, acc);
+      acc_store(dst, ldd, i0, j0, ni, nj, cc);
+      return;
+    }
     tile_load(t1, x.dinv + k0 * NB, NB, 0, 0, NB, NB, false);  // inv(L_kk) (k < K - 1)
     tile_load(t0, x.a, lda, i0, k0, ni, NB, false);            // A_ik
     if (t1t) {
@@ -498,18 +519,53 @@ __device__ __forceinline__ void step_t(const StepArgs &x, double (*P0)[NB + 1], 
   }
 }
 
+// the panel of split step k: task p < nPL: L_ik = A_ik inv(L_kk)' (i = k + 1 + p) into lp tile i; else
+// X_kj = inv(L_kk) B_kj (j = p - nPL) into xr tile j -- the products the self-contained tasks derive
+__device__ __forceinline__ void step_p(const StepArgs &x, double (*P0)[NB + 1], double (*P1)[NB + 1], int p) {
+  const int64_t n = x.n;
+  const int k = x.k;
+  const int64_t k0 = (int64_t)k * NB;
+  auto bsize = [n](int b) { return std::min<int64_t>(NB, n - (int64_t)b * NB); };
+  TileRegs t0, t1;
+  v4d acc[2][2];
+  tile_load(t1, x.dinv + k0 * NB, NB, 0, 0, NB, NB, false);  // inv(L_kk)
+  if (p < x.nPL) {
+    const int i = k + 1 + p;
+    const int64_t ni = bsize(i);
+    tile_load(t0, x.a, x.lda, (int64_t)i * NB, k0, ni, NB, false);  // A_ik
+    tile_to_lds(P1, t1, false);
+    tile_to_lds(P0, t0, false);
+    __syncthreads();
+    acc_zero(acc);
+    mm_abt(P0, P1, acc);
+    acc_store(x.lp + (int64_t)i * NB * NB, NB, 0, 0, ni, NB, acc);
+  } else {
+    const int j = p - x.nPL;
+    const int64_t nj = bsize(j);
+    tile_load(t0, x.linv, n, k0, (int64_t)j * NB, NB, nj, false);  // B_kj
+    tile_to_lds(P1, t1, false);
+    tile_to_lds(P0, t0, true);
+    __syncthreads();
+    acc_zero(acc);
+    mm_abt(P1, P0, acc);
+    acc_store(x.xr + (int64_t)j * NB * NB, NB, 0, 0, NB, nj, acc);
+  }
+}
+
 // ROLE 0: the D task alone (one workgroup; the 64 x 64 factor takes ~340 registers); ROLE 1: the
 // product tasks alone, two workgroups per CU (188 registers); ROLE 2: both in one launch (task 0 the D
 // task), one workgroup per CU.  cholesky_steps runs 0 and 1 side by side on two streams for the steps
-// with many product tasks, 2 for the others.
+// with many product tasks, 2 for the others; ROLE 3: the split step's panel (step_p).
 template <int ROLE>
-__global__ __launch_bounds__(256, ROLE == 1 ? 2 : 1) void chol_step_kernel(StepArgs x) {
+__global__ __launch_bounds__(256, ROLE == 1 || ROLE == 3 ? 2 : 1) void chol_step_kernel(StepArgs x) {
   __shared__ double P0[NB][NB + 1];
   __shared__ double P1[NB][NB + 1];
   __shared__ double piv[NB];
   CHOL_TASK_BEGIN;
   const int task = ROLE == 1 ? x.nD + (int)blockIdx.x : (int)blockIdx.x;
-  if (ROLE == 0 || (ROLE == 2 && task < x.nD))
+  if (ROLE == 3)
+    step_p(x, P0, P1, task);
+  else if (ROLE == 0 || (ROLE == 2 && task < x.nD))
     step_d(x, P0, P1, piv);
   else
     step_t(x, P0, P1, task - x.nD);
@@ -536,10 +592,13 @@ __global__ void copy_block_kernel(int kb, const double *src, double *dst, int64_
 // The factorisation, X = L^-1 into linv (n x n) when given and V^-1 = X'X into vinv (n x n, full; needs
 // linv) when given.  Step k's D task and product tasks touch disjoint blocks; D(k) needs T(k - 1) (its
 // block's last updates) and T(k) needs D(k - 1) (inv(L_kk)).  A step with at least CHOL_SPLIT product
-// tasks runs D (chol_step_kernel<0>) on a side stream beside them (chol_step_kernel<1>, two workgroups
-// per CU), two events carrying those edges; the others run as one launch (<2>, or <1> without a D
-// task) on s: a cross-stream edge costs ~10 us per step, which only a long product launch repays
-// (REML at n = 5,000: 11.7 -> 10.3 ms per iteration split at every step, n = 2,000: 1.33 -> 1.72).
+// tasks runs D (chol_step_kernel<0>) on a side stream beside its panel (<3>: L_ik and X_kj once, into
+// scratch tiles) and its product tasks (<1>, two workgroups per CU, one product each instead of
+// deriving their panel tiles), two events carrying the edges; the others run as one launch (<2>, or
+// <1> without a D task) on s: a cross-stream edge costs ~10 us per step, which only a long product
+// launch repays (REML at n = 2,000 split at every step: 1.33 -> 1.72 ms per iteration).  REML at
+// n = 5,000 (5 GRMs): 11.7 ms per iteration as one launch per step, 10.3 with D beside the
+// self-deriving products, 8.0 with the panel launch (same bits).
 constexpr int CHOL_SPLIT = 768;
 namespace {
 // the D stream: one per device, created on first use and kept (a pooled stream would be synchronised
@@ -583,6 +642,7 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
     hipStream_t s2 = nullptr;
     StepEvents ev;
   } ss;
+  DBuf lp, xr;  // split steps' panel tiles (declared after ss: freed first, after the synchronise)
   bool d_pending = false;              // ed holds a D launch that s has not waited for
   for (int k = -1; k <= K + (vinv ? 1 : 0); ++k) {
     StepArgs x{};
@@ -621,6 +681,17 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
       hipLaunchKernelGGL(chol_step_kernel<0>, dim3(1), dim3(256), 0, ss.s2, x);
       GMAT_HIP(hipGetLastError());
       if (d_pending) GMAT_HIP(hipStreamWaitEvent(s, ss.ev.ed, 0));
+      // the panel of step k, then its product tasks with one product each
+      if (!lp.p) {
+        GMAT_TRY(lp.alloc((size_t)K * NB * NB * sizeof(double)));
+        if (linv) GMAT_TRY(xr.alloc((size_t)K * NB * NB * sizeof(double)));
+      }
+      x.lp = lp.as<double>();
+      x.xr = linv ? xr.as<double>() : nullptr;
+      x.nPL = K - 1 - k;
+      x.nPX = linv ? k + 1 : 0;
+      hipLaunchKernelGGL(chol_step_kernel<3>, dim3((unsigned)(x.nPL + x.nPX)), dim3(256), 0, s, x);
+      GMAT_HIP(hipGetLastError());
       hipLaunchKernelGGL(chol_step_kernel<1>, dim3((unsigned)grid), dim3(256), 0, s, x);
       GMAT_HIP(hipGetLastError());
       GMAT_HIP(hipEventRecord(ss.ev.ed, ss.s2));
@@ -636,6 +707,7 @@ int cholesky_steps(hipStream_t s, int64_t n, double *a, int64_t lda, double *din
     }
   }
   if (d_pending) GMAT_HIP(hipStreamWaitEvent(s, ss.ev.ed, 0));  // the last D before s's later work
+  if (lp.p) GMAT_HIP(hipStreamSynchronize(s));  // the panel scratch goes back to the pool below
   return GMAT_OK;
 }
 

@@ -2,6 +2,7 @@
 kernels (chol.hip, dgemm.hip): the configs[1] shape (2 GRMs, n = 2,000) and the configs[4] shape
 (5 GRMs, n = 5,000, fixed iteration count), random SPD relationship matrices.
    GMAT_HIP_LIB=ab/lib_x.so python tools/reml_ab.py NAME"""
+import hashlib
 import json
 import os
 import sys
@@ -30,7 +31,8 @@ def main():
         ks = [k if i % 2 == 0 else k * ks[0] for i, k in enumerate(ks)]
         y = 1.0 + rng.standard_normal(n)
         _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), ks, maxiter=3)
-        _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), ks, maxiter=iters, cc_par=-1.0, cc_gra=-1.0)
+        var = _wemai_multi_gmat(y, np.ones((n, 1)), identity(n, format="csr"), ks, maxiter=iters, cc_par=-1.0,
+                                cc_gra=-1.0)
         st = np.zeros(4)
         N.check(lib.gmat_reml_stats(N.ptr(st)), "gmat_reml_stats")
         a = ks[0] + n * 1e-3 * np.eye(n)
@@ -43,7 +45,8 @@ def main():
         err = float(np.abs(ai @ a - np.eye(n)).max())
         out["n%d_g%d" % (n, ng)] = {"iters": int(st[1]), "ms_per_iter": st[2] * 1e3,
                                      "fp64_tflops": st[3] / st[2] / 1e12, "spd_inverse_ms": 1e3 * min(t),
-                                     "inverse_residual": err}
+                                     "inverse_residual": err,
+                                     "sha": hashlib.sha256(ai.tobytes() + np.asarray(var).tobytes()).hexdigest()[:12]}
     print(json.dumps(out))
 
 
