@@ -599,7 +599,9 @@ __global__ void copy_block_kernel(int kb, const double *src, double *dst, int64_
 // launch repays (REML at n = 2,000 split at every step: 1.33 -> 1.72 ms per iteration).  REML at
 // n = 5,000 (5 GRMs): 11.7 ms per iteration as one launch per step, 10.3 with D beside the
 // self-deriving products, 8.0 with the panel launch (same bits).
-constexpr int CHOL_SPLIT = 768;
+// (Threshold A/B at n = 5,000: 384 / 768 / 1,536 tasks 8.02-8.32 / 8.10-8.66 / 7.92-8.01 ms per iteration;
+// at n = 2,000, 384 splits its first steps: 1.49-1.56 against 1.32-1.34 ms.)
+constexpr int CHOL_SPLIT = 1536;
 namespace {
 // the D stream: one per device, created on first use and kept (a pooled stream would be synchronised
 // by the host on release, after the whole factorisation)
