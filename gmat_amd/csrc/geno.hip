@@ -231,6 +231,8 @@ struct GrmWork {
   const int *stile;  // per segment: tile, first and end stage (the segment's slot = its index)
   const int *sit0, *sit1;
   const int *ta, *tb;  // per tile: row / column tile
+  const int *wrec;     // per workgroup, 8 ints: its segments [s0, s1) and its first segment's tile, first
+                       // and end stage, row and column tile (one scalar load at the start, not a chain of 3)
 };
 
 typedef int v8i_g __attribute__((ext_vector_type(8)));
@@ -265,11 +267,29 @@ __global__ __launch_bounds__(GNT) void grm_partial_kernel(const uint8_t *__restr
   // XCD-aware: workgroup b runs on XCD b mod 8, so the work ranges are dealt in 8 contiguous
   // groups -- the workgroups of one XCD stream neighbouring tiles (shared row panels) in its L2
   const int nx = gridDim.x % 8 == 0 ? 8 : 1, bl = (blockIdx.x % nx) * (gridDim.x / nx) + blockIdx.x / nx;
-  const int s0 = wk.seg0[bl], s1 = wk.seg0[bl + 1];
+  // the workgroup's record in two 16-byte loads issued together (the table starts with the records)
+  const v4i wa = ((const v4i *)wk.wrec)[2 * bl], wb = ((const v4i *)wk.wrec)[2 * bl + 1];
+  const int s0 = __builtin_amdgcn_readfirstlane(wa[0]), s1 = __builtin_amdgcn_readfirstlane(wa[1]);
   const unsigned voff = 16u * lane;
   for (int sg = s0; sg < s1; ++sg) {
-    const int t = wk.stile[sg], it0 = wk.sit0[sg], it1 = wk.sit1[sg];
-    const int64_t rb0 = (int64_t)(op ? wk.tb[t] : wk.ta[t]) * (GT / 32);
+    int t, it0, it1, ta, tb;
+    if (sg == s0) {
+      t = wa[2];
+      it0 = wa[3];
+      it1 = wb[0];
+      ta = wb[1];
+      tb = wb[2];
+    } else {
+      t = wk.stile[sg];
+      it0 = wk.sit0[sg];
+      it1 = wk.sit1[sg];
+      ta = wk.ta[t];
+      tb = wk.tb[t];
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    it0 = __builtin_amdgcn_readfirstlane(it0);
+    it1 = __builtin_amdgcn_readfirstlane(it1);
+    const int64_t rb0 = (int64_t)__builtin_amdgcn_readfirstlane(op ? tb : ta) * (GT / 32);
     const uint8_t *src[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) src[u] = img + (rb0 + q0 + u) * S * 1024;
@@ -570,7 +590,21 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   for (int sg = 0; sg < nseg; ++sg) slot0[st[sg] + 1] = sg + 1;  // segments are in tile order
   for (int t = 0; t < ntile; ++t) slot0[t + 1] = std::max(slot0[t + 1], slot0[t]);
   std::vector<int> tabl;
-  for (auto *v : {&seg0, &st, &s0, &s1, &ta, &tb, &slot0}) tabl.insert(tabl.end(), v->begin(), v->end());
+  std::vector<int> wrec(8 * (size_t)W, 0);
+  for (int w = 0; w < W; ++w) {
+    const int f = seg0[w];
+    int *r8 = &wrec[8 * (size_t)w];
+    r8[0] = seg0[w];
+    r8[1] = seg0[w + 1];
+    if (f < seg0[w + 1]) {
+      r8[2] = st[f];
+      r8[3] = s0[f];
+      r8[4] = s1[f];
+      r8[5] = ta[st[f]];
+      r8[6] = tb[st[f]];
+    }
+  }
+  for (auto *v : {&wrec, &seg0, &st, &s0, &s1, &ta, &tb, &slot0}) tabl.insert(tabl.end(), v->begin(), v->end());
   DBuf dc, dr, dpart, dk, dtab, dpar, dimg;
   const int64_t nd_img = (int64_t)nt * GT / 16;  // image dword positions: every tile row
   const int64_t nd = cdiv(nb, 4);
@@ -586,8 +620,9 @@ extern "C" int gmat_grm(gmat_geno *g, int kind, double small_val, double *kin, d
   GMAT_HIP(hipMemcpy(dtab.p, tabl.data(), tabl.size() * sizeof(int), hipMemcpyHostToDevice));
   const int *tp = dtab.as<int>();
   GrmWork wk;
-  wk.seg0 = tp;
-  wk.stile = tp + (W + 1);
+  wk.wrec = tp;  // first: 32-byte records at the buffer's (aligned) start
+  wk.seg0 = tp + 8 * (size_t)W;
+  wk.stile = wk.seg0 + (W + 1);
   wk.sit0 = wk.stile + nseg;
   wk.sit1 = wk.sit0 + nseg;
   wk.ta = wk.sit1 + nseg;
